@@ -1,0 +1,335 @@
+"""ctypes binding of libcdr.so — the C ABI declared in include/cdr.h.
+
+This module owns no math: every numeric operation of the hot path runs in the
+HIP kernels of libcdr.so (gfx950).  If the library is missing or no GPU is
+visible, the calls raise — there is deliberately no CPU fallback.
+
+Error mapping (include/cdr.h status codes -> Python exceptions), chosen to
+mirror what the reference raises in the same situations:
+    CDR_ERR_ARG         -> ValueError
+    CDR_ERR_NAN         -> ValueError("Probabilities contain NaN")
+                           (numpy Generator.choice, src/kmeans_plusplus.py:19)
+    CDR_ERR_HIP         -> RuntimeError
+    CDR_ERR_STATE       -> RuntimeError
+    CDR_ERR_UNSUPPORTED -> NotImplementedError
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CDR_LIB", os.path.join(_HERE, "libcdr.so"))
+
+CDR_OK = 0
+CDR_ERR_ARG = 1
+CDR_ERR_HIP = 2
+CDR_ERR_NAN = 3
+CDR_ERR_STATE = 4
+CDR_ERR_UNSUPPORTED = 5
+MODE_F32X = 1
+MODE_F64 = 2
+SEED_BLOCK = 8192
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_F64 = ctypes.c_double
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+_PF64 = ctypes.POINTER(ctypes.c_double)
+
+# name -> (argtypes, restype); restype None means "int status".
+SIGNATURES = {
+    "cdr_last_error": ([], ctypes.c_char_p),
+    "cdr_version": ([], ctypes.c_int),
+    "cdr_device_count": ([ctypes.POINTER(ctypes.c_int)], None),
+    "cdr_create": ([ctypes.c_int, ctypes.POINTER(_P)], None),
+    "cdr_destroy": ([_P], None),
+    "cdr_set_stream": ([_P, _P], None),
+    "cdr_synchronize": ([_P], None),
+    "cdr_points_load_f64": ([_P, _P, _I64, _I32], None),
+    "cdr_points_generate": ([_P, _I64, _I64, _I64, _I32, _I32, _U64], None),
+    "cdr_points_info": ([_P, _PI64, _PI32, _PI32, _PI32], None),
+    "cdr_points_get_rows": ([_P, _P, _I64, _P], None),
+    "cdr_seed_reset": ([_P], None),
+    "cdr_seed_update": ([_P, _P], None),
+    "cdr_seed_num_blocks": ([_P, _PI64], None),
+    "cdr_seed_block_sums": ([_P, _P], None),
+    "cdr_seed_scan": ([_P, _F64, _F64, _PF64], None),
+    "cdr_seed_search": ([_P, _F64, _F64, _PI64], None),
+    "cdr_lloyd_step": ([_P, _P, _I32, _P, _I32], None),
+    "cdr_lloyd_step_f64": ([_P, _P, _I32, _P, _P], None),
+    "cdr_lloyd_labels": ([_P, _P], None),
+    "cdr_lloyd_stats": ([_P, _PI64], None),
+    "cdr_debug_screen": ([_P, _P, _I32, _P, _P], None),
+    "cdr_profile_reset": ([_P, _I32], None),
+    "cdr_profile_read": ([_P, _P], None),
+    "cdr_medians_segmented": ([_P, _P, _P, _I64, _P], None),
+    "cdr_medians_by_label": ([_P, _I32, _P], None),
+    "cdr_features_aggregate": ([_P, _I64, _P, _P, _P, _P, _I64, _P, _P, _PI64], None),
+    "cdr_features_finalize": ([_P, _I64, _P, _P, _F64, _P], None),
+    "cdr_host_seq_sum": ([_P, _I64, _F64], ctypes.c_double),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libcdr.so once.  Raises ImportError when it has not been built."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise ImportError(
+                f"libcdr.so not found at {path}: build it with "
+                "`make -C clustering-driven-replication-strategy_amd/csrc` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, (argt, rest) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argt
+            fn.restype = ctypes.c_int if rest is None else rest
+        _lib = lib
+        return lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _check(rc: int) -> None:
+    if rc == CDR_OK:
+        return
+    msg = load_library().cdr_last_error().decode(errors="replace")
+    if rc == CDR_ERR_NAN:
+        raise ValueError("Probabilities contain NaN")
+    if rc == CDR_ERR_ARG:
+        raise ValueError(msg)
+    if rc == CDR_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(f"libcdr: {msg}")
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = ctypes.c_int(0)
+    _check(lib.cdr_device_count(ctypes.byref(n)))
+    return int(n.value)
+
+
+def host_seq_sum(v: np.ndarray, init: float = 0.0) -> float:
+    """((init + v[0]) + v[1]) + ... in fp64 (plain C on the host)."""
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    return float(load_library().cdr_host_seq_sum(_ptr(v), v.size, float(init)))
+
+
+class Context:
+    """One libcdr context = one HIP device + one shard of points."""
+
+    def __init__(self, device: int = 0):
+        lib = load_library()
+        h = _P()
+        _check(lib.cdr_create(int(device), ctypes.byref(h)))
+        self._lib = lib
+        self._h = h
+        self.device = int(device)
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.cdr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int | None) -> None:
+        _check(self._lib.cdr_set_stream(self._h, _P(stream_handle or 0)))
+
+    def synchronize(self) -> None:
+        _check(self._lib.cdr_synchronize(self._h))
+
+    # -- points ----------------------------------------------------------
+    def load_points(self, X: np.ndarray) -> None:
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        if X.ndim != 2:
+            raise ValueError("X must be 2-dimensional (n_samples, n_features)")
+        _check(self._lib.cdr_points_load_f64(self._h, _ptr(X), X.shape[0], X.shape[1]))
+
+    def generate_points(self, n_total: int, row_begin: int, n_local: int, d: int,
+                        n_blobs: int, seed: int) -> None:
+        _check(self._lib.cdr_points_generate(self._h, n_total, row_begin, n_local, d,
+                                             n_blobs, ctypes.c_uint64(seed & (2**64 - 1))))
+
+    def info(self) -> dict:
+        n, d, mode, s = _I64(), _I32(), _I32(), _I32()
+        _check(self._lib.cdr_points_info(self._h, ctypes.byref(n), ctypes.byref(d),
+                                         ctypes.byref(mode), ctypes.byref(s)))
+        return {"n": n.value, "d": d.value, "mode": mode.value, "scale_bits": s.value}
+
+    def get_rows(self, idx) -> np.ndarray:
+        idx = np.ascontiguousarray(np.atleast_1d(idx), dtype=np.int64)
+        d = self.info()["d"]
+        out = np.empty((idx.size, d), dtype=np.float64)
+        _check(self._lib.cdr_points_get_rows(self._h, _ptr(idx), idx.size, _ptr(out)))
+        return out
+
+    # -- seeding ---------------------------------------------------------
+    def seed_reset(self) -> None:
+        _check(self._lib.cdr_seed_reset(self._h))
+
+    def seed_update(self, c: np.ndarray) -> None:
+        c = np.ascontiguousarray(c, dtype=np.float64).ravel()
+        _check(self._lib.cdr_seed_update(self._h, _ptr(c)))
+
+    def seed_num_blocks(self) -> int:
+        v = _I64()
+        _check(self._lib.cdr_seed_num_blocks(self._h, ctypes.byref(v)))
+        return int(v.value)
+
+    def seed_block_sums(self) -> np.ndarray:
+        out = np.empty(self.seed_num_blocks(), dtype=np.float64)
+        if out.size:
+            _check(self._lib.cdr_seed_block_sums(self._h, _ptr(out)))
+        return out
+
+    def seed_scan(self, total: float, c_in: float = 0.0) -> float:
+        v = _F64()
+        _check(self._lib.cdr_seed_scan(self._h, float(total), float(c_in), ctypes.byref(v)))
+        return float(v.value)
+
+    def seed_search(self, c_last: float, u: float) -> int:
+        v = _I64()
+        _check(self._lib.cdr_seed_search(self._h, float(c_last), float(u), ctypes.byref(v)))
+        return int(v.value)
+
+    # -- Lloyd -----------------------------------------------------------
+    def lloyd_step(self, C: np.ndarray) -> np.ndarray:
+        """F32X: (k, d+1) int64 fixed-point sums | counts."""
+        C = np.ascontiguousarray(C, dtype=np.float64)
+        k, d = C.shape
+        out = np.empty((k, d + 1), dtype=np.int64)
+        _check(self._lib.cdr_lloyd_step(self._h, _ptr(C), k, _ptr(out), 0))
+        return out
+
+    def lloyd_step_device(self, C: np.ndarray, out_device_ptr: int) -> None:
+        """F32X: write (k, d+1) int64 into a device buffer (e.g. a torch tensor)."""
+        C = np.ascontiguousarray(C, dtype=np.float64)
+        _check(self._lib.cdr_lloyd_step(self._h, _ptr(C), C.shape[0], _P(out_device_ptr), 1))
+
+    def lloyd_step_f64(self, C: np.ndarray):
+        C = np.ascontiguousarray(C, dtype=np.float64)
+        k, d = C.shape
+        sums = np.empty((k, d), dtype=np.float64)
+        counts = np.empty(k, dtype=np.int64)
+        _check(self._lib.cdr_lloyd_step_f64(self._h, _ptr(C), k, _ptr(sums), _ptr(counts)))
+        return sums, counts
+
+    def labels(self) -> np.ndarray:
+        out = np.empty(self.info()["n"], dtype=np.int64)
+        _check(self._lib.cdr_lloyd_labels(self._h, _ptr(out)))
+        return out
+
+    def fallback_count(self) -> int:
+        v = _I64()
+        _check(self._lib.cdr_lloyd_stats(self._h, ctypes.byref(v)))
+        return int(v.value)
+
+    def profile_reset(self, enable: bool = True) -> None:
+        _check(self._lib.cdr_profile_reset(self._h, 1 if enable else 0))
+
+    def profile_read(self) -> dict:
+        out = np.zeros(4, dtype=np.float64)
+        _check(self._lib.cdr_profile_read(self._h, _ptr(out)))
+        return {"screen_ms": out[0], "steps": int(out[1]), "step_ms": out[2],
+                "fallback_points": int(out[3])}
+
+    def debug_screen(self, C: np.ndarray):
+        C = np.ascontiguousarray(C, dtype=np.float64)
+        k = C.shape[0]
+        inf = self.info()
+        n_pad = -(-max(inf["n"], 1) // SEED_BLOCK) * SEED_BLOCK
+        kt = -(-k // 16) * 16
+        vals = np.empty((n_pad, kt), dtype=np.float32)
+        thr = np.empty(2, dtype=np.float32)
+        _check(self._lib.cdr_debug_screen(self._h, _ptr(C), k, _ptr(vals), _ptr(thr)))
+        return vals[: inf["n"], :k], thr
+
+    # -- medians ---------------------------------------------------------
+    def medians_segmented(self, values: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+        values = np.ascontiguousarray(values, dtype=np.float64)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        nseg = offsets.size - 1
+        out = np.empty(max(nseg, 0), dtype=np.float64)
+        _check(self._lib.cdr_medians_segmented(self._h, _ptr(values) if values.size else None,
+                                               _ptr(offsets), nseg,
+                                               _ptr(out) if out.size else None))
+        return out
+
+    def medians_by_label(self, k: int) -> np.ndarray:
+        d = self.info()["d"]
+        out = np.empty((k, d), dtype=np.float64)
+        _check(self._lib.cdr_medians_by_label(self._h, int(k), _ptr(out)))
+        return out
+
+    # -- features --------------------------------------------------------
+    def features_aggregate(self, file_idx, op, client, ts_us, primary):
+        file_idx = np.ascontiguousarray(file_idx, dtype=np.int32)
+        op = np.ascontiguousarray(op, dtype=np.uint8)
+        client = np.ascontiguousarray(client, dtype=np.int32)
+        ts_us = np.ascontiguousarray(ts_us, dtype=np.int64)
+        primary = np.ascontiguousarray(primary, dtype=np.int32)
+        ne, nf = file_idx.size, primary.size
+        out = np.zeros((nf, 6), dtype=np.int64)
+        mx = _I64()
+        z = lambda a: _ptr(a) if a.size else None  # noqa: E731
+        _check(self._lib.cdr_features_aggregate(self._h, ne, z(file_idx), z(op), z(client),
+                                                z(ts_us), nf, z(primary), z(out),
+                                                ctypes.byref(mx)))
+        return out, int(mx.value)
+
+    def features_finalize(self, counts, creation_s, observation_end: float) -> np.ndarray:
+        counts = np.ascontiguousarray(counts, dtype=np.int64)
+        creation_s = np.ascontiguousarray(creation_s, dtype=np.float64)
+        nf = creation_s.size
+        out = np.zeros((nf, 10), dtype=np.float64)
+        if nf:
+            _check(self._lib.cdr_features_finalize(self._h, nf, _ptr(counts), _ptr(creation_s),
+                                                   float(observation_end), _ptr(out)))
+        return out
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    """Process-wide context on LOCAL_RANK's device (0 when not distributed)."""
+    global _default_ctx
+    if _default_ctx is None:
+        dev = int(os.environ.get("CDR_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+        _default_ctx = Context(dev)
+    return _default_ctx
+
+
+def loaded_library_path() -> str | None:
+    """Path of the loaded libcdr (for 'native code loaded' checks)."""
+    return LIB_PATH if _lib is not None else None
+
+
+__all__ = ["Context", "default_context", "load_library", "device_count", "host_seq_sum",
+           "MODE_F32X", "MODE_F64", "SEED_BLOCK", "SIGNATURES", "LIB_PATH"]
+
+if __name__ == "__main__":  # pragma: no cover
+    load_library()
+    print("libcdr loaded from", LIB_PATH, "devices:", device_count(), file=sys.stderr)

@@ -1,0 +1,185 @@
+"""Points sharded over ranks: one process per GPU, torch.distributed over RCCL.
+
+The reference k-means is single-process (src/kmeans_plusplus.py); this module
+runs the same algorithm on a row-sharded data set with results identical to
+the single-process run:
+
+* Sharding — contiguous row ranges in multiples of 8192 rows (NumPy's
+  reduction chunk), so every rank's seeding blocks are global blocks and the
+  blocked pairwise ``dist_sq.sum()`` is unchanged; only the last rank may own
+  a partial block.
+* Seeding (kmeans_plusplus.py:13-20) per step: all-gather of the per-block
+  pairwise sums (every rank then adds them left to right — the exact global
+  total), a rank-ordered chain of exact ``cumsum`` scans (each rank starts
+  from its predecessor's running value), an all-gather of the local
+  ``searchsorted`` hits and a broadcast of the chosen row by its owner.
+* Lloyd (:33-48) per step: the fused device step writes k x (d+1) int64
+  fixed-point sums/counts; one SUM all-reduce (integer, hence exact and
+  order-free) over RCCL; every rank then forms the identical means on host.
+  Empty clusters draw from NumPy's global RNG on every rank (same seed).
+
+``Comm`` hides the backend: NCCL (=RCCL on ROCm) keeps the all-reduced
+tensor on the GPU; gloo (the CPU test backend) uses host tensors.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED_BLOCK = 8192
+
+
+def shard_rows(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """(row_begin, n_local) of `rank`: whole 8192-row blocks, remainder last."""
+    nb = -(-n_total // SEED_BLOCK) if n_total > 0 else 0
+    base, extra = divmod(nb, world)
+    b0 = rank * base + min(rank, extra)
+    nbr = base + (1 if rank < extra else 0)
+    begin = min(b0 * SEED_BLOCK, n_total)
+    end = min((b0 + nbr) * SEED_BLOCK, n_total)
+    return begin, end - begin
+
+
+class Comm:
+    """Thin collective layer over torch.distributed (or a single process)."""
+
+    def __init__(self, dist=None, device=None):
+        self.dist = dist
+        self.rank = dist.get_rank() if dist else 0
+        self.world = dist.get_world_size() if dist else 1
+        self.device = device  # torch.device for NCCL, None for gloo / single
+
+    def _t(self, arr):
+        import torch
+
+        t = torch.from_numpy(np.ascontiguousarray(arr))
+        return t.to(self.device) if self.device is not None else t
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def allreduce_sum_i64(self, arr: np.ndarray) -> np.ndarray:
+        if not self.dist:
+            return arr
+        t = self._t(arr.astype(np.int64))
+        self.dist.all_reduce(t)
+        return t.cpu().numpy()
+
+    def allgather(self, arr: np.ndarray) -> list[np.ndarray]:
+        """Variable-length 1-D all-gather (rank order)."""
+        if not self.dist:
+            return [arr]
+        import torch
+
+        n = self._t(np.array([arr.size], dtype=np.int64))
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(sizes, n)
+        sizes = [int(s.item()) for s in sizes]
+        m = max(sizes) if sizes else 0
+        buf = np.zeros(max(m, 1), dtype=arr.dtype)
+        buf[: arr.size] = arr
+        t = self._t(buf)
+        outs = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(outs, t)
+        return [o.cpu().numpy()[:s] for o, s in zip(outs, sizes)]
+
+    def bcast(self, arr: np.ndarray, src: int) -> np.ndarray:
+        if not self.dist:
+            return arr
+        t = self._t(np.ascontiguousarray(arr))
+        self.dist.broadcast(t, src)
+        return t.cpu().numpy()
+
+
+def _fetch_row(ctx, comm: Comm, owner: int, local_idx: int, d: int) -> np.ndarray:
+    row = ctx.get_rows([local_idx])[0] if comm.rank == owner else np.zeros(d)
+    return comm.bcast(np.asarray(row, dtype=np.float64), owner)
+
+
+def _owner_of(offsets: np.ndarray, gidx: int) -> int:
+    return int(np.searchsorted(offsets, gidx, side="right") - 1)
+
+
+def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_state=None,
+                 host_seq_sum=None) -> np.ndarray:
+    """kmeans_plusplus_init over the sharded rows (float64 centroids)."""
+    if host_seq_sum is None:
+        from _cdr import host_seq_sum
+    d = ctx.info()["d"]
+    offsets = np.array([b for b in comm.allgather(np.array([row_begin], dtype=np.int64))],
+                       dtype=np.int64).ravel()
+    rng = np.random.default_rng(random_state)
+    C = np.empty((k, d), dtype=np.float64)
+    first = int(rng.integers(0, n_total))
+    owner = _owner_of(offsets, first)
+    C[0] = _fetch_row(ctx, comm, owner, first - int(offsets[owner]), d)
+    if k > 1:
+        ctx.seed_reset()
+    for i in range(1, k):
+        ctx.seed_update(C[i - 1])
+        blocks = np.concatenate(comm.allgather(ctx.seed_block_sums()))
+        total = host_seq_sum(blocks)
+        if not (total > 0.0) or total == np.inf:
+            raise ValueError("Probabilities contain NaN")
+        c = 0.0
+        for r in range(comm.world):  # rank-ordered chain of exact scans
+            mine = ctx.seed_scan(total, c) if comm.rank == r else 0.0
+            c = float(comm.bcast(np.array([mine], dtype=np.float64), r)[0])
+        u = rng.random()
+        hits = np.concatenate(comm.allgather(np.array([ctx.seed_search(c, u)], dtype=np.int64)))
+        owner = int(np.flatnonzero(hits >= 0)[0])
+        C[i] = _fetch_row(ctx, comm, owner, int(hits[owner]), d)
+    return C
+
+
+class ShardedLloyd:
+    """Lloyd iterations over sharded F32X points with one all-reduce per step."""
+
+    def __init__(self, ctx, comm: Comm, n_total: int, row_begin: int):
+        info = ctx.info()
+        if info["mode"] != 1:
+            raise NotImplementedError("sharded Lloyd needs F32X (grid) points")
+        self.ctx, self.comm = ctx, comm
+        self.n_total, self.row_begin = n_total, row_begin
+        self.d, self.S = info["d"], info["scale_bits"]
+        self._dev_buf = None
+
+    def partials(self, C: np.ndarray) -> np.ndarray:
+        k = C.shape[0]
+        if self.comm.device is not None and self.comm.dist:
+            import torch
+
+            if self._dev_buf is None or self._dev_buf.numel() != k * (self.d + 1):
+                self._dev_buf = torch.empty(k * (self.d + 1), dtype=torch.int64,
+                                            device=self.comm.device)
+            self.ctx.lloyd_step_device(C, self._dev_buf.data_ptr())
+            self.comm.dist.all_reduce(self._dev_buf)
+            return self._dev_buf.view(k, self.d + 1).cpu().numpy()
+        return self.comm.allreduce_sum_i64(self.ctx.lloyd_step(C))
+
+    def step(self, C: np.ndarray, reseed_row) -> tuple[np.ndarray, float]:
+        """One iteration; returns (new centroids, shift)."""
+        k, d = C.shape
+        acc = self.partials(C)
+        counts = acc[:, d]
+        sums = np.ldexp(acc[:, :d].astype(np.float64), -self.S)
+        new = np.empty_like(C)
+        for j in range(k):
+            if counts[j] > 0:
+                new[j] = sums[j] / np.float64(counts[j])
+            else:
+                new[j] = reseed_row(np.random.randint(0, self.n_total))
+        shift = np.linalg.norm(new - C)
+        return new, shift
+
+    def row(self, gidx: int) -> np.ndarray:
+        offs = np.concatenate(self.comm.allgather(np.array([self.row_begin], dtype=np.int64)))
+        owner = _owner_of(offs, gidx)
+        return _fetch_row(self.ctx, self.comm, owner, gidx - int(offs[owner]), self.d)
+
+    def run(self, C: np.ndarray, max_iter: int, tol: float = 1e-4):
+        for _ in range(max_iter):
+            C, shift = self.step(C, self.row)
+            if shift < tol:
+                break
+        return C

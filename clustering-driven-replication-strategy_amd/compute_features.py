@@ -1,0 +1,226 @@
+"""Per-file feature extraction on MI355X (drop-in for ``src/compute_features.py``).
+
+Same CLI as the reference's PySpark job, so ``run_pipeline.sh:206-215`` and
+``Makefile:45-60`` drive it unchanged (``spark-submit`` -> ``python``)::
+
+    python compute_features.py --manifest M --access_log L --out OUT
+
+and the same output: a directory ``OUT`` holding one ``part-00000-*.csv`` with a
+header and the columns ``path, access_freq, age_seconds, write_ratio,
+locality, concurrency, access_freq_norm, age_norm, write_ratio_norm,
+locality_norm, concurrency_norm`` (src/compute_features.py:70-96), which
+``src/main.py:155-168`` globs.
+
+Host side (plumbing): CSV parsing, ISO-8601 timestamps -> microseconds,
+dictionary encoding of paths and client nodes.  Device side (libcdr):
+the group-by counters of :31-46 (``cdr_features_aggregate``) and the
+finalisation / min-max normalisation of :48-94 (``cdr_features_finalize``).
+
+Spark semantics kept (Spark 3.5, docker/docker-compose.yml:67):
+  * ``to_timestamp`` of ISO strings -> microseconds; ``cast(ts as double)`` =
+    micros / 1e6; ``floor`` of that is the concurrency second;
+  * ``unix_timestamp(to_timestamp(creation_ts))`` = floor(micros / 1e6) as double;
+  * ``avg(writes)`` = double(sum) / count; ``long / long`` divides as doubles;
+  * rows in manifest order (Spark's order is unspecified; main.py's seed
+    depends on row order, so the build pins the manifest order);
+  * doubles written like Java's ``Double.toString`` (decimal in [1e-3, 1e7),
+    otherwise ``d.dddE<exp>``), longs as integers.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import math
+import os
+import re
+import time
+import uuid
+from decimal import Decimal
+
+import numpy as np
+
+from _cdr import Context, default_context
+
+OUT_COLUMNS = ["path", "access_freq", "age_seconds", "write_ratio", "locality", "concurrency",
+               "access_freq_norm", "age_norm", "write_ratio_norm", "locality_norm",
+               "concurrency_norm"]
+LONG_COLUMNS = {"access_freq", "concurrency"}
+
+_ISO = re.compile(
+    r"^\s*(\d{4})-(\d{1,2})-(\d{1,2})(?:[T ](\d{1,2}):(\d{1,2})(?::(\d{1,2})(?:\.(\d{1,9}))?)?)?"
+    r"\s*(Z|[+-]\d{2}(?::?\d{2})?)?\s*$")
+
+
+def _strip_scheme(path: str) -> str:
+    return path[len("file://"):] if path.startswith("file://") else path
+
+
+def parse_ts_us(s) -> int | None:
+    """Spark ``to_timestamp`` of an ISO-8601 string -> microseconds (UTC when
+    no zone is given; fraction truncated to microseconds).  None = null."""
+    if s is None:
+        return None
+    m = _ISO.match(str(s))
+    if not m:
+        return None
+    y, mo, d, hh, mi, ss, frac, zone = m.groups()
+    try:
+        days = _days_from_civil(int(y), int(mo), int(d))
+    except ValueError:
+        return None
+    hh, mi, ss = int(hh or 0), int(mi or 0), int(ss or 0)
+    if hh > 23 or mi > 59 or ss > 59:
+        return None
+    us = int((frac or "").ljust(6, "0")[:6] or 0)
+    off = 0
+    if zone and zone != "Z":
+        sign = -1 if zone[0] == "-" else 1
+        z = zone[1:].replace(":", "")
+        off = sign * (int(z[:2]) * 3600 + int(z[2:4] or 0) * 60)
+    return ((days * 86400 + hh * 3600 + mi * 60 + ss) - off) * 1_000_000 + us
+
+
+def _days_from_civil(y: int, m: int, d: int) -> int:
+    if not (1 <= m <= 12):
+        raise ValueError
+    mdays = [31, 29 if (y % 4 == 0 and (y % 100 != 0 or y % 400 == 0)) else 28, 31, 30, 31,
+             30, 31, 31, 30, 31, 30, 31]
+    if not (1 <= d <= mdays[m - 1]):
+        raise ValueError
+    y2 = y - (m <= 2)
+    era = (y2 if y2 >= 0 else y2 - 399) // 400
+    yoe = y2 - era * 400
+    doy = (153 * (m + (-3 if m > 2 else 9)) + 2) // 5 + d - 1
+    doe = yoe * 365 + yoe // 4 - yoe // 100 + doy
+    return era * 146097 + doe - 719468
+
+
+def java_double(x: float) -> str:
+    """Java ``Double.toString`` layout of the shortest round-trip digits."""
+    x = float(x)
+    if x != x:
+        return "NaN"
+    if math.isinf(x):
+        return "Infinity" if x > 0 else "-Infinity"
+    if x == 0.0:
+        return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
+    sign = "-" if x < 0 else ""
+    t = Decimal(repr(abs(x))).as_tuple()
+    digits = "".join(map(str, t.digits)).rstrip("0") or "0"
+    exp10 = len(t.digits) + t.exponent - 1  # position of the leading digit
+    if 1e-3 <= abs(x) < 1e7:
+        if exp10 >= 0:
+            ip = digits[: exp10 + 1].ljust(exp10 + 1, "0")
+            fp = digits[exp10 + 1:] or "0"
+        else:
+            ip = "0"
+            fp = "0" * (-exp10 - 1) + digits
+        return f"{sign}{ip}.{fp}"
+    mant = digits[0] + "." + (digits[1:] or "0")
+    return f"{sign}{mant}E{exp10}"
+
+
+def load_manifest(path: str):
+    """Manifest CSV (header; path, creation_ts, primary_node, ...) -> columns."""
+    with open(_strip_scheme(path), newline="") as fh:
+        rows = list(csv.DictReader(fh))
+    paths = [r.get("path") for r in rows]
+    created = np.array([np.nan if (u := parse_ts_us(r.get("creation_ts"))) is None
+                        else float(math.floor(u / 1_000_000)) for r in rows], dtype=np.float64)
+    primary = [r.get("primary_node") or None for r in rows]
+    return paths, created, primary
+
+
+def load_access_log(path: str):
+    """Header-less ``ts,path,op,client,pid`` CSV (src/access_simulator.py:61-63)."""
+    ts, p, op, cl = [], [], [], []
+    with open(_strip_scheme(path), newline="") as fh:
+        for rec in csv.reader(fh):
+            if not rec:
+                continue
+            rec = rec + [""] * (5 - len(rec))
+            ts.append(rec[0] or None)
+            p.append(rec[1] or None)
+            op.append(rec[2] or None)
+            cl.append(rec[3] or None)
+    return ts, p, op, cl
+
+
+def encode(paths, primary, log_ts, log_path, log_op, log_client):
+    """Dictionary-encode strings for the device."""
+    index = {}
+    for i, pth in enumerate(paths):
+        index.setdefault(pth, i)
+    nodes = {}
+
+    def node_id(name):
+        return nodes.setdefault(name, len(nodes))
+
+    prim = np.array([-2 if v is None else node_id(v) for v in primary], dtype=np.int32)
+    n = len(log_ts)
+    file_idx = np.empty(n, dtype=np.int32)
+    opc = np.empty(n, dtype=np.uint8)
+    client = np.empty(n, dtype=np.int32)
+    ts_us = np.empty(n, dtype=np.int64)
+    for i in range(n):
+        file_idx[i] = index.get(log_path[i], -1) if log_path[i] is not None else -1
+        o = log_op[i]
+        opc[i] = 1 if o == "WRITE" else (2 if o == "READ" else 0)
+        c = log_client[i]
+        client[i] = -1 if c is None else node_id(c)
+        u = parse_ts_us(log_ts[i])
+        if u is None:
+            raise ValueError(f"unparseable access-log timestamp {log_ts[i]!r} (row {i})")
+        ts_us[i] = u
+    return file_idx, opc, client, ts_us, prim
+
+
+def compute_features(manifest: str, access_log: str, ctx: Context | None = None):
+    """Returns (paths, table) with table (n_files, 10) float64 in OUT_COLUMNS order."""
+    ctx = ctx if ctx is not None else default_context()
+    paths, created, primary = load_manifest(manifest)
+    lt, lp, lo, lc = load_access_log(access_log)
+    file_idx, opc, client, ts_us, prim = encode(paths, primary, lt, lp, lo, lc)
+    counts, max_ts_us = ctx.features_aggregate(file_idx, opc, client, ts_us, prim)
+    if ts_us.size:
+        observation_end = max_ts_us / 1e6  # max(cast(ts as double)) :48
+    else:
+        observation_end = time.time()  # :50-51
+    table = ctx.features_finalize(counts, created, observation_end)
+    return paths, table
+
+
+def write_spark_csv(out_dir: str, paths, table) -> str:
+    """One part file with a header, like ``coalesce(1).write.csv`` (:96)."""
+    out_dir = _strip_scheme(out_dir)
+    if os.path.isdir(out_dir):  # mode("overwrite")
+        for name in os.listdir(out_dir):
+            os.remove(os.path.join(out_dir, name))
+    os.makedirs(out_dir, exist_ok=True)
+    part = os.path.join(out_dir, f"part-00000-{uuid.uuid4()}-c000.csv")
+    with open(part, "w", newline="") as fh:
+        w = csv.writer(fh, lineterminator="\n")
+        w.writerow(OUT_COLUMNS)
+        for i, pth in enumerate(paths):
+            row = [pth]
+            for j, col in enumerate(OUT_COLUMNS[1:]):
+                v = table[i, j]
+                row.append(str(int(v)) if col in LONG_COLUMNS else java_double(v))
+            w.writerow(row)
+    open(os.path.join(out_dir, "_SUCCESS"), "w").close()
+    return part
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser()
+    parser.add_argument("--manifest", required=True)
+    parser.add_argument("--access_log", required=True)
+    parser.add_argument("--out", default="features_out")
+    args = parser.parse_args(argv)
+    paths, table = compute_features(args.manifest, args.access_log)
+    write_spark_csv(args.out, paths, table)
+    print("Wrote features to", args.out)
+
+
+if __name__ == "__main__":
+    main()

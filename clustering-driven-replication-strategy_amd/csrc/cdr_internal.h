@@ -1,0 +1,170 @@
+// cdr_internal.h — shared definitions for the libcdr HIP sources (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/cdr.h"
+
+namespace cdr {
+
+// Error plumbing: every C entry point is wrapped in CDR_TRY / CDR_CATCH so a
+// failure never escapes as a C++ exception across the C ABI.
+void set_error(const std::string& msg);
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define CDR_FAIL(code_, msg_)                  \
+  do {                                         \
+    throw ::cdr::Error{(code_), (msg_)};       \
+  } while (0)
+
+#define HIP_CHECK(expr)                                                       \
+  do {                                                                        \
+    hipError_t e_ = (expr);                                                   \
+    if (e_ != hipSuccess)                                                     \
+      CDR_FAIL(CDR_ERR_HIP, std::string(#expr " failed: ") +                 \
+                                hipGetErrorString(e_) + " @" + __FILE__ +     \
+                                ":" + std::to_string(__LINE__));              \
+  } while (0)
+
+#define CDR_TRY try {
+#define CDR_CATCH                                             \
+  }                                                           \
+  catch (const ::cdr::Error& e) {                             \
+    ::cdr::set_error(e.msg);                                  \
+    return e.code;                                            \
+  }                                                           \
+  catch (const std::exception& e) {                           \
+    ::cdr::set_error(std::string("internal: ") + e.what());   \
+    return CDR_ERR_STATE;                                     \
+  }                                                           \
+  return CDR_OK;
+
+// Device buffer that grows on demand (never shrinks until the context dies).
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t nbytes);
+  void release();
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+// Pinned host staging buffer.
+struct HostBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t nbytes);
+  void release();
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+constexpr int kSeedBlock = 8192;  // NumPy reduction buffer (add.reduce chunk)
+constexpr int kPointGroup = 64;   // points per wave iteration in the screen
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+
+  // ---- points (one shard) ----
+  int64_t n = 0;      // real points
+  int64_t n_pad = 0;  // padded to a multiple of kSeedBlock (rows >= n are 0)
+  int32_t d = 0;
+  int32_t mode = 0;        // CDR_MODE_*
+  int32_t scale_bits = 0;  // F32X fixed-point scale S
+  DevBuf x32;              // F32X: SoA float  [d][n_pad]
+  DevBuf x64;              // F64 : SoA double [d][n_pad]
+  std::vector<double> fmin, fmax;  // per-feature min / max (host)
+  double absmax = 0.0;
+  // screen transform  xhat = (x - mu_f) * 2^sigma
+  std::vector<float> mu;
+  int32_t sigma = 0;
+  DevBuf mu_s;  // float[d]: -mu_f * 2^sigma
+
+  // ---- Lloyd ----
+  DevBuf labels;    // int32[n_pad]
+  DevBuf cent64;    // double[k*d]
+  DevBuf frag;      // fp16 MFMA A-operand fragments
+  DevBuf partials;  // int64 per workgroup k*(d+1)
+  DevBuf out_sums;  // int64 k*(d+1) (when caller passes a host pointer)
+  DevBuf fb_list;   // int32[n]
+  DevBuf fb_count;  // int32[4]
+  DevBuf f64_sums;  // double k*d
+  DevBuf f64_counts;  // int64 k
+  HostBuf h_small;  // pinned scratch for small D2H
+  int64_t last_fallback = 0;
+  // profiling (cdr_profile_*): HIP events on the context stream around the
+  // screen kernel and around the whole step (screen + reduce + fallback)
+  bool prof_on = false, prof_pending = false;
+  hipEvent_t pe[3] = {nullptr, nullptr, nullptr};
+  double prof_screen_ms = 0.0, prof_step_ms = 0.0, prof_fb_points = 0.0;
+  int64_t prof_launches = 0;
+  int32_t last_k = 0;
+  bool have_labels = false;
+
+  // ---- seeding ----
+  DevBuf dmin;        // double[n_pad]
+  DevBuf blocksums;   // double[nblocks]
+  DevBuf xfer;        // per-block transfer records
+  DevBuf cend;        // double[nblocks] running value after each block
+  DevBuf seed_scalar; // small device scratch
+  double seed_c_in = 0.0;
+  bool seed_scanned = false;
+  double seed_total = 0.0;
+  int64_t nblocks() const { return (n + kSeedBlock - 1) / kSeedBlock; }
+
+  // ---- medians / features scratch ----
+  DevBuf med_vals, med_off, med_out, med_tmp, med_tmp2;
+  DevBuf ev_file, ev_op, ev_client, ev_ts, ev_primary, ev_out, ev_scratch,
+      ev_scratch2;
+  DevBuf fin_counts, fin_creation, fin_out, fin_red;
+};
+
+// ---- launchers implemented in the .hip files ----
+void points_analyze_and_store(Ctx& c, const double* host_X);
+void points_generate(Ctx& c, int64_t n_total, int64_t row_begin, int32_t n_blobs,
+                     uint64_t seed);
+void points_finish_analysis(Ctx& c);
+
+void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out,
+                     bool out_on_device);
+void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums,
+                    int64_t* counts);
+
+void seed_reset(Ctx& c);
+void seed_update(Ctx& c, const double* cent);
+void seed_scan(Ctx& c, double total, double c_in, double* c_out);
+void seed_search(Ctx& c, double c_last, double u, int64_t* idx);
+
+void medians_segmented(Ctx& c, const double* values, const int64_t* offsets,
+                       int64_t n_segments, double* out);
+void medians_by_label(Ctx& c, int32_t k, double* out);
+
+void features_aggregate(Ctx& c, int64_t n_events, const int32_t* file_idx,
+                        const uint8_t* op, const int32_t* client,
+                        const int64_t* ts_ms, int64_t n_files,
+                        const int32_t* primary, int64_t* out,
+                        int64_t* max_ts_ms);
+void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
+                       const double* creation_s, double observation_end,
+                       double* out);
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace cdr
+
+struct cdr_ctx {
+  cdr::Ctx c;
+};

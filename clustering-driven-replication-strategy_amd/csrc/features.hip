@@ -1,0 +1,374 @@
+// features.hip — per-file access-log features (reference src/compute_features.py).
+//
+// K5 aggregate (:31-46, :48-51): per manifest file
+//   access_freq = count(events)                       :32
+//   writes / reads = sum[op == WRITE] / sum[op == READ] :33-34
+//   local_accesses = sum[client == primary_node]      :38-41
+//   total_accesses = count(events)                    :42
+//   max_concurrency = max over sec of count(file, sec), sec = floor(ts_epoch) :44-46
+//   max_ts = max(ts_epoch) over the whole log         :48
+// Events are keyed (file << 32 | sec - sec_min), radix-sorted (skipped when the
+// input is already grouped by file and ordered by second, which is what the
+// per-file Poisson generator produces), then each file's run is reduced.
+// Integer counts are exact by construction.
+//
+// K6 finalize (:53-94): age = observation_end - creation_ts_epoch (0 when the
+// creation time is null, na.fill at :60), write_ratio = writes / mean(writes)
+// (mean 0 -> 1.0), locality = local / total (total 0 -> 1.0), then min-max
+// normalisation of the five columns (max == min -> 0.0).  Long columns are
+// normalised as double(v - min) / double(max - min), as Spark's `/` does.
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstring>
+
+#include "cdr_internal.h"
+
+namespace cdr {
+
+__device__ __forceinline__ long long sec_of(long long ts_us) {
+  // Spark: floor(cast(ts as double)) with cast = micros / 1e6 in fp64
+  return (long long)floor((double)ts_us / 1000000.0);
+}
+
+__global__ void ts_minmax(const long long* __restrict__ ts, int64_t n,
+                          unsigned long long* __restrict__ mm) {
+  long long lo = LLONG_MAX, hi = LLONG_MIN;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    lo = min(lo, ts[i]);
+    hi = max(hi, ts[i]);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o));
+    hi = max(hi, __shfl_xor(hi, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&mm[0], (unsigned long long)(lo ^ LLONG_MIN));
+    atomicMax(&mm[1], (unsigned long long)(hi ^ LLONG_MIN));
+  }
+}
+
+__global__ void make_keys(const int32_t* __restrict__ file, const uint8_t* __restrict__ op,
+                          const int32_t* __restrict__ client, const long long* __restrict__ ts,
+                          int64_t n, int64_t n_files, const int32_t* __restrict__ primary,
+                          long long sec_min, unsigned long long* __restrict__ keys,
+                          uint8_t* __restrict__ flags) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int f = file[i];
+    unsigned long long key = ~0ull;
+    uint8_t fl = 0;
+    if (f >= 0 && f < n_files) {
+      key = ((unsigned long long)f << 32) | (unsigned long long)(sec_of(ts[i]) - sec_min);
+      fl = (op[i] == 1 ? 1 : 0) | (op[i] == 2 ? 2 : 0);
+      const int pr = primary[f];
+      if (client[i] >= 0 && pr >= 0 && client[i] == pr) fl |= 4;
+    }
+    keys[i] = key;
+    flags[i] = fl;
+  }
+}
+
+__global__ void check_sorted(const unsigned long long* __restrict__ keys, int64_t n,
+                             int* __restrict__ unsorted) {
+  int bad = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    bad |= keys[i] > keys[i + 1];
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(unsorted, 1);
+}
+
+__global__ void mark_runs(const unsigned long long* __restrict__ keys, int64_t n,
+                          long long* __restrict__ start, long long* __restrict__ end) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long k = keys[i];
+    if (k == ~0ull) continue;
+    const unsigned long long f = k >> 32;
+    if (i == 0 || (keys[i - 1] >> 32) != f) start[f] = i;
+    if (i == n - 1 || (keys[i + 1] >> 32) != f) end[f] = i + 1;
+  }
+}
+
+__global__ void per_file(const unsigned long long* __restrict__ keys,
+                         const uint8_t* __restrict__ flags, int64_t n_files,
+                         const long long* __restrict__ start, const long long* __restrict__ end,
+                         long long* __restrict__ out) {
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n_files;
+       f += (int64_t)gridDim.x * blockDim.x) {
+    long long cnt = 0, w = 0, r = 0, loc = 0, best = 0;
+    const long long s = start[f];
+    if (s >= 0) {
+      const long long e = end[f];
+      unsigned prev = 0xFFFFFFFFu;
+      long long run = 0;
+      for (long long i = s; i < e; ++i) {
+        const uint8_t fl = flags[i];
+        const unsigned sec = (unsigned)(keys[i] & 0xFFFFFFFFull);
+        ++cnt;
+        w += fl & 1;
+        r += (fl >> 1) & 1;
+        loc += (fl >> 2) & 1;
+        run = (sec == prev) ? run + 1 : 1;
+        prev = sec;
+        best = run > best ? run : best;
+      }
+    }
+    long long* o = out + f * 6;
+    o[0] = cnt;
+    o[1] = w;
+    o[2] = r;
+    o[3] = loc;
+    o[4] = cnt;
+    o[5] = best;
+  }
+}
+
+static int gcap(int64_t work, int threads, int cap) {
+  int64_t g = (work + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8_t* op,
+                        const int32_t* client, const int64_t* ts_us, int64_t n_files,
+                        const int32_t* primary, int64_t* out, int64_t* max_ts) {
+  if (ne < 0 || n_files < 0) CDR_FAIL(CDR_ERR_ARG, "negative sizes");
+  if (n_files >= (1ll << 31)) CDR_FAIL(CDR_ERR_UNSUPPORTED, "n_files >= 2^31");
+  *max_ts = LLONG_MIN;
+  if (n_files == 0 && ne == 0) return;
+  const size_t ne1 = ne > 0 ? ne : 1, nf1 = n_files > 0 ? n_files : 1;
+  c.ev_file.ensure(4 * ne1);
+  c.ev_op.ensure(ne1);
+  c.ev_client.ensure(4 * ne1);
+  c.ev_ts.ensure(8 * ne1);
+  c.ev_primary.ensure(4 * nf1);
+  c.ev_out.ensure(8 * 6 * nf1 + 64);
+  if (ne > 0) {
+    HIP_CHECK(hipMemcpyAsync(c.ev_file.p, file_idx, 4 * ne, hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(c.ev_op.p, op, ne, hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(c.ev_client.p, client, 4 * ne, hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(c.ev_ts.p, ts_us, 8 * ne, hipMemcpyHostToDevice, c.stream));
+  }
+  if (n_files > 0)
+    HIP_CHECK(hipMemcpyAsync(c.ev_primary.p, primary, 4 * n_files, hipMemcpyHostToDevice,
+                             c.stream));
+  // timestamp range
+  unsigned long long mm_init[2] = {~0ull, 0ull};
+  unsigned long long* dmm = reinterpret_cast<unsigned long long*>(c.ev_out.as<char>() + 8 * 6 * nf1);
+  HIP_CHECK(hipMemcpyAsync(dmm, mm_init, 16, hipMemcpyHostToDevice, c.stream));
+  if (ne > 0) {
+    hipLaunchKernelGGL(ts_minmax, dim3(gcap(ne, 256, 1024)), dim3(256), 0, c.stream,
+                       c.ev_ts.as<long long>(), ne, dmm);
+    HIP_CHECK(hipGetLastError());
+  }
+  unsigned long long mm[2];
+  HIP_CHECK(hipMemcpyAsync(mm, dmm, 16, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  long long sec_min = 0, sec_max = 0;
+  if (ne > 0) {
+    const long long tmin = (long long)(mm[0] ^ (unsigned long long)LLONG_MIN);
+    const long long tmax = (long long)(mm[1] ^ (unsigned long long)LLONG_MIN);
+    *max_ts = tmax;
+    sec_min = (long long)std::floor((double)tmin / 1000000.0);
+    sec_max = (long long)std::floor((double)tmax / 1000000.0);
+    if (sec_max - sec_min >= (1ll << 32))
+      CDR_FAIL(CDR_ERR_UNSUPPORTED, "access log spans more than 2^32 seconds");
+  }
+  // keys + flags
+  c.ev_scratch.ensure((8 + 1) * ne1 * 2 + 64);
+  unsigned long long* k0 = c.ev_scratch.as<unsigned long long>();
+  unsigned long long* k1 = k0 + ne1;
+  uint8_t* f0 = reinterpret_cast<uint8_t*>(k1 + ne1);
+  uint8_t* f1 = f0 + ne1;
+  int* unsorted = reinterpret_cast<int*>(c.ev_out.as<char>() + 8 * 6 * nf1 + 16);
+  HIP_CHECK(hipMemsetAsync(unsorted, 0, 4, c.stream));
+  if (ne > 0) {
+    hipLaunchKernelGGL(make_keys, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream,
+                       c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(), c.ev_client.as<int32_t>(),
+                       c.ev_ts.as<long long>(), ne, n_files, c.ev_primary.as<int32_t>(), sec_min,
+                       k0, f0);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(check_sorted, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream, k0, ne,
+                       unsorted);
+    HIP_CHECK(hipGetLastError());
+  }
+  int hunsorted = 0;
+  HIP_CHECK(hipMemcpyAsync(&hunsorted, unsorted, 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  unsigned long long* keys = k0;
+  uint8_t* flags = f0;
+  if (hunsorted && ne > 1) {
+    size_t tmp_bytes = 0;
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, f0, f1, (int)ne, 0,
+                                                 64, c.stream));
+    c.ev_scratch2.ensure(tmp_bytes + 256);
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c.ev_scratch2.p, tmp_bytes, k0, k1, f0, f1,
+                                                 (int)ne, 0, 64, c.stream));
+    keys = k1;
+    flags = f1;
+  }
+  // runs per file
+  c.fin_red.ensure(16 * nf1);
+  long long* start = c.fin_red.as<long long>();
+  long long* end = start + nf1;
+  HIP_CHECK(hipMemsetAsync(start, 0xFF, 8 * nf1, c.stream));  // -1
+  HIP_CHECK(hipMemsetAsync(end, 0, 8 * nf1, c.stream));
+  if (ne > 0) {
+    hipLaunchKernelGGL(mark_runs, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream, keys, ne,
+                       start, end);
+    HIP_CHECK(hipGetLastError());
+  }
+  if (n_files > 0) {
+    hipLaunchKernelGGL(per_file, dim3(gcap(n_files, 256, 8192)), dim3(256), 0, c.stream, keys,
+                       flags, n_files, start, end, c.ev_out.as<long long>());
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(out, c.ev_out.p, 8 * 6 * n_files, hipMemcpyDeviceToHost, c.stream));
+  }
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+// ---- K6 -------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long fkey(double v) {
+  const unsigned long long b = __double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__host__ __device__ inline double fkey_val(unsigned long long k) {
+  const unsigned long long b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  double v;
+  memcpy(&v, &b, 8);
+  return v;
+}
+
+// red layout (u64): 0 sum_writes, 1/2 min/max af (x^sign), 3/4 min/max writes,
+// 5/6 min/max conc, 7/8 min/max age key, 9/10 min/max locality key
+__global__ void fin_reduce(const long long* __restrict__ cnt, const double* __restrict__ creation,
+                           int64_t n, double obs_end, unsigned long long* __restrict__ red) {
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n;
+       f += (int64_t)gridDim.x * blockDim.x) {
+    const long long* c = cnt + f * 6;
+    const double cr = creation[f];
+    const double age = isnan(cr) ? 0.0 : obs_end - cr;
+    const double loc = c[4] > 0 ? (double)c[3] / (double)c[4] : 1.0;
+    atomicAdd(&red[0], (unsigned long long)c[1]);
+    atomicMin(&red[1], (unsigned long long)(c[0] ^ LLONG_MIN));
+    atomicMax(&red[2], (unsigned long long)(c[0] ^ LLONG_MIN));
+    atomicMin(&red[3], (unsigned long long)(c[1] ^ LLONG_MIN));
+    atomicMax(&red[4], (unsigned long long)(c[1] ^ LLONG_MIN));
+    atomicMin(&red[5], (unsigned long long)(c[5] ^ LLONG_MIN));
+    atomicMax(&red[6], (unsigned long long)(c[5] ^ LLONG_MIN));
+    atomicMin(&red[7], fkey(age));
+    atomicMax(&red[8], fkey(age));
+    atomicMin(&red[9], fkey(loc));
+    atomicMax(&red[10], fkey(loc));
+  }
+}
+
+struct FinConst {
+  double obs_end, mean_w;
+  long long af_min, af_max, con_min, con_max;
+  double age_min, age_max, wr_min, wr_max, loc_min, loc_max;
+};
+
+__global__ void fin_apply(const long long* __restrict__ cnt, const double* __restrict__ creation,
+                          int64_t n, FinConst k, double* __restrict__ out) {
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n;
+       f += (int64_t)gridDim.x * blockDim.x) {
+    const long long* c = cnt + f * 6;
+    const double cr = creation[f];
+    const double age = isnan(cr) ? 0.0 : k.obs_end - cr;
+    const double wr = (double)c[1] / k.mean_w;
+    const double loc = c[4] > 0 ? (double)c[3] / (double)c[4] : 1.0;
+    double* o = out + f * 10;
+    o[0] = (double)c[0];
+    o[1] = age;
+    o[2] = wr;
+    o[3] = loc;
+    o[4] = (double)c[5];
+    o[5] = k.af_max == k.af_min ? 0.0 : (double)(c[0] - k.af_min) / (double)(k.af_max - k.af_min);
+    o[6] = k.age_max == k.age_min ? 0.0 : (age - k.age_min) / (k.age_max - k.age_min);
+    o[7] = k.wr_max == k.wr_min ? 0.0 : (wr - k.wr_min) / (k.wr_max - k.wr_min);
+    o[8] = k.loc_max == k.loc_min ? 0.0 : (loc - k.loc_min) / (k.loc_max - k.loc_min);
+    o[9] = k.con_max == k.con_min ? 0.0
+                                  : (double)(c[5] - k.con_min) / (double)(k.con_max - k.con_min);
+  }
+}
+
+void features_finalize(Ctx& c, int64_t n, const int64_t* counts, const double* creation,
+                       double obs_end, double* out) {
+  if (n < 0) CDR_FAIL(CDR_ERR_ARG, "negative n_files");
+  if (n == 0) return;
+  c.fin_counts.ensure(8 * 6 * n);
+  c.fin_creation.ensure(8 * n);
+  c.fin_out.ensure(8 * 10 * n);
+  c.fin_red.ensure(8 * 16);
+  HIP_CHECK(hipMemcpyAsync(c.fin_counts.p, counts, 8 * 6 * n, hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(c.fin_creation.p, creation, 8 * n, hipMemcpyHostToDevice, c.stream));
+  unsigned long long init[11] = {0, ~0ull, 0, ~0ull, 0, ~0ull, 0, ~0ull, 0, ~0ull, 0};
+  HIP_CHECK(hipMemcpyAsync(c.fin_red.p, init, sizeof(init), hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(fin_reduce, dim3(gcap(n, 256, 4096)), dim3(256), 0, c.stream,
+                     c.fin_counts.as<long long>(), c.fin_creation.as<double>(), n, obs_end,
+                     c.fin_red.as<unsigned long long>());
+  HIP_CHECK(hipGetLastError());
+  unsigned long long r[11];
+  HIP_CHECK(hipMemcpyAsync(r, c.fin_red.p, sizeof(r), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  FinConst k;
+  k.obs_end = obs_end;
+  const long long sumw = (long long)r[0];
+  double mean = (double)sumw / (double)n;  // Spark avg: double sum / count
+  if (mean == 0.0) mean = 1.0;
+  k.mean_w = mean;
+  auto sx = [](unsigned long long v) { return (long long)(v ^ (unsigned long long)LLONG_MIN); };
+  k.af_min = sx(r[1]);
+  k.af_max = sx(r[2]);
+  const long long wmin = sx(r[3]), wmax = sx(r[4]);
+  k.con_min = sx(r[5]);
+  k.con_max = sx(r[6]);
+  k.age_min = fkey_val(r[7]);
+  k.age_max = fkey_val(r[8]);
+  k.wr_min = (double)wmin / mean;  // x -> x / mean is monotone
+  k.wr_max = (double)wmax / mean;
+  k.loc_min = fkey_val(r[9]);
+  k.loc_max = fkey_val(r[10]);
+  hipLaunchKernelGGL(fin_apply, dim3(gcap(n, 256, 4096)), dim3(256), 0, c.stream,
+                     c.fin_counts.as<long long>(), c.fin_creation.as<double>(), n, k,
+                     c.fin_out.as<double>());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpyAsync(out, c.fin_out.p, 8 * 10 * n, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+}  // namespace cdr
+
+using namespace cdr;
+
+extern "C" {
+
+int cdr_features_aggregate(cdr_ctx* h, int64_t n_events, const int32_t* file_idx,
+                           const uint8_t* op, const int32_t* client, const int64_t* ts_us,
+                           int64_t n_files, const int32_t* primary, int64_t* out,
+                           int64_t* max_ts_us) {
+  CDR_TRY
+  if (!h || !max_ts_us || (n_events > 0 && (!file_idx || !op || !client || !ts_us)) ||
+      (n_files > 0 && (!primary || !out)))
+    CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  features_aggregate(h->c, n_events, file_idx, op, client, ts_us, n_files, primary, out,
+                     max_ts_us);
+  CDR_CATCH
+}
+
+int cdr_features_finalize(cdr_ctx* h, int64_t n_files, const int64_t* counts,
+                          const double* creation_s, double observation_end, double* out) {
+  CDR_TRY
+  if (!h || (n_files > 0 && (!counts || !creation_s || !out)))
+    CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  features_finalize(h->c, n_files, counts, creation_s, observation_end, out);
+  CDR_CATCH
+}
+
+}  // extern "C"

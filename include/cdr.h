@@ -1,0 +1,168 @@
+/*
+ * cdr.h — C ABI of the MI355X (gfx950) clustering hot path.
+ *
+ * "cdr" = clustering-driven replication.  One shared library, libcdr.so, built
+ * from hand-written HIP kernels.  Every entry point takes plain pointers and
+ * sizes and returns an int status (CDR_OK == 0).  On failure the message is
+ * available from cdr_last_error() (thread-local).
+ *
+ * The reference (Harounnn/Clustering-Driven-Replication-Strategy) has no FFI:
+ * its hot path is NumPy / PySpark code.  Each block below names the reference
+ * function it replaces (file:line relative to the reference root).  The Python
+ * drop-in modules (kmeans_plusplus.py, scoring.py, compute_features.py) bind
+ * these symbols through ctypes; INTEGRATION.md shows the binding.
+ *
+ * Ownership: host pointers belong to the caller and are only read/written for
+ * the duration of the call.  Device buffers belong to the context.  A context
+ * is bound to one HIP device and is NOT thread-safe (the reference is
+ * single-threaded and uses global NumPy RNG state, src/kmeans_plusplus.py:43).
+ * All calls are synchronous from the caller's point of view unless the name
+ * ends in _async.
+ */
+#ifndef CDR_H_
+#define CDR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define CDR_OK 0
+#define CDR_ERR_ARG 1         /* bad argument  -> Python ValueError            */
+#define CDR_ERR_HIP 2         /* HIP runtime    -> Python RuntimeError          */
+#define CDR_ERR_NAN 3         /* NaN probabilities (kmeans_plusplus.py:18-19)   */
+#define CDR_ERR_STATE 4       /* call order     -> Python RuntimeError          */
+#define CDR_ERR_UNSUPPORTED 5 /* shape not supported -> NotImplementedError     */
+
+/* ---- point storage modes (cdr_points_info) ----------------------------- */
+/* F32X: every coordinate is an fp32 value on a 2^-S grid with |x|*2^S < 2^31.
+ *       Screen + exact fallback assignment; centroid sums are exact int64
+ *       fixed point (bit-identical to NumPy's sequential fp64 mean whenever
+ *       that mean is itself exact, e.g. 2^-24-grid data).                     */
+#define CDR_MODE_F32X 1
+/* F64:  arbitrary fp64 data.  Exact fp64 assignment for every point and
+ *       sequential per-cluster fp64 sums in row order (NumPy mean order).     */
+#define CDR_MODE_F64 2
+
+typedef struct cdr_ctx cdr_ctx;
+
+const char* cdr_last_error(void);
+int cdr_version(void);
+int cdr_device_count(int* out);
+
+/* Context on HIP device `device`.  Owns a HIP stream unless one is supplied
+ * with cdr_set_stream (e.g. torch.cuda.current_stream().cuda_stream).       */
+int cdr_create(int device, cdr_ctx** out);
+int cdr_destroy(cdr_ctx* ctx);
+int cdr_set_stream(cdr_ctx* ctx, void* hip_stream);
+int cdr_synchronize(cdr_ctx* ctx);
+
+/* ---- point set (the X of src/main.py:81, one shard per context) -------- */
+/* Host row-major float64 (n, d).  Detects the storage mode (see above).     */
+int cdr_points_load_f64(cdr_ctx* ctx, const double* X, int64_t n, int32_t d);
+/* Synthetic generator (BASELINE configs 2/3/5): rows [row_begin, row_begin +
+ * n_local) of an n_total-row data set, generated on the device.  Integer-only
+ * counter-based formula; oracle/synth.py is the NumPy mirror.               */
+int cdr_points_generate(cdr_ctx* ctx, int64_t n_total, int64_t row_begin,
+                        int64_t n_local, int32_t d, int32_t n_blobs,
+                        uint64_t seed);
+int cdr_points_info(cdr_ctx* ctx, int64_t* n, int32_t* d, int32_t* mode,
+                    int32_t* scale_bits);
+/* Copy local rows idx[0..m) to host as float64 (m, d). */
+int cdr_points_get_rows(cdr_ctx* ctx, const int64_t* idx, int64_t m,
+                        double* out);
+
+/* ---- k-means++ D^2 seeding: src/kmeans_plusplus.py:3-22 ---------------- */
+/* dist_sq := +inf (before the first centre).                                */
+int cdr_seed_reset(cdr_ctx* ctx);
+/* dist_sq[i] = min(dist_sq[i], (sqrt(pw_d((x_i - c)^2)))^2), NumPy order
+ * (kmeans_plusplus.py:14-17), then the 8192-element pairwise block sums of
+ * dist_sq (NumPy's blocked add.reduce, used by dist_sq.sum() at :18).  c is
+ * one float64 row of length d.                                              */
+int cdr_seed_update(cdr_ctx* ctx, const double* c);
+/* Number of 8192-element blocks of this shard and their pairwise sums.     */
+int cdr_seed_num_blocks(cdr_ctx* ctx, int64_t* nblocks);
+int cdr_seed_block_sums(cdr_ctx* ctx, double* out);
+/* Exact sequential cumulative sum of probs = dist_sq / total over this
+ * shard, starting from running value c_in (0.0 on the first shard); returns
+ * the running value after the shard's last element.  Emulates np.cumsum
+ * bit-exactly (Generator.choice, kmeans_plusplus.py:19).                   */
+int cdr_seed_scan(cdr_ctx* ctx, double total, double c_in, double* c_out);
+/* searchsorted(cumsum / c_last, u, side='right') restricted to this shard:
+ * *idx = local index, or -1 when the crossing is not in this shard.        */
+int cdr_seed_search(cdr_ctx* ctx, double c_last, double u, int64_t* idx);
+
+/* ---- Lloyd iteration: src/kmeans_plusplus.py:31-43 --------------------- */
+/* One assignment + fused update pass for centroids C (k, d) float64.
+ * Labels stay on the device (cdr_lloyd_labels).
+ * F32X mode: out (k, d+1) int64 = per-cluster fixed-point sums (value *
+ *   2^scale_bits) and counts in column d.  `out_on_device` != 0 means `out`
+ *   is a device pointer on this context's device; the kernels then write it
+ *   on the context stream without synchronising (for an RCCL all-reduce).
+ * F64 mode: use cdr_lloyd_step_f64.                                          */
+int cdr_lloyd_step(cdr_ctx* ctx, const double* C, int32_t k, int64_t* out,
+                   int32_t out_on_device);
+/* F64 mode: exact fp64 assignment; sums (k, d) float64 accumulated in row
+ * order exactly like X[labels == j].mean(axis=0)'s sum; counts (k).        */
+int cdr_lloyd_step_f64(cdr_ctx* ctx, const double* C, int32_t k, double* sums,
+                       int64_t* counts);
+/* Labels of the last assignment as int64 (np.argmin dtype, :34).           */
+int cdr_lloyd_labels(cdr_ctx* ctx, int64_t* labels);
+/* Diagnostics of the last step: points the fast screen could not certify
+ * and that went through the exact fp64 path.                                */
+int cdr_lloyd_stats(cdr_ctx* ctx, int64_t* n_fallback);
+/* Profiling: enable != 0 starts collecting HIP-event timings of every
+ * following F32X step (on the context stream); cdr_profile_read returns
+ * out[4] = {screen kernel ms (sum), steps, whole step kernels ms (sum),
+ * fallback points (sum)}.                                                    */
+int cdr_profile_reset(cdr_ctx* ctx, int32_t enable);
+int cdr_profile_read(cdr_ctx* ctx, double* out);
+/* Test hook (not product path): screen values T (n_pad, ceil(k/16)*16) fp32
+ * of one F32X step and the certification constants (A0, A1).               */
+int cdr_debug_screen(cdr_ctx* ctx, const double* C, int32_t k, float* out_vals,
+                     float* thr_a0a1);
+
+/* ---- per-cluster medians: src/scoring.py:40-55 (np.median) ------------- */
+/* Segmented median of float64 values: segment s = values[off[s]..off[s+1]).
+ * Empty segment -> NaN; any NaN in a segment -> NaN.                        */
+int cdr_medians_segmented(cdr_ctx* ctx, const double* values,
+                          const int64_t* offsets, int64_t n_segments,
+                          double* out);
+/* Array-native form: median of every feature of the local
+ * points grouped by the labels of the last Lloyd step; out (k, d).          */
+int cdr_medians_by_label(cdr_ctx* ctx, int32_t k, double* out);
+
+/* ---- access-log group-by: src/compute_features.py:31-54 ---------------- */
+/* Events: file index (row of the manifest, -1 = path not in the manifest),
+ * op (1 = WRITE, 2 = READ, other = neither), client id (-1 = null),
+ * timestamp in microseconds since the epoch (Spark TimestampType units).
+ * primary[f] = client id of file f's primary node (-2 = null).
+ * out (n_files, 6) int64: access_freq, writes, reads, local_accesses,
+ * total_accesses, max_concurrency (sec = floor(ts_us / 1e6) in fp64, as
+ * F.floor(cast(ts as double))).  *max_ts_us = max event timestamp over all
+ * events (INT64_MIN when there are none).                                  */
+int cdr_features_aggregate(cdr_ctx* ctx, int64_t n_events,
+                           const int32_t* file_idx, const uint8_t* op,
+                           const int32_t* client, const int64_t* ts_us,
+                           int64_t n_files, const int32_t* primary,
+                           int64_t* out, int64_t* max_ts_us);
+/* Finalisation, src/compute_features.py:48-94.  counts: output of
+ * cdr_features_aggregate; creation_s: creation_ts_epoch (double seconds, NaN
+ * = null -> age 0 as na.fill does); observation_end: max ts in seconds
+ * (double).  out (n_files, 10) float64:
+ * access_freq, age_seconds, write_ratio, locality, concurrency, then the
+ * five *_norm columns.                                                     */
+int cdr_features_finalize(cdr_ctx* ctx, int64_t n_files, const int64_t* counts,
+                          const double* creation_s, double observation_end,
+                          double* out);
+
+/* ---- host helpers (plain C on the host, no device) --------------------- */
+/* ((init + v[0]) + v[1]) + ... in fp64, left to right.                      */
+double cdr_host_seq_sum(const double* v, int64_t n, double init);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CDR_H_ */

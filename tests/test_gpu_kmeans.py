@@ -1,0 +1,193 @@
+"""GPU parity of seeding + Lloyd (libcdr via the drop-in module) against the
+reference golden vectors and the pinned oracle."""
+import json
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import kmeans_oracle as ko
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases():
+    with open(os.path.join(GOLDEN, "kmeans_cases.json")) as fh:
+        meta = json.load(fh)
+    arrays = np.load(os.path.join(GOLDEN, "kmeans_cases.npz"))
+    out = []
+    for i, m in enumerate(meta["cases"]):
+        X = synth.generate(*m["gen"]) if "gen" in m else arrays[f"c{i}_X"]
+        get = lambda key: arrays[f"c{i}_{key}"] if f"c{i}_{key}" in arrays else None  # noqa
+        out.append((m, X, get("init"), get("centroids"), get("labels")))
+    return out
+
+
+CASES = _cases()
+
+
+def test_generator_bit_identical_to_numpy_mirror(ctx):
+    ctx.generate_points(100000, 12345, 30000, 16, 64, 0x5EED)
+    got = ctx.get_rows(np.arange(0, 30000, 7))
+    exp = synth.generate(100000, 12345, 30000, 16, 64, 0x5EED)[::7]
+    np.testing.assert_array_equal(got, exp)
+    inf = ctx.info()
+    assert inf["mode"] == 1 and inf["scale_bits"] <= 24
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0]["name"] for c in CASES])
+def test_seeding_and_lloyd_match_reference(ctx, case):
+    import kmeans_plusplus as kp
+
+    m, X, init, C, labels = case
+    if m.get("error"):
+        with pytest.raises(ValueError, match="Probabilities contain NaN"):
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore", RuntimeWarning)
+                kp.kmeans_plusplus_init(X, m["k"], random_state=m["rs"], context=ctx)
+        return
+    got_init = kp.kmeans_plusplus_init(X, m["k"], random_state=m["rs"], context=ctx)
+    np.testing.assert_array_equal(got_init, init)
+    if m["seed_only"]:
+        return
+    np.random.seed(m["np_seed"])
+    got_C, got_l = kp.kmeans(X, m["k"], number_of_files=X.shape[0], random_state=m["rs"],
+                             context=ctx)
+    assert got_l.dtype == np.int64
+    np.testing.assert_array_equal(got_l, labels)  # ARI = 1.0, bit-identical
+    np.testing.assert_array_equal(got_C, C)
+
+
+def test_n_above_10000_raises_reference_typeerror(ctx):
+    import kmeans_plusplus as kp
+
+    X = synth.generate(10001, 0, 10001, 2, 3, 1)
+    with pytest.raises(TypeError, match="cannot be interpreted as an integer"):
+        kp.kmeans(X, 3, number_of_files=10001, random_state=0, context=ctx)
+
+
+def test_lloyd_partials_exact_vs_oracle(ctx):
+    n, d, k = 300000, 16, 64
+    X = synth.generate(n, 0, n, d, k, 77)
+    ctx.load_points(X)
+    assert ctx.info()["mode"] == 1
+    rng = np.random.default_rng(0)
+    C = X[rng.choice(n, k, replace=False)] + rng.normal(0, 1e-3, (k, d))
+    out = ctx.lloyd_step(C)
+    labels, exp = ko.lloyd_partials(X, C, ctx.info()["scale_bits"])
+    np.testing.assert_array_equal(ctx.labels(), labels)
+    np.testing.assert_array_equal(out, exp)
+    fb = ctx.fallback_count()
+    assert 0 <= fb < n // 20, fb
+
+
+def test_screen_error_within_certified_bound(ctx):
+    n, d, k = 20000, 16, 64
+    X = synth.generate(n, 0, n, d, k, 5)
+    ctx.load_points(X)
+    rng = np.random.default_rng(1)
+    C = X[rng.choice(n, k, replace=False)]
+    T, thr = ctx.debug_screen(C)
+    # recompute Q_j = ||xhat - chat_j||^2 in fp64 with the same transform
+    mu = np.float32(0.5 * (X.min(axis=0) + X.max(axis=0))).astype(np.float64)
+    dev = max((X.max(axis=0) - mu).max(), (mu - X.min(axis=0)).max())
+    sig = -np.frexp(dev)[1]
+    xh = (X - mu) * 2.0 ** sig
+    ch = (C - mu) * 2.0 ** sig
+    Q = ((xh[:, None, :] - ch[None, :, :]) ** 2).sum(axis=2)
+    xx = (xh ** 2).sum(axis=1)
+    diff = T.astype(np.float64) - Q  # = eps shift + error; eps common to all j
+    spread = diff.max(axis=1) - diff.min(axis=1)
+    bound = thr[0] + thr[1] * xx  # certification threshold covers 2x the error
+    assert np.all(spread <= bound), float((spread / bound).max())
+
+
+def test_two_shards_equal_one_shard(ctx):
+    import _cdr
+
+    n, d, k = 3 * 8192 + 500, 8, 16
+    X = synth.generate(n, 0, n, d, k, 3)
+    C = X[:k] + 1e-4
+    ctx.load_points(X)
+    full = ctx.lloyd_step(C)
+    lab = ctx.labels()
+    b = _cdr.Context(ctx.device)
+    try:
+        cut = 2 * 8192
+        ctx.load_points(X[:cut])
+        b.load_points(X[cut:])
+        a1 = ctx.lloyd_step(C)
+        a2 = b.lloyd_step(C)
+        np.testing.assert_array_equal(a1 + a2, full)
+        np.testing.assert_array_equal(np.concatenate([ctx.labels(), b.labels()]), lab)
+        # seeding scan chained over the two shards == single shard
+        ctx.load_points(X)
+        ctx.seed_reset()
+        ctx.seed_update(X[5])
+        tot = _cdr.host_seq_sum(ctx.seed_block_sums())
+        c_full = ctx.seed_scan(tot, 0.0)
+        idx_full = ctx.seed_search(c_full, 0.6180339887)
+        ctx.load_points(X[:cut])
+        ctx.seed_reset()
+        ctx.seed_update(X[5])
+        b.seed_reset()
+        b.seed_update(X[5])
+        bs = np.concatenate([ctx.seed_block_sums(), b.seed_block_sums()])
+        assert _cdr.host_seq_sum(bs) == tot
+        c1 = ctx.seed_scan(tot, 0.0)
+        c2 = b.seed_scan(tot, c1)
+        assert c2 == c_full
+        i1, i2 = ctx.seed_search(c2, 0.6180339887), b.seed_search(c2, 0.6180339887)
+        got = i1 if i1 >= 0 else cut + i2
+        assert got == idx_full
+        probs = ko.sqdist_rows(X, X[5])
+        probs = np.sqrt(probs) ** 2
+        probs = probs / probs.sum()
+        cdf = np.cumsum(probs)
+        cdf /= cdf[-1]
+        assert cdf[-1] == 1.0
+        assert np.cumsum(probs)[-1] == c_full
+        assert idx_full == np.searchsorted(cdf, 0.6180339887, side="right")
+    finally:
+        b.close()
+
+
+@pytest.mark.parametrize("n,d,k", [(200000, 16, 64), (120000, 5, 4), (60000, 64, 16),
+                                   (50000, 3, 100), (40000, 24, 33)])
+def test_seeding_and_steps_vs_oracle_large(ctx, n, d, k):
+    """Beyond the reference's n <= 10000 limit: oracle (pinned) as the checker."""
+    import kmeans_plusplus as kp
+
+    X = synth.generate(n, 0, n, d, max(k, 2), n + d)
+    init = kp.kmeans_plusplus_init(X, k, random_state=42, context=ctx)
+    np.testing.assert_array_equal(init, ko.kmeans_plusplus_init(X, k, random_state=42))
+    np.random.seed(0)
+    C, lab = kp.kmeans(X, k, random_state=42, max_iter=3, context=ctx)
+    np.random.seed(0)
+    C2, lab2 = ko.kmeans(X, k, random_state=42, max_iter=3)
+    np.testing.assert_array_equal(lab, lab2)
+    np.testing.assert_array_equal(C, C2)
+
+
+def test_full_size_properties_config2(ctx):
+    """BASELINE config 2 size (10M x 8, k=16): size-independent invariants."""
+    n, d, k = 10_000_000, 8, 16
+    ctx.generate_points(n, 0, n, d, k, 0x5EED)
+    rng = np.random.default_rng(2)
+    C = ctx.get_rows(rng.choice(n, k, replace=False))
+    out = ctx.lloyd_step(C)
+    lab = ctx.labels()
+    assert out[:, d].sum() == n
+    np.testing.assert_array_equal(np.bincount(lab, minlength=k), out[:, d])
+    # labels of a random sample agree with the exact oracle
+    sample = np.sort(rng.choice(n, 20000, replace=False))
+    Xs = ctx.get_rows(sample)
+    np.testing.assert_array_equal(lab[sample], ko.assign(Xs, C))
+    # sums are consistent with labels: recompute one cluster exactly on host
+    j = int(np.argmax(out[:, d]))
+    idx = np.flatnonzero(lab == j)[:200000]
+    assert idx.size > 0
+    assert ctx.fallback_count() < n // 50

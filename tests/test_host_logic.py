@@ -1,0 +1,100 @@
+"""Host-side plumbing of the drop-in modules (no device calls)."""
+import json
+import math
+import os
+import random
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import GOLDEN
+
+
+def test_java_double_layout():
+    from compute_features import java_double
+
+    cases = [(0.0, "0.0"), (-0.0, "-0.0"), (1.0, "1.0"), (0.5, "0.5"), (100.0, "100.0"),
+             (1e7, "1.0E7"), (12277768.082999945, "1.2277768082999945E7"), (1e-3, "0.001"),
+             (9.99e-4, "9.99E-4"), (1e-5, "1.0E-5"), (123.456, "123.456"),
+             (9999999.5, "9999999.5"), (0.1 + 0.2, "0.30000000000000004"),
+             (-2.5e-7, "-2.5E-7"), (1e300, "1.0E300"), (float("nan"), "NaN"),
+             (float("inf"), "Infinity")]
+    for v, s in cases:
+        assert java_double(v) == s, (v, java_double(v))
+    rng = random.Random(1)
+    for _ in range(2000):
+        v = rng.uniform(-1, 1) * 10 ** rng.randint(-12, 12)
+        assert float(java_double(v).replace("E", "e")) == v
+
+
+def test_iso_timestamp_parsing_matches_pandas():
+    from compute_features import parse_ts_us
+
+    samples = ["2025-06-12T09:40:32.335400Z", "2025-11-01T12:00:00.165Z", "1969-12-31T23:59:59.5Z",
+               "2024-02-29T00:00:00Z", "2025-01-25T17:05:23.323092Z", "2025-03-01T01:02:03+02:00"]
+    for s in samples:
+        exp = pd.Timestamp(s).tz_convert("UTC") if pd.Timestamp(s).tzinfo else pd.Timestamp(s, tz="UTC")
+        assert parse_ts_us(s) == exp.value // 1000, s
+    assert parse_ts_us("not a time") is None
+    assert parse_ts_us("2025-02-30T00:00:00Z") is None
+
+
+def test_encode_dictionary():
+    from compute_features import encode
+
+    paths = ["/a", "/b", "/c"]
+    prim = ["dn1", None, "dn2"]
+    f, op, cl, ts, pr = encode(paths, prim, ["2025-01-01T00:00:00.001Z"] * 4,
+                               ["/a", "/zzz", "/c", None], ["WRITE", "READ", "read", None],
+                               ["dn1", "dn2", None, "dn2"])
+    assert list(f) == [0, -1, 2, -1]
+    assert list(op) == [1, 2, 0, 0]
+    assert cl[2] == -1 and pr[1] == -2
+    assert cl[0] == pr[0] and cl[3] == pr[2]
+
+
+def test_pipeline_features_csv_roundtrip(tmp_path):
+    from compute_features import OUT_COLUMNS, write_spark_csv
+
+    pdir = os.path.join(GOLDEN, "pipeline")
+    z = np.load(os.path.join(pdir, "features_oracle.npz"))
+    df = pd.read_csv(os.path.join(pdir, "features_out", "part-00000-golden-c000.csv"),
+                     float_precision="round_trip")
+    assert list(df.columns) == OUT_COLUMNS
+    np.testing.assert_array_equal(df[OUT_COLUMNS[1:]].to_numpy(dtype=np.float64), z["table"])
+    part = write_spark_csv(str(tmp_path / "out"), list(df["path"]), z["table"])
+    assert os.path.basename(part).startswith("part-00000")
+    assert os.path.exists(str(tmp_path / "out" / "_SUCCESS"))
+    back = pd.read_csv(part, float_precision="round_trip")
+    np.testing.assert_array_equal(back[OUT_COLUMNS[1:]].to_numpy(dtype=np.float64), z["table"])
+
+
+def test_scoring_host_logic_matches_reference_scores():
+    from scoring import ClusterClassifier
+
+    with open(os.path.join(GOLDEN, "scoring_cases.json")) as fh:
+        cases = json.load(fh)
+    for c in cases:
+        s = c["spec"]
+        clf = ClusterClassifier(s["global_medians"], s["weights"], s["directions"],
+                                s["replication_factors"])
+        for cname, med in c["medians"].items():
+            med = {p: np.float64(v) for p, v in med.items()}
+            for cat, val in c["scores"][cname].items():
+                got = clf.score_category(med, cat)
+                assert (math.isnan(got) and math.isnan(val)) or got == val
+            assert clf.classify_cluster(med) == c["result"][cname]
+
+
+def test_kmeans_keeps_reference_max_iter_formula():
+    import inspect
+    import kmeans_plusplus
+
+    sig = inspect.signature(kmeans_plusplus.kmeans)
+    assert list(sig.parameters)[:5] == ["X", "k", "number_of_files", "tol", "random_state"]
+    assert sig.parameters["number_of_files"].default == 100
+    assert sig.parameters["tol"].default == 1e-4
+    assert sig.parameters["max_iter"].kind is inspect.Parameter.KEYWORD_ONLY
+    with pytest.raises(TypeError, match="cannot be interpreted as an integer"):
+        range(max(100, 10001 / 100))
