@@ -490,7 +490,7 @@ static size_t screen_lds_bytes(int KT, int DCH, int k, int d) {
 
 bool screen_supported(const Ctx& c, int k) {
   const int DCH = (c.d + 15) / 16, KT = (k + 15) / 16;
-  return c.d <= 64 && DCH <= 4 && screen_lds_bytes(KT, DCH, k, c.d) <= 96 * 1024;
+  return c.d <= 64 && DCH <= 4 && screen_lds_bytes(KT, DCH, k, c.d) <= 64 * 1024;
 }
 
 // Upload centroids (row-major fp64) for the exact kernels.
