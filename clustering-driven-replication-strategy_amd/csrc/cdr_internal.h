@@ -70,6 +70,16 @@ struct HostBuf {
 };
 
 constexpr int kSeedBlock = 8192;  // NumPy reduction buffer (add.reduce chunk)
+
+// Point layout in HBM ("quad-interleaved SoA"): features are grouped in quads;
+// quad q of point i is 4 consecutive values at ((q * n_pad) + i) * 4.  One
+// 16-byte load gives a lane four features of one point, and a wave reading
+// quad q of 64 consecutive points reads 1 KiB contiguously.  d is padded to
+// d4 = ceil(d/4)*4 with zero features.
+__host__ __device__ __forceinline__ int64_t xidx(int64_t f, int64_t i, int64_t n_pad) {
+  return (((f >> 2) * n_pad) + i) * 4 + (f & 3);
+}
+__host__ __device__ __forceinline__ int d4_of(int d) { return (d + 3) & ~3; }
 constexpr int kPointGroup = 64;   // points per wave iteration in the screen
 
 struct Ctx {
@@ -84,8 +94,8 @@ struct Ctx {
   int32_t d = 0;
   int32_t mode = 0;        // CDR_MODE_*
   int32_t scale_bits = 0;  // F32X fixed-point scale S
-  DevBuf x32;              // F32X: SoA float  [d][n_pad]
-  DevBuf x64;              // F64 : SoA double [d][n_pad]
+  DevBuf x32;              // F32X: float  [d4/4][n_pad][4]   (xidx)
+  DevBuf x64;              // F64 : double [d4/4][n_pad][4]   (xidx)
   std::vector<double> fmin, fmax;  // per-feature min / max (host)
   double absmax = 0.0;
   // screen transform  xhat = (x - mu_f) * 2^sigma
@@ -99,8 +109,9 @@ struct Ctx {
   DevBuf frag;      // fp16 MFMA A-operand fragments
   DevBuf partials;  // int64 per workgroup k*(d+1)
   DevBuf out_sums;  // int64 k*(d+1) (when caller passes a host pointer)
-  DevBuf fb_list;   // int32[n]
-  DevBuf fb_count;  // int32[4]
+  DevBuf fb_list;   // int32: one region of fb_cap entries per screen wave
+  DevBuf fb_count;  // int32[fb_regions + 1]: per-region counts, then the total
+  int fb_regions = 0;
   DevBuf f64_sums;  // double k*d
   DevBuf f64_counts;  // int64 k
   HostBuf h_small;  // pinned scratch for small D2H
@@ -113,6 +124,7 @@ struct Ctx {
   int64_t prof_launches = 0;
   int32_t last_k = 0;
   bool have_labels = false;
+  int screen_ablate = 0;  // timing experiments only
 
   // ---- seeding ----
   DevBuf dmin;        // double[n_pad]

@@ -1,10 +1,10 @@
 // cdr_runtime.hip — context, buffers, point loading / generation and the C ABI
 // entry points of libcdr.so (declared in include/cdr.h).
 //
-// Point layout in HBM: structure of arrays, one row per feature, padded to a
-// multiple of 8192 points (the NumPy reduction block, see seeding):
-//     F32X: float  X[f * n_pad + i]      F64: double X[f * n_pad + i]
-// Rows i >= n are zero and never produce labels, sums or probabilities.
+// Point layout in HBM: quad-interleaved structure of arrays (xidx() in
+// cdr_internal.h), padded to a multiple of 8192 points (the NumPy reduction
+// block, see seeding).  Rows i >= n and features f >= d are zero and never
+// produce labels, sums or probabilities.
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -77,7 +77,7 @@ __global__ void stats_kernel(const T* __restrict__ X, int64_t n, int64_t n_pad,
   int not32 = 0, nonfin = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    double v = (double)X[(int64_t)f * n_pad + i];
+    double v = (double)X[xidx(f, i, n_pad)];
     if (!isfinite(v)) {
       nonfin = 1;
       continue;
@@ -113,7 +113,7 @@ __global__ void rowmajor_to_soa64(const double* __restrict__ src, int64_t rows,
        t < rows * d; t += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = t / d;
     int f = (int)(t - r * d);
-    dst[(int64_t)f * n_pad + row0 + r] = src[t];
+    dst[xidx(f, row0 + r, n_pad)] = src[t];
   }
 }
 
@@ -157,7 +157,7 @@ __global__ void generate_kernel(float* __restrict__ X, int64_t row_begin,
                         (int64_t)((hn >> 32) & 0xFFFF) + (int64_t)(hn >> 48);
       int64_t u = center + 13 * (s - 131070);
       u = u < 0 ? 0 : (u > 0xFFFFFF ? 0xFFFFFF : u);
-      X[(int64_t)f * n_pad + i] = (float)u * (1.0f / 16777216.0f);
+      X[xidx(f, i, n_pad)] = (float)u * (1.0f / 16777216.0f);
     }
   }
 }
@@ -242,10 +242,10 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   HIP_CHECK(hipMemcpyAsync(c.mu_s.p, ms.data(), sizeof(float) * d,
                            hipMemcpyHostToDevice, c.stream));
   if (c.mode == CDR_MODE_F32X && have_f64_copy) {
-    c.x32.ensure(sizeof(float) * (size_t)d * c.n_pad);
-    hipLaunchKernelGGL(soa64_to_soa32, dim3(grid_for((int64_t)d * c.n_pad, 256)),
+    c.x32.ensure(sizeof(float) * (size_t)d4_of(d) * c.n_pad);
+    hipLaunchKernelGGL(soa64_to_soa32, dim3(grid_for((int64_t)d4_of(d) * c.n_pad, 256)),
                        dim3(256), 0, c.stream, c.x64.as<double>(),
-                       (int64_t)d * c.n_pad, c.x32.as<float>());
+                       (int64_t)d4_of(d) * c.n_pad, c.x32.as<float>());
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(c.stream));
     c.x64.release();
@@ -267,8 +267,8 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
 
 void points_analyze_and_store(Ctx& c, const double* hX) {
   const int d = c.d;
-  c.x64.ensure(sizeof(double) * (size_t)d * c.n_pad);
-  HIP_CHECK(hipMemsetAsync(c.x64.p, 0, sizeof(double) * (size_t)d * c.n_pad, c.stream));
+  c.x64.ensure(sizeof(double) * (size_t)d4_of(d) * c.n_pad);
+  HIP_CHECK(hipMemsetAsync(c.x64.p, 0, sizeof(double) * (size_t)d4_of(d) * c.n_pad, c.stream));
   const int64_t chunk_rows = std::max<int64_t>(1, (int64_t)(32 << 20) / d);
   DevBuf stage;
   stage.ensure(sizeof(double) * (size_t)std::min<int64_t>(chunk_rows, std::max<int64_t>(c.n, 1)) * d);
@@ -293,8 +293,8 @@ void points_generate(Ctx& c, int64_t n_total, int64_t row_begin, int32_t n_blobs
   if (n_blobs < 1) CDR_FAIL(CDR_ERR_ARG, "generate: n_blobs must be >= 1");
   if (row_begin < 0 || row_begin + c.n > n_total)
     CDR_FAIL(CDR_ERR_ARG, "generate: rows out of range");
-  c.x32.ensure(sizeof(float) * (size_t)c.d * c.n_pad);
-  HIP_CHECK(hipMemsetAsync(c.x32.p, 0, sizeof(float) * (size_t)c.d * c.n_pad, c.stream));
+  c.x32.ensure(sizeof(float) * (size_t)d4_of(c.d) * c.n_pad);
+  HIP_CHECK(hipMemsetAsync(c.x32.p, 0, sizeof(float) * (size_t)d4_of(c.d) * c.n_pad, c.stream));
   hipLaunchKernelGGL(generate_kernel, dim3(grid_for(c.n, 256, 8192)), dim3(256), 0,
                      c.stream, c.x32.as<float>(), row_begin, c.n, c.n_pad, c.d,
                      n_blobs, seed);
@@ -315,7 +315,7 @@ __global__ void gather_rows_kernel(const float* __restrict__ x32,
     int64_t r = t / d;
     int f = (int)(t - r * d);
     int64_t i = idx[r];
-    out[t] = x32 ? (double)x32[(int64_t)f * n_pad + i] : x64[(int64_t)f * n_pad + i];
+    out[t] = x32 ? (double)x32[xidx(f, i, n_pad)] : x64[xidx(f, i, n_pad)];
   }
 }
 
@@ -356,6 +356,7 @@ int cdr_create(int device, cdr_ctx** out) {
     HIP_CHECK(e);
   }
   h->c.own_stream = true;
+  if (const char* ab = getenv("CDR_SCREEN_ABLATE")) h->c.screen_ablate = atoi(ab);
   *out = h;
   CDR_CATCH
 }

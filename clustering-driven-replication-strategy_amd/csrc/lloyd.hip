@@ -44,9 +44,12 @@ struct ScreenArgs {
   float thrA0, thrA1;
   int32_t* labels;
   unsigned long long* partials;
-  int32_t* fb_list;
-  int32_t* fb_count;
+  int32_t* fb_list;   // per-wave regions of fb_cap entries
+  int32_t* fb_count;  // [waves] entries per region, [waves] = total
+  int fb_cap;
   float* dbg;  // optional: screen values (n_pad x KT*16) for tests
+  int ablate;  // timing experiments only (CDR_SCREEN_ABLATE): 1 no update,
+               // 2 no argmin, 4 no MFMA, 8 no loads; results are garbage
 };
 
 // Running (best, runner-up) of unsigned keys: second = med3(best, v, second)
@@ -85,6 +88,9 @@ __global__ __launch_bounds__(256) void screen_kernel(ScreenArgs a) {
   const unsigned kmask = PACK6 ? 63u : 15u;
   const int wpb = blockDim.x >> 6;
   const int64_t ngroups = a.n_pad >> 6;
+  const int wave_id = blockIdx.x * wpb + (threadIdx.x >> 6);
+  int32_t* fb_region = a.fb_list + (size_t)wave_id * a.fb_cap;
+  int fb_used = 0;
   for (int64_t G = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); G < ngroups;
        G += (int64_t)gridDim.x * wpb) {
     const int64_t base = G << 6;
@@ -97,8 +103,16 @@ __global__ __launch_bounds__(256) void screen_kernel(ScreenArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int f = 16 * c + 4 * g + i;
-          xr[p][c][i] = fok[c][i] ? a.X[(int64_t)f * a.n_pad + base + 16 * p + col] : 0.0f;
+          xr[p][c][i] = fok[c][i] ? a.X[xidx(f, base + 16 * p + col, a.n_pad)] : 0.0f;
         }
+    if (a.ablate & 8) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int c = 0; c < DCH; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xr[p][c][i] = (float)((int)(base + p * 16 + col + i) & 255) * 0x1p-8f;
+    }
     h8 b1[4][DCH], b2[4][DCH];
     float xx[4];
 #pragma unroll
@@ -158,10 +172,21 @@ __global__ __launch_bounds__(256) void screen_kernel(ScreenArgs a) {
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (a.ablate & 4) {
+          acc[0] = (float)b1[p][0][0] + (float)A1[0][1];
+          acc[1] = (float)b2[p][0][1] + (float)A2[0][2];
+          acc[2] = (float)b1[p][0][2] + t;
+          acc[3] = xx[p];
+        } else {
 #pragma unroll
-        for (int c = 0; c < DCH; ++c) {
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[c], b1[p][c], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A2[c], b2[p][c], acc, 0, 0, 0);
+          for (int c = 0; c < DCH; ++c) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[c], b1[p][c], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A2[c], b2[p][c], acc, 0, 0, 0);
+          }
+        }
+        if (a.ablate & 2) {
+          bk[p] ^= __float_as_uint(acc[0] + acc[1] + acc[2] + acc[3]);
+          continue;
         }
         if constexpr (DBG) {
           const int64_t pt = base + 16 * p + col;
@@ -206,23 +231,24 @@ __global__ __launch_bounds__(256) void screen_kernel(ScreenArgs a) {
       const float vb = __uint_as_float(b & ~kmask);
       const float vs = __uint_as_float(s & ~kmask);
       const float lim = fmaf(vb, 1.0f + 0x1p-15f, fmaf(a.thrA1, xx[p], a.thrA0));
-      const bool cert = vs > lim;  // NaN-safe: a NaN runner-up never certifies
+      const bool cert = (a.ablate & 2) ? true : vs > lim;  // NaN: never certifies
       const int64_t pt = base + 16 * p + col;
       const bool real = pt < a.n;
       if (g == 0 && real) a.labels[pt] = label;
       const bool need = (g == 0) && real && !cert;
       const unsigned long long m = __ballot(need);
       if (m) {
-        const int leader = __builtin_ctzll(m);
-        int basei = 0;
-        if (lane == leader) basei = atomicAdd(a.fb_count, __popcll(m));
-        basei = __shfl(basei, leader);
         const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-        if (need) a.fb_list[basei + rank] = (int32_t)pt;
+        if (need) fb_region[fb_used + rank] = (int32_t)pt;
+        fb_used += __popcll(m);
+      }
+      if (a.ablate & 1) {
+        asm volatile("" ::"v"(xr[p][0][0]), "v"(xr[p][0][3]), "v"(label));
+        continue;
       }
       if (real && cert) {
-        unsigned long long* row = tbl + (size_t)label * kd1;
+        unsigned long long* row = tbl + (size_t)((unsigned)label < (unsigned)a.k ? label : 0) * kd1;
 #pragma unroll
         for (int c = 0; c < DCH; ++c)
 #pragma unroll
@@ -235,17 +261,309 @@ __global__ __launch_bounds__(256) void screen_kernel(ScreenArgs a) {
       }
     }
   }
+  if (lane == 0) {
+    a.fb_count[wave_id] = fb_used;
+    if (fb_used) atomicAdd(a.fb_count + (int64_t)gridDim.x * wpb, fb_used);
+  }
   __syncthreads();
   unsigned long long* dst = a.partials + (size_t)blockIdx.x * a.k * kd1;
   for (int i = threadIdx.x; i < a.k * kd1; i += blockDim.x) dst[i] = tbl[i];
 }
 
-__global__ void reduce_partials(const long long* __restrict__ part, int nwg, int len,
-                                long long* __restrict__ out) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
-    long long s = 0;
-    for (int w = 0; w < nwg; ++w) s += part[(size_t)w * len + i];
-    out[i] = s;
+
+// ---------------------------------------------------------------------------
+// screen_fast: the k*d <= 64*16 regime (KT*DCH <= 4), the BASELINE configs.
+// A fragments live in registers for the whole kernel; one wave processes 64
+// points per iteration as four 16-point tiles and prefetches the next group's
+// quads while it computes.  Per tile and lane: one 16-byte load per 16
+// features, packed fp32->fp16 hi/lo split, 2*KT*DCH MFMAs, 3 VALU ops per
+// screen value for the running (best, runner-up) keys, two permlane-swap
+// rounds for the cross-row reduction, one label store, and for certified
+// points 4 LDS u64 adds (+1 count).  Fragment k-slot order (must match
+// build_screen_plan):  B1 = [hi0..3, lo0..3]  B2 = [hi0..3, e0, e1, e2, 0]
+//                      A1 = [-2chi0..3, -2chi0..3]  A2 = [-2clo0..3, x0, x1, x2, 0]
+// ---------------------------------------------------------------------------
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned pack_h2(float a, float b) {
+  h2v h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+
+template <int DCH, int KT>
+struct FastTile {
+  f4 acc[KT];
+  float xx;
+};
+
+#ifndef CDR_FAST_WAVES
+#define CDR_FAST_WAVES 4  // waves per SIMD the register allocation must allow
+#endif
+template <int DCH, int KT, bool NONNEG, bool FULL, int ABL = 0>
+__global__ __launch_bounds__(256, CDR_FAST_WAVES) void screen_fast(ScreenArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned long long* tbl = reinterpret_cast<unsigned long long*>(smem);
+  const int d = a.d;
+  const int d4 = (d + 3) & ~3;
+  const int KS = d4 + 1;  // table row: d4 sums (padding features add 0) + count
+  for (int i = threadIdx.x; i < a.k * KS; i += blockDim.x) tbl[i] = 0ull;
+
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int col = lane & 15;
+  h8 A1[KT][DCH], A2[KT][DCH];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int c = 0; c < DCH; ++c) {
+      A1[t][c] = a.frag[((t * DCH + c) * 2 + 0) * 64 + lane];
+      A2[t][c] = a.frag[((t * DCH + c) * 2 + 1) * 64 + lane];
+    }
+  f4v ms[DCH];
+  bool qok[DCH];
+  const f4v* Xq = reinterpret_cast<const f4v*>(a.X);
+#pragma unroll
+  for (int c = 0; c < DCH; ++c) {
+    const int f0 = 16 * c + 4 * g;
+    qok[c] = FULL || f0 < d4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ms[c][i] = (f0 + i < d) ? a.mu_s[f0 + i] : 0.0f;
+  }
+  // chunk-0 spare k-slots, branch-free: lane group 0 takes the point-norm
+  // split (mask m0), lane group 1 the 1.0 multipliers of the centroid norms
+  const unsigned m0 = g == 0 ? 0xFFFFFFFFu : 0u;
+  const unsigned one01 = g == 1 ? pack_h2(1.0f, 1.0f) : 0u;
+  const unsigned one2 = g == 1 ? pack_h2(1.0f, 0.0f) : 0u;
+  const float sig = a.sig, fx = a.fx, thrA0 = a.thrA0, thrA1 = a.thrA1;
+  const int wpb = blockDim.x >> 6;
+  const int64_t ngroups = a.n_pad >> 6;
+  const int64_t gstride = (int64_t)gridDim.x * wpb;
+  int64_t G = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+  const int wave_id = (int)G;
+  int32_t* fb_region = a.fb_list + (size_t)wave_id * a.fb_cap;
+  int fb_used = 0;
+  constexpr int ablate = ABL;  // timing experiments only (separate instances)
+  __syncthreads();
+
+  auto load = [&](f4v (&buf)[4][DCH], int64_t grp) {
+    if constexpr ((ablate & 8) != 0) {  // synthetic points, no HBM reads
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int c = 0; c < DCH; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            buf[p][c][i] = (float)(((int)grp + 7 * p + 3 * i + col) & 255) * 0x1p-8f;
+      return;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int c = 0; c < DCH; ++c) {
+        if (FULL) {
+          buf[p][c] = Xq[(int64_t)(4 * c + g) * a.n_pad + (grp << 6) + 16 * p + col];
+        } else {
+          f4v v = {0.f, 0.f, 0.f, 0.f};
+          if (qok[c]) v = Xq[(int64_t)(4 * c + g) * a.n_pad + (grp << 6) + 16 * p + col];
+          buf[p][c] = v;
+        }
+      }
+  };
+
+  // B fragments + MFMAs of one 16-point tile
+  auto screen_tile = [&](const f4v (&xq)[DCH], FastTile<DCH, KT>& ts) {
+    h8 b1[DCH], b2[DCH];
+    float xxp = 0.0f;
+#pragma unroll
+    for (int c = 0; c < DCH; ++c) {
+      f4v xt;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xt[i] = fmaf(xq[c][i], sig, ms[c][i]);
+      const unsigned h01 = pack_h2(xt[0], xt[1]), h23 = pack_h2(xt[2], xt[3]);
+      const h2v hh01 = __builtin_bit_cast(h2v, h01), hh23 = __builtin_bit_cast(h2v, h23);
+      // residual x - hi straight from the packed halves (v_fma_mix_f32)
+      const unsigned l01 = pack_h2(fmaf((float)hh01[0], -1.0f, xt[0]),
+                                   fmaf((float)hh01[1], -1.0f, xt[1]));
+      const unsigned l23 = pack_h2(fmaf((float)hh23[0], -1.0f, xt[2]),
+                                   fmaf((float)hh23[1], -1.0f, xt[3]));
+      xxp = fmaf(xt[0], xt[0], xxp);
+      xxp = fmaf(xt[1], xt[1], xxp);
+      xxp = fmaf(xt[2], xt[2], xxp);
+      xxp = fmaf(xt[3], xt[3], xxp);
+      u4v w1 = {h01, h23, l01, l23};
+      u4v w2 = {h01, h23, 0u, 0u};
+      b1[c] = __builtin_bit_cast(h8, w1);
+      b2[c] = __builtin_bit_cast(h8, w2);
+    }
+    {
+      auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(xxp), __float_as_uint(xxp),
+                                                  false, false);
+      xxp = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
+      auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(xxp), __float_as_uint(xxp),
+                                                  false, false);
+      xxp = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
+    }
+    ts.xx = xxp;
+    {
+      const _Float16 e0 = (_Float16)xxp;
+      const float r1 = xxp - (float)e0;
+      const _Float16 e1 = (_Float16)r1;
+      const _Float16 e2 = (_Float16)(r1 - (float)e1);
+      h2v p01 = {e0, e1}, p2 = {e2, (_Float16)0.0f};
+      const unsigned x01 = __builtin_bit_cast(unsigned, p01), x2 = __builtin_bit_cast(unsigned, p2);
+      u4v w2 = __builtin_bit_cast(u4v, b2[0]);
+      w2[2] = (x01 & m0) | one01;
+      w2[3] = (x2 & m0) | one2;
+      b2[0] = __builtin_bit_cast(h8, w2);
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      ts.acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int c = 0; c < DCH; ++c) {
+        ts.acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[t][c], b1[c], ts.acc[t], 0, 0, 0);
+        ts.acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A2[t][c], b2[c], ts.acc[t], 0, 0, 0);
+      }
+    }
+  };
+
+  // certified argmin, label, fallback list, fused fixed-point update
+  auto finish_tile = [&](const FastTile<DCH, KT>& ts, const f4v (&xq)[DCH], int64_t pt) {
+    if constexpr ((ablate & 2) != 0) {  // no argmin / update
+      float z = ts.xx;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) z += ts.acc[t][0] + ts.acc[t][1] + ts.acc[t][2] + ts.acc[t][3];
+      asm volatile("" ::"v"(z));
+      return;
+    }
+    // one (best, runner-up) chain per centroid tile, merged pairwise: short
+    // dependency chains instead of one 16-deep min/med3 chain
+    unsigned cb[KT], cs[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      cb[t] = (__float_as_uint(ts.acc[t][0]) & ~63u) | (unsigned)(16 * t);
+      cs[t] = 0xFFFFFFFFu;
+#pragma unroll
+      for (int r = 1; r < 4; ++r)
+        push_key(cb[t], cs[t], (__float_as_uint(ts.acc[t][r]) & ~63u) | (unsigned)(16 * t + r));
+    }
+#pragma unroll
+    for (int w = 1; w < KT; w <<= 1)
+#pragma unroll
+      for (int t = 0; t + w < KT; t += 2 * w) {
+        const unsigned nb = min(cb[t], cb[t + w]);
+        cs[t] = min(max(cb[t], cb[t + w]), min(cs[t], cs[t + w]));
+        cb[t] = nb;
+      }
+    unsigned bk = cb[0], sk = cs[0];
+    bk |= (unsigned)g << 2;
+    sk |= (unsigned)g << 2;
+    {
+      auto b = __builtin_amdgcn_permlane16_swap(bk, bk, false, false);
+      auto q = __builtin_amdgcn_permlane16_swap(sk, sk, false, false);
+      sk = min(max(b[0], b[1]), min(q[0], q[1]));
+      bk = min(b[0], b[1]);
+      b = __builtin_amdgcn_permlane32_swap(bk, bk, false, false);
+      q = __builtin_amdgcn_permlane32_swap(sk, sk, false, false);
+      sk = min(max(b[0], b[1]), min(q[0], q[1]));
+      bk = min(b[0], b[1]);
+    }
+    const int label = (int)(bk & 63u);
+    const float vb = __uint_as_float(bk & ~63u);
+    const float vs = __uint_as_float(sk & ~63u);
+    const bool cert = vs > fmaf(vb, 1.0f + 0x1p-15f, fmaf(thrA1, ts.xx, thrA0));
+    a.labels[pt] = label;  // 4 identical stores per point; pt < n_pad
+    const bool real = pt < a.n;
+    const unsigned long long need = __ballot(g == 0 && real && !cert);
+    if (need) {  // private region: no returning atomic, no vmcnt(0) stall
+      const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+      if (g == 0 && real && !cert) fb_region[fb_used + rank] = (int32_t)pt;
+      fb_used += __popcll(need);
+    }
+    if constexpr ((ablate & 1) != 0) {  // no update
+      asm volatile("" ::"v"(xq[0][0]), "v"(xq[0][3]));
+      return;
+    }
+    if (cert && real) {
+      unsigned long long* row = tbl + (size_t)label * KS;
+#pragma unroll
+      for (int c = 0; c < DCH; ++c)
+        if (qok[c]) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int u = (int)(xq[c][i] * fx);
+            const unsigned long long v =
+                NONNEG ? (unsigned long long)(unsigned)u : (unsigned long long)(long long)u;
+            atomicAdd(&row[16 * c + 4 * g + i], v);
+          }
+        }
+      if (g == 0) atomicAdd(&row[d4], 1ull);
+    }
+  };
+
+  auto process = [&](const f4v (&buf)[4][DCH], int64_t grp) {
+    const int64_t base = grp << 6;
+    if (base >= a.n) return;  // wave-uniform: padding group
+    FastTile<DCH, KT> t0, t1;
+    screen_tile(buf[0], t0);
+    screen_tile(buf[1], t1);
+    finish_tile(t0, buf[0], base + col);
+    screen_tile(buf[2], t0);
+    finish_tile(t1, buf[1], base + 16 + col);
+    screen_tile(buf[3], t1);
+    finish_tile(t0, buf[2], base + 32 + col);
+    finish_tile(t1, buf[3], base + 48 + col);
+  };
+
+  f4v bufA[4][DCH], bufB[4][DCH];
+  if (G < ngroups) load(bufA, G);
+  while (G < ngroups) {
+    const int64_t G1 = G + gstride;
+    if (G1 < ngroups) load(bufB, G1);
+    process(bufA, G);
+    if (G1 >= ngroups) break;
+    const int64_t G2 = G1 + gstride;
+    if (G2 < ngroups) load(bufA, G2);
+    process(bufB, G1);
+    G = G2;
+  }
+  if (lane == 0) {
+    a.fb_count[wave_id] = fb_used;
+    if (fb_used) atomicAdd(a.fb_count + (int64_t)gstride, fb_used);
+  }
+  __syncthreads();
+  unsigned long long* dst = a.partials + (size_t)blockIdx.x * a.k * KS;
+  for (int i = threadIdx.x; i < a.k * KS; i += blockDim.x) dst[i] = tbl[i];
+}
+
+// Sum the per-workgroup tables: block (x, y) covers 64 entries and the y-th
+// slice of the workgroups; 4 waves split that slice, combine in LDS and add
+// into the (zeroed) output with one integer atomic per entry and slice.
+constexpr int kReduceSlices = 16;
+__global__ __launch_bounds__(256) void reduce_partials(const long long* __restrict__ part,
+                                                       int nwg, int len, int d, int KS,
+                                                       unsigned long long* __restrict__ out) {
+  __shared__ long long red[4][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);  // (j, f) of the (k, d+1) output
+  const int sub = threadIdx.x >> 6;
+  const int per = (nwg + kReduceSlices - 1) / kReduceSlices;
+  const int w0 = blockIdx.y * per, w1 = min(nwg, w0 + per);
+  const int j = e / (d + 1), f = e % (d + 1);
+  const int src = j * KS + (f < d ? f : KS - 1);
+  const int slen = (len / (d + 1)) * KS;
+  long long s = 0;
+  if (e < len)
+    for (int w = w0 + sub; w < w1; w += 4) s += part[(size_t)w * slen + src];
+  red[sub][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sub == 0 && e < len) {
+    const long long t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                        red[3][threadIdx.x];
+    if (t) atomicAdd(&out[e], (unsigned long long)t);
   }
 }
 
@@ -283,14 +601,57 @@ __global__ void fallback_exact_f32x(const float* __restrict__ X, int64_t n_pad, 
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < cnt;
        idx += gridDim.x * blockDim.x) {
     const int64_t pt = list[idx];
-    auto xv = [&](int f) { return (double)X[(int64_t)f * n_pad + pt]; };
+    auto xv = [&](int f) { return (double)X[xidx(f, pt, n_pad)]; };
     const int jb = exact_argmin(xv, C, k, d);
     labels[pt] = jb;
     for (int f = 0; f < d; ++f) {
-      const long long u = (long long)(int)(X[(int64_t)f * n_pad + pt] * fx);
+      const long long u = (long long)(int)(X[xidx(f, pt, n_pad)] * fx);
       atomicAdd(&out[(size_t)jb * kd1 + f], (unsigned long long)u);
     }
     atomicAdd(&out[(size_t)jb * kd1 + d], 1ull);
+  }
+}
+
+// Fallback for uncertified points: one wave per point, lane j computes the
+// exact NumPy-order distance to centroids j, j+64, ...; the point's
+// coordinates are wave-uniform (scalar loads).  argmin keeps the first index
+// of the smallest sqrt, as np.argmin(np.linalg.norm(...)) does.
+__global__ __launch_bounds__(256) void fallback_exact_wave(
+    const float* __restrict__ X, int64_t n_pad, int d, const double* __restrict__ C, int k,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ count, int nregions,
+    int cap, int32_t* __restrict__ labels, unsigned long long* __restrict__ out, float fx) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int kd1 = d + 1;
+  for (int reg = wave; reg < nregions; reg += nwaves)
+  for (int e = 0, cnt = count[reg]; e < cnt; ++e) {
+    const int64_t pt = __builtin_amdgcn_readfirstlane(list[(size_t)reg * cap + e]);
+    auto xv = [&](int f) { return (double)X[xidx(f, pt, n_pad)]; };
+    double rb = INFINITY;
+    int jb = k;
+    for (int j = lane; j < k; j += 64) {
+      const double* cj = C + (size_t)j * d;
+      const double r = sqrt(np_sqdist(xv, [&](int f) { return cj[f]; }, d));
+      if (r < rb || jb == k) {  // j increases per lane: strict < keeps the first
+        rb = r;
+        jb = j;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double orb = __shfl_xor(rb, o);
+      const int ojb = __shfl_xor(jb, o);
+      if (orb < rb || (orb == rb && ojb < jb)) {
+        rb = orb;
+        jb = ojb;
+      }
+    }
+    if (lane == 0) labels[pt] = jb;
+    for (int f = lane; f <= d; f += 64) {
+      const unsigned long long v =
+          f < d ? (unsigned long long)(long long)(int)(X[xidx(f, pt, n_pad)] * fx) : 1ull;
+      atomicAdd(&out[(size_t)jb * kd1 + f], v);
+    }
   }
 }
 
@@ -302,7 +663,7 @@ __global__ void assign_exact_all(const T* __restrict__ X, int64_t n, int64_t n_p
                                  int32_t* __restrict__ labels) {
   for (int64_t pt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pt < n;
        pt += (int64_t)gridDim.x * blockDim.x) {
-    auto xv = [&](int f) { return (double)X[(int64_t)f * n_pad + pt]; };
+    auto xv = [&](int f) { return (double)X[xidx(f, pt, n_pad)]; };
     labels[pt] = exact_argmin(xv, C, k, d);
   }
 }
@@ -322,7 +683,7 @@ __global__ __launch_bounds__(256) void update_from_labels_f32x(
     const int j = labels[pt];
     unsigned long long* row = tbl + (size_t)j * kd1;
     for (int f = 0; f < d; ++f)
-      atomicAdd(&row[f], (unsigned long long)(long long)(int)(X[(int64_t)f * n_pad + pt] * fx));
+      atomicAdd(&row[f], (unsigned long long)(long long)(int)(X[xidx(f, pt, n_pad)] * fx));
     atomicAdd(&row[d], 1ull);
   }
   __syncthreads();
@@ -346,11 +707,11 @@ __global__ void seq_sums_f64(const double* __restrict__ X, int64_t n, int64_t n_
     counts[j] = c;
     return;
   }
-  const double* col = X + (int64_t)f * n_pad;
+  auto col = [&](int64_t i) { return X[xidx(f, i, n_pad)]; };
   if (d >= 2) {
     double s = 0.0;
     for (int64_t i = 0; i < n; ++i)
-      if (labels[i] == j) s = s + col[i];
+      if (labels[i] == j) s = s + col(i);
     sums[(size_t)j * d + f] = s;
     return;
   }
@@ -359,7 +720,7 @@ __global__ void seq_sums_f64(const double* __restrict__ X, int64_t n, int64_t n_
   int64_t cursor = 0;
   auto next = [&](int64_t) -> double {
     while (labels[cursor] != j) ++cursor;
-    return col[cursor++];
+    return col(cursor++);
   };
   double res = 0.0;
   for (long long done = 0; done < m; done += kSeedBlock) {
@@ -390,14 +751,15 @@ static int num_cus(int device) {
 
 struct ScreenPlan {
   int DCH, KT;
-  bool pack6;
+  bool pack6, fast;
   float thrA0, thrA1;
   std::vector<h8> frag;
 };
 
 // Build the fp16 A-operand fragments and the certification constants
 // (derivation: DESIGN.md §3 "screen error bound").
-static void build_screen_plan(const Ctx& c, const double* C, int k, ScreenPlan& pl) {
+static void build_screen_plan(const Ctx& c, const double* C, int k, ScreenPlan& pl,
+                              bool allow_fast = true) {
   const int d = c.d;
   pl.DCH = (d + 15) / 16;
   pl.KT = (k + 15) / 16;
@@ -430,6 +792,7 @@ static void build_screen_plan(const Ctx& c, const double* C, int k, ScreenPlan& 
   pl.thrA0 *= 1.0001f;
   pl.thrA1 *= 1.0001f;
 
+  pl.fast = allow_fast && pl.KT * pl.DCH <= 4;
   pl.frag.assign((size_t)pl.KT * pl.DCH * 2 * 64, h8{});
   for (int t = 0; t < pl.KT; ++t)
     for (int cch = 0; cch < pl.DCH; ++cch)
@@ -437,20 +800,25 @@ static void build_screen_plan(const Ctx& c, const double* C, int k, ScreenPlan& 
         const int j = 16 * t + (lane & 15);
         const int g = lane >> 4;
         h8 A1 = {}, A2 = {};
+        // k-slot of (feature i, part): fast kernel [hi0..3 | lo0..3],
+        // generic kernel interleaved [hi0, lo0, hi1, lo1, ...]
+        auto slot_hi = [&](int i) { return pl.fast ? i : 2 * i; };
+        auto slot_lo = [&](int i) { return pl.fast ? 4 + i : 2 * i + 1; };
+        auto slot_ex = [&](int e) { return pl.fast ? 4 + e : 2 * e + 1; };
         for (int i = 0; i < 4; ++i) {
           const int f = 16 * cch + 4 * g + i;
           if (j < k && f < d) {
             const double v = ch[(size_t)j * d + f];
             const _Float16 hi = (_Float16)v;
             const _Float16 lo = (_Float16)(v - (double)hi);
-            A1[2 * i] = (_Float16)(-2.0 * (double)hi);
-            A1[2 * i + 1] = (_Float16)(-2.0 * (double)hi);
-            A2[2 * i] = (_Float16)(-2.0 * (double)lo);
+            A1[slot_hi(i)] = (_Float16)(-2.0 * (double)hi);
+            A1[slot_lo(i)] = (_Float16)(-2.0 * (double)hi);
+            A2[slot_hi(i)] = (_Float16)(-2.0 * (double)lo);
           }
         }
         if (cch == 0) {
           if (g == 0) {
-            A2[1] = A2[3] = A2[5] = (_Float16)1.0f;
+            A2[slot_ex(0)] = A2[slot_ex(1)] = A2[slot_ex(2)] = (_Float16)1.0f;
           } else if (g == 1) {
             if (j < k) {
               const double v = cc[j] + eps;
@@ -459,17 +827,65 @@ static void build_screen_plan(const Ctx& c, const double* C, int k, ScreenPlan& 
               const _Float16 p1 = (_Float16)r1;
               const double r2 = r1 - (double)p1;
               const _Float16 p2 = (_Float16)r2;
-              A2[1] = p0;
-              A2[3] = p1;
-              A2[5] = p2;
+              A2[slot_ex(0)] = p0;
+              A2[slot_ex(1)] = p1;
+              A2[slot_ex(2)] = p2;
             } else {
-              A2[1] = (_Float16)30000.0f;  // padding centroid: never the best
+              A2[slot_ex(0)] = (_Float16)30000.0f;  // padding centroid: never the best
             }
           }
         }
         pl.frag[(((size_t)t * pl.DCH + cch) * 2 + 0) * 64 + lane] = A1;
         pl.frag[(((size_t)t * pl.DCH + cch) * 2 + 1) * 64 + lane] = A2;
       }
+}
+
+template <int DCH, int KT>
+static void launch_fast(bool nonneg, bool full, dim3 grid, size_t lds, hipStream_t s,
+                        const ScreenArgs& a) {
+  if (nonneg) {
+    if (full) hipLaunchKernelGGL((screen_fast<DCH, KT, true, true>), grid, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((screen_fast<DCH, KT, true, false>), grid, dim3(256), lds, s, a);
+  } else {
+    if (full) hipLaunchKernelGGL((screen_fast<DCH, KT, false, true>), grid, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((screen_fast<DCH, KT, false, false>), grid, dim3(256), lds, s, a);
+  }
+}
+
+static int fast_blocks_per_cu(int DCH, int KT, size_t lds) {
+  int nb = 0;
+  hipError_t e = hipErrorInvalidValue;
+#define CDR_OCC(D, K)                                                                      \
+  if (DCH == D && KT == K)                                                                  \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen_fast<D, K, true, true>, 256, \
+                                                     lds);
+  CDR_OCC(1, 1) CDR_OCC(1, 2) CDR_OCC(1, 3) CDR_OCC(1, 4) CDR_OCC(2, 1) CDR_OCC(2, 2)
+  CDR_OCC(3, 1) CDR_OCC(4, 1)
+#undef CDR_OCC
+  if (e != hipSuccess || nb < 1) nb = 2;
+  return nb > 8 ? 8 : nb;
+}
+
+static void dispatch_fast(int DCH, int KT, bool nonneg, bool full, dim3 grid, size_t lds,
+                          hipStream_t s, const ScreenArgs& a) {
+  if (a.ablate && DCH == 1 && KT == 4 && nonneg && full) {  // timing experiments
+    switch (a.ablate) {
+      case 1: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 1>), grid, dim3(256), lds, s, a); return;
+      case 2: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 2>), grid, dim3(256), lds, s, a); return;
+      case 8: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 8>), grid, dim3(256), lds, s, a); return;
+      case 9: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 9>), grid, dim3(256), lds, s, a); return;
+      case 10: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 10>), grid, dim3(256), lds, s, a); return;
+      default: break;
+    }
+  }
+  if (DCH == 1 && KT == 1) launch_fast<1, 1>(nonneg, full, grid, lds, s, a);
+  else if (DCH == 1 && KT == 2) launch_fast<1, 2>(nonneg, full, grid, lds, s, a);
+  else if (DCH == 1 && KT == 3) launch_fast<1, 3>(nonneg, full, grid, lds, s, a);
+  else if (DCH == 1 && KT == 4) launch_fast<1, 4>(nonneg, full, grid, lds, s, a);
+  else if (DCH == 2 && KT == 1) launch_fast<2, 1>(nonneg, full, grid, lds, s, a);
+  else if (DCH == 2 && KT == 2) launch_fast<2, 2>(nonneg, full, grid, lds, s, a);
+  else if (DCH == 3 && KT == 1) launch_fast<3, 1>(nonneg, full, grid, lds, s, a);
+  else launch_fast<4, 1>(nonneg, full, grid, lds, s, a);
 }
 
 template <int DCH>
@@ -533,8 +949,8 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     c.out_sums.ensure(sizeof(long long) * len);
     dout = c.out_sums.as<long long>();
   }
-  c.fb_count.ensure(16);
-  HIP_CHECK(hipMemsetAsync(c.fb_count.p, 0, 16, c.stream));
+  // fallback regions: one per screen wave (sized below), zeroed every step
+  HIP_CHECK(hipMemsetAsync(dout, 0, sizeof(long long) * len, c.stream));
   c.fb_list.ensure(sizeof(int32_t) * (c.n > 0 ? c.n : 1));
   const float fx = (float)std::ldexp(1.0, c.scale_bits);
   const int cus = num_cus(c.device);
@@ -543,15 +959,29 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   const bool prof = c.prof_on;
   if (screen_supported(c, k)) {
     ScreenPlan pl;
-    build_screen_plan(c, C, k, pl);
+    build_screen_plan(c, C, k, pl, g_dbg_ptr == nullptr);
     c.frag.ensure(pl.frag.size() * sizeof(h8));
     HIP_CHECK(hipMemcpyAsync(c.frag.p, pl.frag.data(), pl.frag.size() * sizeof(h8),
                              hipMemcpyHostToDevice, c.stream));
-    const size_t lds = screen_lds_bytes(pl.KT, pl.DCH, k, d);
+    const int d4 = d4_of(d);
+    const int KS = pl.fast ? d4 + 1 : kd1;
+    const size_t lds = pl.fast ? (size_t)k * KS * 8 : screen_lds_bytes(pl.KT, pl.DCH, k, d);
     const int64_t groups = c.n_pad / 64;
-    int nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * 4);
+    int nwg;
+    if (pl.fast) {
+      const int bpc = fast_blocks_per_cu(pl.DCH, pl.KT, lds);
+      nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * bpc);
+    } else {
+      nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * 4);
+    }
     if (nwg < 1) nwg = 1;
-    c.partials.ensure(sizeof(long long) * (size_t)nwg * len);
+    c.partials.ensure(sizeof(long long) * (size_t)nwg * k * KS);
+    const int nwaves = nwg * 4;
+    const int cap = (int)(ceil_div(groups, nwaves) * 64);
+    c.fb_list.ensure(sizeof(int32_t) * (size_t)nwaves * cap);
+    c.fb_count.ensure(sizeof(int32_t) * (nwaves + 1));
+    HIP_CHECK(hipMemsetAsync(c.fb_count.p, 0, sizeof(int32_t) * (nwaves + 1), c.stream));
+    c.fb_regions = nwaves;
     ScreenArgs a;
     a.X = c.x32.as<float>();
     a.n = c.n;
@@ -569,23 +999,32 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     a.partials = c.partials.as<unsigned long long>();
     a.fb_list = c.fb_list.as<int32_t>();
     a.fb_count = c.fb_count.as<int32_t>();
+    a.fb_cap = cap;
     a.dbg = g_dbg_ptr;
+    a.ablate = c.screen_ablate;
     const bool dbg = g_dbg_ptr != nullptr;
     if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
-    switch (pl.DCH) {
-      case 1: launch_screen<1>(pl.pack6, dbg, dim3(nwg), lds, c.stream, a); break;
-      case 2: launch_screen<2>(pl.pack6, dbg, dim3(nwg), lds, c.stream, a); break;
-      case 3: launch_screen<3>(pl.pack6, dbg, dim3(nwg), lds, c.stream, a); break;
-      default: launch_screen<4>(pl.pack6, dbg, dim3(nwg), lds, c.stream, a); break;
+    if (pl.fast) {
+      bool nonneg = true;
+      for (int f = 0; f < d; ++f) nonneg = nonneg && c.fmin[f] >= 0.0;
+      dispatch_fast(pl.DCH, pl.KT, nonneg, d4 == 16 * pl.DCH, dim3(nwg), lds, c.stream, a);
+    } else {
+      switch (pl.DCH) {
+        case 1: launch_screen<1>(pl.pack6, dbg, dim3(nwg), lds, c.stream, a); break;
+        case 2: launch_screen<2>(pl.pack6, dbg, dim3(nwg), lds, c.stream, a); break;
+        case 3: launch_screen<3>(pl.pack6, dbg, dim3(nwg), lds, c.stream, a); break;
+        default: launch_screen<4>(pl.pack6, dbg, dim3(nwg), lds, c.stream, a); break;
+      }
     }
     HIP_CHECK(hipGetLastError());
     if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
-    hipLaunchKernelGGL(reduce_partials, dim3((len + 255) / 256), dim3(256), 0, c.stream,
-                       c.partials.as<long long>(), nwg, len, dout);
+    hipLaunchKernelGGL(reduce_partials, dim3((len + 63) / 64, kReduceSlices), dim3(256), 0,
+                       c.stream, c.partials.as<long long>(), nwg, len, d,
+                       KS, reinterpret_cast<unsigned long long*>(dout));
     HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(fallback_exact_f32x, dim3(cus * 4), dim3(256), 0, c.stream,
-                       c.x32.as<float>(), c.n_pad, d, c.cent64.as<double>(), k,
-                       c.fb_list.as<int32_t>(), c.fb_count.as<int32_t>(),
+    hipLaunchKernelGGL(fallback_exact_wave, dim3(std::max(1, nwaves / 4)), dim3(256), 0,
+                       c.stream, c.x32.as<float>(), c.n_pad, d, c.cent64.as<double>(), k,
+                       c.fb_list.as<int32_t>(), c.fb_count.as<int32_t>(), nwaves, cap,
                        c.labels.as<int32_t>(), reinterpret_cast<unsigned long long*>(dout), fx);
     HIP_CHECK(hipGetLastError());
   } else {
@@ -602,8 +1041,9 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
                        c.x32.as<float>(), c.n, c.n_pad, d, k, c.labels.as<int32_t>(), fx,
                        c.partials.as<unsigned long long>());
     HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(reduce_partials, dim3((len + 255) / 256), dim3(256), 0, c.stream,
-                       c.partials.as<long long>(), nwg, len, dout);
+    hipLaunchKernelGGL(reduce_partials, dim3((len + 63) / 64, kReduceSlices), dim3(256), 0,
+                       c.stream, c.partials.as<long long>(), nwg, len, d, kd1,
+                       reinterpret_cast<unsigned long long*>(dout));
     HIP_CHECK(hipGetLastError());
   }
   if (prof && screen_supported(c, k)) {
@@ -617,8 +1057,9 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     HIP_CHECK(hipMemcpyAsync(c.h_small.p, dout, sizeof(long long) * len,
                              hipMemcpyDeviceToHost, c.stream));
     int32_t fb = 0;
-    HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                             c.stream));
+    if (screen_supported(c, k))
+      HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.as<int32_t>() + c.fb_regions, sizeof(int32_t),
+                               hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
     memcpy(out, c.h_small.p, sizeof(long long) * len);
     c.last_fallback = screen_supported(c, k) ? fb : c.n;
@@ -718,12 +1159,20 @@ int cdr_lloyd_stats(cdr_ctx* h, int64_t* n_fallback) {
   if (c.last_fallback < 0) {
     HIP_CHECK(hipSetDevice(c.device));
     int32_t fb = 0;
-    HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                             c.stream));
+    if (screen_supported(c, c.last_k))
+      HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.as<int32_t>() + c.fb_regions, sizeof(int32_t),
+                               hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
     c.last_fallback = screen_supported(c, c.last_k) ? fb : c.n;
   }
   *n_fallback = c.last_fallback;
+  CDR_CATCH
+}
+
+int cdr_debug_screen_ablate(cdr_ctx* h, int32_t mask) {
+  CDR_TRY
+  if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
+  h->c.screen_ablate = mask;
   CDR_CATCH
 }
 

@@ -150,7 +150,7 @@ __global__ void scatter_by_label(const V* __restrict__ X, int64_t n, int64_t n_p
        i += (int64_t)gridDim.x * blockDim.x) {
     const int j = labels[i];
     const unsigned long long pos = atomicAdd(&cursor[j], 1ull);
-    for (int f = 0; f < d; ++f) dst[(int64_t)f * n + seg_off[j] + (int64_t)pos] = X[(int64_t)f * n_pad + i];
+    for (int f = 0; f < d; ++f) dst[(int64_t)f * n + seg_off[j] + (int64_t)pos] = X[xidx(f, i, n_pad)];
   }
 }
 

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
       const int64_t i = base + qi;
       double v = 0.0;
       if (qi < m) {
-        auto xv = [&](int f) { return (double)X[(int64_t)f * n_pad + i]; };
+        auto xv = [&](int f) { return (double)X[xidx(f, i, n_pad)]; };
         auto cv = [&](int f) { return cen[f]; };
         const double R = np_sqdist(xv, cv, d);
         const double r = sqrt(R);

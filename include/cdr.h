@@ -118,6 +118,9 @@ int cdr_lloyd_stats(cdr_ctx* ctx, int64_t* n_fallback);
  * out[4] = {screen kernel ms (sum), steps, whole step kernels ms (sum),
  * fallback points (sum)}.                                                    */
 int cdr_profile_reset(cdr_ctx* ctx, int32_t enable);
+/* Timing experiments only: skip parts of the screen kernel (1 update,
+ * 2 argmin, 4 MFMA, 8 loads).  Results are garbage while mask != 0.       */
+int cdr_debug_screen_ablate(cdr_ctx* ctx, int32_t mask);
 int cdr_profile_read(cdr_ctx* ctx, double* out);
 /* Test hook (not product path): screen values T (n_pad, ceil(k/16)*16) fp32
  * of one F32X step and the certification constants (A0, A1).               */
