@@ -273,15 +273,20 @@ __global__ __launch_bounds__(256) void screen_kernel(ScreenArgs a) {
 
 // ---------------------------------------------------------------------------
 // screen_fast: the k*d <= 64*16 regime (KT*DCH <= 4), the BASELINE configs.
-// A fragments live in registers for the whole kernel; one wave processes 64
-// points per iteration as four 16-point tiles and prefetches the next group's
-// quads while it computes.  Per tile and lane: one 16-byte load per 16
-// features, packed fp32->fp16 hi/lo split, 2*KT*DCH MFMAs, 3 VALU ops per
-// screen value for the running (best, runner-up) keys, two permlane-swap
-// rounds for the cross-row reduction, one label store, and for certified
-// points 4 LDS u64 adds (+1 count).  Fragment k-slot order (must match
-// build_screen_plan):  B1 = [hi0..3, lo0..3]  B2 = [hi0..3, e0, e1, e2, 0]
-//                      A1 = [-2chi0..3, -2chi0..3]  A2 = [-2clo0..3, x0, x1, x2, 0]
+// A fragments live in registers for the whole kernel; one wave processes a
+// 64-point group per iteration as four 16-point tiles and prefetches the
+// next group's quads while it computes.  Per tile and lane: one 16-byte load
+// per 16 features, packed fp32->fp16 hi/lo split, 2*KT*DCH MFMAs whose first
+// C operand is the point norm ||xhat||^2, 2.5 VALU ops per screen value for
+// the running (best, runner-up) keys.  Per group: the four tiles' (best,
+// runner-up) pairs are reduced across the lane groups by a 4x4 permlane
+// transpose, after which lane group g owns tile g's points — one coalesced
+// label store, one certification test, one fallback ballot — and the
+// per-point verdicts are broadcast back for the LDS u64 adds (4 per 16
+// features, +1 count) of the certified points.
+// Fragment k-slot order (must match build_screen_plan):
+//   B1 = [hi0..3, lo0..3]      B2 = [hi0..3, (g==1: 1, 1, 1, 0)]
+//   A1 = [-2chi0..3, -2chi0..3]  A2 = [-2clo0..3, (g==1: cc parts p0, p1, p2, 0)]
 // ---------------------------------------------------------------------------
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -293,17 +298,32 @@ __device__ __forceinline__ unsigned pack_h2(float a, float b) {
   return __builtin_bit_cast(unsigned, h);
 }
 
-template <int DCH, int KT>
-struct FastTile {
-  f4 acc[KT];
-  float xx;
-};
+__device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
+  return max(min(a, b), min(max(a, b), c));  // v_med3_u32
+}
 
-#ifndef CDR_FAST_WAVES
-#define CDR_FAST_WAVES 4  // waves per SIMD the register allocation must allow
-#endif
-template <int DCH, int KT, bool NONNEG, bool FULL, int ABL = 0>
-__global__ __launch_bounds__(256, CDR_FAST_WAVES) void screen_fast(ScreenArgs a) {
+// (best, runner-up) of two (best, runner-up) pairs
+__device__ __forceinline__ void merge_top2(unsigned& b, unsigned& s, unsigned b2, unsigned s2) {
+  const unsigned nb = min(b, b2);
+  s = min(max(b, b2), min(s, s2));
+  b = nb;
+}
+
+// Exchange halves between x and y: permlane32 pairs lane L < 32 with L + 32,
+// permlane16 pairs row 2r with row 2r + 1 (rows of 16 lanes).
+__device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
+  auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+__device__ __forceinline__ void swap16(unsigned& x, unsigned& y) {
+  auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+
+template <int DCH, int KT, bool NONNEG, bool FULL, int ABL = 0, int WAVES = 4>
+__global__ __launch_bounds__(256, WAVES) void screen_fast(ScreenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long* tbl = reinterpret_cast<unsigned long long*>(smem);
   const int d = a.d;
@@ -332,9 +352,8 @@ __global__ __launch_bounds__(256, CDR_FAST_WAVES) void screen_fast(ScreenArgs a)
 #pragma unroll
     for (int i = 0; i < 4; ++i) ms[c][i] = (f0 + i < d) ? a.mu_s[f0 + i] : 0.0f;
   }
-  // chunk-0 spare k-slots, branch-free: lane group 0 takes the point-norm
-  // split (mask m0), lane group 1 the 1.0 multipliers of the centroid norms
-  const unsigned m0 = g == 0 ? 0xFFFFFFFFu : 0u;
+  // chunk-0 spare k-slots: lane group 1 holds the 1.0 multipliers of the
+  // three fp16 parts of ||c_j||^2 + eps (constants, no per-tile work)
   const unsigned one01 = g == 1 ? pack_h2(1.0f, 1.0f) : 0u;
   const unsigned one2 = g == 1 ? pack_h2(1.0f, 0.0f) : 0u;
   const float sig = a.sig, fx = a.fx, thrA0 = a.thrA0, thrA1 = a.thrA1;
@@ -373,8 +392,9 @@ __global__ __launch_bounds__(256, CDR_FAST_WAVES) void screen_fast(ScreenArgs a)
       }
   };
 
-  // B fragments + MFMAs of one 16-point tile
-  auto screen_tile = [&](const f4v (&xq)[DCH], FastTile<DCH, KT>& ts) {
+  // B fragments + MFMAs of one 16-point tile; the point norm (summed over the
+  // four lane groups) enters as the first MFMA's C operand.  Returns it.
+  auto screen_tile = [&](const f4v (&xq)[DCH], f4 (&acc)[KT]) -> float {
     h8 b1[DCH], b2[DCH];
     float xxp = 0.0f;
 #pragma unroll
@@ -394,7 +414,7 @@ __global__ __launch_bounds__(256, CDR_FAST_WAVES) void screen_fast(ScreenArgs a)
       xxp = fmaf(xt[2], xt[2], xxp);
       xxp = fmaf(xt[3], xt[3], xxp);
       u4v w1 = {h01, h23, l01, l23};
-      u4v w2 = {h01, h23, 0u, 0u};
+      u4v w2 = {h01, h23, c == 0 ? one01 : 0u, c == 0 ? one2 : 0u};
       b1[c] = __builtin_bit_cast(h8, w1);
       b2[c] = __builtin_bit_cast(h8, w2);
     }
@@ -406,130 +426,138 @@ __global__ __launch_bounds__(256, CDR_FAST_WAVES) void screen_fast(ScreenArgs a)
                                                   false, false);
       xxp = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
     }
-    ts.xx = xxp;
-    {
-      const _Float16 e0 = (_Float16)xxp;
-      const float r1 = xxp - (float)e0;
-      const _Float16 e1 = (_Float16)r1;
-      const _Float16 e2 = (_Float16)(r1 - (float)e1);
-      h2v p01 = {e0, e1}, p2 = {e2, (_Float16)0.0f};
-      const unsigned x01 = __builtin_bit_cast(unsigned, p01), x2 = __builtin_bit_cast(unsigned, p2);
-      u4v w2 = __builtin_bit_cast(u4v, b2[0]);
-      w2[2] = (x01 & m0) | one01;
-      w2[3] = (x2 & m0) | one2;
-      b2[0] = __builtin_bit_cast(h8, w2);
-    }
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      ts.acc[t] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+      acc[t] = f4{xxp, xxp, xxp, xxp};
 #pragma unroll
       for (int c = 0; c < DCH; ++c) {
-        ts.acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[t][c], b1[c], ts.acc[t], 0, 0, 0);
-        ts.acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A2[t][c], b2[c], ts.acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[t][c], b1[c], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A2[t][c], b2[c], acc[t], 0, 0, 0);
       }
     }
+    return xxp;
   };
 
-  // certified argmin, label, fallback list, fused fixed-point update
-  auto finish_tile = [&](const FastTile<DCH, KT>& ts, const f4v (&xq)[DCH], int64_t pt) {
-    if constexpr ((ablate & 2) != 0) {  // no argmin / update
-      float z = ts.xx;
+  // (best, runner-up) keys of the lane's 4*KT screen values: value bits with
+  // the low 6 replaced by the row index 16t + r (the lane group's 4g is added
+  // once per group); values taken in pairs, b = min3, s = min(s, med3)
+  auto tile_top2 = [&](const f4 (&acc)[KT], unsigned& bk, unsigned& sk) {
+    auto key = [&](int t, int r) {
+      return (__float_as_uint(acc[t][r]) & ~63u) | (unsigned)(16 * t + r);
+    };
+    auto chain = [&](int t0, int t1, unsigned& b, unsigned& s) {
+      const unsigned k0 = key(t0, 0), k1 = key(t0, 1);
+      b = min(k0, k1);
+      s = max(k0, k1);
 #pragma unroll
-      for (int t = 0; t < KT; ++t) z += ts.acc[t][0] + ts.acc[t][1] + ts.acc[t][2] + ts.acc[t][3];
-      asm volatile("" ::"v"(z));
-      return;
-    }
-    // one (best, runner-up) chain per centroid tile, merged pairwise: short
-    // dependency chains instead of one 16-deep min/med3 chain
-    unsigned cb[KT], cs[KT];
-#pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      cb[t] = (__float_as_uint(ts.acc[t][0]) & ~63u) | (unsigned)(16 * t);
-      cs[t] = 0xFFFFFFFFu;
-#pragma unroll
-      for (int r = 1; r < 4; ++r)
-        push_key(cb[t], cs[t], (__float_as_uint(ts.acc[t][r]) & ~63u) | (unsigned)(16 * t + r));
-    }
-#pragma unroll
-    for (int w = 1; w < KT; w <<= 1)
-#pragma unroll
-      for (int t = 0; t + w < KT; t += 2 * w) {
-        const unsigned nb = min(cb[t], cb[t + w]);
-        cs[t] = min(max(cb[t], cb[t + w]), min(cs[t], cs[t + w]));
-        cb[t] = nb;
+      for (int q = 2; q < 4 * (t1 - t0); q += 2) {
+        const unsigned x = key(t0 + q / 4, q & 3), y = key(t0 + q / 4, (q & 3) + 1);
+        s = min(s, umed3(b, x, y));
+        b = min(min(b, x), y);
       }
-    unsigned bk = cb[0], sk = cs[0];
-    bk |= (unsigned)g << 2;
-    sk |= (unsigned)g << 2;
-    {
-      auto b = __builtin_amdgcn_permlane16_swap(bk, bk, false, false);
-      auto q = __builtin_amdgcn_permlane16_swap(sk, sk, false, false);
-      sk = min(max(b[0], b[1]), min(q[0], q[1]));
-      bk = min(b[0], b[1]);
-      b = __builtin_amdgcn_permlane32_swap(bk, bk, false, false);
-      q = __builtin_amdgcn_permlane32_swap(sk, sk, false, false);
-      sk = min(max(b[0], b[1]), min(q[0], q[1]));
-      bk = min(b[0], b[1]);
-    }
-    const int label = (int)(bk & 63u);
-    const float vb = __uint_as_float(bk & ~63u);
-    const float vs = __uint_as_float(sk & ~63u);
-    const bool cert = vs > fmaf(vb, 1.0f + 0x1p-15f, fmaf(thrA1, ts.xx, thrA0));
-    a.labels[pt] = label;  // 4 identical stores per point; pt < n_pad
-    const bool real = pt < a.n;
-    const unsigned long long need = __ballot(g == 0 && real && !cert);
-    if (need) {  // private region: no returning atomic, no vmcnt(0) stall
-      const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
-      if (g == 0 && real && !cert) fb_region[fb_used + rank] = (int32_t)pt;
-      fb_used += __popcll(need);
-    }
-    if constexpr ((ablate & 1) != 0) {  // no update
-      asm volatile("" ::"v"(xq[0][0]), "v"(xq[0][3]));
-      return;
-    }
-    if (cert && real) {
-      unsigned long long* row = tbl + (size_t)label * KS;
-#pragma unroll
-      for (int c = 0; c < DCH; ++c)
-        if (qok[c]) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int u = (int)(xq[c][i] * fx);
-            const unsigned long long v =
-                NONNEG ? (unsigned long long)(unsigned)u : (unsigned long long)(long long)u;
-            atomicAdd(&row[16 * c + 4 * g + i], v);
-          }
-        }
-      if (g == 0) atomicAdd(&row[d4], 1ull);
+    };
+    if constexpr (KT >= 2) {  // two independent chains, one merge
+      unsigned b2, s2;
+      chain(0, KT / 2, bk, sk);
+      chain(KT / 2, KT, b2, s2);
+      merge_top2(bk, sk, b2, s2);
+    } else {
+      chain(0, 1, bk, sk);
     }
   };
 
   auto process = [&](const f4v (&buf)[4][DCH], int64_t grp) {
     const int64_t base = grp << 6;
     if (base >= a.n) return;  // wave-uniform: padding group
-    FastTile<DCH, KT> t0, t1;
-    screen_tile(buf[0], t0);
-    screen_tile(buf[1], t1);
-    finish_tile(t0, buf[0], base + col);
-    screen_tile(buf[2], t0);
-    finish_tile(t1, buf[1], base + 16 + col);
-    screen_tile(buf[3], t1);
-    finish_tile(t0, buf[2], base + 32 + col);
-    finish_tile(t1, buf[3], base + 48 + col);
+    unsigned bk[4], sk[4];
+    float xx[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      f4 acc[KT];
+      xx[p] = screen_tile(buf[p], acc);
+      if constexpr ((ablate & 2) != 0) {  // no argmin / update
+        float z = xx[p];
+#pragma unroll
+        for (int t = 0; t < KT; ++t) z += acc[t][0] + acc[t][1] + acc[t][2] + acc[t][3];
+        asm volatile("" ::"v"(z));
+      } else {
+        tile_top2(acc, bk[p], sk[p]);
+        bk[p] |= (unsigned)g << 2;
+      }
+    }
+    if constexpr ((ablate & 2) != 0) return;
+    // 4x4 transpose-reduce across lane groups: afterwards lane group g holds
+    // the (best, runner-up) of tile g's point `col` (merges are symmetric,
+    // so the swap orientation does not matter here)
+    swap32(bk[0], bk[2]);
+    swap32(sk[0], sk[2]);
+    merge_top2(bk[0], sk[0], bk[2], sk[2]);
+    swap32(bk[1], bk[3]);
+    swap32(sk[1], sk[3]);
+    merge_top2(bk[1], sk[1], bk[3], sk[3]);
+    swap16(bk[0], bk[1]);
+    swap16(sk[0], sk[1]);
+    merge_top2(bk[0], sk[0], bk[1], sk[1]);
+    const float xxg = g == 0 ? xx[0] : g == 1 ? xx[1] : g == 2 ? xx[2] : xx[3];
+    const int64_t pt = base + 16 * g + col;  // < n_pad
+    const int label = (int)(bk[0] & 63u);
+    const float vb = __uint_as_float(bk[0] & ~63u);
+    const float vs = __uint_as_float(sk[0] & ~63u);
+    const bool cert = vs > fmaf(vb, 1.0f + 0x1p-15f, fmaf(thrA1, xxg, thrA0));
+    a.labels[pt] = label;  // one coalesced 256-byte store per group
+    const bool real = pt < a.n;
+    const unsigned long long need = __ballot(real && !cert);
+    if (need) {  // private region: no returning atomic, no vmcnt(0) stall
+      const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+      if (real && !cert) fb_region[fb_used + rank] = (int32_t)pt;
+      fb_used += __popcll(need);
+    }
+    if constexpr ((ablate & 1) != 0) return;  // no update
+    // broadcast each tile's verdict (label, or -1) to all four lane groups
+    unsigned v0 = (cert && real) ? (unsigned)label : 0xFFFFFFFFu;
+    unsigned v1 = v0;
+    swap16(v0, v1);  // rows (0,1): v0 = tile 0, v1 = tile 1; rows (2,3): tiles 2, 3
+    unsigned v2 = v0, v3 = v1;
+    swap32(v0, v2);  // v0 = tile 0, v2 = tile 2 in every lane
+    swap32(v1, v3);  // v1 = tile 1, v3 = tile 3
+    const unsigned vt[4] = {v0, v1, v2, v3};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int lp = (int)vt[p];
+      if (lp >= 0) {
+        unsigned long long* row = tbl + (size_t)lp * KS;
+#pragma unroll
+        for (int c = 0; c < DCH; ++c)
+          if (qok[c]) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int u = (int)(buf[p][c][i] * fx);
+              const unsigned long long v =
+                  NONNEG ? (unsigned long long)(unsigned)u : (unsigned long long)(long long)u;
+              atomicAdd(&row[16 * c + 4 * g + i], v);
+            }
+          }
+        if (g == 0) atomicAdd(&row[d4], 1ull);
+      }
+    }
   };
 
-  f4v bufA[4][DCH], bufB[4][DCH];
-  if (G < ngroups) load(bufA, G);
-  while (G < ngroups) {
-    const int64_t G1 = G + gstride;
-    if (G1 < ngroups) load(bufB, G1);
-    process(bufA, G);
-    if (G1 >= ngroups) break;
-    const int64_t G2 = G1 + gstride;
-    if (G2 < ngroups) load(bufA, G2);
-    process(bufB, G1);
-    G = G2;
+  // one group in flight ahead of the one being processed
+  f4v cur[4][DCH], nxt[4][DCH];
+  if (G < ngroups) load(cur, G);
+  // drain before the loop: otherwise the waitcnt pass merges this load into
+  // the loop header state and puts a vmcnt wait for the freshly issued
+  // prefetch in front of every tile (vmcnt(0), lgkmcnt/expcnt untouched)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  for (; G < ngroups; G += gstride) {
+    const int64_t Gn = G + gstride;
+    if (Gn < ngroups) load(nxt, Gn);
+    process(cur, G);
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int c = 0; c < DCH; ++c) cur[p][c] = nxt[p][c];
   }
   if (lane == 0) {
     a.fb_count[wave_id] = fb_used;
@@ -875,6 +903,8 @@ static void dispatch_fast(int DCH, int KT, bool nonneg, bool full, dim3 grid, si
       case 8: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 8>), grid, dim3(256), lds, s, a); return;
       case 9: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 9>), grid, dim3(256), lds, s, a); return;
       case 10: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 10>), grid, dim3(256), lds, s, a); return;
+      case 16: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 0, 2>), grid, dim3(256), lds, s, a); return;
+      case 18: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 0, 1>), grid, dim3(256), lds, s, a); return;
       default: break;
     }
   }
@@ -969,7 +999,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     const int64_t groups = c.n_pad / 64;
     int nwg;
     if (pl.fast) {
-      const int bpc = fast_blocks_per_cu(pl.DCH, pl.KT, lds);
+      int bpc = fast_blocks_per_cu(pl.DCH, pl.KT, lds);
       nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * bpc);
     } else {
       nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * 4);
