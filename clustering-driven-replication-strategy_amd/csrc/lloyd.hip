@@ -618,68 +618,121 @@ __device__ __forceinline__ int exact_argmin(XF xv, const double* __restrict__ C,
   return jb;
 }
 
-__global__ void fallback_exact_f32x(const float* __restrict__ X, int64_t n_pad, int d,
-                                    const double* __restrict__ C, int k,
-                                    const int32_t* __restrict__ list,
-                                    const int32_t* __restrict__ count,
-                                    int32_t* __restrict__ labels,
-                                    unsigned long long* __restrict__ out, float fx) {
-  const int cnt = *count;
-  const int kd1 = d + 1;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < cnt;
-       idx += gridDim.x * blockDim.x) {
-    const int64_t pt = list[idx];
-    auto xv = [&](int f) { return (double)X[xidx(f, pt, n_pad)]; };
-    const int jb = exact_argmin(xv, C, k, d);
-    labels[pt] = jb;
-    for (int f = 0; f < d; ++f) {
-      const long long u = (long long)(int)(X[xidx(f, pt, n_pad)] * fx);
-      atomicAdd(&out[(size_t)jb * kd1 + f], (unsigned long long)u);
-    }
-    atomicAdd(&out[(size_t)jb * kd1 + d], 1ull);
-  }
+// Wave-wide minimum, result in every lane: row_ror 8/4/2/1 inside each row of
+// 16 lanes (DPP), then the permlane16 / permlane32 swaps across rows.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const unsigned hi =
+      (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_min_f64(double v) {
+  v = fmin(v, dpp_f64<0x128>(v));
+  v = fmin(v, dpp_f64<0x124>(v));
+  v = fmin(v, dpp_f64<0x122>(v));
+  v = fmin(v, dpp_f64<0x121>(v));
+  auto mk = [](unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+  };
+  unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  auto l16 = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
+  auto h16 = __builtin_amdgcn_permlane16_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+  v = fmin(mk(l16[0], h16[0]), mk(l16[1], h16[1]));
+  u = (unsigned long long)__double_as_longlong(v);
+  auto l32 = __builtin_amdgcn_permlane32_swap((unsigned)u, (unsigned)u, false, false);
+  auto h32 = __builtin_amdgcn_permlane32_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+  return fmin(mk(l32[0], h32[0]), mk(l32[1], h32[1]));
+}
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+  v = min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false));
+  v = min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false));
+  v = min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xF, 0xF, false));
+  v = min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xF, 0xF, false));
+  auto r16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = min(r16[0], r16[1]);
+  auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return min(r32[0], r32[1]);
 }
 
-// Fallback for uncertified points: one wave per point, lane j computes the
-// exact NumPy-order distance to centroids j, j+64, ...; the point's
-// coordinates are wave-uniform (scalar loads).  argmin keeps the first index
-// of the smallest sqrt, as np.argmin(np.linalg.norm(...)) does.
+// Exact assignment of the points the screen did not certify: one wave per
+// point, lane j computes the NumPy-order fp64 distance to centroids j, j+64,
+// ... and its correctly rounded sqrt; first index on ties of the roots, as
+// np.argmin sees them (reference src/kmeans_plusplus.py:33-34).  Workgroup b's
+// waves take the screen's fallback regions 4b..4b+3, so the grid equals the
+// screen's; lane f holds feature f of the point (prefetched one point ahead)
+// and broadcasts it with readlane.  Sums go to an LDS table laid out like the
+// screen's (row stride KS, count at KS-1), which is then added into the
+// screen's partial row b — reduce_partials runs afterwards, so there are no
+// global atomics.  CLDS: centroids staged transposed ([d][k]) in LDS.
+// Requires d <= 64.
+template <bool CLDS>
 __global__ __launch_bounds__(256) void fallback_exact_wave(
     const float* __restrict__ X, int64_t n_pad, int d, const double* __restrict__ C, int k,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ count, int nregions,
-    int cap, int32_t* __restrict__ labels, unsigned long long* __restrict__ out, float fx) {
+    const int32_t* __restrict__ list, const int32_t* __restrict__ count, int cap, int KS,
+    int32_t* __restrict__ labels, unsigned long long* __restrict__ partials, float fx) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned long long* tbl = reinterpret_cast<unsigned long long*>(smem);
+  double* ct = reinterpret_cast<double*>(tbl + (size_t)k * KS);
+  const int tk = k * KS;
+  for (int i = threadIdx.x; i < tk; i += blockDim.x) tbl[i] = 0ull;
+  if (CLDS)
+    for (int i = threadIdx.x; i < k * d; i += blockDim.x) {
+      const int j = i / d, f = i - j * d;
+      ct[f * k + j] = C[i];
+    }
+  __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  const int kd1 = d + 1;
-  for (int reg = wave; reg < nregions; reg += nwaves)
-  for (int e = 0, cnt = count[reg]; e < cnt; ++e) {
-    const int64_t pt = __builtin_amdgcn_readfirstlane(list[(size_t)reg * cap + e]);
-    auto xv = [&](int f) { return (double)X[xidx(f, pt, n_pad)]; };
+  const int reg = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int cnt = count[reg];
+  const int32_t* lst = list + (size_t)reg * cap;
+  auto cval = [&](int f, int j) -> double { return CLDS ? ct[f * k + j] : C[(size_t)j * d + f]; };
+  int chunk = 0;  // list entries 64m .. 64m+63, one per lane
+  int64_t pt = 0;
+  float xf = 0.0f;
+  if (cnt > 0) {
+    chunk = lst[lane < cnt ? lane : 0];
+    pt = __builtin_amdgcn_readfirstlane(chunk);
+    if (lane < d) xf = X[xidx(lane, pt, n_pad)];
+  }
+  for (int e = 0; e < cnt; ++e) {
+    const int64_t cpt = pt;
+    const int cx = __float_as_int(xf);
+    if (e + 1 < cnt) {  // prefetch the next point
+      const int e1 = e + 1;
+      if ((e1 & 63) == 0) chunk = lst[e1 + lane < cnt ? e1 + lane : e1];
+      pt = __builtin_amdgcn_readlane(chunk, e1 & 63);
+      if (lane < d) xf = X[xidx(lane, pt, n_pad)];
+    }
+    auto xv = [&](int f) { return (double)__int_as_float(__builtin_amdgcn_readlane(cx, f)); };
     double rb = INFINITY;
     int jb = k;
     for (int j = lane; j < k; j += 64) {
-      const double* cj = C + (size_t)j * d;
-      const double r = sqrt(np_sqdist(xv, [&](int f) { return cj[f]; }, d));
-      if (r < rb || jb == k) {  // j increases per lane: strict < keeps the first
+      const double r = sqrt(np_sqdist(xv, [&](int f) { return cval(f, j); }, d));
+      if (r < rb) {  // j increases per lane: strict < keeps the first index
         rb = r;
         jb = j;
       }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      const double orb = __shfl_xor(rb, o);
-      const int ojb = __shfl_xor(jb, o);
-      if (orb < rb || (orb == rb && ojb < jb)) {
-        rb = orb;
-        jb = ojb;
-      }
+    const double m = wave_min_f64(rb);
+    int jmin;
+    if (k <= 64) {
+      jmin = (int)__builtin_ctzll(__ballot(rb == m));  // lane == j
+    } else {
+      jmin = (int)wave_min_u32(rb == m ? (unsigned)jb : 0xFFFFFFFFu);
     }
-    if (lane == 0) labels[pt] = jb;
-    for (int f = lane; f <= d; f += 64) {
-      const unsigned long long v =
-          f < d ? (unsigned long long)(long long)(int)(X[xidx(f, pt, n_pad)] * fx) : 1ull;
-      atomicAdd(&out[(size_t)jb * kd1 + f], v);
-    }
+    if (lane == 0) labels[cpt] = jmin;
+    if (lane < d)
+      atomicAdd(&tbl[(size_t)jmin * KS + lane],
+                (unsigned long long)(long long)(int)(__int_as_float(cx) * fx));
+    if (lane == 0) atomicAdd(&tbl[(size_t)jmin * KS + KS - 1], 1ull);  // d may be 64
+  }
+  __syncthreads();
+  unsigned long long* dst = partials + (size_t)blockIdx.x * tk;
+  for (int i = threadIdx.x; i < tk; i += blockDim.x) {
+    const unsigned long long v = tbl[i];
+    if (v) dst[i] += v;
   }
 }
 
@@ -1048,14 +1101,23 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     }
     HIP_CHECK(hipGetLastError());
     if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
+    // fallback first: it adds into the screen's partial rows
+    const size_t fb_lds = (size_t)k * KS * 8;
+    const size_t fb_lds_c = fb_lds + (size_t)k * d * 8;
+    if (fb_lds_c <= 64 * 1024)
+      hipLaunchKernelGGL(fallback_exact_wave<true>, dim3(nwg), dim3(256), fb_lds_c, c.stream,
+                         c.x32.as<float>(), c.n_pad, d, c.cent64.as<double>(), k,
+                         c.fb_list.as<int32_t>(), c.fb_count.as<int32_t>(), cap, KS,
+                         c.labels.as<int32_t>(), c.partials.as<unsigned long long>(), fx);
+    else
+      hipLaunchKernelGGL(fallback_exact_wave<false>, dim3(nwg), dim3(256), fb_lds, c.stream,
+                         c.x32.as<float>(), c.n_pad, d, c.cent64.as<double>(), k,
+                         c.fb_list.as<int32_t>(), c.fb_count.as<int32_t>(), cap, KS,
+                         c.labels.as<int32_t>(), c.partials.as<unsigned long long>(), fx);
+    HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(reduce_partials, dim3((len + 63) / 64, kReduceSlices), dim3(256), 0,
                        c.stream, c.partials.as<long long>(), nwg, len, d,
                        KS, reinterpret_cast<unsigned long long*>(dout));
-    HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(fallback_exact_wave, dim3(std::max(1, nwaves / 4)), dim3(256), 0,
-                       c.stream, c.x32.as<float>(), c.n_pad, d, c.cent64.as<double>(), k,
-                       c.fb_list.as<int32_t>(), c.fb_count.as<int32_t>(), nwaves, cap,
-                       c.labels.as<int32_t>(), reinterpret_cast<unsigned long long*>(dout), fx);
     HIP_CHECK(hipGetLastError());
   } else {
     // exact assignment for every point, then fixed-point sums from labels
