@@ -124,6 +124,13 @@ struct Ctx {
   int64_t prof_launches = 0;
   int32_t last_k = 0;
   bool have_labels = false;
+  bool last_screened = false;
+  // screen32 incremental update: exact int64 running sums/counts (k, d+1) that
+  // belong to the labels in `labels` (valid after a screen32 step with run_k)
+  DevBuf run_sums;
+  bool run_valid = false;
+  int32_t run_k = 0;
+  bool last_delta = false;
   int screen_ablate = 0;  // timing experiments only
 
   // ---- seeding ----

@@ -251,6 +251,7 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
     c.x64.release();
   }
   c.have_labels = false;
+  c.run_valid = false;
   c.seed_scanned = false;
 }
 
@@ -261,6 +262,7 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
   c.n = n;
   c.d = d;
   c.n_pad = ceil_div(n > 0 ? n : 1, kSeedBlock) * kSeedBlock;
+  c.run_valid = false;
   c.labels.ensure(sizeof(int32_t) * c.n_pad);
   HIP_CHECK(hipMemsetAsync(c.labels.p, 0, sizeof(int32_t) * c.n_pad, c.stream));
 }
@@ -373,7 +375,7 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.seed_scalar, &c.med_vals, &c.med_off, &c.med_out, &c.med_tmp,
                     &c.med_tmp2, &c.ev_file, &c.ev_op, &c.ev_client, &c.ev_ts,
                     &c.ev_primary, &c.ev_out, &c.ev_scratch, &c.ev_scratch2,
-                    &c.fin_counts, &c.fin_creation, &c.fin_out, &c.fin_red};
+                    &c.fin_counts, &c.fin_creation, &c.fin_out, &c.fin_red, &c.run_sums};
   for (DevBuf* b : bufs) b->release();
   c.h_small.release();
   for (hipEvent_t& e : c.pe)

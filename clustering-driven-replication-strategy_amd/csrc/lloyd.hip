@@ -821,7 +821,7 @@ __global__ void count_labels(const int32_t* __restrict__ labels, int64_t n, int 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-static int num_cus(int device) {
+int lloyd_num_cus(int device) {
   static int cached[64] = {0};
   if (device >= 0 && device < 64 && cached[device]) return cached[device];
   int v = 0;
@@ -1006,6 +1006,11 @@ static void check_k(const Ctx& c, int k) {
 }
 
 float* g_dbg_ptr = nullptr;  // set by cdr_debug_screen (tests only)
+float g_dbg_thr[2] = {0.f, 0.f};
+
+bool screen32_supported(const Ctx& c, int k);
+bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, float* dbg,
+                   float* thr_out);
 
 // Fold the last step's event pair into the profile accumulators.
 void prof_collect(Ctx& c) {
@@ -1036,11 +1041,17 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   HIP_CHECK(hipMemsetAsync(dout, 0, sizeof(long long) * len, c.stream));
   c.fb_list.ensure(sizeof(int32_t) * (c.n > 0 ? c.n : 1));
   const float fx = (float)std::ldexp(1.0, c.scale_bits);
-  const int cus = num_cus(c.device);
+  const int cus = lloyd_num_cus(c.device);
 
   prof_collect(c);
   const bool prof = c.prof_on;
-  if (screen_supported(c, k)) {
+  bool screened = false;
+  if (screen32_supported(c, k) &&
+      screen32_step(c, C, k, dout, prof, g_dbg_ptr, g_dbg_ptr ? g_dbg_thr : nullptr)) {
+    screened = true;
+  } else if (screen_supported(c, k)) {
+    c.run_valid = false;  // the screen_fast / screen_kernel path keeps no running sums
+    screened = true;
     ScreenPlan pl;
     build_screen_plan(c, C, k, pl, g_dbg_ptr == nullptr);
     c.frag.ensure(pl.frag.size() * sizeof(h8));
@@ -1120,6 +1131,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
                        KS, reinterpret_cast<unsigned long long*>(dout));
     HIP_CHECK(hipGetLastError());
   } else {
+    c.run_valid = false;
     // exact assignment for every point, then fixed-point sums from labels
     hipLaunchKernelGGL(assign_exact_all<float>, dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 8))),
                        dim3(256), 0, c.stream, c.x32.as<float>(), c.n, c.n_pad, d,
@@ -1138,7 +1150,8 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
                        reinterpret_cast<unsigned long long*>(dout));
     HIP_CHECK(hipGetLastError());
   }
-  if (prof && screen_supported(c, k)) {
+  c.last_screened = screened;
+  if (prof && screened) {
     HIP_CHECK(hipEventRecord(c.pe[2], c.stream));
     c.prof_pending = true;
   }
@@ -1149,12 +1162,12 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     HIP_CHECK(hipMemcpyAsync(c.h_small.p, dout, sizeof(long long) * len,
                              hipMemcpyDeviceToHost, c.stream));
     int32_t fb = 0;
-    if (screen_supported(c, k))
+    if (screened)
       HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.as<int32_t>() + c.fb_regions, sizeof(int32_t),
                                hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
     memcpy(out, c.h_small.p, sizeof(long long) * len);
-    c.last_fallback = screen_supported(c, k) ? fb : c.n;
+    c.last_fallback = screened ? fb : c.n;
     if (c.prof_pending) c.prof_fb_points += fb;
     prof_collect(c);
   } else {
@@ -1165,8 +1178,9 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
 void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* counts) {
   check_k(c, k);
   if (c.mode != CDR_MODE_F64) CDR_FAIL(CDR_ERR_STATE, "lloyd_step_f64: points are not F64");
+  c.run_valid = false;
   const int d = c.d;
-  const int cus = num_cus(c.device);
+  const int cus = lloyd_num_cus(c.device);
   upload_centroids(c, C, k);
   hipLaunchKernelGGL(assign_exact_all<double>,
                      dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 8))),
@@ -1251,11 +1265,11 @@ int cdr_lloyd_stats(cdr_ctx* h, int64_t* n_fallback) {
   if (c.last_fallback < 0) {
     HIP_CHECK(hipSetDevice(c.device));
     int32_t fb = 0;
-    if (screen_supported(c, c.last_k))
+    if (c.last_screened)
       HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.as<int32_t>() + c.fb_regions, sizeof(int32_t),
                                hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
-    c.last_fallback = screen_supported(c, c.last_k) ? fb : c.n;
+    c.last_fallback = c.last_screened ? fb : c.n;
   }
   *n_fallback = c.last_fallback;
   CDR_CATCH
@@ -1321,10 +1335,15 @@ int cdr_debug_screen(cdr_ctx* h, const double* C, int32_t k, float* out_vals,
   HIP_CHECK(hipMemcpy(out_vals, dbg.p, sizeof(float) * (size_t)c.n_pad * KT * 16,
                       hipMemcpyDeviceToHost));
   if (thr_a0a1) {
-    ScreenPlan pl;
-    build_screen_plan(c, C, k, pl);
-    thr_a0a1[0] = pl.thrA0;
-    thr_a0a1[1] = pl.thrA1;
+    if (screen32_supported(c, k)) {
+      thr_a0a1[0] = g_dbg_thr[0];
+      thr_a0a1[1] = g_dbg_thr[1];
+    } else {
+      ScreenPlan pl;
+      build_screen_plan(c, C, k, pl);
+      thr_a0a1[0] = pl.thrA0;
+      thr_a0a1[1] = pl.thrA1;
+    }
   }
   CDR_CATCH
 }

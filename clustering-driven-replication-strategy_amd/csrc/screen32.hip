@@ -1,0 +1,684 @@
+// screen32.hip — Lloyd assign + fused update for small d and k (d <= 16,
+// k <= 64: BASELINE configs 2 and 3), reference src/kmeans_plusplus.py:33-41.
+//
+// One wave handles a group of 64 points as two 32-point tiles.  Distances come
+// from v_mfma_f32_32x32x16_f16 in the ||x||^2 - 2 x.c + ||c||^2 form with the
+// point norm replaced by a launch constant D (argmin is unchanged by a per-point
+// shift; D keeps every screen value >= 0 so raw fp32 bits order as unsigned):
+//
+//   S_j = fl32( C_j + sum_f -2 chi_jf (hi_f + lo_f) - 2 clo_jf hi_f ),
+//   C_j = fl32(||chat_j||^2 + D)  (the MFMA C operand, a per-lane constant)
+//
+// with xhat = (x - mu) 2^sigma split into fp16 hi + lo and chat likewise
+// (chi + clo).  Per 32 centroids and 32 points that is three MFMAs for d = 16:
+//   A1 x H  (H = [hi(q0), hi(q1)],  A1 = [-2chi(q0), -2chi(q1)])
+//   A1 x L  (L = [lo(q0), lo(q1)])
+//   A3 x H  (A3 = [-2clo(q0), -2clo(q1)])
+// where lane half h owns the feature quads q0 = QH*h, q1 = QH*h + 1; for d <= 8
+// (QH = 1) H = [hi(q0), lo(q0)], A1 = [-2chi, -2chi], A3 = [-2clo, 0] and the
+// two MFMAs are A1 x H, A3 x H.  Every B operand is one 4-register tuple.
+//
+// Argmin: every lane keeps (best, runner-up) unsigned keys of its 32 values
+// (value bits with the low 6 replaced by the row index), the two lane halves
+// of a point are merged with one permlane32 swap per pair of tiles, after which
+// lane l owns point base + l: one coalesced label store, one certification
+// test, one fallback ballot.  A point is certified when
+//     key_s > key_b * (1 + 2^-17) + T0
+// (T0 = twice the rigorous screen error + the reference's rounding slack,
+// derived in build_plan32 / DESIGN.md §4); uncertified points go to a per-wave
+// fallback region and are re-done in exact fp64 NumPy order (fallback32).
+//
+// Update: certified points add their fp32 features (exact in fp64: grid data,
+// see screen32_supported) into a per-workgroup LDS table sum[f][j] with
+// ds_add_f64 and their count with ds_add_u32; reduce32 converts every
+// workgroup's sums to exact int64 fixed point and adds them.
+#include <cmath>
+#include <cstring>
+
+#include "cdr_internal.h"
+#include "exact_math.h"
+
+namespace cdr {
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16 __attribute__((ext_vector_type(16)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+struct S32Args {
+  const float* X;
+  int64_t n, n_pad;
+  int d, k, Q;         // Q = number of stored feature quads (d4 / 4)
+  const h8* frag;      // [MT][2][64]: A1, A3
+  const float* cinit;  // [MT][16][64]
+  const float* mu_s;   // [d] -mu_f 2^sigma
+  float sig;
+  float thr0, thr_rel;
+  int32_t* labels;
+  double* partials;  // per workgroup: sums [d4][KP] then counts [KP] (as double)
+  int KP;
+  int32_t* fb_list;
+  int32_t* fb_count;
+  int fb_cap;
+  float* dbg;  // tests only: screen values (n_pad x dbg_ld) when non-null
+  int dbg_ld;   // ceil(k / 16) * 16 (the cdr_debug_screen layout)
+};
+
+__device__ __forceinline__ unsigned pack_h2(float a, float b) {
+  h2 h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+
+// hi = fp16(x) pairs, lo = fp16(x - hi) pairs: 2 v_cvt_pk_f16_f32 + 4 v_fma_mix.
+// x - hi is exact in fp32; v_fma_mix reads hi as f16 (op_sel_hi) and rounds
+// x - hi once to f16 into the low / high half of the destination.
+__device__ __forceinline__ void split4(const f4& x, unsigned& h01, unsigned& h23,
+                                       unsigned& l01, unsigned& l23) {
+  h01 = pack_h2(x[0], x[1]);
+  h23 = pack_h2(x[2], x[3]);
+  unsigned a, b;
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %2, -1.0, %4 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, %3, -1.0, %6 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %2, -1.0, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, %3, -1.0, %7 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(a), "=&v"(b)
+      : "v"(h01), "v"(h23), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
+  l01 = a;
+  l23 = b;
+}
+
+__device__ __forceinline__ void merge_top2(unsigned& b, unsigned& s, unsigned b2, unsigned s2) {
+  const unsigned nb = min(b, b2);
+  s = min(max(b, b2), min(s, s2));
+  b = nb;
+}
+
+__device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
+  auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+
+}  // namespace
+
+// QH: feature quads per lane half (1: d <= 8, 2: d <= 16); MT: 32-centroid
+// tiles (1: k <= 32, 2: k <= 64).
+// FULLQ: all 2*QH quads of the lane halves exist in memory (d4 == 8 QH).
+// LDS table: sums [8 QH][KP] (rows of missing quads stay 0) + counts [KP].
+// DELTA: `labels` holds the previous step's labels and the per-workgroup
+// tables receive only the changes (+x into the new cluster, -x out of the old
+// one) of points whose label changed; otherwise every certified point is added.
+// ABL (timing experiments only, results are garbage): 1 no update, 2 no
+// argmin (values folded into one key), 8 no HBM loads (synthetic points).
+template <int QH, int MT, bool FULLQ, bool DELTA, bool DBG, int ABL = 0>
+__global__ __launch_bounds__(256) void screen32(S32Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int KP = 32 * MT;
+  constexpr int NF = 8 * QH;
+  double* tsum = reinterpret_cast<double*>(smem);                      // [NF][KP]
+  int* tcnt = reinterpret_cast<int*>(tsum + (size_t)NF * KP);          // [KP]
+  for (int i = threadIdx.x; i < NF * KP; i += blockDim.x) tsum[i] = 0.0;
+  for (int i = threadIdx.x; i < KP; i += blockDim.x) tcnt[i] = 0;
+
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int p = lane & 31;
+  h8 A[MT][2];  // [0] = A1 (-2chi), [1] = A3 (-2clo)
+  f16v Ci[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) A[m][u] = a.frag[(m * 2 + u) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Ci[m][i] = a.cinit[(m * 16 + i) * 64 + lane];
+  }
+  // this lane's quads and centering constants
+  int qd[QH];
+  bool qok[QH];
+  f4 ms[QH];
+#pragma unroll
+  for (int u = 0; u < QH; ++u) {
+    qd[u] = QH * h + u;
+    qok[u] = FULLQ || qd[u] < a.Q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = 4 * qd[u] + i;
+      ms[u][i] = f < a.d ? a.mu_s[f] : 0.0f;
+    }
+  }
+  const float sig = a.sig, thr0 = a.thr0, thr_rel = a.thr_rel;
+  const f4* Xq = reinterpret_cast<const f4*>(a.X);
+  const int wpb = blockDim.x >> 6;
+  const int64_t ngroups = a.n_pad >> 6;
+  const int64_t gstride = (int64_t)gridDim.x * wpb;
+  int64_t G = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+  const int wave_id = (int)G;
+  int32_t* fb_region = a.fb_list + (size_t)wave_id * a.fb_cap;
+  int fb_used = 0;
+  __syncthreads();
+
+  auto load = [&](f4 (&buf)[2][QH], int64_t grp) {
+    if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < QH; ++u)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            buf[t][u][i] = (float)((((int)grp * 7 + 13 * t + 5 * u + 3 * i + p) * 2654435761u) >> 8) *
+                           0x1p-24f;
+      return;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < QH; ++u) {
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (FULLQ || qok[u]) v = Xq[(int64_t)qd[u] * a.n_pad + (grp << 6) + 32 * t + p];
+        buf[t][u] = v;
+      }
+  };
+
+  // screen values of one 32-point tile -> (best, runner-up) keys of this lane
+  auto tile = [&](const f4 (&xq)[QH], unsigned& bk, unsigned& sk, int64_t tbase) {
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    u4v H, L;
+#pragma unroll
+    for (int u = 0; u < QH; ++u) {
+      f4 xt;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xt[i] = fmaf(xq[u][i], sig, ms[u][i]);
+      unsigned h01, h23, l01, l23;
+      split4(xt, h01, h23, l01, l23);
+      if (QH == 1) {
+        H = u4v{h01, h23, l01, l23};
+      } else {
+        H[2 * u] = h01;
+        H[2 * u + 1] = h23;
+        L[2 * u] = l01;
+        L[2 * u + 1] = l23;
+      }
+    }
+    const h8 BH = __builtin_bit_cast(h8, H);
+    f16v acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BH, Ci[m], 0, 0, 0);
+      if constexpr (QH == 2) {
+        const h8 BL = __builtin_bit_cast(h8, L);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BL, acc[m], 0, 0, 0);
+      }
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][1], BH, acc[m], 0, 0, 0);
+    }
+    if constexpr (DBG) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+        {
+          const int row = 32 * m + 8 * (i >> 2) + 4 * h + (i & 3);
+          if (row < a.dbg_ld) a.dbg[(tbase + p) * a.dbg_ld + row] = acc[m][i];
+        }
+    }
+    if constexpr ((ABL & 2) != 0) {
+      unsigned z = 0;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) z ^= __float_as_uint(acc[m][i]);
+      bk = (z & ~63u) | (unsigned)p;
+      sk = 0xFFFFFFFFu;
+      return;
+    }
+    // keys: reg i of tile m is row 32m + 8(i/4) + 4h + (i%4); 4h is OR-ed later
+    auto key = [&](int m, int i) {
+      return (__float_as_uint(acc[m][i]) & ~63u) | (unsigned)(32 * m + 8 * (i >> 2) + (i & 3));
+    };
+    unsigned b, s;
+    {
+      const unsigned k0 = key(0, 0), k1 = key(0, 1);
+      b = min(k0, k1);
+      s = max(k0, k1);
+    }
+#pragma unroll
+    for (int q = 2; q < 16 * MT; q += 2) {
+      const unsigned x = key(q >> 4, q & 15), y = key(q >> 4, (q & 15) + 1);
+      s = min(s, max(min(b, x), min(max(b, x), y)));  // med3(b, x, y)
+      b = min(min(b, x), y);
+    }
+    bk = b | ((unsigned)h << 2);
+    sk = s | ((unsigned)h << 2);
+  };
+
+  f4 cur[2][QH], nxt[2][QH];
+  int ocur = -1, onxt = -1;  // DELTA: previous label of point base + lane
+  if (G < ngroups) {
+    load(cur, G);
+    if (DELTA) ocur = a.labels[(G << 6) + lane];
+  }
+  // drain before the loop, otherwise the waitcnt pass merges these loads into
+  // the loop-header state and waits for the fresh prefetch in every iteration
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  for (; G < ngroups; G += gstride) {
+    const int64_t Gn = G + gstride;
+    if (Gn < ngroups) {
+      load(nxt, Gn);
+      if (DELTA) onxt = a.labels[(Gn << 6) + lane];
+    }
+    const int64_t base = G << 6;
+    if (base < a.n) {  // wave-uniform: padding groups have no real points
+      unsigned bA, sA, bB, sB;
+      tile(cur[0], bA, sA, base);
+      tile(cur[1], bB, sB, base + 32);
+      // lanes < 32: tile A's point l; lanes >= 32: tile B's point l - 32
+      swap32(bA, bB);
+      swap32(sA, sB);
+      merge_top2(bA, sA, bB, sB);
+      const int64_t pt = base + lane;
+      const int label = (int)(bA & 63u);
+      const float vb = __uint_as_float(bA & ~63u);
+      const float vs = __uint_as_float(sA & ~63u);
+      const bool cert = vs > fmaf(vb, thr_rel, thr0);  // NaN: never certified
+      const bool real = pt < a.n;
+      const bool ok = cert && real;
+      bool put = ok;
+      if (DELTA) put = ok && label != ocur;
+      if (put) a.labels[pt] = label;
+      const unsigned long long need = __ballot(real && !cert);
+      if (need) {
+        const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+        if (real && !cert) fb_region[fb_used + rank] = (int32_t)pt;
+        fb_used += __popcll(need);
+      }
+      if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int u = 0; u < QH; ++u) asm volatile("" ::"v"(cur[t][u]));
+        goto next_group;
+      }
+      {
+      // verdicts of tile A / tile B point p to both lane halves
+      unsigned vA = put ? (unsigned)label : 0xFFFFFFFFu;
+      unsigned vB = vA;
+      swap32(vA, vB);
+      unsigned oA = 0xFFFFFFFFu, oB = 0xFFFFFFFFu;
+      if (DELTA) {
+        oA = put ? (unsigned)ocur : 0xFFFFFFFFu;
+        oB = oA;
+        swap32(oA, oB);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int lp = (int)(t == 0 ? vA : vB);
+        if (lp >= 0) {
+          double* row = tsum + 4 * QH * h * KP + lp;  // feature 4 qd[0] of label lp
+#pragma unroll
+          for (int u = 0; u < QH; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) atomicAdd(&row[(4 * u + i) * KP], (double)cur[t][u][i]);
+          if (DELTA) {
+            const int lo = (int)(t == 0 ? oA : oB);
+            double* orow = tsum + 4 * QH * h * KP + lo;
+#pragma unroll
+            for (int u = 0; u < QH; ++u)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) atomicAdd(&orow[(4 * u + i) * KP], -(double)cur[t][u][i]);
+          }
+        }
+      }
+      const int lc = (int)(h == 0 ? vA : vB);
+      if (lc >= 0) {
+        atomicAdd(&tcnt[lc], 1);
+        if (DELTA) atomicAdd(&tcnt[(int)(h == 0 ? oA : oB)], -1);
+      }
+      }
+    }
+  next_group:
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < QH; ++u) cur[t][u] = nxt[t][u];
+    ocur = onxt;
+  }
+  if (lane == 0) {
+    a.fb_count[wave_id] = fb_used;
+    if (fb_used) atomicAdd(a.fb_count + gstride, fb_used);
+  }
+  __syncthreads();
+  double* dst = a.partials + (size_t)blockIdx.x * (NF + 1) * KP;
+  for (int i = threadIdx.x; i < NF * KP; i += blockDim.x) dst[i] = tsum[i];
+  for (int i = threadIdx.x; i < KP; i += blockDim.x) dst[NF * KP + i] = (double)tcnt[i];
+}
+
+// Exact assignment of the points the screen did not certify (one wave per
+// point, lane j computes centroid j's NumPy-order fp64 distance and its
+// correctly rounded sqrt; first index on ties of the roots, as np.argmin of
+// np.linalg.norm sees them, src/kmeans_plusplus.py:33-34).  Workgroup b's waves
+// take the screen's fallback regions 4b..4b+3 and add into partial table b.
+// Centroids are staged transposed ([d][k]) in LDS.  k <= 64, d <= 16.
+__global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, int64_t n_pad,
+                                                  int d, int Q, const double* __restrict__ C,
+                                                  int k, const int32_t* __restrict__ list,
+                                                  const int32_t* __restrict__ count, int cap,
+                                                  int KP, int32_t* __restrict__ labels,
+                                                  double* __restrict__ partials, int delta) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int d4 = Q;  // table rows (NF of the screen)
+  double* ct = reinterpret_cast<double*>(smem);  // [d][k]
+  double* tsum = ct + (size_t)d * k;             // [d4][KP]
+  int* tcnt = reinterpret_cast<int*>(tsum + (size_t)d4 * KP);
+  for (int i = threadIdx.x; i < k * d; i += blockDim.x) {
+    const int j = i / d, f = i - j * d;
+    ct[f * k + j] = C[i];
+  }
+  for (int i = threadIdx.x; i < d4 * KP; i += blockDim.x) tsum[i] = 0.0;
+  for (int i = threadIdx.x; i < KP; i += blockDim.x) tcnt[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int reg = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int cnt = count[reg];
+  const int32_t* lst = list + (size_t)reg * cap;
+  int any = 0;
+  for (int e = 0; e < cnt; ++e) {
+    const int64_t pt = lst[e];
+    float xf = lane < d ? X[xidx(lane, pt, n_pad)] : 0.0f;
+    const int cx = __float_as_int(xf);
+    auto xv = [&](int f) { return (double)__int_as_float(__builtin_amdgcn_readlane(cx, f)); };
+    double rb = INFINITY;
+    if (lane < k) rb = sqrt(np_sqdist(xv, [&](int f) { return ct[f * k + lane]; }, d));
+    // first lane holding the minimum (lanes >= k hold +inf; k >= 1)
+    double m = rb;
+    for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o));
+    const int jmin = (int)__builtin_ctzll(__ballot(rb == m));
+    const int old = delta ? labels[pt] : -1;  // not yet overwritten by the screen
+    if (jmin != old) {
+      if (lane == 0) labels[pt] = jmin;
+      if (lane < d) atomicAdd(&tsum[lane * KP + jmin], (double)xf);
+      if (lane == 0) atomicAdd(&tcnt[jmin], 1);
+      if (old >= 0) {
+        if (lane < d) atomicAdd(&tsum[lane * KP + old], -(double)xf);
+        if (lane == 0) atomicAdd(&tcnt[old], -1);
+      }
+      any = 1;
+    }
+  }
+  __syncthreads();
+  if (!__syncthreads_or(any)) return;
+  double* dst = partials + (size_t)blockIdx.x * (d4 + 1) * KP;
+  for (int i = threadIdx.x; i < d4 * KP; i += blockDim.x) {
+    const double v = tsum[i];
+    if (v != 0.0) dst[i] += v;
+  }
+  for (int i = threadIdx.x; i < KP; i += blockDim.x)
+    if (tcnt[i]) dst[d4 * KP + i] += (double)tcnt[i];
+}
+
+// out (k, d+1) int64 = sum over workgroups of the exact fixed-point values.
+// Block (x, y): 64 outputs, the y-th slice of the workgroups.
+constexpr int kR32Slices = 16;
+__global__ __launch_bounds__(256) void reduce32(const double* __restrict__ part, int nwg, int k,
+                                                int d, int d4, int KP, double fx,
+                                                unsigned long long* __restrict__ out) {
+  __shared__ long long red[4][64];
+  const int len = k * (d + 1);
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sub = threadIdx.x >> 6;
+  const int per = (nwg + kR32Slices - 1) / kR32Slices;
+  const int w0 = blockIdx.y * per, w1 = min(nwg, w0 + per);
+  long long s = 0;
+  if (e < len) {
+    const int j = e / (d + 1), f = e % (d + 1);
+    const int src = (f < d ? f : d4) * KP + j;
+    const size_t stride = (size_t)(d4 + 1) * KP;
+    for (int w = w0 + sub; w < w1; w += 4) {
+      const double v = part[(size_t)w * stride + src];
+      s += f < d ? __double2ll_rn(v * fx) : __double2ll_rn(v);
+    }
+  }
+  red[sub][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sub == 0 && e < len) {
+    const long long t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                        red[3][threadIdx.x];
+    if (t) atomicAdd(&out[e], (unsigned long long)t);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct Plan32 {
+  int QH, MT;
+  float thr0, thr_rel;
+  std::vector<h8> frag;      // [MT][3][64]
+  std::vector<float> cinit;  // [MT][16][64]
+};
+
+extern int lloyd_num_cus(int device);
+
+// Shapes and data this kernel covers: F32X points, d <= 16, k <= 64, and every
+// per-workgroup fp64 sum exact: |x| 2^S < 2^30 (F32X) and a workgroup sees at
+// most ceil(groups / nwg) * 64 points, so its sums stay below 2^53 grid units
+// when that count is < 2^23.  nwg >= #CUs (screen32_step).
+bool screen32_supported(const Ctx& c, int k) {
+  if (c.mode != CDR_MODE_F32X || c.d > 16 || k > 64 || k < 1) return false;
+  if (std::getenv("CDR_NO_SCREEN32")) return false;
+  const int64_t groups = c.n_pad / 64;
+  const int64_t per_wg = ceil_div(groups, lloyd_num_cus(c.device)) * 64;
+  return per_wg < (int64_t(1) << 23);
+}
+
+// Fragments, C operand and certification constants.
+static bool build_plan32(const Ctx& c, const double* C, int k, Plan32& pl) {
+  const int d = c.d;
+  const int Q = d4_of(d) / 4;
+  pl.QH = Q <= 2 ? 1 : 2;
+  pl.MT = k <= 32 ? 1 : 2;
+  const double sc = std::ldexp(1.0, c.sigma);
+  std::vector<double> ch((size_t)k * d), cc(k, 0.0);
+  double ccmax = 0.0, l1c = 0.0, cabs = 0.0;
+  for (int j = 0; j < k; ++j) {
+    double s = 0.0, l1 = 0.0;
+    for (int f = 0; f < d; ++f) {
+      const double v = (C[(size_t)j * d + f] - (double)c.mu[f]) * sc;
+      ch[(size_t)j * d + f] = v;
+      s += v * v;
+      l1 += std::fabs(v);
+      cabs = std::fmax(cabs, std::fabs(v));
+    }
+    cc[j] = s;
+    ccmax = std::fmax(ccmax, s);
+    l1c = std::fmax(l1c, l1);
+  }
+  if (!(cabs <= 1024.0)) return false;  // fp16 split range (and NaN) guard
+  // point side: |xhat_f| <= max(fmax - mu, mu - fmin) 2^sigma
+  double xxmax = 0.0, l1x = 0.0;
+  for (int f = 0; f < d; ++f) {
+    const double dev =
+        std::fmax(c.fmax[f] - (double)c.mu[f], (double)c.mu[f] - c.fmin[f]) * sc;
+    xxmax += dev * dev;
+    l1x += dev;
+  }
+  xxmax *= 1.0 + 1e-6;
+  const double u = std::ldexp(1.0, -24);
+  const int nmfma = pl.QH == 2 ? 3 : 2;
+  const double N = 16.0 * nmfma + 1.0;
+  // fp32 accumulation inside the MFMA chain, order unknown, each addition
+  // erring by at most 2u (no assumption on internal extra precision)
+  const double gamma = 2.0 * u * N / (1.0 - 2.0 * u * N);
+  // D >= max ||xhat||^2 + margin so that every screen value stays >= 0
+  const double E0 = gamma * (2.0 * ccmax + 2.0 * xxmax + 4.0) + 2.4 * std::ldexp(1.0, -22) *
+                    (ccmax + xxmax) + u * (ccmax + 2.0 * xxmax + 4.0) +
+                    std::ldexp(1.0, -24) * (l1c + l1x) + std::ldexp(1.0, -40);
+  const double D = xxmax + 4.0 * E0 + std::ldexp(1.0, -20);
+  const double sum_abs = (ccmax + D) * (1.0 + u) + (1.0 + std::ldexp(1.0, -9)) * (ccmax + xxmax);
+  const double E = gamma * sum_abs + 2.4 * std::ldexp(1.0, -22) * (ccmax + xxmax) +
+                   u * (ccmax + D) + std::ldexp(1.0, -24) * (l1c + l1x) +
+                   std::ldexp(1.0, -46) * (ccmax + D);
+  // reference slack: the fp64 distances and roots must not tie or flip
+  const double Wmax = (std::sqrt(ccmax) + std::sqrt(xxmax)) * (std::sqrt(ccmax) + std::sqrt(xxmax));
+  const double slack = std::ldexp(Wmax + 1.0, -38);
+  pl.thr0 = (float)((2.0 * E + slack) * 1.001);
+  pl.thr_rel = 1.0f + std::ldexp(1.0f, -16);  // the 64-ulp key truncation (2^-18 rel.)
+  const int MT = pl.MT;
+  pl.frag.assign((size_t)MT * 2 * 64, h8{});
+  pl.cinit.assign((size_t)MT * 16 * 64, 0.0f);
+  for (int m = 0; m < MT; ++m)
+    for (int lane = 0; lane < 64; ++lane) {
+      const int h = lane >> 5;
+      const int j = 32 * m + (lane & 31);  // A row
+      h8 A1 = {}, A3 = {};
+      for (int uq = 0; uq < pl.QH; ++uq) {
+        const int q = pl.QH * h + uq;
+        for (int i = 0; i < 4; ++i) {
+          const int f = 4 * q + i;
+          if (j >= k || f >= d) continue;
+          const double v = ch[(size_t)j * d + f];
+          const _Float16 hi = (_Float16)v;
+          const _Float16 lo = (_Float16)(v - (double)hi);
+          const _Float16 m2hi = (_Float16)(-2.0 * (double)hi);
+          const _Float16 m2lo = (_Float16)(-2.0 * (double)lo);
+          if (pl.QH == 1) {  // H = [hi(q0), lo(q0)]
+            A1[i] = m2hi;
+            A1[4 + i] = m2hi;
+            A3[i] = m2lo;
+          } else {  // H = [hi(q0), hi(q1)], L = [lo(q0), lo(q1)]
+            A1[4 * uq + i] = m2hi;
+            A3[4 * uq + i] = m2lo;
+          }
+        }
+      }
+      pl.frag[(m * 2 + 0) * 64 + lane] = A1;
+      pl.frag[(m * 2 + 1) * 64 + lane] = A3;
+      for (int i = 0; i < 16; ++i) {
+        const int row = 32 * m + 8 * (i >> 2) + 4 * h + (i & 3);
+        pl.cinit[(m * 16 + i) * 64 + lane] = row < k ? (float)(cc[row] + D) : 1.0e30f;
+      }
+    }
+  return true;
+}
+
+static int s32_blocks_per_cu(int QH, int MT, size_t lds) {
+  int nb = 0;
+  hipError_t e = hipErrorInvalidValue;
+  if (QH == 1 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 1, true, true, false>, 256, lds);
+  if (QH == 1 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 2, true, true, false>, 256, lds);
+  if (QH == 2 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 1, true, true, false>, 256, lds);
+  if (QH == 2 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 2, true, true, false>, 256, lds);
+  if (e != hipSuccess || nb < 1) nb = 2;
+  return nb > 8 ? 8 : nb;
+}
+
+// One F32X Lloyd step through screen32; returns false (nothing launched) when
+// the centroids are out of the fp16 split range.
+bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, float* dbg,
+                   float* thr_out) {
+  Plan32 pl;
+  if (!build_plan32(c, C, k, pl)) return false;
+  // incremental update when the device labels and running sums belong to the
+  // previous step of this point set and k
+  const bool delta = c.run_valid && c.run_k == k && !dbg && !std::getenv("CDR_NO_DELTA");
+  const int len = k * (c.d + 1);
+  c.run_sums.ensure(sizeof(long long) * len);
+  if (!delta) HIP_CHECK(hipMemsetAsync(c.run_sums.p, 0, sizeof(long long) * len, c.stream));
+  c.run_valid = false;
+  c.last_delta = delta;
+  if (thr_out) {
+    thr_out[0] = pl.thr0;
+    thr_out[1] = 0.0f;
+  }
+  const int d = c.d, Q = d4_of(d) / 4;
+  const int KP = 32 * pl.MT, NF = 8 * pl.QH;
+  c.frag.ensure(pl.frag.size() * sizeof(h8) + pl.cinit.size() * sizeof(float));
+  h8* dfrag = c.frag.as<h8>();
+  float* dcinit = reinterpret_cast<float*>(dfrag + pl.frag.size());
+  HIP_CHECK(hipMemcpyAsync(dfrag, pl.frag.data(), pl.frag.size() * sizeof(h8),
+                           hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(dcinit, pl.cinit.data(), pl.cinit.size() * sizeof(float),
+                           hipMemcpyHostToDevice, c.stream));
+  const size_t lds = (size_t)NF * KP * 8 + (size_t)KP * 4;
+  const int64_t groups = c.n_pad / 64;
+  const int cus = lloyd_num_cus(c.device);
+  const int bpc = s32_blocks_per_cu(pl.QH, pl.MT, lds);
+  int nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * bpc);
+  if (nwg < 1) nwg = 1;
+  const int nwaves = nwg * 4;
+  const int cap = (int)(ceil_div(groups, nwaves) * 64);
+  c.partials.ensure(sizeof(double) * (size_t)nwg * (NF + 1) * KP);
+  c.fb_list.ensure(sizeof(int32_t) * (size_t)nwaves * cap);
+  c.fb_count.ensure(sizeof(int32_t) * (nwaves + 1));
+  HIP_CHECK(hipMemsetAsync(c.fb_count.p, 0, sizeof(int32_t) * (nwaves + 1), c.stream));
+  c.fb_regions = nwaves;
+  S32Args a;
+  a.X = c.x32.as<float>();
+  a.n = c.n;
+  a.n_pad = c.n_pad;
+  a.d = d;
+  a.k = k;
+  a.Q = Q;
+  a.frag = dfrag;
+  a.cinit = dcinit;
+  a.mu_s = c.mu_s.as<float>();
+  a.sig = (float)std::ldexp(1.0, c.sigma);
+  a.thr0 = pl.thr0;
+  a.thr_rel = pl.thr_rel;
+  a.labels = c.labels.as<int32_t>();
+  a.partials = c.partials.as<double>();
+  a.KP = KP;
+  a.fb_list = c.fb_list.as<int32_t>();
+  a.fb_count = c.fb_count.as<int32_t>();
+  a.fb_cap = cap;
+  a.dbg = dbg;
+  a.dbg_ld = (k + 15) / 16 * 16;
+  if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
+  const dim3 grid(nwg), blk(256);
+  const bool fullq = Q == 2 * pl.QH;
+#define CDR_S32(QH_, MT_)                                                                       \
+  if (dbg) hipLaunchKernelGGL((screen32<QH_, MT_, false, false, true>), grid, blk, lds, c.stream, a); \
+  else if (fullq && delta) hipLaunchKernelGGL((screen32<QH_, MT_, true, true, false>), grid, blk, lds, c.stream, a); \
+  else if (fullq) hipLaunchKernelGGL((screen32<QH_, MT_, true, false, false>), grid, blk, lds, c.stream, a); \
+  else if (delta) hipLaunchKernelGGL((screen32<QH_, MT_, false, true, false>), grid, blk, lds, c.stream, a); \
+  else hipLaunchKernelGGL((screen32<QH_, MT_, false, false, false>), grid, blk, lds, c.stream, a);
+  const int abl = c.screen_ablate;
+  if (abl && pl.QH == 2 && pl.MT == 2 && fullq && delta) {  // timing experiments only
+    switch (abl) {
+      case 1: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 1>), grid, blk, lds, c.stream, a); break;
+      case 2: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 2>), grid, blk, lds, c.stream, a); break;
+      case 3: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 3>), grid, blk, lds, c.stream, a); break;
+      case 8: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 8>), grid, blk, lds, c.stream, a); break;
+      case 9: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 9>), grid, blk, lds, c.stream, a); break;
+      case 11: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 11>), grid, blk, lds, c.stream, a); break;
+      default: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 0>), grid, blk, lds, c.stream, a); break;
+    }
+  } else
+  if (pl.QH == 1 && pl.MT == 1) { CDR_S32(1, 1) }
+  else if (pl.QH == 1) { CDR_S32(1, 2) }
+  else if (pl.MT == 1) { CDR_S32(2, 1) }
+  else { CDR_S32(2, 2) }
+#undef CDR_S32
+  HIP_CHECK(hipGetLastError());
+  if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
+  const size_t fb_lds = (size_t)k * d * 8 + lds;
+  hipLaunchKernelGGL(fallback32, grid, blk, fb_lds, c.stream, c.x32.as<float>(), c.n_pad, d, NF,
+                     c.cent64.as<double>(), k, c.fb_list.as<int32_t>(),
+                     c.fb_count.as<int32_t>(), cap, KP, c.labels.as<int32_t>(),
+                     c.partials.as<double>(), delta ? 1 : 0);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(reduce32, dim3((len + 63) / 64, kR32Slices), dim3(256), 0, c.stream,
+                     c.partials.as<double>(), nwg, k, d, NF, KP, std::ldexp(1.0, c.scale_bits),
+                     c.run_sums.as<unsigned long long>());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpyAsync(dout, c.run_sums.p, sizeof(long long) * len, hipMemcpyDeviceToDevice,
+                           c.stream));
+  c.run_valid = dbg == nullptr;
+  c.run_k = k;
+  return true;
+}
+
+}  // namespace cdr

@@ -191,3 +191,38 @@ def test_full_size_properties_config2(ctx):
     idx = np.flatnonzero(lab == j)[:200000]
     assert idx.size > 0
     assert ctx.fallback_count() < n // 50
+
+
+@pytest.mark.parametrize("n,d,k", [(150000, 16, 64), (70000, 8, 16), (30000, 5, 40),
+                                   (20000, 12, 7)])
+def test_incremental_update_equals_full_recompute(ctx, n, d, k, monkeypatch):
+    """screen32 keeps exact int64 running sums and applies only the changes of
+    points that switched cluster; every step must equal a from-scratch step
+    (and the oracle), including steps where clusters empty out."""
+    X = synth.generate(n, 0, n, d, max(k, 2), 1000 + n + d)
+    ctx.load_points(X)
+    S = ctx.info()["scale_bits"]
+    rng = np.random.default_rng(d)
+    C = X[rng.choice(n, k, replace=False)].copy()
+    C[-1] = 7.0  # far away: an empty cluster from the first step on
+    for step in range(5):
+        out = ctx.lloyd_step(C)
+        lab = ctx.labels()
+        exp_lab, exp = ko.lloyd_partials(X, C, S)
+        np.testing.assert_array_equal(lab, exp_lab)
+        np.testing.assert_array_equal(out, exp)
+        # same step from scratch (full update) on a second context
+        monkeypatch.setenv("CDR_NO_DELTA", "1")
+        import _cdr
+        b = _cdr.Context(ctx.device)
+        try:
+            b.load_points(X)
+            np.testing.assert_array_equal(b.lloyd_step(C), out)
+        finally:
+            b.close()
+            monkeypatch.delenv("CDR_NO_DELTA")
+        cnt = out[:, d]
+        means = np.ldexp(out[:, :d].astype(np.float64), -S) / np.maximum(cnt, 1)[:, None]
+        C = np.where(cnt[:, None] > 0, means, C)
+        if step == 2:  # reseed the empty cluster onto a point, as the reference does
+            C[-1] = X[12345 % n]
