@@ -356,20 +356,33 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
   for (int i = threadIdx.x; i < KP; i += blockDim.x) dst[NF * KP + i] = (double)tcnt[i];
 }
 
-// Exact assignment of the points the screen did not certify (one wave per
-// point, lane j computes centroid j's NumPy-order fp64 distance and its
-// correctly rounded sqrt; first index on ties of the roots, as np.argmin of
-// np.linalg.norm sees them, src/kmeans_plusplus.py:33-34).  Workgroup b's waves
-// take the screen's fallback regions 4b..4b+3 and add into partial table b.
-// Centroids are staged transposed ([d][k]) in LDS.  k <= 64, d <= 16.
+// Exact assignment of the points the screen did not certify: one THREAD per
+// point (the 256 threads of workgroup b share the points of the screen's
+// fallback regions 4b..4b+3, so a crowded region is spread over the whole
+// workgroup).  Each thread walks the k centroids (staged transposed, [d][k],
+// in LDS: every lane reads the same word, a broadcast) computing the
+// NumPy-order fp64 squared distance and its correctly rounded sqrt, and keeps
+// the first minimum of the roots — np.argmin of np.linalg.norm
+// (src/kmeans_plusplus.py:33-34).  Changes go into partial table b.
+// k <= 64, d = D <= 16 (compile time: the point lives in registers).
+template <int D>
 __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, int64_t n_pad,
-                                                  int d, int Q, const double* __restrict__ C,
+                                                  int Q, const double* __restrict__ C,
                                                   int k, const int32_t* __restrict__ list,
                                                   const int32_t* __restrict__ count, int cap,
                                                   int KP, int32_t* __restrict__ labels,
                                                   double* __restrict__ partials, int delta) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int d4 = Q;  // table rows (NF of the screen)
+  const int reg0 = blockIdx.x * (blockDim.x >> 6);
+  int cnt[4], tot = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    cnt[r] = count[reg0 + r];
+    tot += cnt[r];
+  }
+  if (tot == 0) return;  // uniform: nothing to add to this workgroup's table
+  constexpr int d = D;
   double* ct = reinterpret_cast<double*>(smem);  // [d][k]
   double* tsum = ct + (size_t)d * k;             // [d4][KP]
   int* tcnt = reinterpret_cast<int*>(tsum + (size_t)d4 * KP);
@@ -380,36 +393,37 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
   for (int i = threadIdx.x; i < d4 * KP; i += blockDim.x) tsum[i] = 0.0;
   for (int i = threadIdx.x; i < KP; i += blockDim.x) tcnt[i] = 0;
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int reg = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int cnt = count[reg];
-  const int32_t* lst = list + (size_t)reg * cap;
-  int any = 0;
-  for (int e = 0; e < cnt; ++e) {
-    const int64_t pt = lst[e];
-    float xf = lane < d ? X[xidx(lane, pt, n_pad)] : 0.0f;
-    const int cx = __float_as_int(xf);
-    auto xv = [&](int f) { return (double)__int_as_float(__builtin_amdgcn_readlane(cx, f)); };
+  for (int e = threadIdx.x; e < tot; e += blockDim.x) {
+    int r = 0, i = e;
+    while (i >= cnt[r]) i -= cnt[r++];
+    const int64_t pt = list[(size_t)(reg0 + r) * cap + i];
+    double x[D];
+#pragma unroll
+    for (int f = 0; f < D; ++f) x[f] = (double)X[xidx(f, pt, n_pad)];
     double rb = INFINITY;
-    if (lane < k) rb = sqrt(np_sqdist(xv, [&](int f) { return ct[f * k + lane]; }, d));
-    // first lane holding the minimum (lanes >= k hold +inf; k >= 1)
-    double m = rb;
-    for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o));
-    const int jmin = (int)__builtin_ctzll(__ballot(rb == m));
+    int jmin = 0;
+    for (int j = 0; j < k; ++j) {
+      const double s = np_sqdist([&](int f) { return x[f]; }, [&](int f) { return ct[f * k + j]; }, d);
+      const double r2 = sqrt(s);
+      if (r2 < rb) {  // strict: first index on ties of the roots
+        rb = r2;
+        jmin = j;
+      }
+    }
     const int old = delta ? labels[pt] : -1;  // not yet overwritten by the screen
     if (jmin != old) {
-      if (lane == 0) labels[pt] = jmin;
-      if (lane < d) atomicAdd(&tsum[lane * KP + jmin], (double)xf);
-      if (lane == 0) atomicAdd(&tcnt[jmin], 1);
+      labels[pt] = jmin;
+#pragma unroll
+      for (int f = 0; f < D; ++f) atomicAdd(&tsum[f * KP + jmin], x[f]);
+      atomicAdd(&tcnt[jmin], 1);
       if (old >= 0) {
-        if (lane < d) atomicAdd(&tsum[lane * KP + old], -(double)xf);
-        if (lane == 0) atomicAdd(&tcnt[old], -1);
+#pragma unroll
+        for (int f = 0; f < D; ++f) atomicAdd(&tsum[f * KP + old], -x[f]);
+        atomicAdd(&tcnt[old], -1);
       }
-      any = 1;
     }
   }
   __syncthreads();
-  if (!__syncthreads_or(any)) return;
   double* dst = partials + (size_t)blockIdx.x * (d4 + 1) * KP;
   for (int i = threadIdx.x; i < d4 * KP; i += blockDim.x) {
     const double v = tsum[i];
@@ -665,10 +679,19 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   HIP_CHECK(hipGetLastError());
   if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
   const size_t fb_lds = (size_t)k * d * 8 + lds;
-  hipLaunchKernelGGL(fallback32, grid, blk, fb_lds, c.stream, c.x32.as<float>(), c.n_pad, d, NF,
-                     c.cent64.as<double>(), k, c.fb_list.as<int32_t>(),
-                     c.fb_count.as<int32_t>(), cap, KP, c.labels.as<int32_t>(),
-                     c.partials.as<double>(), delta ? 1 : 0);
+  {
+    typedef void (*FbFn)(const float*, int64_t, int, const double*, int, const int32_t*,
+                         const int32_t*, int, int, int32_t*, double*, int);
+    static const FbFn fb_fns[17] = {nullptr,        fallback32<1>,  fallback32<2>,  fallback32<3>,
+                                    fallback32<4>,  fallback32<5>,  fallback32<6>,  fallback32<7>,
+                                    fallback32<8>,  fallback32<9>,  fallback32<10>, fallback32<11>,
+                                    fallback32<12>, fallback32<13>, fallback32<14>, fallback32<15>,
+                                    fallback32<16>};
+    hipLaunchKernelGGL(fb_fns[d], grid, blk, fb_lds, c.stream, c.x32.as<float>(), c.n_pad, NF,
+                       c.cent64.as<double>(), k, c.fb_list.as<int32_t>(),
+                       c.fb_count.as<int32_t>(), cap, KP, c.labels.as<int32_t>(),
+                       c.partials.as<double>(), delta ? 1 : 0);
+  }
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(reduce32, dim3((len + 63) / 64, kR32Slices), dim3(256), 0, c.stream,
                      c.partials.as<double>(), nwg, k, d, NF, KP, std::ldexp(1.0, c.scale_bits),
