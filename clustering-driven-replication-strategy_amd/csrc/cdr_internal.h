@@ -102,6 +102,11 @@ struct Ctx {
   std::vector<float> mu;
   int32_t sigma = 0;
   DevBuf mu_s;  // float[d]: -mu_f * 2^sigma
+  // pre-centred copy for screen32: float [d4/4][n_pad][4] of (x - mu) 2^sigma,
+  // exact (pre_ok, decided with the mode); built on the first screen32 step
+  DevBuf xt32;
+  DevBuf muf;  // int64[d]: mu_f 2^S (reduce32 restores x sums from xt sums)
+  bool pre_ok = false, xt_valid = false;
 
   // ---- Lloyd ----
   DevBuf labels;    // int32[n_pad]

@@ -227,6 +227,10 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   double maxdev = 0.0;
   for (int f = 0; f < d; ++f) {
     c.mu[f] = (float)(0.5 * (c.fmin[f] + c.fmax[f]));
+    if (f32x) {  // on the data grid, so that x - mu is a whole number of grid steps
+      const float g = (float)std::ldexp(std::rint(std::ldexp((double)c.mu[f], S)), -S);
+      if (std::isfinite(g)) c.mu[f] = g;
+    }
     maxdev = std::fmax(maxdev, std::fmax(c.fmax[f] - (double)c.mu[f],
                                          (double)c.mu[f] - c.fmin[f]));
   }
@@ -238,6 +242,18 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   }
   std::vector<float> ms(d);
   for (int f = 0; f < d; ++f) ms[f] = (float)(-std::ldexp((double)c.mu[f], c.sigma));
+  // Pre-centred screen copy xt = (x - mu) 2^sigma (screen32.hip) is exact in
+  // fp32 when every |x - mu| is < 2^24 grid steps, mu is itself on the grid and
+  // the smallest step 2^(sigma - S) is a normal float.
+  c.pre_ok = c.mode == CDR_MODE_F32X && c.n > 0 && (c.sigma - S) >= -126;
+  for (int f = 0; f < d && c.pre_ok; ++f) {
+    const double mu = (double)c.mu[f];
+    if (std::ldexp(std::rint(std::ldexp(mu, S)), -S) != mu) c.pre_ok = false;
+    const double dev = std::fmax(c.fmax[f] - mu, mu - c.fmin[f]);
+    if (!(std::ldexp(dev, S) < 16777216.0)) c.pre_ok = false;
+    if ((double)ms[f] != -std::ldexp(mu, c.sigma)) c.pre_ok = false;
+  }
+  c.xt_valid = false;
   c.mu_s.ensure(sizeof(float) * (d > 0 ? d : 1));
   HIP_CHECK(hipMemcpyAsync(c.mu_s.p, ms.data(), sizeof(float) * d,
                            hipMemcpyHostToDevice, c.stream));
@@ -259,6 +275,9 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
   if (n < 0 || d <= 0) CDR_FAIL(CDR_ERR_ARG, "points: need n >= 0 and d >= 1");
   c.x32.release();
   c.x64.release();
+  c.xt32.release();
+  c.xt_valid = false;
+  c.pre_ok = false;
   c.n = n;
   c.d = d;
   c.n_pad = ceil_div(n > 0 ? n : 1, kSeedBlock) * kSeedBlock;
@@ -369,7 +388,7 @@ int cdr_destroy(cdr_ctx* h) {
   Ctx& c = h->c;
   (void)hipSetDevice(c.device);
   (void)hipStreamSynchronize(c.stream);
-  DevBuf* bufs[] = {&c.x32, &c.x64, &c.mu_s, &c.labels, &c.cent64, &c.frag,
+  DevBuf* bufs[] = {&c.x32, &c.x64, &c.xt32, &c.muf, &c.mu_s, &c.labels, &c.cent64, &c.frag,
                     &c.partials, &c.out_sums, &c.fb_list, &c.fb_count, &c.f64_sums,
                     &c.f64_counts, &c.dmin, &c.blocksums, &c.xfer, &c.cend,
                     &c.seed_scalar, &c.med_vals, &c.med_off, &c.med_out, &c.med_tmp,

@@ -72,13 +72,14 @@ __device__ __forceinline__ unsigned pack_h2(float a, float b) {
   return __builtin_bit_cast(unsigned, h);
 }
 
-// hi = fp16(x) pairs, lo = fp16(x - hi) pairs: 2 v_cvt_pk_f16_f32 + 4 v_fma_mix.
+// hi = fp16(x) pairs (round to nearest even), lo = fp16(x - hi) pairs:
+// 2 v_cvt_pk_f16_f32 + 4 v_fma_mix.
 // x - hi is exact in fp32; v_fma_mix reads hi as f16 (op_sel_hi) and rounds
 // x - hi once to f16 into the low / high half of the destination.
 __device__ __forceinline__ void split4(const f4& x, unsigned& h01, unsigned& h23,
                                        unsigned& l01, unsigned& l23) {
-  h01 = pack_h2(x[0], x[1]);
-  h23 = pack_h2(x[2], x[3]);
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h01) : "v"(x[0]), "v"(x[1]));
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h23) : "v"(x[2]), "v"(x[3]));
   unsigned a, b;
   asm volatile(
       "v_fma_mixlo_f16 %0, %2, -1.0, %4 op_sel_hi:[1,0,0]\n\t"
@@ -114,7 +115,9 @@ __device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
 // one) of points whose label changed; otherwise every certified point is added.
 // ABL (timing experiments only, results are garbage): 1 no update, 2 no
 // argmin (values folded into one key), 8 no HBM loads (synthetic points).
-template <int QH, int MT, bool FULLQ, bool DELTA, bool DBG, int ABL = 0>
+// PRE: a.X is the pre-centred copy xt = (x - mu) 2^sigma (exact, Ctx::pre_ok):
+// the screen uses it as loaded and the tables sum xt (reduce32 restores x).
+template <int QH, int MT, bool FULLQ, bool DELTA, bool DBG, bool PRE, int ABL = 0>
 __global__ __launch_bounds__(256) void screen32(S32Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int KP = 32 * MT;
@@ -190,8 +193,12 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
 #pragma unroll
     for (int u = 0; u < QH; ++u) {
       f4 xt;
+      if constexpr (PRE) {
+        xt = xq[u];
+      } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) xt[i] = fmaf(xq[u][i], sig, ms[u][i]);
+        for (int i = 0; i < 4; ++i) xt[i] = fmaf(xq[u][i], sig, ms[u][i]);
+      }
       unsigned h01, h23, l01, l23;
       split4(xt, h01, h23, l01, l23);
       if (QH == 1) {
@@ -247,8 +254,10 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
 #pragma unroll
     for (int q = 2; q < 16 * MT; q += 2) {
       const unsigned x = key(q >> 4, q & 15), y = key(q >> 4, (q & 15) + 1);
-      s = min(s, max(min(b, x), min(max(b, x), y)));  // med3(b, x, y)
-      b = min(min(b, x), y);
+      unsigned t;  // second smallest of {b, x, y}; then b = min of the three
+      asm("v_med3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(b), "v"(x), "v"(y));
+      asm("v_min3_u32 %0, %1, %2, %3" : "=v"(b) : "v"(b), "v"(x), "v"(y));
+      s = min(s, t);
     }
     bk = b | ((unsigned)h << 2);
     sk = s | ((unsigned)h << 2);
@@ -371,7 +380,8 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
                                                   int k, const int32_t* __restrict__ list,
                                                   const int32_t* __restrict__ count, int cap,
                                                   int KP, int32_t* __restrict__ labels,
-                                                  double* __restrict__ partials, int delta) {
+                                                  double* __restrict__ partials, int delta,
+                                                  const float* __restrict__ pre_ms, float sig) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int d4 = Q;  // table rows (NF of the screen)
   const int reg0 = blockIdx.x * (blockDim.x >> 6);
@@ -413,6 +423,10 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
     const int old = delta ? labels[pt] : -1;  // not yet overwritten by the screen
     if (jmin != old) {
       labels[pt] = jmin;
+      if (pre_ms) {  // the screen's tables hold xt = (x - mu) 2^sigma (exact)
+#pragma unroll
+        for (int f = 0; f < D; ++f) x[f] = (double)fmaf((float)x[f], sig, pre_ms[f]);
+      }
 #pragma unroll
       for (int f = 0; f < D; ++f) atomicAdd(&tsum[f * KP + jmin], x[f]);
       atomicAdd(&tcnt[jmin], 1);
@@ -436,8 +450,11 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
 // out (k, d+1) int64 = sum over workgroups of the exact fixed-point values.
 // Block (x, y): 64 outputs, the y-th slice of the workgroups.
 constexpr int kR32Slices = 16;
+// With the pre-centred copy (muf != null) the table sums are of xt = (x - mu)
+// 2^sigma: sum x 2^S = sum xt 2^(S - sigma) + count mu 2^S, both exact.
 __global__ __launch_bounds__(256) void reduce32(const double* __restrict__ part, int nwg, int k,
                                                 int d, int d4, int KP, double fx,
+                                                const long long* __restrict__ muf,
                                                 unsigned long long* __restrict__ out) {
   __shared__ long long red[4][64];
   const int len = k * (d + 1);
@@ -450,9 +467,11 @@ __global__ __launch_bounds__(256) void reduce32(const double* __restrict__ part,
     const int j = e / (d + 1), f = e % (d + 1);
     const int src = (f < d ? f : d4) * KP + j;
     const size_t stride = (size_t)(d4 + 1) * KP;
+    const long long mf = (muf && f < d) ? muf[f] : 0;
     for (int w = w0 + sub; w < w1; w += 4) {
       const double v = part[(size_t)w * stride + src];
       s += f < d ? __double2ll_rn(v * fx) : __double2ll_rn(v);
+      if (mf) s += __double2ll_rn(part[(size_t)w * stride + (size_t)d4 * KP + j]) * mf;
     }
   }
   red[sub][threadIdx.x & 63] = s;
@@ -461,6 +480,22 @@ __global__ __launch_bounds__(256) void reduce32(const double* __restrict__ part,
     const long long t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
                         red[3][threadIdx.x];
     if (t) atomicAdd(&out[e], (unsigned long long)t);
+  }
+}
+
+// xt = (x - mu) 2^sigma = fma(x, 2^sigma, -mu 2^sigma), exact (Ctx::pre_ok).
+// Padding rows and feature slots >= d stay 0.
+__global__ void precenter_kernel(const float* __restrict__ x, int64_t n, int64_t n_pad, int d,
+                                 const float* __restrict__ ms, float sig, float* __restrict__ xt) {
+  const int d4 = d4_of(d);
+  const int64_t total = (int64_t)d4 * n_pad;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = t / (4 * n_pad);  // SoA [d4/4][n_pad][4]
+    const int64_t r = t - q * 4 * n_pad;
+    const int64_t i = r >> 2;
+    const int f = (int)(4 * q + (r & 3));
+    xt[t] = (f < d && i < n) ? fmaf(x[t], sig, ms[f]) : 0.0f;
   }
 }
 
@@ -581,10 +616,10 @@ static bool build_plan32(const Ctx& c, const double* C, int k, Plan32& pl) {
 static int s32_blocks_per_cu(int QH, int MT, size_t lds) {
   int nb = 0;
   hipError_t e = hipErrorInvalidValue;
-  if (QH == 1 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 1, true, true, false>, 256, lds);
-  if (QH == 1 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 2, true, true, false>, 256, lds);
-  if (QH == 2 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 1, true, true, false>, 256, lds);
-  if (QH == 2 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 2, true, true, false>, 256, lds);
+  if (QH == 1 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 1, true, true, false, true>, 256, lds);
+  if (QH == 1 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 2, true, true, false, true>, 256, lds);
+  if (QH == 2 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 1, true, true, false, true>, 256, lds);
+  if (QH == 2 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 2, true, true, false, true>, 256, lds);
   if (e != hipSuccess || nb < 1) nb = 2;
   return nb > 8 ? 8 : nb;
 }
@@ -629,8 +664,24 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   c.fb_count.ensure(sizeof(int32_t) * (nwaves + 1));
   HIP_CHECK(hipMemsetAsync(c.fb_count.p, 0, sizeof(int32_t) * (nwaves + 1), c.stream));
   c.fb_regions = nwaves;
+  // pre-centred screen copy (exact; built once per point set)
+  const bool pre = c.pre_ok && !std::getenv("CDR_NO_PRE");
+  if (pre && !c.xt_valid) {
+    c.xt32.ensure(sizeof(float) * (size_t)d4_of(d) * c.n_pad);
+    hipLaunchKernelGGL(precenter_kernel, dim3(4096), dim3(256), 0, c.stream, c.x32.as<float>(),
+                       c.n, c.n_pad, d, c.mu_s.as<float>(), (float)std::ldexp(1.0, c.sigma),
+                       c.xt32.as<float>());
+    HIP_CHECK(hipGetLastError());
+    std::vector<long long> muf(d);
+    for (int f = 0; f < d; ++f) muf[f] = std::llrint(std::ldexp((double)c.mu[f], c.scale_bits));
+    c.muf.ensure(sizeof(long long) * d);
+    HIP_CHECK(hipMemcpyAsync(c.muf.p, muf.data(), sizeof(long long) * d, hipMemcpyHostToDevice,
+                             c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));  // muf is a stack vector
+    c.xt_valid = true;
+  }
   S32Args a;
-  a.X = c.x32.as<float>();
+  a.X = pre ? c.xt32.as<float>() : c.x32.as<float>();
   a.n = c.n;
   a.n_pad = c.n_pad;
   a.d = d;
@@ -653,35 +704,38 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
   const dim3 grid(nwg), blk(256);
   const bool fullq = Q == 2 * pl.QH;
-#define CDR_S32(QH_, MT_)                                                                       \
-  if (dbg) hipLaunchKernelGGL((screen32<QH_, MT_, false, false, true>), grid, blk, lds, c.stream, a); \
-  else if (fullq && delta) hipLaunchKernelGGL((screen32<QH_, MT_, true, true, false>), grid, blk, lds, c.stream, a); \
-  else if (fullq) hipLaunchKernelGGL((screen32<QH_, MT_, true, false, false>), grid, blk, lds, c.stream, a); \
-  else if (delta) hipLaunchKernelGGL((screen32<QH_, MT_, false, true, false>), grid, blk, lds, c.stream, a); \
-  else hipLaunchKernelGGL((screen32<QH_, MT_, false, false, false>), grid, blk, lds, c.stream, a);
+#define CDR_S32P(QH_, MT_, P_)                                                                  \
+  if (dbg) hipLaunchKernelGGL((screen32<QH_, MT_, false, false, true, P_>), grid, blk, lds, c.stream, a); \
+  else if (fullq && delta) hipLaunchKernelGGL((screen32<QH_, MT_, true, true, false, P_>), grid, blk, lds, c.stream, a); \
+  else if (fullq) hipLaunchKernelGGL((screen32<QH_, MT_, true, false, false, P_>), grid, blk, lds, c.stream, a); \
+  else if (delta) hipLaunchKernelGGL((screen32<QH_, MT_, false, true, false, P_>), grid, blk, lds, c.stream, a); \
+  else hipLaunchKernelGGL((screen32<QH_, MT_, false, false, false, P_>), grid, blk, lds, c.stream, a);
+#define CDR_S32(QH_, MT_) \
+  if (pre) { CDR_S32P(QH_, MT_, true) } else { CDR_S32P(QH_, MT_, false) }
   const int abl = c.screen_ablate;
-  if (abl && pl.QH == 2 && pl.MT == 2 && fullq && delta) {  // timing experiments only
+  if (abl && pl.QH == 2 && pl.MT == 2 && fullq && delta && pre) {  // timing experiments only
     switch (abl) {
-      case 1: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 1>), grid, blk, lds, c.stream, a); break;
-      case 2: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 2>), grid, blk, lds, c.stream, a); break;
-      case 3: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 3>), grid, blk, lds, c.stream, a); break;
-      case 8: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 8>), grid, blk, lds, c.stream, a); break;
-      case 9: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 9>), grid, blk, lds, c.stream, a); break;
-      case 11: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 11>), grid, blk, lds, c.stream, a); break;
-      default: hipLaunchKernelGGL((screen32<2, 2, true, true, false, 0>), grid, blk, lds, c.stream, a); break;
+      case 1: hipLaunchKernelGGL((screen32<2, 2, true, true, false, true, 1>), grid, blk, lds, c.stream, a); break;
+      case 2: hipLaunchKernelGGL((screen32<2, 2, true, true, false, true, 2>), grid, blk, lds, c.stream, a); break;
+      case 3: hipLaunchKernelGGL((screen32<2, 2, true, true, false, true, 3>), grid, blk, lds, c.stream, a); break;
+      case 8: hipLaunchKernelGGL((screen32<2, 2, true, true, false, true, 8>), grid, blk, lds, c.stream, a); break;
+      case 9: hipLaunchKernelGGL((screen32<2, 2, true, true, false, true, 9>), grid, blk, lds, c.stream, a); break;
+      case 11: hipLaunchKernelGGL((screen32<2, 2, true, true, false, true, 11>), grid, blk, lds, c.stream, a); break;
+      default: hipLaunchKernelGGL((screen32<2, 2, true, true, false, true, 0>), grid, blk, lds, c.stream, a); break;
     }
   } else
   if (pl.QH == 1 && pl.MT == 1) { CDR_S32(1, 1) }
   else if (pl.QH == 1) { CDR_S32(1, 2) }
   else if (pl.MT == 1) { CDR_S32(2, 1) }
   else { CDR_S32(2, 2) }
+#undef CDR_S32P
 #undef CDR_S32
   HIP_CHECK(hipGetLastError());
   if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
   const size_t fb_lds = (size_t)k * d * 8 + lds;
   {
     typedef void (*FbFn)(const float*, int64_t, int, const double*, int, const int32_t*,
-                         const int32_t*, int, int, int32_t*, double*, int);
+                         const int32_t*, int, int, int32_t*, double*, int, const float*, float);
     static const FbFn fb_fns[17] = {nullptr,        fallback32<1>,  fallback32<2>,  fallback32<3>,
                                     fallback32<4>,  fallback32<5>,  fallback32<6>,  fallback32<7>,
                                     fallback32<8>,  fallback32<9>,  fallback32<10>, fallback32<11>,
@@ -690,12 +744,14 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
     hipLaunchKernelGGL(fb_fns[d], grid, blk, fb_lds, c.stream, c.x32.as<float>(), c.n_pad, NF,
                        c.cent64.as<double>(), k, c.fb_list.as<int32_t>(),
                        c.fb_count.as<int32_t>(), cap, KP, c.labels.as<int32_t>(),
-                       c.partials.as<double>(), delta ? 1 : 0);
+                       c.partials.as<double>(), delta ? 1 : 0,
+                       pre ? c.mu_s.as<float>() : nullptr, (float)std::ldexp(1.0, c.sigma));
   }
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(reduce32, dim3((len + 63) / 64, kR32Slices), dim3(256), 0, c.stream,
-                     c.partials.as<double>(), nwg, k, d, NF, KP, std::ldexp(1.0, c.scale_bits),
-                     c.run_sums.as<unsigned long long>());
+                     c.partials.as<double>(), nwg, k, d, NF, KP,
+                     std::ldexp(1.0, c.scale_bits - (pre ? c.sigma : 0)),
+                     pre ? c.muf.as<long long>() : nullptr, c.run_sums.as<unsigned long long>());
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipMemcpyAsync(dout, c.run_sums.p, sizeof(long long) * len, hipMemcpyDeviceToDevice,
                            c.stream));
