@@ -163,12 +163,10 @@ class ShardedLloyd:
         acc = self.partials(C)
         counts = acc[:, d]
         sums = np.ldexp(acc[:, :d].astype(np.float64), -self.S)
-        new = np.empty_like(C)
-        for j in range(k):
-            if counts[j] > 0:
-                new[j] = sums[j] / np.float64(counts[j])
-            else:
-                new[j] = reseed_row(np.random.randint(0, self.n_total))
+        with np.errstate(invalid="ignore", divide="ignore"):
+            new = sums / counts[:, None].astype(np.float64)
+        for j in np.flatnonzero(counts == 0):  # j order, as the reference draws
+            new[j] = reseed_row(np.random.randint(0, self.n_total))
         shift = np.linalg.norm(new - C)
         return new, shift
 

@@ -120,6 +120,9 @@ struct Ctx {
   DevBuf f64_sums;  // double k*d
   DevBuf f64_counts;  // int64 k
   HostBuf h_small;  // pinned scratch for small D2H
+  HostBuf h_up;     // pinned staging of the per-step screen32 upload
+  hipEvent_t up_event = nullptr;  // recorded after that upload
+  bool up_pending = false;
   int64_t last_fallback = 0;
   // profiling (cdr_profile_*): HIP events on the context stream around the
   // screen kernel and around the whole step (screen + reduce + fallback)

@@ -397,6 +397,8 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.fin_counts, &c.fin_creation, &c.fin_out, &c.fin_red, &c.run_sums};
   for (DevBuf* b : bufs) b->release();
   c.h_small.release();
+  c.h_up.release();
+  if (c.up_event) (void)hipEventDestroy(c.up_event);
   for (hipEvent_t& e : c.pe)
     if (e) (void)hipEventDestroy(e);
   if (c.own_stream && c.stream) (void)hipStreamDestroy(c.stream);

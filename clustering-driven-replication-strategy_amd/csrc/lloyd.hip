@@ -1029,7 +1029,6 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   check_k(c, k);
   if (c.mode != CDR_MODE_F32X) CDR_FAIL(CDR_ERR_STATE, "lloyd_step: points are not F32X");
   const int d = c.d, kd1 = d + 1, len = k * kd1;
-  upload_centroids(c, C, k);
   long long* dout;
   if (out_dev) {
     dout = reinterpret_cast<long long*>(out);
@@ -1037,17 +1036,23 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     c.out_sums.ensure(sizeof(long long) * len);
     dout = c.out_sums.as<long long>();
   }
-  // fallback regions: one per screen wave (sized below), zeroed every step
-  HIP_CHECK(hipMemsetAsync(dout, 0, sizeof(long long) * len, c.stream));
-  c.fb_list.ensure(sizeof(int32_t) * (c.n > 0 ? c.n : 1));
   const float fx = (float)std::ldexp(1.0, c.scale_bits);
   const int cus = lloyd_num_cus(c.device);
 
   prof_collect(c);
   const bool prof = c.prof_on;
   bool screened = false;
-  if (screen32_supported(c, k) &&
-      screen32_step(c, C, k, dout, prof, g_dbg_ptr, g_dbg_ptr ? g_dbg_thr : nullptr)) {
+  // screen32 uploads its own operands (one pinned copy) and leaves the totals
+  // in c.run_sums; it copies them to a device `out` itself
+  bool s32 = screen32_supported(c, k) &&
+             screen32_step(c, C, k, out_dev ? dout : nullptr, prof, g_dbg_ptr,
+                           g_dbg_ptr ? g_dbg_thr : nullptr);
+  if (!s32) {
+    upload_centroids(c, C, k);
+    HIP_CHECK(hipMemsetAsync(dout, 0, sizeof(long long) * len, c.stream));
+    c.fb_list.ensure(sizeof(int32_t) * (c.n > 0 ? c.n : 1));
+  }
+  if (s32) {
     screened = true;
   } else if (screen_supported(c, k)) {
     c.run_valid = false;  // the screen_fast / screen_kernel path keeps no running sums
@@ -1159,13 +1164,16 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   c.have_labels = true;
   if (!out_dev) {
     c.h_small.ensure(sizeof(long long) * len + 64);
-    HIP_CHECK(hipMemcpyAsync(c.h_small.p, dout, sizeof(long long) * len,
+    const void* src = s32 ? c.run_sums.p : (const void*)dout;
+    HIP_CHECK(hipMemcpyAsync(c.h_small.p, src, sizeof(long long) * len,
                              hipMemcpyDeviceToHost, c.stream));
-    int32_t fb = 0;
+    int32_t* hfb = reinterpret_cast<int32_t*>(c.h_small.as<long long>() + len);
+    *hfb = 0;
     if (screened)
-      HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.as<int32_t>() + c.fb_regions, sizeof(int32_t),
+      HIP_CHECK(hipMemcpyAsync(hfb, c.fb_count.as<int32_t>() + c.fb_regions, sizeof(int32_t),
                                hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
+    const int32_t fb = *hfb;
     memcpy(out, c.h_small.p, sizeof(long long) * len);
     c.last_fallback = screened ? fb : c.n;
     if (c.prof_pending) c.prof_fb_points += fb;

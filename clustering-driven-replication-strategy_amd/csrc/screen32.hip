@@ -164,6 +164,13 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
   int fb_used = 0;
   __syncthreads();
 
+  // running per-lane pointers of the next group to load (quad u; labels),
+  // advanced by one grid stride per prefetch
+  const int64_t gstep = (int64_t)gridDim.x * wpb * 64;
+  const f4* pq[QH];
+#pragma unroll
+  for (int u = 0; u < QH; ++u) pq[u] = Xq + (int64_t)qd[u] * a.n_pad + (G << 6) + p;
+  const int32_t* plab = a.labels + (G << 6) + lane;
   auto load = [&](f4 (&buf)[2][QH], int64_t grp) {
     if constexpr ((ABL & 8) != 0) {
 #pragma unroll
@@ -181,7 +188,7 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
 #pragma unroll
       for (int u = 0; u < QH; ++u) {
         f4 v = {0.f, 0.f, 0.f, 0.f};
-        if (FULLQ || qok[u]) v = Xq[(int64_t)qd[u] * a.n_pad + (grp << 6) + 32 * t + p];
+        if (FULLQ || qok[u]) v = pq[u][32 * t];  // tile t: immediate offset 512 B
         buf[t][u] = v;
       }
   };
@@ -263,98 +270,136 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
     sk = s | ((unsigned)h << 2);
   };
 
+  // one group of 64 points (the wave's registers xb, previous labels ob)
+  auto process = [&](const f4 (&xb)[2][QH], int ob, int64_t Gp) {
+    const int64_t base = Gp << 6;
+    if (base >= a.n) return;  // wave-uniform: padding groups have no real points
+    unsigned bA, sA, bB, sB;
+    tile(xb[0], bA, sA, base);
+    tile(xb[1], bB, sB, base + 32);
+    // lanes < 32: tile A's point l; lanes >= 32: tile B's point l - 32
+    swap32(bA, bB);
+    swap32(sA, sB);
+    merge_top2(bA, sA, bB, sB);
+    const int64_t pt = base + lane;
+    const int label = (int)(bA & 63u);
+    const float vb = __uint_as_float(bA & ~63u);
+    const float vs = __uint_as_float(sA & ~63u);
+    const bool cert = vs > fmaf(vb, thr_rel, thr0);  // NaN: never certified
+    const bool real = pt < a.n;
+    const bool ok = cert && real;
+    bool put = ok;
+    if (DELTA) put = ok && label != ob;
+    if (put) a.labels[pt] = label;
+    const unsigned long long need = __ballot(real && !cert);
+    if (need) {
+      const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+      if (real && !cert) fb_region[fb_used + rank] = (int32_t)pt;
+      fb_used += __popcll(need);
+    }
+    if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < QH; ++u) asm volatile("" ::"v"(xb[t][u]));
+      return;
+    }
+    // verdicts of tile A / tile B point p to both lane halves
+    unsigned vA = put ? (unsigned)label : 0xFFFFFFFFu;
+    unsigned vB = vA;
+    swap32(vA, vB);
+    unsigned oA = 0xFFFFFFFFu, oB = 0xFFFFFFFFu;
+    if (DELTA) {
+      oA = put ? (unsigned)ob : 0xFFFFFFFFu;
+      oB = oA;
+      swap32(oA, oB);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int lp = (int)(t == 0 ? vA : vB);
+      if (lp >= 0) {
+        double* row = tsum + 4 * QH * h * KP + lp;  // feature 4 qd[0] of label lp
+#pragma unroll
+        for (int u = 0; u < QH; ++u)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(&row[(4 * u + i) * KP], (double)xb[t][u][i]);
+        if (DELTA) {
+          const int lo = (int)(t == 0 ? oA : oB);
+          double* orow = tsum + 4 * QH * h * KP + lo;
+#pragma unroll
+          for (int u = 0; u < QH; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) atomicAdd(&orow[(4 * u + i) * KP], -(double)xb[t][u][i]);
+        }
+      }
+    }
+    const int lc = (int)(h == 0 ? vA : vB);
+    if (lc >= 0) {
+      atomicAdd(&tcnt[lc], 1);
+      if (DELTA) atomicAdd(&tcnt[(int)(h == 0 ? oA : oB)], -1);
+    }
+  };
+  auto prefetch = [&](f4 (&buf)[2][QH], int& ob, int64_t Gp) {
+    if (Gp < ngroups) {
+      load(buf, Gp);
+      if (DELTA) ob = *plab;
+    }
+#pragma unroll
+    for (int u = 0; u < QH; ++u) pq[u] += gstep;
+    plab += gstep;
+  };
+
+#ifndef CDR_S32_DEPTH
+#define CDR_S32_DEPTH 1
+#endif
+#if CDR_S32_DEPTH == 3
+  // three register sets: loads run two groups ahead
+  f4 x0[2][QH], x1[2][QH], x2[2][QH];
+  int o0 = -1, o1 = -1, o2 = -1;  // DELTA: previous label of point base + lane
+  prefetch(x0, o0, G);
+  prefetch(x1, o1, G + gstride);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see below
+  for (; G < ngroups; G += 3 * gstride) {
+    prefetch(x2, o2, G + 2 * gstride);
+    process(x0, o0, G);
+    if (G + gstride >= ngroups) break;
+    prefetch(x0, o0, G + 3 * gstride);
+    process(x1, o1, G + gstride);
+    if (G + 2 * gstride >= ngroups) break;
+    prefetch(x1, o1, G + 4 * gstride);
+    process(x2, o2, G + 2 * gstride);
+  }
+#elif CDR_S32_DEPTH == 2
+  // two register sets used alternately (no copies between iterations)
+  f4 xa[2][QH], xb2[2][QH];
+  int oa = -1, ob2 = -1;  // DELTA: previous label of point base + lane
+  prefetch(xa, oa, G);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see below
+  for (; G < ngroups; G += 2 * gstride) {
+    prefetch(xb2, ob2, G + gstride);
+    process(xa, oa, G);
+    if (G + gstride >= ngroups) break;
+    prefetch(xa, oa, G + 2 * gstride);
+    process(xb2, ob2, G + gstride);
+  }
+#else
   f4 cur[2][QH], nxt[2][QH];
   int ocur = -1, onxt = -1;  // DELTA: previous label of point base + lane
-  if (G < ngroups) {
-    load(cur, G);
-    if (DELTA) ocur = a.labels[(G << 6) + lane];
-  }
+  prefetch(cur, ocur, G);
   // drain before the loop, otherwise the waitcnt pass merges these loads into
   // the loop-header state and waits for the fresh prefetch in every iteration
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   for (; G < ngroups; G += gstride) {
-    const int64_t Gn = G + gstride;
-    if (Gn < ngroups) {
-      load(nxt, Gn);
-      if (DELTA) onxt = a.labels[(Gn << 6) + lane];
-    }
-    const int64_t base = G << 6;
-    if (base < a.n) {  // wave-uniform: padding groups have no real points
-      unsigned bA, sA, bB, sB;
-      tile(cur[0], bA, sA, base);
-      tile(cur[1], bB, sB, base + 32);
-      // lanes < 32: tile A's point l; lanes >= 32: tile B's point l - 32
-      swap32(bA, bB);
-      swap32(sA, sB);
-      merge_top2(bA, sA, bB, sB);
-      const int64_t pt = base + lane;
-      const int label = (int)(bA & 63u);
-      const float vb = __uint_as_float(bA & ~63u);
-      const float vs = __uint_as_float(sA & ~63u);
-      const bool cert = vs > fmaf(vb, thr_rel, thr0);  // NaN: never certified
-      const bool real = pt < a.n;
-      const bool ok = cert && real;
-      bool put = ok;
-      if (DELTA) put = ok && label != ocur;
-      if (put) a.labels[pt] = label;
-      const unsigned long long need = __ballot(real && !cert);
-      if (need) {
-        const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
-        if (real && !cert) fb_region[fb_used + rank] = (int32_t)pt;
-        fb_used += __popcll(need);
-      }
-      if constexpr ((ABL & 1) != 0) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int u = 0; u < QH; ++u) asm volatile("" ::"v"(cur[t][u]));
-        goto next_group;
-      }
-      {
-      // verdicts of tile A / tile B point p to both lane halves
-      unsigned vA = put ? (unsigned)label : 0xFFFFFFFFu;
-      unsigned vB = vA;
-      swap32(vA, vB);
-      unsigned oA = 0xFFFFFFFFu, oB = 0xFFFFFFFFu;
-      if (DELTA) {
-        oA = put ? (unsigned)ocur : 0xFFFFFFFFu;
-        oB = oA;
-        swap32(oA, oB);
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int lp = (int)(t == 0 ? vA : vB);
-        if (lp >= 0) {
-          double* row = tsum + 4 * QH * h * KP + lp;  // feature 4 qd[0] of label lp
-#pragma unroll
-          for (int u = 0; u < QH; ++u)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) atomicAdd(&row[(4 * u + i) * KP], (double)cur[t][u][i]);
-          if (DELTA) {
-            const int lo = (int)(t == 0 ? oA : oB);
-            double* orow = tsum + 4 * QH * h * KP + lo;
-#pragma unroll
-            for (int u = 0; u < QH; ++u)
-#pragma unroll
-              for (int i = 0; i < 4; ++i) atomicAdd(&orow[(4 * u + i) * KP], -(double)cur[t][u][i]);
-          }
-        }
-      }
-      const int lc = (int)(h == 0 ? vA : vB);
-      if (lc >= 0) {
-        atomicAdd(&tcnt[lc], 1);
-        if (DELTA) atomicAdd(&tcnt[(int)(h == 0 ? oA : oB)], -1);
-      }
-      }
-    }
-  next_group:
+    prefetch(nxt, onxt, G + gstride);
+    process(cur, ocur, G);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int u = 0; u < QH; ++u) cur[t][u] = nxt[t][u];
     ocur = onxt;
   }
+#endif
   if (lane == 0) {
     a.fb_count[wave_id] = fb_used;
     if (fb_used) atomicAdd(a.fb_count + gstride, fb_used);
@@ -392,14 +437,8 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
     tot += cnt[r];
   }
   if (tot == 0) return;  // uniform: nothing to add to this workgroup's table
-  constexpr int d = D;
-  double* ct = reinterpret_cast<double*>(smem);  // [d][k]
-  double* tsum = ct + (size_t)d * k;             // [d4][KP]
+  double* tsum = reinterpret_cast<double*>(smem);  // [d4][KP]
   int* tcnt = reinterpret_cast<int*>(tsum + (size_t)d4 * KP);
-  for (int i = threadIdx.x; i < k * d; i += blockDim.x) {
-    const int j = i / d, f = i - j * d;
-    ct[f * k + j] = C[i];
-  }
   for (int i = threadIdx.x; i < d4 * KP; i += blockDim.x) tsum[i] = 0.0;
   for (int i = threadIdx.x; i < KP; i += blockDim.x) tcnt[i] = 0;
   __syncthreads();
@@ -410,14 +449,21 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
     double x[D];
 #pragma unroll
     for (int f = 0; f < D; ++f) x[f] = (double)X[xidx(f, pt, n_pad)];
-    double rb = INFINITY;
+    // centroid j is wave-uniform: its row comes through scalar loads
+    double sb = INFINITY, rb = INFINITY;
     int jmin = 0;
     for (int j = 0; j < k; ++j) {
-      const double s = np_sqdist([&](int f) { return x[f]; }, [&](int f) { return ct[f * k + j]; }, d);
-      const double r2 = sqrt(s);
-      if (r2 < rb) {  // strict: first index on ties of the roots
-        rb = r2;
-        jmin = j;
+      const double* cj = C + (size_t)j * D;
+      const double s = np_sqdist([&](int f) { return x[f]; }, [&](int f) { return cj[f]; }, D);
+      // sqrt is monotone: a root can only undercut the best root when s < sb,
+      // and then the roots decide (strict: first index on ties of the roots)
+      if (s < sb) {
+        const double r2 = sqrt(s);
+        sb = s;
+        if (r2 < rb) {
+          rb = r2;
+          jmin = j;
+        }
       }
     }
     const int old = delta ? labels[pt] : -1;  // not yet overwritten by the screen
@@ -644,13 +690,26 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   }
   const int d = c.d, Q = d4_of(d) / 4;
   const int KP = 32 * pl.MT, NF = 8 * pl.QH;
-  c.frag.ensure(pl.frag.size() * sizeof(h8) + pl.cinit.size() * sizeof(float));
+  // one pinned upload per step: fragments | C operand | centroids (fp64, for
+  // fallback32); the previous step's copy must have left the staging buffer
+  const size_t b_frag = pl.frag.size() * sizeof(h8);
+  const size_t b_cinit = pl.cinit.size() * sizeof(float);
+  const size_t b_cent = sizeof(double) * (size_t)k * c.d;
+  const size_t b_all = b_frag + b_cinit + b_cent;
+  if (c.up_pending) HIP_CHECK(hipEventSynchronize(c.up_event));
+  c.h_up.ensure(b_all);
+  memcpy(c.h_up.p, pl.frag.data(), b_frag);
+  memcpy(static_cast<char*>(c.h_up.p) + b_frag, pl.cinit.data(), b_cinit);
+  memcpy(static_cast<char*>(c.h_up.p) + b_frag + b_cinit, C, b_cent);
+  c.frag.ensure(b_all);
+  HIP_CHECK(hipMemcpyAsync(c.frag.p, c.h_up.p, b_all, hipMemcpyHostToDevice, c.stream));
+  if (!c.up_event) HIP_CHECK(hipEventCreateWithFlags(&c.up_event, hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(c.up_event, c.stream));
+  c.up_pending = true;
   h8* dfrag = c.frag.as<h8>();
-  float* dcinit = reinterpret_cast<float*>(dfrag + pl.frag.size());
-  HIP_CHECK(hipMemcpyAsync(dfrag, pl.frag.data(), pl.frag.size() * sizeof(h8),
-                           hipMemcpyHostToDevice, c.stream));
-  HIP_CHECK(hipMemcpyAsync(dcinit, pl.cinit.data(), pl.cinit.size() * sizeof(float),
-                           hipMemcpyHostToDevice, c.stream));
+  float* dcinit = reinterpret_cast<float*>(static_cast<char*>(c.frag.p) + b_frag);
+  const double* dcent =
+      reinterpret_cast<const double*>(static_cast<char*>(c.frag.p) + b_frag + b_cinit);
   const size_t lds = (size_t)NF * KP * 8 + (size_t)KP * 4;
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
@@ -732,7 +791,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
 #undef CDR_S32
   HIP_CHECK(hipGetLastError());
   if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
-  const size_t fb_lds = (size_t)k * d * 8 + lds;
+  const size_t fb_lds = lds;
   {
     typedef void (*FbFn)(const float*, int64_t, int, const double*, int, const int32_t*,
                          const int32_t*, int, int, int32_t*, double*, int, const float*, float);
@@ -742,7 +801,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
                                     fallback32<12>, fallback32<13>, fallback32<14>, fallback32<15>,
                                     fallback32<16>};
     hipLaunchKernelGGL(fb_fns[d], grid, blk, fb_lds, c.stream, c.x32.as<float>(), c.n_pad, NF,
-                       c.cent64.as<double>(), k, c.fb_list.as<int32_t>(),
+                       dcent, k, c.fb_list.as<int32_t>(),
                        c.fb_count.as<int32_t>(), cap, KP, c.labels.as<int32_t>(),
                        c.partials.as<double>(), delta ? 1 : 0,
                        pre ? c.mu_s.as<float>() : nullptr, (float)std::ldexp(1.0, c.sigma));
@@ -753,8 +812,9 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
                      std::ldexp(1.0, c.scale_bits - (pre ? c.sigma : 0)),
                      pre ? c.muf.as<long long>() : nullptr, c.run_sums.as<unsigned long long>());
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipMemcpyAsync(dout, c.run_sums.p, sizeof(long long) * len, hipMemcpyDeviceToDevice,
-                           c.stream));
+  if (dout)
+    HIP_CHECK(hipMemcpyAsync(dout, c.run_sums.p, sizeof(long long) * len,
+                             hipMemcpyDeviceToDevice, c.stream));
   c.run_valid = dbg == nullptr;
   c.run_k = k;
   return true;

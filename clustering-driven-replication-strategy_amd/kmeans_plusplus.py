@@ -115,11 +115,9 @@ def kmeans(X, k, number_of_files=100, tol=1e-4, random_state=None, *,
         calc = np.asarray(centroids, dtype=np.float64)
         means, counts = _cluster_means(ctx, calc, mode, scale_bits)
         new_centroids = np.empty_like(centroids)
-        for j in range(k):
-            if counts[j] > 0:
-                new_centroids[j] = means[j]
-            else:
-                new_centroids[j] = X[np.random.randint(0, n_samples)]
+        new_centroids[...] = means
+        for j in np.flatnonzero(counts == 0):  # j order, as the reference draws (:43)
+            new_centroids[j] = X[np.random.randint(0, n_samples)]
         shift = np.linalg.norm(new_centroids - centroids)
         centroids = new_centroids
         if shift < tol:

@@ -1,0 +1,15 @@
+# One GPU call: all GPU tests, bench config 3 (with CPU leg) and 2, rocprofv3
+# kernel stats of the config-3 bench, PMC passes for configs 3 and 2.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench3.json 2> gpurun_out/bench3.err || { echo BENCH3_FAIL; tail -20 gpurun_out/bench3.err; exit 2; }
+cat gpurun_out/bench3.json
+timeout -k 10 300 python -u bench.py --config 2 --steps 50 --warmup 3 --no-cpu-baseline > gpurun_out/bench2.json 2> gpurun_out/bench2.err || { echo BENCH2_FAIL; tail -20 gpurun_out/bench2.err; exit 3; }
+cat gpurun_out/bench2.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof3.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof3.log; exit 4; }
+bash tools/pmc_lloyd.sh 100000000 16 64 c3 || exit 5
+bash tools/pmc_lloyd.sh 10000000 8 16 c2 || exit 6
+echo ALL_OK

@@ -1,6 +1,7 @@
 """Summarise the rocprofv3 --pmc passes of tools/pmc_lloyd.sh (per dispatch).
 
-    python tools/pmc_summary.py gpurun_out/pmc > profiles/rNN_pmc_screen32.txt
+    python tools/pmc_summary.py gpurun_out/pmc_c3 > profiles/rNN_pmc_screen32.txt
+    python tools/pmc_summary.py gpurun_out/pmc_c3 --json 3 100000000   # -> profiles/pmc_traffic.json
 
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes
 of wide coalesced streaming reads (MI355X_MICROARCH.md §HBM), so the HBM read
@@ -13,6 +14,10 @@ import os
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+json_cfg = None
+if "--json" in sys.argv:
+    i = sys.argv.index("--json")
+    json_cfg, json_n = sys.argv[i + 1], int(sys.argv[i + 2])
 agg = collections.defaultdict(dict)
 names = {}
 for f in sorted(glob.glob(os.path.join(root, "*", "*_counter_collection.csv"))):
@@ -38,3 +43,20 @@ for key in sorted(agg):
                  f" issue-stall {c.get('SQ_WAIT_INST_ANY', 0) / w:.2f}"
                  f" waitcnt {c.get('SQ_WAIT_ANY', 0) / w:.2f}")
     print(line)
+
+if json_cfg is not None:
+    # HBM bytes of the last steady-state (DELTA) screen32 launch: read + write
+    import json
+    f = [k for k in agg if "screen32" in names[k] and "FETCH_SIZE" in agg[k]]
+    w = [k for k in agg if "screen32" in names[k] and "WRITE_SIZE" in agg[k]]
+    if f and w:
+        rb = agg[max(f, key=lambda k: k[1])]["FETCH_SIZE"] * 2048
+        wb = agg[max(w, key=lambda k: k[1])]["WRITE_SIZE"] * 1024
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "profiles", "pmc_traffic.json")
+        rec = json.load(open(path)) if os.path.exists(path) else {}
+        rec[json_cfg] = {"n_local": json_n, "hbm_bytes_per_launch": rb + wb, "read_bytes": rb,
+                         "write_bytes": wb, "source": root,
+                         "note": "FETCH_SIZE KiB x2 (gfx950 half-count) + WRITE_SIZE KiB"}
+        json.dump(rec, open(path, "w"), indent=1)
+        print("wrote", path, rec[json_cfg])
