@@ -175,7 +175,7 @@ def main() -> None:
                              "int64 fixed-point sums (results bit-identical to fp64 NumPy)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                     "kernel": "screen_kernel<1,true,false>",
+                     "kernel": ctx.profile_kernel(),
                      "alg_bytes_per_launch": alg_bytes, "kernel_ms": screen_ms},
         "step_kernels_ms": step_kernel_ms,
         "fallback_frac": fb_frac,

@@ -70,6 +70,7 @@ SIGNATURES = {
     "cdr_debug_screen": ([_P, _P, _I32, _P, _P], None),
     "cdr_profile_reset": ([_P, _I32], None),
     "cdr_profile_read": ([_P, _P], None),
+    "cdr_profile_kernel": ([_P, _P, _I32], None),
     "cdr_debug_screen_ablate": ([_P, _I32], None),
     "cdr_medians_segmented": ([_P, _P, _P, _I64, _P], None),
     "cdr_medians_by_label": ([_P, _I32, _P], None),
@@ -255,6 +256,11 @@ class Context:
         _check(self._lib.cdr_profile_read(self._h, _ptr(out)))
         return {"screen_ms": out[0], "steps": int(out[1]), "step_ms": out[2],
                 "fallback_points": int(out[3])}
+
+    def profile_kernel(self) -> str:
+        buf = ctypes.create_string_buffer(96)
+        _check(self._lib.cdr_profile_kernel(self._h, buf, 96))
+        return buf.value.decode()
 
     def debug_ablate(self, mask: int) -> None:
         _check(self._lib.cdr_debug_screen_ablate(self._h, int(mask)))

@@ -130,6 +130,7 @@ struct Ctx {
   hipEvent_t pe[3] = {nullptr, nullptr, nullptr};
   double prof_screen_ms = 0.0, prof_step_ms = 0.0, prof_fb_points = 0.0;
   int64_t prof_launches = 0;
+  char prof_kernel[96] = {0};  // name of the last screen kernel launched
   int32_t last_k = 0;
   bool have_labels = false;
   bool last_screened = false;

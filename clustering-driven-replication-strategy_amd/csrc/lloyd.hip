@@ -22,6 +22,7 @@
 // row-ordered fp64 sum per (cluster, feature) — NumPy's X[mask].mean(axis=0)
 // is a sequential row-order sum for d >= 2 and the blocked pairwise sum for
 // d == 1 (oracle/kmeans_oracle.py pins both against NumPy).
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 
@@ -1102,6 +1103,10 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     a.dbg = g_dbg_ptr;
     a.ablate = c.screen_ablate;
     const bool dbg = g_dbg_ptr != nullptr;
+    if (pl.fast)
+      snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_fast<%d,%d>", pl.DCH, pl.KT);
+    else
+      snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_kernel<%d>", pl.DCH);
     if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
     if (pl.fast) {
       bool nonneg = true;
@@ -1315,6 +1320,13 @@ int cdr_profile_read(cdr_ctx* h, double* out) {
   out[1] = (double)c.prof_launches;
   out[2] = c.prof_step_ms;
   out[3] = c.prof_fb_points;
+  CDR_CATCH
+}
+
+int cdr_profile_kernel(cdr_ctx* h, char* buf, int32_t len) {
+  CDR_TRY
+  if (!h || !buf || len < 1) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  snprintf(buf, (size_t)len, "%s", h->c.prof_kernel);
   CDR_CATCH
 }
 

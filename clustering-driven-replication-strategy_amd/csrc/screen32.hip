@@ -32,6 +32,7 @@
 // see screen32_supported) into a per-workgroup LDS table sum[f][j] with
 // ds_add_f64 and their count with ds_add_u32; reduce32 converts every
 // workgroup's sums to exact int64 fixed point and adds them.
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 
@@ -760,6 +761,9 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   a.fb_cap = cap;
   a.dbg = dbg;
   a.dbg_ld = (k + 15) / 16 * 16;
+  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32<%d,%d,%s,%s,%s,%s>", pl.QH, pl.MT,
+           Q == 2 * pl.QH ? "true" : "false", delta ? "true" : "false", dbg ? "true" : "false",
+           pre ? "true" : "false");
   if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
   const dim3 grid(nwg), blk(256);
   const bool fullq = Q == 2 * pl.QH;

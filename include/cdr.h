@@ -122,6 +122,9 @@ int cdr_profile_reset(cdr_ctx* ctx, int32_t enable);
  * 2 argmin, 4 MFMA, 8 loads).  Results are garbage while mask != 0.       */
 int cdr_debug_screen_ablate(cdr_ctx* ctx, int32_t mask);
 int cdr_profile_read(cdr_ctx* ctx, double* out);
+/* Name of the last screen kernel launched (for the bench's roofline line);
+ * NUL-terminated, truncated to len.                                          */
+int cdr_profile_kernel(cdr_ctx* ctx, char* buf, int32_t len);
 /* Test hook (not product path): screen values T (n_pad, ceil(k/16)*16) fp32
  * of one F32X step and the certification constants (A0, A1).               */
 int cdr_debug_screen(cdr_ctx* ctx, const double* C, int32_t k, float* out_vals,

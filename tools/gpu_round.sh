@@ -11,5 +11,8 @@ timeout -k 10 300 python -u bench.py --config 2 --steps 50 --warmup 3 --no-cpu-b
 cat gpurun_out/bench2.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof3.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof3.log; exit 4; }
 bash tools/pmc_lloyd.sh 100000000 16 64 c3 || exit 5
+python tools/pmc_summary.py gpurun_out/pmc_c3 --json 3 100000000 > gpurun_out/pmc_c3.txt || exit 7
 bash tools/pmc_lloyd.sh 10000000 8 16 c2 || exit 6
+python tools/pmc_summary.py gpurun_out/pmc_c2 --json 2 10000000 > gpurun_out/pmc_c2.txt || exit 8
+cp profiles/pmc_traffic.json gpurun_out/ || true
 echo ALL_OK
