@@ -20,6 +20,8 @@
 //   applying whole blocks inside a binade and walking element by element only
 //   across the ~log2(c_last/c_first) binade crossings.
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "cdr_internal.h"
@@ -91,73 +93,134 @@ __device__ double pw_tree(int64_t n, LF leaf) {
 
 // One workgroup (256 threads) per 8192-point block.  The block is handled in
 // two halves of 4096 (pw(8192) = pw(4096) + pw(4096)); each half's values sit
-// in LDS with one pad slot per 128 (conflict-free leaf reads).
-template <typename T>
+// in LDS (one pad slot per 16).
+//
+// Full blocks (TAIL = false): the 32 pairwise leaves of 128 of a half are
+// summed by 8 threads each — thread (leaf L, j) adds NumPy's accumulator r_j
+// = a(j) + a(j + 8) + ... sequentially, shfl_xor 1, 2, 4 forms
+// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), shfl_xor 8, 16, 32 and
+// then a 4-wave LDS step combine the leaves in the balanced tree of
+// pw(4096).
+// TAIL = true: the one partial block (m < 8192) at b_off; its pairwise tree
+// is enumerated by one thread (a stack: scratch memory, kept out of the
+// full-block kernel).
+// D > 0 (float points, d == D <= 16): each thread takes 4 points per
+// iteration with all their 16-byte feature-quad loads and dmin loads issued
+// before any arithmetic, and the NumPy-order distance unrolled for that d.
+template <typename T, int D, bool TAIL>
 __global__ __launch_bounds__(256) void seed_update_kernel(
     const T* __restrict__ X, int64_t n, int64_t n_pad, int d, const double* __restrict__ cen,
-    double* __restrict__ dmin, double* __restrict__ blocksums) {
-  __shared__ double sdm[4096 + 32];
-  __shared__ double sleaf[160];
-  __shared__ int soff[160], slen[160];
-  __shared__ int sleaves;
-  const int64_t b = blockIdx.x;
+    double* __restrict__ dmin, double* __restrict__ blocksums, int64_t b_off) {
+  constexpr int kHalf = 4096;
+  __shared__ double sdm[kHalf + kHalf / 16];
+  __shared__ double swave[4];
+  const int64_t b = blockIdx.x + b_off;
   const int64_t base = b * kSeedBlock;
-  const int m = (int)((n - base) < kSeedBlock ? (n - base) : kSeedBlock);
+  const int m = TAIL ? (int)(n - base) : kSeedBlock;
+  auto spos = [](int q) { return q + (q >> 4); };
   double halves[2] = {0.0, 0.0};
   for (int h = 0; h < 2; ++h) {
-    for (int q = threadIdx.x; q < 4096; q += blockDim.x) {
-      const int qi = h * 4096 + q;
-      const int64_t i = base + qi;
-      double v = 0.0;
-      if (qi < m) {
-        auto xv = [&](int f) { return (double)X[xidx(f, i, n_pad)]; };
-        auto cv = [&](int f) { return cen[f]; };
-        const double R = np_sqdist(xv, cv, d);
-        const double r = sqrt(R);
-        const double t = r * r;
-        const double old = dmin[i];
-        v = t < old ? t : old;
-        dmin[i] = v;
+    if constexpr (D > 0) {
+      constexpr int Q = (D + 3) / 4;
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v* X4 = reinterpret_cast<const f4v*>(X);
+      double cr[D];
+#pragma unroll
+      for (int f = 0; f < D; ++f) cr[f] = cen[f];
+      for (int q0 = threadIdx.x; q0 < kHalf; q0 += 4 * 256) {
+        f4v xv[4][Q];
+        double old[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int qi = h * kHalf + q0 + 256 * u;
+          const int64_t i = base + qi;
+          if (!TAIL || qi < m) {
+#pragma unroll
+            for (int qq = 0; qq < Q; ++qq) xv[u][qq] = X4[(int64_t)qq * n_pad + i];
+            old[u] = dmin[i];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int q = q0 + 256 * u;
+          const int qi = h * kHalf + q;
+          double v = 0.0;
+          if (!TAIL || qi < m) {
+            auto xf = [&](int f) { return (double)xv[u][f >> 2][f & 3]; };
+            auto cf = [&](int f) { return cr[f]; };
+            const double R = np_sqdist(xf, cf, D);
+            const double r = sqrt(R);
+            const double t = r * r;
+            v = t < old[u] ? t : old[u];
+            dmin[base + qi] = v;
+          }
+          sdm[spos(q)] = v;
+        }
       }
-      sdm[q + (q >> 7)] = v;
+    } else {
+      for (int q = threadIdx.x; q < kHalf; q += blockDim.x) {
+        const int qi = h * kHalf + q;
+        const int64_t i = base + qi;
+        double v = 0.0;
+        if (!TAIL || qi < m) {
+          auto xv = [&](int f) { return (double)X[xidx(f, i, n_pad)]; };
+          auto cv = [&](int f) { return cen[f]; };
+          const double R = np_sqdist(xv, cv, d);
+          const double r = sqrt(R);
+          const double t = r * r;
+          const double old = dmin[i];
+          v = t < old ? t : old;
+          dmin[i] = v;
+        }
+        sdm[spos(q)] = v;
+      }
     }
     __syncthreads();
-    if (m == kSeedBlock && threadIdx.x < 32) {
-      const int l = threadIdx.x;
-      double s = np_pw_leaf([&](int i) { return sdm[129 * l + i]; }, 128);
-      for (int o = 1; o < 32; o <<= 1) s = s + __shfl_xor(s, o);
-      if (l == 0) halves[h] = s;
+    if constexpr (!TAIL) {
+      const int t = threadIdx.x;
+      const int L = t >> 3, j = t & 7;
+      double r = sdm[spos(128 * L + j)];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) r = r + sdm[spos(128 * L + j + 8 * i)];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) r = r + __shfl_xor(r, o);
+      if ((t & 63) == 0) swave[t >> 6] = r;
+      __syncthreads();
+      if (t == 0) halves[h] = (swave[0] + swave[1]) + (swave[2] + swave[3]);
+      __syncthreads();
     }
-    __syncthreads();
   }
-  if (m == kSeedBlock) {
+  if constexpr (!TAIL) {
     if (threadIdx.x == 0) blocksums[b] = halves[0] + halves[1];
-    return;
-  }
-  // partial (last) block: enumerate the pairwise leaves, sum them in
-  // parallel from global memory, combine in tree order.
-  __threadfence_block();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int cnt = 0;
-    pw_tree((int64_t)m, [&](int64_t off, int len) {
-      soff[cnt] = (int)off;
-      slen[cnt] = len;
-      ++cnt;
-      return 0.0;
-    });
-    sleaves = cnt;  // <= 128 leaves of (64, 128] elements for m < 8192
-  }
-  __syncthreads();
-  const int cnt = sleaves;
-  if (threadIdx.x < cnt) {
-    const int off = soff[threadIdx.x], len = slen[threadIdx.x];
-    sleaf[threadIdx.x] = np_pw_leaf([&](int i) { return dmin[base + off + i]; }, len);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int cur = 0;
-    blocksums[b] = pw_tree((int64_t)m, [&](int64_t, int) { return sleaf[cur++]; });
+  } else {
+    __shared__ double sleaf[160];
+    __shared__ int soff[160], slen[160];
+    __shared__ int sleaves;
+    // partial (last) block: enumerate the pairwise leaves, sum them in
+    // parallel from global memory, combine in tree order.
+    __threadfence_block();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int cnt = 0;
+      pw_tree((int64_t)m, [&](int64_t off, int len) {
+        soff[cnt] = (int)off;
+        slen[cnt] = len;
+        ++cnt;
+        return 0.0;
+      });
+      sleaves = cnt;  // <= 128 leaves of (64, 128] elements for m < 8192
+    }
+    __syncthreads();
+    const int cnt = sleaves;
+    if (threadIdx.x < cnt) {
+      const int off = soff[threadIdx.x], len = slen[threadIdx.x];
+      sleaf[threadIdx.x] = np_pw_leaf([&](int i) { return dmin[base + off + i]; }, len);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int cur = 0;
+      blocksums[b] = pw_tree((int64_t)m, [&](int64_t, int) { return sleaf[cur++]; });
+    }
   }
 }
 
@@ -169,14 +232,15 @@ __device__ __forceinline__ void compose(long long L0, long long L1, long long R0
   o1 = L1 + ((L1 & 1) ? R0 : R1);
 }
 
-// Transfer of elements [lo, hi) of dmin under binade exponent e.
-__device__ void range_transfer(const double* __restrict__ dmin, double S, int64_t lo,
-                               int64_t hi, int e, long long& D0, long long& D1, int& valid) {
+// Transfer of elements [lo, hi) (values v(i)) under binade exponent e.
+template <typename V>
+__device__ __forceinline__ void range_transfer_v(V v, double S, int64_t lo, int64_t hi, int e,
+                                                 long long& D0, long long& D1, int& valid) {
   D0 = 0;
   D1 = 0;
   valid = 1;
   for (int64_t i = lo; i < hi; ++i) {
-    const double p = dmin[i] / S;
+    const double p = v(i) / S;
     const double f = ldexp(p, 52 - e);
     if (!(f < 4503599627370496.0)) {  // >= 2^52 (or NaN): leaves the binade
       valid = 0;
@@ -200,6 +264,11 @@ __device__ void range_transfer(const double* __restrict__ dmin, double S, int64_
   if (D0 >= (1ll << 52) || D1 >= (1ll << 52)) valid = 0;
 }
 
+__device__ void range_transfer(const double* __restrict__ dmin, double S, int64_t lo,
+                               int64_t hi, int e, long long& D0, long long& D1, int& valid) {
+  range_transfer_v([&](int64_t i) { return dmin[i]; }, S, lo, hi, e, D0, D1, valid);
+}
+
 __device__ __forceinline__ bool binade_of(double c, int& e, long long& N) {
   const unsigned long long bits = __double_as_longlong(c);
   const int ef = (int)((bits >> 52) & 0x7FF);
@@ -214,40 +283,80 @@ __device__ __forceinline__ double from_binade(int e, long long N) {
   return __longlong_as_double(bits);
 }
 
-// Per-block transfers under the guessed binade of the block's start.
+// Per-block transfers under the guessed binade of the block's start.  One
+// wave per 8192-element block, in 8 passes of 1024: the pass is loaded
+// coalesced (16 B per lane per load) into LDS with one pad slot per 16
+// elements, then lane l walks elements [16 l, 16 l + 16) of the pass from LDS
+// (conflict-free ds_read_b64), the 64 lane transfers are composed in order and
+// the pass transfer is composed onto the block's.
+constexpr int kPass = 1024;
+constexpr int kPassPad = kPass + kPass / 16;
+
 __global__ __launch_bounds__(256) void xfer_kernel(const double* __restrict__ dmin, int64_t n,
                                                    double S, const double* __restrict__ approx,
                                                    int64_t nblocks, Xfer* __restrict__ out) {
+  __shared__ double sbuf[4][kPassPad];
   const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (b >= nblocks) return;
-  const double ca = approx[b];
+  const int w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * 4 + w;
+  const bool live = b < nblocks;
+  double* sb = sbuf[w];
   int e = 0;
   long long Ndummy;
-  const bool okg = binade_of(ca, e, Ndummy);
+  const bool okg = live && binade_of(approx[b], e, Ndummy);
   const int64_t base = b * kSeedBlock;
-  const int64_t lo = base + (int64_t)lane * kSub;
-  int64_t hi = lo + kSub;
-  if (hi > n) hi = n;
-  long long D0 = 0, D1 = 0;
-  int valid = okg ? 1 : 0;
-  if (okg && lo < hi) range_transfer(dmin, S, lo, hi, e, D0, D1, valid);
-  // ordered reduction over lanes: lane l absorbs lane l+o
-  for (int o = 1; o < 64; o <<= 1) {
-    const long long r0 = __shfl_down(D0, o), r1 = __shfl_down(D1, o);
-    const int rv = __shfl_down(valid, o);
-    if ((lane & (2 * o - 1)) == 0 && lane + o < 64) {
-      long long n0, n1;
-      compose(D0, D1, r0, r1, n0, n1);
-      D0 = n0;
-      D1 = n1;
-      valid &= rv;
+  long long T0 = 0, T1 = 0;
+  int tv = okg ? 1 : 0;
+  for (int ps = 0; ps < kSeedBlock / kPass; ++ps) {
+    const int64_t pb = base + (int64_t)ps * kPass;
+    const bool act = okg && pb < n;  // wave-uniform
+    if (act) {
+      // dmin is allocated to n_pad (a multiple of the block): whole passes load
+      const double2* src = reinterpret_cast<const double2*>(dmin + pb);
+#pragma unroll
+      for (int j = 0; j < kPass / 128; ++j) {
+        const double2 v = src[j * 64 + lane];
+        const int el = j * 128 + 2 * lane;
+        const int pos = el + (el >> 4);
+        sb[pos] = v.x;
+        sb[pos + 1] = v.y;
+      }
     }
+    __syncthreads();
+    if (act) {
+      const int64_t lo = pb + (int64_t)lane * 16;
+      const int64_t hi = (lo + 16) < n ? (lo + 16) : n;
+      long long D0 = 0, D1 = 0;
+      int valid = 1;
+      const double* sl = sb + lane * 17;
+      if (lo < hi)
+        range_transfer_v([&](int64_t i) { return sl[i - lo]; }, S, lo, hi, e, D0, D1, valid);
+      // ordered reduction over lanes: lane l absorbs lane l+o
+      for (int o = 1; o < 64; o <<= 1) {
+        const long long r0 = __shfl_down(D0, o), r1 = __shfl_down(D1, o);
+        const int rv = __shfl_down(valid, o);
+        if ((lane & (2 * o - 1)) == 0 && lane + o < 64) {
+          long long n0, n1;
+          compose(D0, D1, r0, r1, n0, n1);
+          D0 = n0;
+          D1 = n1;
+          valid &= rv;
+        }
+      }
+      long long n0, n1;
+      compose(T0, T1, D0, D1, n0, n1);
+      tv &= valid;
+      // saturate: keeps the composition of later passes from overflowing
+      if (n0 >= (1ll << 52) || n1 >= (1ll << 52)) {
+        tv = 0;
+        n0 = n1 = 0;
+      }
+      T0 = n0;
+      T1 = n1;
+    }
+    __syncthreads();
   }
-  if (lane == 0) {
-    if (D0 >= (1ll << 52) || D1 >= (1ll << 52)) valid = 0;
-    out[b] = Xfer{D0, D1, e, valid, 0};
-  }
+  if (live && lane == 0) out[b] = Xfer{T0, T1, e, tv, 0};
 }
 
 // approx[b] = c_in + sum_{b' < b} blocksums[b'] / S   (guesses only)
@@ -281,99 +390,174 @@ __global__ __launch_bounds__(1024) void approx_prefix_kernel(const double* __res
 // Wave-parallel exact walk of elements [lo, hi) starting from running value c.
 // If `search`, stops at the first element m with fl(c_m / c_last) > u and
 // returns its index in *found (else *found stays -1).  Returns the running
-// value after the last element processed.  Executed by all 64 lanes of a wave.
+// value after the last element processed.  Executed by all 64 lanes of a
+// single-wave workgroup (it synchronises the workgroup).
+//
+// The range is taken in segments of 4096: p = fl(dmin / S) of the segment is
+// staged in LDS (coalesced loads, one pad slot per 64 so that lane l's
+// sub-chunk [64 l, 64 l + 64) reads conflict-free), then sub-chunk transfers
+// are applied in bulk while they stay in the binade and the sub-chunk that
+// leaves it is walked element by element.
+constexpr int kSeg = 4096;
+constexpr int kSegSub = kSeg / 64;
+
 __device__ double fine_walk(const double* __restrict__ dmin, double S, int64_t lo, int64_t hi,
                             double c, bool search, double c_last, double u, int64_t* found) {
+  __shared__ double sp[kSeg + kSeg / kSegSub];
   const int lane = threadIdx.x & 63;
-  int64_t pos = lo;
-  while (pos < hi) {
-    int e;
-    long long N;
-    const bool inb = binade_of(c, e, N);
-    int L = 0;  // sub-chunks applied in bulk
-    if (inb) {
-      const int64_t slo = pos + (int64_t)lane * kSub;
-      int64_t shi = slo + kSub;
-      if (shi > hi) shi = hi;
-      long long D0 = 0, D1 = 0;
-      int valid = 1;
-      if (slo < hi) range_transfer(dmin, S, slo, shi, e, D0, D1, valid);
-      else valid = 0;
-      // inclusive ordered prefix over lanes
-      for (int o = 1; o < 64; o <<= 1) {
-        const long long l0 = __shfl_up(D0, o), l1 = __shfl_up(D1, o);
-        const int lv = __shfl_up(valid, o);
-        if (lane >= o) {
-          long long n0, n1;
-          compose(l0, l1, D0, D1, n0, n1);
-          D0 = n0;
-          D1 = n1;
-          valid &= lv;
+  for (int64_t s0 = lo; s0 < hi; s0 += kSeg) {
+    const int m = (int)((hi - s0) < kSeg ? (hi - s0) : kSeg);
+    __syncthreads();  // the previous segment's reads are done
+    if (m == kSeg && (s0 & 1) == 0) {
+      // whole segment: 32 independent 16-byte loads per lane in flight
+      // (a rolled load/divide/store loop would pay the full HBM latency per
+      // element pair)
+      const double2* src = reinterpret_cast<const double2*>(dmin + s0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double2 v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = src[(h * 16 + j) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int i = ((h * 16 + j) * 64 + lane) * 2;
+          sp[i + i / kSegSub] = v[j].x / S;
+          sp[i + 1 + (i + 1) / kSegSub] = v[j].y / S;
         }
       }
-      const long long Dq = (N & 1) ? D1 : D0;
-      const long long Nend = N + Dq;
-      bool ok = valid && slo < hi && Dq < (1ll << 52) && Nend < (1ll << 53);
-      bool hit = false;
-      if (ok && search) hit = (from_binade(e, Nend) / c_last) > u;
-      const unsigned long long okm = __ballot(ok && !hit);
-      // number of leading lanes that are ok and not yet past the target
-      L = (okm == ~0ull) ? 64 : __builtin_ctzll(~okm);
-      if (L > 0) {
-        const long long DL = __shfl(Dq, L - 1);
-        c = from_binade(e, N + DL);
-        pos += (int64_t)L * kSub;
-        if (pos > hi) pos = hi;
-      }
-      if (pos >= hi) break;
-      if (L == 64) continue;  // every sub-chunk applied: next bulk round
-    }
-    // element-wise over (at most) one sub-chunk; lane 0 computes, broadcasts
-    const int64_t ehi = (pos + kSub) < hi ? (pos + kSub) : hi;
-    double cc = c;
-    int64_t hitidx = -1;
-    if (lane == 0) {
-      for (int64_t i = pos; i < ehi; ++i) {
-        cc = cc + dmin[i] / S;
-        if (search && (cc / c_last) > u) {
-          hitidx = i;
-          break;
+    } else {
+      for (int i0 = 0; i0 < m; i0 += 64 * 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = i0 + j * 64 + lane;
+          v[j] = i < m ? dmin[s0 + i] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = i0 + j * 64 + lane;
+          if (i < m) sp[i + i / kSegSub] = v[j] / S;
         }
       }
     }
-    cc = __shfl(cc, 0);
-    hitidx = __shfl(hitidx, 0);
-    c = cc;
-    if (hitidx >= 0) {
-      *found = hitidx;
-      return c;
+    __syncthreads();
+    auto pv = [&](int i) { return sp[i + i / kSegSub]; };
+    int pos = 0;
+    while (pos < m) {
+      int e;
+      long long N;
+      const bool inb = binade_of(c, e, N);
+      int L = 0;  // sub-chunks applied in bulk
+      if (inb) {
+        const int slo = pos + lane * kSegSub;
+        const int shi = (slo + kSegSub) < m ? (slo + kSegSub) : m;
+        long long D0 = 0, D1 = 0;
+        int valid = 1;
+        if (slo < m)
+          range_transfer_v([&](int64_t i) { return pv((int)i); }, 1.0, slo, shi, e, D0, D1,
+                           valid);
+        else
+          valid = 0;
+        // inclusive ordered prefix over lanes
+        for (int o = 1; o < 64; o <<= 1) {
+          const long long l0 = __shfl_up(D0, o), l1 = __shfl_up(D1, o);
+          const int lv = __shfl_up(valid, o);
+          if (lane >= o) {
+            long long n0, n1;
+            compose(l0, l1, D0, D1, n0, n1);
+            D0 = n0;
+            D1 = n1;
+            valid &= lv;
+          }
+        }
+        const long long Dq = (N & 1) ? D1 : D0;
+        const long long Nend = N + Dq;
+        bool ok = valid && slo < m && Dq < (1ll << 52) && Nend < (1ll << 53);
+        bool hit = false;
+        if (ok && search) hit = (from_binade(e, Nend) / c_last) > u;
+        const unsigned long long okm = __ballot(ok && !hit);
+        // number of leading lanes that are ok and not yet past the target
+        L = (okm == ~0ull) ? 64 : __builtin_ctzll(~okm);
+        if (L > 0) {
+          const long long DL = __shfl(Dq, L - 1);
+          c = from_binade(e, N + DL);
+          pos += L * kSegSub;
+          if (pos > m) pos = m;
+        }
+        if (pos >= m) break;
+        if (L == 64) continue;  // every sub-chunk applied: next bulk round
+      }
+      // element-wise over (at most) one sub-chunk; lane 0 computes, broadcasts
+      const int ehi = (pos + kSegSub) < m ? (pos + kSegSub) : m;
+      double cc = c;
+      int hitidx = -1;
+      if (lane == 0) {
+        for (int i = pos; i < ehi; ++i) {
+          cc = cc + pv(i);
+          if (search && (cc / c_last) > u) {
+            hitidx = i;
+            break;
+          }
+        }
+      }
+      cc = __shfl(cc, 0);
+      hitidx = __shfl(hitidx, 0);
+      c = cc;
+      if (hitidx >= 0) {
+        *found = s0 + hitidx;
+        return c;
+      }
+      pos = ehi;
     }
-    pos = ehi;
   }
   return c;
 }
 
 // Single wave: exact running value through every block, cend[b] = value after
-// block b.  Whole 64-block chunks are applied at once when they stay inside
-// one binade.
+// block b.  Each round takes the next 64 blocks: the leading run of blocks
+// whose transfers apply in the current binade is applied at once (an ordered
+// prefix of the transfers), the first block that does not is done alone
+// (its transfer if it applies from the new value, else an element walk), and
+// the next round starts after it.
+constexpr int kXWin = 1024;  // block transfers staged in LDS per window (32 KB)
+
 __global__ __launch_bounds__(64) void walk_kernel(const double* __restrict__ dmin, int64_t n,
                                                   double S, const Xfer* __restrict__ xf,
                                                   int64_t nblocks, double c_in,
                                                   double* __restrict__ cend,
-                                                  double* __restrict__ c_out) {
+                                                  double* __restrict__ c_out,
+                                                  long long* __restrict__ stats) {
+  __shared__ Xfer sx[kXWin];
   const int lane = threadIdx.x;
   double c = c_in;
   int64_t dummy = -1;
-  for (int64_t b0 = 0; b0 < nblocks; b0 += 64) {
-    const int64_t b = b0 + lane;
+  int64_t b0 = 0;
+  int64_t win0 = -1;  // first block of the staged window
+  long long st_rounds = 0, st_single = 0, st_fine = 0, st_fcyc = 0;
+  const long long st_t0 = stats ? (long long)clock64() : 0;
+  while (b0 < nblocks) {
     const int nb = (int)((nblocks - b0) < 64 ? (nblocks - b0) : 64);
-    Xfer r = (b < nblocks) ? xf[b] : Xfer{0, 0, 0, 0, 0};
+    if (win0 < 0 || b0 + nb > win0 + kXWin) {
+      // restage [b0, b0 + kXWin): 16 independent loads per lane in flight
+      __syncthreads();
+      win0 = b0;
+      Xfer v[kXWin / 64];
+#pragma unroll
+      for (int j = 0; j < kXWin / 64; ++j) {
+        const int64_t bb = b0 + j * 64 + lane;
+        v[j] = bb < nblocks ? xf[bb] : Xfer{0, 0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int j = 0; j < kXWin / 64; ++j) sx[j * 64 + lane] = v[j];
+      __syncthreads();
+    }
+    const Xfer r = lane < nb ? sx[b0 - win0 + lane] : Xfer{0, 0, 0, 0, 0};
     int e;
     long long N;
     const bool inb = binade_of(c, e, N);
-    // bulk: inclusive prefix of the chunk's transfers
+    // inclusive ordered prefix of the round's transfers
     long long D0 = r.d0, D1 = r.d1;
-    int valid = (b < nblocks) && r.valid && inb && r.e == e;
+    int valid = (lane < nb) && r.valid && inb && r.e == e;
     for (int o = 1; o < 64; o <<= 1) {
       const long long l0 = __shfl_up(D0, o), l1 = __shfl_up(D1, o);
       const int lv = __shfl_up(valid, o);
@@ -387,56 +571,93 @@ __global__ __launch_bounds__(64) void walk_kernel(const double* __restrict__ dmi
     }
     const long long Dq = (N & 1) ? D1 : D0;
     const bool ok = inb && valid && Dq < (1ll << 52) && (N + Dq) < (1ll << 53);
-    const unsigned long long okm = __ballot(ok || lane >= nb);
-    if (okm == ~0ull) {
-      if (lane < nb) cend[b] = from_binade(e, N + Dq);
-      c = from_binade(e, N + __shfl(Dq, nb - 1));
+    const unsigned long long okm = __ballot(ok);
+    int L = (okm == ~0ull) ? 64 : __builtin_ctzll(~okm);
+    if (L > nb) L = nb;
+    if (L > 0) {
+      if (lane < L) cend[b0 + lane] = from_binade(e, N + Dq);
+      c = from_binade(e, N + __shfl(Dq, L - 1));
+    }
+    ++st_rounds;
+    if (L == nb) {
+      b0 += nb;
       continue;
     }
-    // block by block
-    for (int j = 0; j < nb; ++j) {
-      const int64_t bj = b0 + j;
-      const Xfer rj = xf[bj];
-      int ej;
-      long long Nj;
-      bool done = false;
-      if (binade_of(c, ej, Nj) && rj.valid && rj.e == ej) {
-        const long long Dj = (Nj & 1) ? rj.d1 : rj.d0;
-        if (Dj < (1ll << 52) && Nj + Dj < (1ll << 53)) {
-          c = from_binade(ej, Nj + Dj);
-          done = true;
-        }
+    ++st_single;
+    // block bj alone
+    const int64_t bj = b0 + L;
+    const Xfer rj = sx[bj - win0];
+    int ej;
+    long long Nj;
+    bool done = false;
+    if (binade_of(c, ej, Nj) && rj.valid && rj.e == ej) {
+      const long long Dj = (Nj & 1) ? rj.d1 : rj.d0;
+      if (Dj < (1ll << 52) && Nj + Dj < (1ll << 53)) {
+        c = from_binade(ej, Nj + Dj);
+        done = true;
       }
-      if (!done) {
-        const int64_t lo = bj * kSeedBlock;
-        const int64_t hi = (lo + kSeedBlock) < n ? (lo + kSeedBlock) : n;
-        c = fine_walk(dmin, S, lo, hi, c, false, 1.0, 0.0, &dummy);
-      }
-      if (lane == 0) cend[bj] = c;
     }
+    if (!done) {
+      const int64_t lo = bj * kSeedBlock;
+      const int64_t hi = (lo + kSeedBlock) < n ? (lo + kSeedBlock) : n;
+      const long long tf = stats ? (long long)clock64() : 0;
+      c = fine_walk(dmin, S, lo, hi, c, false, 1.0, 0.0, &dummy);
+      if (stats) st_fcyc += (long long)clock64() - tf;
+      ++st_fine;
+    }
+    if (lane == 0) cend[bj] = c;
+    b0 = bj + 1;
   }
   if (lane == 0) *c_out = c;
+  if (stats && lane == 0) {
+    stats[0] += st_rounds;
+    stats[1] += st_single;
+    stats[2] += st_fine;
+    stats[3] += st_fcyc;
+    stats[4] += (long long)clock64() - st_t0;
+  }
 }
 
-// Single wave: first local index m with fl(c_m / c_last) > u (or -1).
+// Single wave: first local index m with fl(c_m / c_last) > u (or -1).  The
+// running values cend are non-decreasing, so hit(b) = fl(cend[b] / c_last) > u
+// is monotone in b: a 64-ary search (64 probes per round) finds the first hit
+// block, then an exact walk of that block finds the element.
 __global__ __launch_bounds__(64) void search_kernel(const double* __restrict__ dmin, int64_t n,
                                                     double S, const double* __restrict__ cend,
                                                     int64_t nblocks, double c_in, double c_last,
                                                     double u, int64_t* __restrict__ result) {
   const int lane = threadIdx.x;
-  int64_t bstar = -1;
-  for (int64_t b0 = 0; b0 < nblocks && bstar < 0; b0 += 64) {
-    const int64_t b = b0 + lane;
-    const bool hit = b < nblocks && (cend[b] / c_last) > u;
+  // invariant: every block < lo misses, block hi hits (hi == nblocks: none)
+  int64_t lo = 0, hi = nblocks;
+  while (hi - lo > 0) {
+    const int64_t span = hi - lo;
+    const int64_t step = (span + 63) / 64;
+    const int64_t pb = lo + (int64_t)lane * step;
+    const bool probe = pb < hi;
+    const bool hit = probe && (cend[pb] / c_last) > u;
     const unsigned long long m = __ballot(hit);
-    if (m) bstar = b0 + __builtin_ctzll(m);
+    const unsigned long long pm = __ballot(probe);
+    if (step == 1) {
+      if (m) hi = lo + __builtin_ctzll(m);
+      break;
+    }
+    // first probing lane that hits: the answer is in (probe[j-1], probe[j]]
+    if (m) {
+      const int j = __builtin_ctzll(m);
+      hi = lo + (int64_t)j * step;
+      lo = j > 0 ? lo + (int64_t)(j - 1) * step + 1 : lo;
+    } else {
+      const int jl = 63 - __builtin_clzll(pm);  // last probe misses
+      lo = lo + (int64_t)jl * step + 1;
+    }
   }
+  const int64_t bstar = hi < nblocks ? hi : -1;
   int64_t found = -1;
   if (bstar >= 0) {
     const double c0 = bstar == 0 ? c_in : cend[bstar - 1];
-    const int64_t lo = bstar * kSeedBlock;
-    const int64_t hi = (lo + kSeedBlock) < n ? (lo + kSeedBlock) : n;
-    fine_walk(dmin, S, lo, hi, c0, true, c_last, u, &found);
+    const int64_t lo2 = bstar * kSeedBlock;
+    const int64_t hi2 = (lo2 + kSeedBlock) < n ? (lo2 + kSeedBlock) : n;
+    fine_walk(dmin, S, lo2, hi2, c0, true, c_last, u, &found);
   }
   if (lane == 0) *result = found;
 }
@@ -466,14 +687,40 @@ void seed_update(Ctx& c, const double* cen) {
   HIP_CHECK(hipMemcpyAsync(c.seed_scalar.p, cen, sizeof(double) * c.d, hipMemcpyHostToDevice,
                            c.stream));
   if (nb > 0) {
-    if (c.mode == CDR_MODE_F32X)
-      hipLaunchKernelGGL(seed_update_kernel<float>, dim3(nb), dim3(256), 0, c.stream,
-                         c.x32.as<float>(), c.n, c.n_pad, c.d, c.seed_scalar.as<double>(),
-                         c.dmin.as<double>(), c.blocksums.as<double>());
-    else
-      hipLaunchKernelGGL(seed_update_kernel<double>, dim3(nb), dim3(256), 0, c.stream,
-                         c.x64.as<double>(), c.n, c.n_pad, c.d, c.seed_scalar.as<double>(),
-                         c.dmin.as<double>(), c.blocksums.as<double>());
+    typedef void (*SeedFn)(const float*, int64_t, int64_t, int, const double*, double*, double*,
+                           int64_t);
+#define CDR_SU(D_) seed_update_kernel<float, D_, false>
+    static const SeedFn fns[17] = {CDR_SU(0),  CDR_SU(1),  CDR_SU(2),  CDR_SU(3),  CDR_SU(4),
+                                   CDR_SU(5),  CDR_SU(6),  CDR_SU(7),  CDR_SU(8),  CDR_SU(9),
+                                   CDR_SU(10), CDR_SU(11), CDR_SU(12), CDR_SU(13), CDR_SU(14),
+                                   CDR_SU(15), CDR_SU(16)};
+#undef CDR_SU
+    const int64_t nfull = c.n / kSeedBlock;
+    const bool f32 = c.mode == CDR_MODE_F32X;
+    if (nfull > 0) {
+      if (f32)
+        hipLaunchKernelGGL(fns[c.d <= 16 ? c.d : 0], dim3(nfull), dim3(256), 0, c.stream,
+                           c.x32.as<float>(), c.n, c.n_pad, c.d, c.seed_scalar.as<double>(),
+                           c.dmin.as<double>(), c.blocksums.as<double>(), (int64_t)0);
+      else
+        hipLaunchKernelGGL((seed_update_kernel<double, 0, false>), dim3(nfull), dim3(256), 0,
+                           c.stream, c.x64.as<double>(), c.n, c.n_pad, c.d,
+                           c.seed_scalar.as<double>(), c.dmin.as<double>(),
+                           c.blocksums.as<double>(), (int64_t)0);
+      HIP_CHECK(hipGetLastError());
+    }
+    if (nb > nfull) {
+      if (f32)
+        hipLaunchKernelGGL((seed_update_kernel<float, 0, true>), dim3(1), dim3(256), 0,
+                           c.stream, c.x32.as<float>(), c.n, c.n_pad, c.d,
+                           c.seed_scalar.as<double>(), c.dmin.as<double>(),
+                           c.blocksums.as<double>(), nfull);
+      else
+        hipLaunchKernelGGL((seed_update_kernel<double, 0, true>), dim3(1), dim3(256), 0,
+                           c.stream, c.x64.as<double>(), c.n, c.n_pad, c.d,
+                           c.seed_scalar.as<double>(), c.dmin.as<double>(),
+                           c.blocksums.as<double>(), nfull);
+    }
     HIP_CHECK(hipGetLastError());
   }
   c.seed_scanned = false;
@@ -497,8 +744,27 @@ void seed_scan(Ctx& c, double total, double c_in, double* c_out) {
   HIP_CHECK(hipGetLastError());
   c.seed_scalar.ensure(sizeof(double) * (c.d + 8));
   double* dres = c.seed_scalar.as<double>() + c.d;
+  static const bool want_stats = std::getenv("CDR_SEED_STATS") != nullptr;
+  long long* dstats = nullptr;
+  if (want_stats) {
+    static long long* ds = nullptr;
+    if (!ds) {
+      HIP_CHECK(hipMalloc(&ds, 8 * sizeof(long long)));
+      HIP_CHECK(hipMemset(ds, 0, 8 * sizeof(long long)));
+    }
+    dstats = ds;
+  }
   hipLaunchKernelGGL(walk_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
-                     total, c.xfer.as<Xfer>(), nb, c_in, c.cend.as<double>(), dres);
+                     total, c.xfer.as<Xfer>(), nb, c_in, c.cend.as<double>(), dres, dstats);
+  if (want_stats) {
+    long long hs[8];
+    HIP_CHECK(hipMemcpyAsync(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    fprintf(stderr,
+            "seed walk stats (cumulative): rounds %lld single %lld fine %lld nb %lld "
+            "fine_cycles %lld total_cycles %lld\n",
+            hs[0], hs[1], hs[2], (long long)nb, hs[3], hs[4]);
+  }
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipMemcpyAsync(c_out, dres, sizeof(double), hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));

@@ -226,3 +226,40 @@ def test_incremental_update_equals_full_recompute(ctx, n, d, k, monkeypatch):
         C = np.where(cnt[:, None] > 0, means, C)
         if step == 2:  # reseed the empty cluster onto a point, as the reference does
             C[-1] = X[12345 % n]
+
+
+@pytest.mark.parametrize("n,outlier", [(3_000_001, False), (1_200_000, True)])
+def test_seeding_many_blocks_vs_oracle(ctx, n, outlier):
+    """Seeding over hundreds of 8192-blocks: the block-transfer walk crosses
+    binades between blocks and inside them, and the 64-ary block search runs
+    several rounds.  The outlier case makes one D^2 dominate (tiny
+    probabilities everywhere else, many crossings in the first blocks)."""
+    import kmeans_plusplus as kp
+
+    X = synth.generate(n, 0, n, 16, 8, 77 + n)
+    if outlier:
+        X[n // 3] = 64.0
+    init = kp.kmeans_plusplus_init(X, 8, random_state=7, context=ctx)
+    np.testing.assert_array_equal(init, ko.kmeans_plusplus_init(X, 8, random_state=7))
+
+
+@pytest.mark.parametrize("n,d", [(8192 * 37 + 1234, 16), (8192 * 5, 5), (5000, 16), (8192 * 3 + 1, 20)])
+def test_seed_block_sums_and_scan_exact(ctx, n, d):
+    """Per-block D^2 sums are NumPy's pairwise add.reduce of each 8192 chunk,
+    the total is dist_sq.sum(), and the device scan's last running value is
+    np.cumsum(dist_sq / total)[-1] — all bit-exact (kmeans_plusplus.py:14-19)."""
+    import _cdr
+
+    X = synth.generate(n, 0, n, d, 8, 1000 + n + d)
+    ctx.load_points(X)
+    ctx.seed_reset()
+    dist = np.full(n, np.inf)
+    for c in (X[3], X[n // 2], X[n - 1]):
+        ctx.seed_update(c)
+        dist = np.minimum(dist, np.sqrt(ko.sqdist_rows(X, c)) ** 2)
+        bs = ctx.seed_block_sums()
+        want = np.array([np.add.reduce(dist[i:i + 8192]) for i in range(0, n, 8192)])
+        np.testing.assert_array_equal(bs, want)
+        total = _cdr.host_seq_sum(bs)
+        assert total == dist.sum()
+        assert ctx.seed_scan(total, 0.0) == np.cumsum(dist / total)[-1]
