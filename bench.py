@@ -86,9 +86,11 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="3", choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=0, help="override n_total (testing only)")
+    ap.add_argument("--n-total", type=int, default=0, help="override n_total (testing only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
+    ap.add_argument("--rccl", action="store_true",
+                    help="use torch.distributed (RCCL) even at WORLD_SIZE=1 (path testing)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,7 +98,7 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = None
-    if world > 1:
+    if world > 1 or args.rccl:
         import torch  # first: libcdr then binds to torch's HIP runtime
         import torch.distributed as tdist
 
@@ -111,8 +113,8 @@ def main() -> None:
     from cdr_dist import Comm, ShardedLloyd, seed_sharded, shard_rows
 
     n_total, d, k, desc = CONFIGS[args.config]
-    if args.n:
-        n_total = args.n
+    if args.n_total:
+        n_total = args.n_total
     begin, n_local = shard_rows(n_total, world, rank)
     comm = Comm(dist, device)
     ctx = _cdr.Context(local_rank)
@@ -135,9 +137,14 @@ def main() -> None:
     comm.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
+    marks = []
     for _ in range(args.steps):
         C, shift = lloyd.step(C, lloyd.row)
+        marks.append(time.perf_counter())
     ctx.synchronize()
+    if os.environ.get("CDR_BENCH_STEP_TIMES"):
+        dts = np.diff([t0] + marks) * 1e3
+        print("step ms:", " ".join(f"{v:.3f}" for v in dts), file=sys.stderr)
     comm.barrier()
     elapsed = time.perf_counter() - t0
     prof = ctx.profile_read()

@@ -51,6 +51,8 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 struct S32Args {
   const float* X;
+  const float* X0;     // original points (x32): the exact fallback reads them
+  const double* cent;  // k x d fp64 centroids (the exact fallback)
   int64_t n, n_pad;
   int d, k, Q;         // Q = number of stored feature quads (d4 / 4)
   const h8* frag;      // [MT][2][64]: A1, A3
@@ -107,6 +109,108 @@ __device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
 
 }  // namespace
 
+// Exact assignment of the points the screen could not certify, run by the
+// wave that found them after its last group (its region of the fallback
+// list; the LDS table is still live, so no global read-modify-write and no
+// extra launch).  4 lanes per point, 16 points per pass: lane c walks the
+// centroids c, c + 4, c + 8, ... (fp64 rows staged in LDS with stride 17
+// doubles) computing the NumPy-order fp64 squared distance and its correctly
+// rounded sqrt and keeping the first minimum of its roots; the 4 candidates
+// merge on (root, index) — np.argmin of np.linalg.norm, first index on ties
+// (src/kmeans_plusplus.py:33-34).  The point's change goes into the table.
+// Loads run ahead of the arithmetic: list entries two passes, the points'
+// feature quads one pass.
+template <int D>
+__device__ __forceinline__ void fallback_points(const S32Args& a, const int32_t* region, int cnt,
+                                                double* tsum, int* tcnt, const double* cs,
+                                                int KP, bool delta, bool pre) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 2, c4 = lane & 3;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int Q = (D + 3) / 4;
+  const f4* X4 = reinterpret_cast<const f4*>(a.X0);
+  __threadfence_block();  // the region was just written by this wave's lanes
+  auto load_pt = [&](int e) -> int32_t { return e < cnt ? region[e] : 0; };
+  auto load_x = [&](int32_t pt, f4 (&v)[Q]) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = X4[(int64_t)q * a.n_pad + pt];
+  };
+  int32_t pt0 = load_pt(g), pt1 = load_pt(16 + g);
+  f4 x0[Q];
+  load_x(pt0, x0);
+  for (int e0 = 0; e0 < cnt; e0 += 16) {
+    const int e = e0 + g;
+    const bool live = e < cnt;
+    const int32_t pt = pt0;
+    double x[D];
+#pragma unroll
+    for (int f = 0; f < D; ++f) x[f] = (double)x0[f >> 2][f & 3];
+    if (e0 + 16 < cnt) {  // wave-uniform
+      pt0 = pt1;
+      load_x(pt0, x0);
+      pt1 = load_pt(e0 + 32 + g);
+    }
+    double sb = INFINITY, rb = INFINITY;
+    int jmin = 0x7fffffff;
+    for (int j = c4; j < a.k; j += 4) {
+      const double* cj = cs + j * 17;
+      const double s = np_sqdist([&](int f) { return x[f]; }, [&](int f) { return cj[f]; }, D);
+      // sqrt is monotone: a root can only undercut the best root when s < sb,
+      // and then the roots decide (strict: first index on ties of the roots)
+      if (s < sb) {
+        const double r2 = sqrt(s);
+        sb = s;
+        if (r2 < rb) {
+          rb = r2;
+          jmin = j;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 2; o > 0; o >>= 1) {
+      const double ro = __shfl_xor(rb, o, 4);
+      const int jo = __shfl_xor(jmin, o, 4);
+      if (ro < rb || (ro == rb && jo < jmin)) {
+        rb = ro;
+        jmin = jo;
+      }
+    }
+    if (live && c4 == 0) {
+      if (jmin >= a.k) jmin = 0;  // every root NaN: np.argmin of all-NaN is 0
+      const int old = delta ? a.labels[pt] : -1;  // the screen left it untouched
+      if (jmin != old) {
+        a.labels[pt] = jmin;
+        if (pre) {  // the tables hold xt = (x - mu) 2^sigma (exact)
+#pragma unroll
+          for (int f = 0; f < D; ++f) x[f] = (double)fmaf((float)x[f], a.sig, a.mu_s[f]);
+        }
+#pragma unroll
+        for (int f = 0; f < D; ++f) atomicAdd(&tsum[f * KP + jmin], x[f]);
+        atomicAdd(&tcnt[jmin], 1);
+        if (old >= 0) {
+#pragma unroll
+          for (int f = 0; f < D; ++f) atomicAdd(&tsum[f * KP + old], -x[f]);
+          atomicAdd(&tcnt[old], -1);
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void fallback_tail(const S32Args& a, const int32_t* region, int cnt,
+                                           double* tsum, int* tcnt, const double* cs, int KP,
+                                           bool delta, bool pre) {
+  switch (a.d) {
+#define CDR_FBT(D_) \
+  case D_: fallback_points<D_>(a, region, cnt, tsum, tcnt, cs, KP, delta, pre); break;
+    CDR_FBT(1) CDR_FBT(2) CDR_FBT(3) CDR_FBT(4) CDR_FBT(5) CDR_FBT(6) CDR_FBT(7) CDR_FBT(8)
+    CDR_FBT(9) CDR_FBT(10) CDR_FBT(11) CDR_FBT(12) CDR_FBT(13) CDR_FBT(14) CDR_FBT(15)
+    CDR_FBT(16)
+#undef CDR_FBT
+    default: break;
+  }
+}
+
 // QH: feature quads per lane half (1: d <= 8, 2: d <= 16); MT: 32-centroid
 // tiles (1: k <= 32, 2: k <= 64).
 // FULLQ: all 2*QH quads of the lane halves exist in memory (d4 == 8 QH).
@@ -125,8 +229,11 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
   constexpr int NF = 8 * QH;
   double* tsum = reinterpret_cast<double*>(smem);                      // [NF][KP]
   int* tcnt = reinterpret_cast<int*>(tsum + (size_t)NF * KP);          // [KP]
+  double* cs = reinterpret_cast<double*>(tcnt + KP);                   // [k][17]
   for (int i = threadIdx.x; i < NF * KP; i += blockDim.x) tsum[i] = 0.0;
   for (int i = threadIdx.x; i < KP; i += blockDim.x) tcnt[i] = 0;
+  for (int i = threadIdx.x; i < a.k * a.d; i += blockDim.x)
+    cs[(i / a.d) * 17 + i % a.d] = a.cent[i];
 
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
@@ -405,21 +512,25 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
     a.fb_count[wave_id] = fb_used;
     if (fb_used) atomicAdd(a.fb_count + gstride, fb_used);
   }
+  if constexpr ((ABL & 1) == 0) {
+    if (fb_used) fallback_tail(a, fb_region, fb_used, tsum, tcnt, cs, KP, DELTA, PRE);
+  }
   __syncthreads();
   double* dst = a.partials + (size_t)blockIdx.x * (NF + 1) * KP;
   for (int i = threadIdx.x; i < NF * KP; i += blockDim.x) dst[i] = tsum[i];
   for (int i = threadIdx.x; i < KP; i += blockDim.x) dst[NF * KP + i] = (double)tcnt[i];
 }
 
-// Exact assignment of the points the screen did not certify: one THREAD per
+// Exact assignment of the points the screen did not certify: 16 lanes per
 // point (the 256 threads of workgroup b share the points of the screen's
 // fallback regions 4b..4b+3, so a crowded region is spread over the whole
-// workgroup).  Each thread walks the k centroids (staged transposed, [d][k],
-// in LDS: every lane reads the same word, a broadcast) computing the
-// NumPy-order fp64 squared distance and its correctly rounded sqrt, and keeps
-// the first minimum of the roots — np.argmin of np.linalg.norm
-// (src/kmeans_plusplus.py:33-34).  Changes go into partial table b.
-// k <= 64, d = D <= 16 (compile time: the point lives in registers).
+// workgroup).  Lane c of a point's 16 walks centroids c, c + 16, c + 32, ...
+// (rows staged in LDS with a pad double: the 16 rows of a group sit in 16
+// different bank pairs) computing the NumPy-order fp64 squared distance and
+// its correctly rounded sqrt, keeping the first minimum of its roots; the 16
+// candidates are merged on (root, index) — np.argmin of np.linalg.norm, first
+// index on ties (src/kmeans_plusplus.py:33-34).  Changes go into partial
+// table b.  k <= 64, d = D <= 16 (compile time: the point lives in registers).
 template <int D>
 __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, int64_t n_pad,
                                                   int Q, const double* __restrict__ C,
@@ -429,7 +540,8 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
                                                   double* __restrict__ partials, int delta,
                                                   const float* __restrict__ pre_ms, float sig) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int d4 = Q;  // table rows (NF of the screen)
+  constexpr int CS = D + 1;  // staged centroid row stride (doubles)
+  const int d4 = Q;          // table rows (NF of the screen)
   const int reg0 = blockIdx.x * (blockDim.x >> 6);
   int cnt[4], tot = 0;
 #pragma unroll
@@ -440,21 +552,28 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
   if (tot == 0) return;  // uniform: nothing to add to this workgroup's table
   double* tsum = reinterpret_cast<double*>(smem);  // [d4][KP]
   int* tcnt = reinterpret_cast<int*>(tsum + (size_t)d4 * KP);
+  double* cs = reinterpret_cast<double*>(tcnt + KP + (KP & 1));  // [k][CS]
   for (int i = threadIdx.x; i < d4 * KP; i += blockDim.x) tsum[i] = 0.0;
   for (int i = threadIdx.x; i < KP; i += blockDim.x) tcnt[i] = 0;
+  for (int i = threadIdx.x; i < k * D; i += blockDim.x) cs[(i / D) * CS + i % D] = C[i];
   __syncthreads();
-  for (int e = threadIdx.x; e < tot; e += blockDim.x) {
-    int r = 0, i = e;
-    while (i >= cnt[r]) i -= cnt[r++];
-    const int64_t pt = list[(size_t)(reg0 + r) * cap + i];
+  const int c16 = threadIdx.x & 15;
+  for (int e0 = 0; e0 < tot; e0 += 16) {
+    const int e = e0 + (threadIdx.x >> 4);
+    const bool live = e < tot;
+    int64_t pt = 0;
+    if (live) {
+      int r = 0, i = e;
+      while (i >= cnt[r]) i -= cnt[r++];
+      pt = list[(size_t)(reg0 + r) * cap + i];
+    }
     double x[D];
 #pragma unroll
-    for (int f = 0; f < D; ++f) x[f] = (double)X[xidx(f, pt, n_pad)];
-    // centroid j is wave-uniform: its row comes through scalar loads
+    for (int f = 0; f < D; ++f) x[f] = live ? (double)X[xidx(f, pt, n_pad)] : 0.0;
     double sb = INFINITY, rb = INFINITY;
-    int jmin = 0;
-    for (int j = 0; j < k; ++j) {
-      const double* cj = C + (size_t)j * D;
+    int jmin = 0x7fffffff;
+    for (int j = c16; j < k; j += 16) {
+      const double* cj = cs + j * CS;
       const double s = np_sqdist([&](int f) { return x[f]; }, [&](int f) { return cj[f]; }, D);
       // sqrt is monotone: a root can only undercut the best root when s < sb,
       // and then the roots decide (strict: first index on ties of the roots)
@@ -467,6 +586,18 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
         }
       }
     }
+    // merge the 16 lanes of the point: smaller root, then smaller index
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const double ro = __shfl_xor(rb, o, 16);
+      const int jo = __shfl_xor(jmin, o, 16);
+      if (ro < rb || (ro == rb && jo < jmin)) {
+        rb = ro;
+        jmin = jo;
+      }
+    }
+    if (!live || c16 != 0) continue;
+    if (jmin >= k) jmin = 0;  // every root NaN: np.argmin of all-NaN is 0
     const int old = delta ? labels[pt] : -1;  // not yet overwritten by the screen
     if (jmin != old) {
       labels[pt] = jmin;
@@ -557,6 +688,13 @@ struct Plan32 {
 };
 
 extern int lloyd_num_cus(int device);
+
+// dst[i] = src[i] for 16-byte words; src is mapped pinned host memory.
+__global__ __launch_bounds__(256) void pull_host_kernel(const uint4* __restrict__ src,
+                                                        uint4* __restrict__ dst, int64_t n16) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) dst[i] = src[i];
+}
 
 // Shapes and data this kernel covers: F32X points, d <= 16, k <= 64, and every
 // per-workgroup fp64 sum exact: |x| 2^S < 2^30 (F32X) and a workgroup sees at
@@ -698,12 +836,23 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   const size_t b_cent = sizeof(double) * (size_t)k * c.d;
   const size_t b_all = b_frag + b_cinit + b_cent;
   if (c.up_pending) HIP_CHECK(hipEventSynchronize(c.up_event));
-  c.h_up.ensure(b_all);
+  c.h_up.ensure((b_all + 15) / 16 * 16);
   memcpy(c.h_up.p, pl.frag.data(), b_frag);
   memcpy(static_cast<char*>(c.h_up.p) + b_frag, pl.cinit.data(), b_cinit);
   memcpy(static_cast<char*>(c.h_up.p) + b_frag + b_cinit, C, b_cent);
-  c.frag.ensure(b_all);
-  HIP_CHECK(hipMemcpyAsync(c.frag.p, c.h_up.p, b_all, hipMemcpyHostToDevice, c.stream));
+  c.frag.ensure((b_all + 15) / 16 * 16);
+  // the device pulls the staging buffer itself (pinned, mapped host memory)
+  // with one small kernel on the stream: no DMA-engine copy in the step (a
+  // runtime H2D copy here stalled the host for 7-16 ms once per run)
+  {
+    void* hdev = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer(&hdev, c.h_up.p, 0));
+    const int64_t n16 = (int64_t)((b_all + 15) / 16);
+    hipLaunchKernelGGL(pull_host_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0,
+                       c.stream, static_cast<const uint4*>(hdev), static_cast<uint4*>(c.frag.p),
+                       n16);
+    HIP_CHECK(hipGetLastError());
+  }
   if (!c.up_event) HIP_CHECK(hipEventCreateWithFlags(&c.up_event, hipEventDisableTiming));
   HIP_CHECK(hipEventRecord(c.up_event, c.stream));
   c.up_pending = true;
@@ -711,7 +860,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   float* dcinit = reinterpret_cast<float*>(static_cast<char*>(c.frag.p) + b_frag);
   const double* dcent =
       reinterpret_cast<const double*>(static_cast<char*>(c.frag.p) + b_frag + b_cinit);
-  const size_t lds = (size_t)NF * KP * 8 + (size_t)KP * 4;
+  const size_t lds = (size_t)NF * KP * 8 + (size_t)KP * 4 + (size_t)k * 17 * 8;
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
   const int bpc = s32_blocks_per_cu(pl.QH, pl.MT, lds);
@@ -742,6 +891,8 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   }
   S32Args a;
   a.X = pre ? c.xt32.as<float>() : c.x32.as<float>();
+  a.X0 = c.x32.as<float>();
+  a.cent = dcent;
   a.n = c.n;
   a.n_pad = c.n_pad;
   a.d = d;
@@ -795,22 +946,6 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
 #undef CDR_S32
   HIP_CHECK(hipGetLastError());
   if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
-  const size_t fb_lds = lds;
-  {
-    typedef void (*FbFn)(const float*, int64_t, int, const double*, int, const int32_t*,
-                         const int32_t*, int, int, int32_t*, double*, int, const float*, float);
-    static const FbFn fb_fns[17] = {nullptr,        fallback32<1>,  fallback32<2>,  fallback32<3>,
-                                    fallback32<4>,  fallback32<5>,  fallback32<6>,  fallback32<7>,
-                                    fallback32<8>,  fallback32<9>,  fallback32<10>, fallback32<11>,
-                                    fallback32<12>, fallback32<13>, fallback32<14>, fallback32<15>,
-                                    fallback32<16>};
-    hipLaunchKernelGGL(fb_fns[d], grid, blk, fb_lds, c.stream, c.x32.as<float>(), c.n_pad, NF,
-                       dcent, k, c.fb_list.as<int32_t>(),
-                       c.fb_count.as<int32_t>(), cap, KP, c.labels.as<int32_t>(),
-                       c.partials.as<double>(), delta ? 1 : 0,
-                       pre ? c.mu_s.as<float>() : nullptr, (float)std::ldexp(1.0, c.sigma));
-  }
-  HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(reduce32, dim3((len + 63) / 64, kR32Slices), dim3(256), 0, c.stream,
                      c.partials.as<double>(), nwg, k, d, NF, KP,
                      std::ldexp(1.0, c.scale_bits - (pre ? c.sigma : 0)),
