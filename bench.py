@@ -11,7 +11,12 @@ SUM all-reduce of the k x (d+1) int64 partials, host means / empty-cluster
 reseed / shift — nothing skipped.  Inputs are generated on the device
 (synthetic, oracle/synth.py formula) and resident in HBM before timing; the
 initial centroids come from the sharded k-means++ seeding (timed separately,
-`seed_s`).  Total work is fixed (100M points) as N grows: "scaling": "strong".
+`seed_s`).  Default "scaling": "weak": every rank holds its own 100M-point
+shard of an N x 100M data set (the points partition; the only exchange is
+the k x (d+1) all-reduce).  `--scaling strong` keeps 100M points in total.
+
+stdout carries exactly one JSON line (rank 0): native libraries that print
+banners (RCCL) are pointed at stderr.
 
 roofline: the dominant kernel is the screen kernel (assign + fused update);
 algorithmic bytes per launch = n_local * (4*d + 4) (read the fp32 point, write
@@ -86,12 +91,17 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="3", choices=sorted(CONFIGS))
-    ap.add_argument("--n-total", type=int, default=0, help="override n_total (testing only)")
+    ap.add_argument("--n-total", type=int, default=0,
+                    help="override the per-config point count (testing only)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: n points per rank (N x n in total); strong: n in total")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
     ap.add_argument("--rccl", action="store_true",
                     help="use torch.distributed (RCCL) even at WORLD_SIZE=1 (path testing)")
     args = ap.parse_args()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)  # RCCL prints its banner on stdout; keep stdout for the JSON line
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -112,9 +122,12 @@ def main() -> None:
     import _cdr
     from cdr_dist import Comm, ShardedLloyd, seed_sharded, shard_rows
 
-    n_total, d, k, desc = CONFIGS[args.config]
+    n_cfg, d, k, desc = CONFIGS[args.config]
     if args.n_total:
-        n_total = args.n_total
+        n_cfg = args.n_total
+    n_total = n_cfg * world if args.scaling == "weak" else n_cfg
+    if args.scaling == "weak" and world > 1:
+        desc += f" per GPU ({world} x {n_cfg} points in total)"
     begin, n_local = shard_rows(n_total, world, rank)
     comm = Comm(dist, device)
     ctx = _cdr.Context(local_rank)
@@ -172,7 +185,7 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device generator, oracle/synth.py formula; 2^-24-grid blobs)",
@@ -192,7 +205,7 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(d, k, args.seed)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

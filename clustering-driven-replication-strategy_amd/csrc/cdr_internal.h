@@ -131,6 +131,8 @@ struct Ctx {
   double prof_screen_ms = 0.0, prof_step_ms = 0.0, prof_fb_points = 0.0;
   int64_t prof_launches = 0;
   char prof_kernel[96] = {0};  // name of the last screen kernel launched
+  int fb_layout = -1;     // screen32: nwaves the fb_count buffer was zeroed for
+  int fb_total_slot = 0;  // fb_count index holding the last step's fallback total
   int32_t last_k = 0;
   bool have_labels = false;
   bool last_screened = false;

@@ -1010,8 +1010,9 @@ float* g_dbg_ptr = nullptr;  // set by cdr_debug_screen (tests only)
 float g_dbg_thr[2] = {0.f, 0.f};
 
 bool screen32_supported(const Ctx& c, int k);
-bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, float* dbg,
-                   float* thr_out);
+bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof);
+bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* hout, bool prof,
+                   float* dbg, float* thr_out);
 
 // Fold the last step's event pair into the profile accumulators.
 void prof_collect(Ctx& c) {
@@ -1045,8 +1046,12 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   bool screened = false;
   // screen32 uploads its own operands (one pinned copy) and leaves the totals
   // in c.run_sums; it copies them to a device `out` itself
+  // host path: screen32 publishes the sums and the fallback total straight
+  // into mapped pinned memory (h_small)
+  if (!out_dev) c.h_small.ensure(sizeof(long long) * (len + 1) + 64);
   bool s32 = screen32_supported(c, k) &&
-             screen32_step(c, C, k, out_dev ? dout : nullptr, prof, g_dbg_ptr,
+             screen32_step(c, C, k, out_dev ? dout : nullptr,
+                           out_dev ? nullptr : c.h_small.as<long long>(), prof, g_dbg_ptr,
                            g_dbg_ptr ? g_dbg_thr : nullptr);
   if (!s32) {
     upload_centroids(c, C, k);
@@ -1082,6 +1087,8 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     c.fb_count.ensure(sizeof(int32_t) * (nwaves + 1));
     HIP_CHECK(hipMemsetAsync(c.fb_count.p, 0, sizeof(int32_t) * (nwaves + 1), c.stream));
     c.fb_regions = nwaves;
+    c.fb_total_slot = nwaves;
+    c.fb_layout = -1;  // screen32 must re-zero its counter layout
     ScreenArgs a;
     a.X = c.x32.as<float>();
     a.n = c.n;
@@ -1140,6 +1147,8 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
                        c.stream, c.partials.as<long long>(), nwg, len, d,
                        KS, reinterpret_cast<unsigned long long*>(dout));
     HIP_CHECK(hipGetLastError());
+  } else if (big_step(c, C, k, dout, prof)) {
+    screened = true;  // large k / d: screen_big levels + update_big
   } else {
     c.run_valid = false;
     // exact assignment for every point, then fixed-point sums from labels
@@ -1168,17 +1177,21 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   c.last_k = k;
   c.have_labels = true;
   if (!out_dev) {
-    c.h_small.ensure(sizeof(long long) * len + 64);
-    const void* src = s32 ? c.run_sums.p : (const void*)dout;
-    HIP_CHECK(hipMemcpyAsync(c.h_small.p, src, sizeof(long long) * len,
-                             hipMemcpyDeviceToHost, c.stream));
-    int32_t* hfb = reinterpret_cast<int32_t*>(c.h_small.as<long long>() + len);
-    *hfb = 0;
-    if (screened)
-      HIP_CHECK(hipMemcpyAsync(hfb, c.fb_count.as<int32_t>() + c.fb_regions, sizeof(int32_t),
+    int32_t fb = 0;
+    if (s32) {
+      HIP_CHECK(hipStreamSynchronize(c.stream));
+      fb = (int32_t)c.h_small.as<long long>()[len];
+    } else {
+      HIP_CHECK(hipMemcpyAsync(c.h_small.p, dout, sizeof(long long) * len,
                                hipMemcpyDeviceToHost, c.stream));
-    HIP_CHECK(hipStreamSynchronize(c.stream));
-    const int32_t fb = *hfb;
+      int32_t* hfb = reinterpret_cast<int32_t*>(c.h_small.as<long long>() + len);
+      *hfb = 0;
+      if (screened)
+        HIP_CHECK(hipMemcpyAsync(hfb, c.fb_count.as<int32_t>() + c.fb_total_slot,
+                                 sizeof(int32_t), hipMemcpyDeviceToHost, c.stream));
+      HIP_CHECK(hipStreamSynchronize(c.stream));
+      fb = *hfb;
+    }
     memcpy(out, c.h_small.p, sizeof(long long) * len);
     c.last_fallback = screened ? fb : c.n;
     if (c.prof_pending) c.prof_fb_points += fb;
@@ -1279,7 +1292,7 @@ int cdr_lloyd_stats(cdr_ctx* h, int64_t* n_fallback) {
     HIP_CHECK(hipSetDevice(c.device));
     int32_t fb = 0;
     if (c.last_screened)
-      HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.as<int32_t>() + c.fb_regions, sizeof(int32_t),
+      HIP_CHECK(hipMemcpyAsync(&fb, c.fb_count.as<int32_t>() + c.fb_total_slot, sizeof(int32_t),
                                hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
     c.last_fallback = c.last_screened ? fb : c.n;

@@ -625,39 +625,65 @@ __global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, i
     if (tcnt[i]) dst[d4 * KP + i] += (double)tcnt[i];
 }
 
-// out (k, d+1) int64 = sum over workgroups of the exact fixed-point values.
-// Block (x, y): 64 outputs, the y-th slice of the workgroups.
-constexpr int kR32Slices = 16;
+// out (k, d+1) int64 += sum over workgroups of the exact fixed-point values
+// (the step's changes).  Block (x, y): 64 consecutive table cells (row r =
+// feature or count, column j: coalesced over j) of the y-th slice of the
+// workgroups.
 // With the pre-centred copy (muf != null) the table sums are of xt = (x - mu)
 // 2^sigma: sum x 2^S = sum xt 2^(S - sigma) + count mu 2^S, both exact.
+constexpr int kR32Slices = 16;
 __global__ __launch_bounds__(256) void reduce32(const double* __restrict__ part, int nwg, int k,
                                                 int d, int d4, int KP, double fx,
                                                 const long long* __restrict__ muf,
                                                 unsigned long long* __restrict__ out) {
   __shared__ long long red[4][64];
-  const int len = k * (d + 1);
-  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int cells = k * (d + 1);
+  const int u = blockIdx.x * 64 + (threadIdx.x & 63);
   const int sub = threadIdx.x >> 6;
   const int per = (nwg + kR32Slices - 1) / kR32Slices;
   const int w0 = blockIdx.y * per, w1 = min(nwg, w0 + per);
   long long s = 0;
-  if (e < len) {
-    const int j = e / (d + 1), f = e % (d + 1);
-    const int src = (f < d ? f : d4) * KP + j;
+  int e = 0;
+  if (u < cells) {
+    const int r = u / k, j = u - r * k;  // r < d: feature r, r == d: count
+    e = j * (d + 1) + r;
+    const int src = (r < d ? r : d4) * KP + j;
     const size_t stride = (size_t)(d4 + 1) * KP;
-    const long long mf = (muf && f < d) ? muf[f] : 0;
+    const long long mf = (muf && r < d) ? muf[r] : 0;
     for (int w = w0 + sub; w < w1; w += 4) {
       const double v = part[(size_t)w * stride + src];
-      s += f < d ? __double2ll_rn(v * fx) : __double2ll_rn(v);
+      s += r < d ? __double2ll_rn(v * fx) : __double2ll_rn(v);
       if (mf) s += __double2ll_rn(part[(size_t)w * stride + (size_t)d4 * KP + j]) * mf;
     }
   }
   red[sub][threadIdx.x & 63] = s;
   __syncthreads();
-  if (sub == 0 && e < len) {
+  if (sub == 0 && u < cells) {
     const long long t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
                         red[3][threadIdx.x];
     if (t) atomicAdd(&out[e], (unsigned long long)t);
+  }
+}
+
+// One block after reduce32 (the kernel boundary orders it after every
+// block's atomics): out -> dout (device, for the all-reduce) and/or hout
+// (mapped pinned host memory, with the fallback total at hout[cells]); the
+// screen's fallback counter fbc[nwaves] moves to fbc[nwaves + 1] and is
+// cleared for the next step — replaces a memset and up to three copies.
+__global__ __launch_bounds__(256) void publish32(const long long* __restrict__ out, int cells,
+                                                 long long* __restrict__ dout,
+                                                 long long* __restrict__ hout,
+                                                 int* __restrict__ fbc, int nwaves) {
+  for (int i = threadIdx.x; i < cells; i += blockDim.x) {
+    const long long v = out[i];
+    if (dout) dout[i] = v;
+    if (hout) hout[i] = v;
+  }
+  if (threadIdx.x == 0) {
+    const int fb = fbc[nwaves];
+    fbc[nwaves] = 0;
+    fbc[nwaves + 1] = fb;
+    if (hout) hout[cells] = fb;
   }
 }
 
@@ -809,10 +835,29 @@ static int s32_blocks_per_cu(int QH, int MT, size_t lds) {
   return nb > 8 ? 8 : nb;
 }
 
+// Build the exact pre-centred copy xt = (x - mu) 2^sigma once per point set
+// (Ctx::pre_ok) and the int64 mu 2^S that restores x sums from xt sums.
+void ensure_precentered(Ctx& c) {
+  if (!c.pre_ok || c.xt_valid) return;
+  const int d = c.d;
+  c.xt32.ensure(sizeof(float) * (size_t)d4_of(d) * c.n_pad);
+  hipLaunchKernelGGL(precenter_kernel, dim3(4096), dim3(256), 0, c.stream, c.x32.as<float>(),
+                     c.n, c.n_pad, d, c.mu_s.as<float>(), (float)std::ldexp(1.0, c.sigma),
+                     c.xt32.as<float>());
+  HIP_CHECK(hipGetLastError());
+  std::vector<long long> muf(d);
+  for (int f = 0; f < d; ++f) muf[f] = std::llrint(std::ldexp((double)c.mu[f], c.scale_bits));
+  c.muf.ensure(sizeof(long long) * d);
+  HIP_CHECK(hipMemcpyAsync(c.muf.p, muf.data(), sizeof(long long) * d, hipMemcpyHostToDevice,
+                           c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));  // muf is a stack vector
+  c.xt_valid = true;
+}
+
 // One F32X Lloyd step through screen32; returns false (nothing launched) when
 // the centroids are out of the fp16 split range.
-bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, float* dbg,
-                   float* thr_out) {
+bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* hout, bool prof,
+                   float* dbg, float* thr_out) {
   Plan32 pl;
   if (!build_plan32(c, C, k, pl)) return false;
   // incremental update when the device labels and running sums belong to the
@@ -870,25 +915,18 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
   const int cap = (int)(ceil_div(groups, nwaves) * 64);
   c.partials.ensure(sizeof(double) * (size_t)nwg * (NF + 1) * KP);
   c.fb_list.ensure(sizeof(int32_t) * (size_t)nwaves * cap);
-  c.fb_count.ensure(sizeof(int32_t) * (nwaves + 1));
-  HIP_CHECK(hipMemsetAsync(c.fb_count.p, 0, sizeof(int32_t) * (nwaves + 1), c.stream));
+  // per-wave counts | running total (screen) | published total: zeroed once
+  // per layout; publish32 clears the running total every step
+  if (c.fb_count.bytes < sizeof(int32_t) * (nwaves + 3) || c.fb_layout != nwaves) {
+    c.fb_count.ensure(sizeof(int32_t) * (nwaves + 3));
+    HIP_CHECK(hipMemsetAsync(c.fb_count.p, 0, sizeof(int32_t) * (nwaves + 3), c.stream));
+    c.fb_layout = nwaves;
+  }
   c.fb_regions = nwaves;
+  c.fb_total_slot = nwaves + 1;
   // pre-centred screen copy (exact; built once per point set)
   const bool pre = c.pre_ok && !std::getenv("CDR_NO_PRE");
-  if (pre && !c.xt_valid) {
-    c.xt32.ensure(sizeof(float) * (size_t)d4_of(d) * c.n_pad);
-    hipLaunchKernelGGL(precenter_kernel, dim3(4096), dim3(256), 0, c.stream, c.x32.as<float>(),
-                       c.n, c.n_pad, d, c.mu_s.as<float>(), (float)std::ldexp(1.0, c.sigma),
-                       c.xt32.as<float>());
-    HIP_CHECK(hipGetLastError());
-    std::vector<long long> muf(d);
-    for (int f = 0; f < d; ++f) muf[f] = std::llrint(std::ldexp((double)c.mu[f], c.scale_bits));
-    c.muf.ensure(sizeof(long long) * d);
-    HIP_CHECK(hipMemcpyAsync(c.muf.p, muf.data(), sizeof(long long) * d, hipMemcpyHostToDevice,
-                             c.stream));
-    HIP_CHECK(hipStreamSynchronize(c.stream));  // muf is a stack vector
-    c.xt_valid = true;
-  }
+  if (pre) ensure_precentered(c);
   S32Args a;
   a.X = pre ? c.xt32.as<float>() : c.x32.as<float>();
   a.X0 = c.x32.as<float>();
@@ -946,14 +984,19 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, bool prof, f
 #undef CDR_S32
   HIP_CHECK(hipGetLastError());
   if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
+  long long* hout_dev = nullptr;
+  if (hout) {
+    void* hp = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer(&hp, hout, 0));
+    hout_dev = static_cast<long long*>(hp);
+  }
   hipLaunchKernelGGL(reduce32, dim3((len + 63) / 64, kR32Slices), dim3(256), 0, c.stream,
                      c.partials.as<double>(), nwg, k, d, NF, KP,
                      std::ldexp(1.0, c.scale_bits - (pre ? c.sigma : 0)),
                      pre ? c.muf.as<long long>() : nullptr, c.run_sums.as<unsigned long long>());
   HIP_CHECK(hipGetLastError());
-  if (dout)
-    HIP_CHECK(hipMemcpyAsync(dout, c.run_sums.p, sizeof(long long) * len,
-                             hipMemcpyDeviceToDevice, c.stream));
+  hipLaunchKernelGGL(publish32, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(), len,
+                     dout, hout_dev, c.fb_count.as<int32_t>(), nwaves);
   c.run_valid = dbg == nullptr;
   c.run_k = k;
   return true;

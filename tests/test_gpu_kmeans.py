@@ -263,3 +263,28 @@ def test_seed_block_sums_and_scan_exact(ctx, n, d):
         total = _cdr.host_seq_sum(bs)
         assert total == dist.sum()
         assert ctx.seed_scan(total, 0.0) == np.cumsum(dist / total)[-1]
+
+
+@pytest.mark.parametrize("n,d,k", [(20000, 64, 1024), (30000, 24, 300), (25000, 40, 700),
+                                   (12000, 64, 129)])
+def test_large_k_path_vs_oracle(ctx, n, d, k):
+    """Config-5 regime (k*(d+1) beyond a workgroup's LDS): screen_big L1
+    one-product MFMA screen, L2 three-product re-screen, L3 exact fp64, and the
+    feature-pass update — labels and centroids bit-identical to the oracle."""
+    import kmeans_plusplus as kp
+
+    X = synth.generate(n, 0, n, d, k, 7 * n + d)
+    rng = np.random.default_rng(k)
+    C0 = X[np.sort(rng.choice(n, k, replace=False))]
+    ctx.load_points(X)
+    out = ctx.lloyd_step(C0)
+    assert ctx.profile_kernel().startswith("screen_big"), ctx.profile_kernel()
+    want_labels, want = ko.lloyd_partials(X, C0, ctx.info()["scale_bits"])
+    np.testing.assert_array_equal(ctx.labels(), want_labels)
+    np.testing.assert_array_equal(out, want)
+    np.random.seed(0)
+    C, lab = kp.kmeans(X, k, random_state=42, max_iter=2, context=ctx)
+    np.random.seed(0)
+    C2, lab2 = ko.kmeans(X, k, random_state=42, max_iter=2)
+    np.testing.assert_array_equal(lab, lab2)
+    np.testing.assert_array_equal(C, C2)
