@@ -651,7 +651,8 @@ static void build_plan_big(const Ctx& c, const double* C, int k, PlanBig& pl) {
 
 template <int DQ>
 static void launch_big_levels(Ctx& c, const BigArgs& a1, const BigArgs& a2, dim3 g1, dim3 g2,
-                              size_t lds1, const double* dC, int32_t* ovf, int32_t* ovf_count) {
+                              size_t lds1, const double* dC, int32_t* ovf, int32_t* ovf_count,
+                              bool prof) {
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&screen_big<DQ, 1, false, true>),
@@ -660,6 +661,7 @@ static void launch_big_levels(Ctx& c, const BigArgs& a1, const BigArgs& a2, dim3
   }
   hipLaunchKernelGGL((screen_big<DQ, 1, false, true>), g1, dim3(kBigThreads), lds1, c.stream, a1);
   HIP_CHECK(hipGetLastError());
+  if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));  // the L1 screen alone
   static const int abl = std::getenv("CDR_BIG_ABL") ? std::atoi(std::getenv("CDR_BIG_ABL")) : 0;
   hipLaunchKernelGGL((cand_big<DQ>), g2, dim3(256), 0, c.stream, a2, c.x32.as<float>(), dC, ovf,
                      ovf_count, abl);
@@ -755,14 +757,11 @@ bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof) {
   snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_big<%d,1,false,true>", DQ);
   if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
   switch (DQ) {
-    case 1: launch_big_levels<1>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count); break;
-    case 2: launch_big_levels<2>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count); break;
-    case 3: launch_big_levels<3>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count); break;
-    default: launch_big_levels<4>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count); break;
+    case 1: launch_big_levels<1>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
+    case 2: launch_big_levels<2>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
+    case 3: launch_big_levels<3>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
+    default: launch_big_levels<4>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
   }
-  // (prof: pe[1] after level 1 would split the launch pair; the screen time
-  // reported for this path is levels 1 + 2)
-  if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
   hipLaunchKernelGGL(exact_big, dim3(cus * 4), dim3(64), 0, c.stream, c.x32.as<float>(), c.n_pad,
                      d, dC, k, ovf, ovf_count, c.labels.as<int32_t>());
   HIP_CHECK(hipGetLastError());
