@@ -49,6 +49,10 @@ CONFIGS = {
     "3": (100_000_000, 16, 64, "config 3: 100M files x d=16, k=64"),
     "5": (50_000_000, 64, 1024, "config 5: 50M files x d=64, k=1024"),
 }
+# config 4 (features): events and manifest files per GPU (1B events over 8 GPUs)
+FEATURES_CFG = (125_000_000, 12_500_000,
+                "config 4: 1B access-log events over 8 GPUs -> per-file features "
+                "(125M events x 12.5M files per GPU)")
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense
 METRIC = "Lloyd point-iters/sec (whole node) + achieved HBM GB/s, 100M files d=16 k=64"
@@ -74,6 +78,92 @@ def cpu_baseline(d: int, k: int, seed: int, rows: int = 1_000_000, iters: int = 
             "seconds": dt}
 
 
+def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
+    """Config 4: the compute_features group-by (src/compute_features.py:31-54)
+    over a device-resident, time-ordered synthetic log.  A step = one full
+    group-by of this rank's events (timestamp range, compact (file, second)
+    keys, radix sort, per-file runs) plus the MAX all-reduce of the log's
+    last timestamp (:48).  Weak scaling: each rank owns its files and events."""
+    import numpy as np
+
+    import _cdr
+
+    ne, nf, desc = FEATURES_CFG
+    if args.n_total:
+        ne, nf = args.n_total, max(1, args.n_total // 10)
+    ctx = _cdr.Context(int(os.environ.get("LOCAL_RANK", "0")))
+    if dist is not None:
+        import torch
+
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.features_generate(ne, nf, seed=args.seed ^ (rank * 0x9E3779B97F4A7C15 & (2**64 - 1)))
+
+    def step():
+        _, mx = ctx.features_aggregate_resident(to_host=False)
+        if dist is not None:
+            import torch
+
+            t = torch.tensor([mx], dtype=torch.int64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            mx = int(t.item())
+        return mx
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    per_step = elapsed / max(args.steps, 1)
+    alg_bytes = ne * (4 + 1 + 4 + 8) + nf * (4 + 6 * 8)  # events read once, counters written
+    achieved = alg_bytes / per_step / 1e9
+    out = {
+        "metric": "access-log events aggregated per second (whole node), compute_features group-by",
+        "value": world * ne * args.steps / elapsed, "unit": "events/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_step * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic time-ordered access log generated on the device (counter-based)",
+        "config": {"workload": desc, "events_per_gpu": ne, "files_per_gpu": nf,
+                   "parallelism": f"files and events partitioned over {world} GPU(s), "
+                                  "RCCL MAX all-reduce of the last timestamp"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel": "features group-by (keys + hipCUB radix sort + runs), whole step",
+                     "alg_bytes_per_launch": alg_bytes, "kernel_ms": per_step * 1e3},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import features_oracle
+
+        s_ne, s_nf = 10_000_000, 1_000_000
+        ctx.features_generate(s_ne, s_nf, seed=args.seed)
+        f, op, cl, ts, pr = ctx.features_events_read()
+        c0 = time.perf_counter()
+        features_oracle.counts_from_arrays(f, op, cl, ts, pr, s_nf)
+        dt = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": s_ne / dt, "unit": "events/s", "cores": 1, "kind": "port",
+                               "sample": f"{s_ne} events x {s_nf} files of the same generator; "
+                                         "NumPy restatement of the group-by (oracle/"
+                                         "features_oracle.counts_from_arrays), 1 thread",
+                               "seconds": dt}
+    if rank == 0:
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def pmc_traffic(config: str, n_local: int):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -91,7 +181,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="3", choices=sorted(CONFIGS) + ["4"])
     ap.add_argument("--n-total", type=int, default=0,
                     help="override the per-config point count (testing only)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
@@ -123,6 +213,9 @@ def main() -> None:
     import _cdr
     from cdr_dist import Comm, ShardedLloyd, seed_sharded, shard_rows
 
+    if args.config == "4":
+        features_bench(args, world, rank, dist, device, json_fd)
+        return
     n_cfg, d, k, desc = CONFIGS[args.config]
     if args.n_total:
         n_cfg = args.n_total

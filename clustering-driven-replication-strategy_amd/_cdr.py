@@ -76,6 +76,9 @@ SIGNATURES = {
     "cdr_medians_by_label": ([_P, _I32, _P], None),
     "cdr_features_aggregate": ([_P, _I64, _P, _P, _P, _P, _I64, _P, _P, _PI64], None),
     "cdr_features_finalize": ([_P, _I64, _P, _P, _F64, _P], None),
+    "cdr_features_generate": ([_P, _I64, _I64, ctypes.c_uint64, _I64, _I64], None),
+    "cdr_features_aggregate_resident": ([_P, _P, _PI64], None),
+    "cdr_features_events_read": ([_P, _P, _P, _P, _P, _P], None),
     "cdr_host_seq_sum": ([_P, _I64, _F64], ctypes.c_double),
 }
 
@@ -308,6 +311,32 @@ class Context:
                                                 z(ts_us), nf, z(primary), z(out),
                                                 ctypes.byref(mx)))
         return out, int(mx.value)
+
+    def features_generate(self, n_events: int, n_files: int, seed: int = 0x5EED,
+                          t0_us: int = 1_700_000_000_000_000, span_us: int = 600_000_000) -> None:
+        _check(self._lib.cdr_features_generate(self._h, int(n_events), int(n_files),
+                                               int(seed) & 0xFFFFFFFFFFFFFFFF, int(t0_us),
+                                               int(span_us)))
+        self._ev = (int(n_events), int(n_files))
+
+    def features_aggregate_resident(self, to_host: bool = True):
+        ne, nf = self._ev
+        out = np.zeros((nf, 6), dtype=np.int64) if to_host else None
+        mx = _I64()
+        _check(self._lib.cdr_features_aggregate_resident(
+            self._h, _ptr(out) if to_host else None, ctypes.byref(mx)))
+        return out, int(mx.value)
+
+    def features_events_read(self):
+        ne, nf = self._ev
+        f = np.empty(ne, dtype=np.int32)
+        op = np.empty(ne, dtype=np.uint8)
+        cl = np.empty(ne, dtype=np.int32)
+        ts = np.empty(ne, dtype=np.int64)
+        pr = np.empty(nf, dtype=np.int32)
+        _check(self._lib.cdr_features_events_read(self._h, _ptr(f), _ptr(op), _ptr(cl), _ptr(ts),
+                                                  _ptr(pr)))
+        return f, op, cl, ts, pr
 
     def features_finalize(self, counts, creation_s, observation_end: float) -> np.ndarray:
         counts = np.ascontiguousarray(counts, dtype=np.int64)

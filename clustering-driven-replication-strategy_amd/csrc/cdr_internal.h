@@ -160,6 +160,7 @@ struct Ctx {
   DevBuf ev_file, ev_op, ev_client, ev_ts, ev_primary, ev_out, ev_scratch,
       ev_scratch2;
   DevBuf fin_counts, fin_creation, fin_out, fin_red;
+  int64_t ev_n = 0, ev_nf = 0;  // resident events of cdr_features_generate
 };
 
 // ---- launchers implemented in the .hip files ----

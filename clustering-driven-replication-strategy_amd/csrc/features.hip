@@ -19,6 +19,7 @@
 // normalised as double(v - min) / double(max - min), as Spark's `/` does.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -27,18 +28,26 @@
 namespace cdr {
 
 __device__ __forceinline__ long long sec_of(long long ts_us) {
-  // Spark: floor(cast(ts as double)) with cast = micros / 1e6 in fp64
+  // Spark: floor(cast(ts as double)) with cast = micros / 1e6 in fp64.  For
+  // 0 <= ts < 9e15 the fp64 quotient never rounds across an integer (an
+  // integer ts is >= 1e-6 below the next multiple, far above half an ulp),
+  // so the integer floor division is the same number and much cheaper.
+  if (ts_us >= 0 && ts_us < 9000000000000000ll) return ts_us / 1000000;
   return (long long)floor((double)ts_us / 1000000.0);
 }
 
 __global__ void ts_minmax(const long long* __restrict__ ts, int64_t n,
-                          unsigned long long* __restrict__ mm) {
+                          unsigned long long* __restrict__ mm, int* __restrict__ unordered) {
   long long lo = LLONG_MAX, hi = LLONG_MIN;
+  int bad = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    lo = min(lo, ts[i]);
-    hi = max(hi, ts[i]);
+    const long long t = ts[i];
+    lo = min(lo, t);
+    hi = max(hi, t);
+    if (i + 1 < n) bad |= t > ts[i + 1];
   }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(unordered, 1);
   for (int o = 32; o > 0; o >>= 1) {
     lo = min(lo, __shfl_xor(lo, o));
     hi = max(hi, __shfl_xor(hi, o));
@@ -52,7 +61,7 @@ __global__ void ts_minmax(const long long* __restrict__ ts, int64_t n,
 __global__ void make_keys(const int32_t* __restrict__ file, const uint8_t* __restrict__ op,
                           const int32_t* __restrict__ client, const long long* __restrict__ ts,
                           int64_t n, int64_t n_files, const int32_t* __restrict__ primary,
-                          long long sec_min, unsigned long long* __restrict__ keys,
+                          long long sec_min, int sbits, unsigned long long* __restrict__ keys,
                           uint8_t* __restrict__ flags) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -60,13 +69,98 @@ __global__ void make_keys(const int32_t* __restrict__ file, const uint8_t* __res
     unsigned long long key = ~0ull;
     uint8_t fl = 0;
     if (f >= 0 && f < n_files) {
-      key = ((unsigned long long)f << 32) | (unsigned long long)(sec_of(ts[i]) - sec_min);
+      key = ((unsigned long long)f << sbits) | (unsigned long long)(sec_of(ts[i]) - sec_min);
       fl = (op[i] == 1 ? 1 : 0) | (op[i] == 2 ? 2 : 0);
       const int pr = primary[f];
       if (client[i] >= 0 && pr >= 0 && client[i] == pr) fl |= 4;
     }
     keys[i] = key;
     flags[i] = fl;
+  }
+}
+
+// Time-ordered logs (the usual case: an access log is appended in time
+// order): a STABLE sort by file alone keeps every file's events in time
+// order, so equal seconds stay adjacent.  Key = file (all ones = not in the
+// manifest, sorts last within fbits), value = client << 32 | (sec - sec_min)
+// << 3 | flags.
+__global__ void make_keys32(const int32_t* __restrict__ file, const uint8_t* __restrict__ op,
+                            const int32_t* __restrict__ client, const long long* __restrict__ ts,
+                            int64_t n, int64_t n_files, const int32_t* __restrict__ primary,
+                            long long sec_min, unsigned invalid, unsigned* __restrict__ keys,
+                            unsigned long long* __restrict__ vals) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int f = file[i];
+    unsigned key = invalid;
+    unsigned long long v = 0;
+    if (f >= 0 && f < n_files) {
+      key = (unsigned)f;
+      const unsigned fl = (op[i] == 1 ? 1u : 0u) | (op[i] == 2 ? 2u : 0u);
+      // the client rides along (the primary node is looked up once per file
+      // after the sort, instead of a random gather per event here)
+      v = ((unsigned long long)(unsigned)client[i] << 32) |
+          (((unsigned)(sec_of(ts[i]) - sec_min) << 3) | fl);
+    }
+    keys[i] = key;
+    vals[i] = v;
+  }
+}
+
+__global__ void check_sorted32(const unsigned* __restrict__ keys, int64_t n,
+                               int* __restrict__ unsorted) {
+  int bad = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    bad |= keys[i] > keys[i + 1];
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(unsorted, 1);
+}
+
+__global__ void mark_runs32(const unsigned* __restrict__ keys, int64_t n, unsigned invalid,
+                            long long* __restrict__ start, long long* __restrict__ end) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned f = keys[i];
+    if (f == invalid) continue;
+    if (i == 0 || keys[i - 1] != f) start[f] = i;
+    if (i == n - 1 || keys[i + 1] != f) end[f] = i + 1;
+  }
+}
+
+__global__ void per_file32(const unsigned long long* __restrict__ vals, int64_t n_files,
+                           const int32_t* __restrict__ primary,
+                           const long long* __restrict__ start, const long long* __restrict__ end,
+                           long long* __restrict__ out) {
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n_files;
+       f += (int64_t)gridDim.x * blockDim.x) {
+    long long cnt = 0, w = 0, r = 0, loc = 0, best = 0;
+    const long long s = start[f];
+    if (s >= 0) {
+      const long long e = end[f];
+      const int pr = primary[f];
+      unsigned prev = 0xFFFFFFFFu;
+      long long run = 0;
+      for (long long i = s; i < e; ++i) {
+        const unsigned long long vv = vals[i];
+        const unsigned v = (unsigned)vv;
+        const int cl = (int)(unsigned)(vv >> 32);
+        const unsigned sec = v >> 3;
+        ++cnt;
+        w += v & 1;
+        r += (v >> 1) & 1;
+        loc += (cl >= 0 && pr >= 0 && cl == pr) ? 1 : 0;
+        run = (sec == prev) ? run + 1 : 1;
+        prev = sec;
+        best = run > best ? run : best;
+      }
+    }
+    long long* o = out + f * 6;
+    o[0] = cnt;
+    o[1] = w;
+    o[2] = r;
+    o[3] = loc;
+    o[4] = cnt;
+    o[5] = best;
   }
 }
 
@@ -79,20 +173,20 @@ __global__ void check_sorted(const unsigned long long* __restrict__ keys, int64_
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(unsorted, 1);
 }
 
-__global__ void mark_runs(const unsigned long long* __restrict__ keys, int64_t n,
+__global__ void mark_runs(const unsigned long long* __restrict__ keys, int64_t n, int sbits,
                           long long* __restrict__ start, long long* __restrict__ end) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long k = keys[i];
     if (k == ~0ull) continue;
-    const unsigned long long f = k >> 32;
-    if (i == 0 || (keys[i - 1] >> 32) != f) start[f] = i;
-    if (i == n - 1 || (keys[i + 1] >> 32) != f) end[f] = i + 1;
+    const unsigned long long f = k >> sbits;
+    if (i == 0 || (keys[i - 1] >> sbits) != f) start[f] = i;
+    if (i == n - 1 || keys[i + 1] == ~0ull || (keys[i + 1] >> sbits) != f) end[f] = i + 1;
   }
 }
 
 __global__ void per_file(const unsigned long long* __restrict__ keys,
-                         const uint8_t* __restrict__ flags, int64_t n_files,
+                         const uint8_t* __restrict__ flags, int64_t n_files, int sbits,
                          const long long* __restrict__ start, const long long* __restrict__ end,
                          long long* __restrict__ out) {
   for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n_files;
@@ -105,7 +199,7 @@ __global__ void per_file(const unsigned long long* __restrict__ keys,
       long long run = 0;
       for (long long i = s; i < e; ++i) {
         const uint8_t fl = flags[i];
-        const unsigned sec = (unsigned)(keys[i] & 0xFFFFFFFFull);
+        const unsigned sec = (unsigned)(keys[i] & ((1ull << sbits) - 1));
         ++cnt;
         w += fl & 1;
         r += (fl >> 1) & 1;
@@ -132,13 +226,7 @@ static int gcap(int64_t work, int threads, int cap) {
   return (int)g;
 }
 
-void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8_t* op,
-                        const int32_t* client, const int64_t* ts_us, int64_t n_files,
-                        const int32_t* primary, int64_t* out, int64_t* max_ts) {
-  if (ne < 0 || n_files < 0) CDR_FAIL(CDR_ERR_ARG, "negative sizes");
-  if (n_files >= (1ll << 31)) CDR_FAIL(CDR_ERR_UNSUPPORTED, "n_files >= 2^31");
-  *max_ts = LLONG_MIN;
-  if (n_files == 0 && ne == 0) return;
+static void ensure_events(Ctx& c, int64_t ne, int64_t n_files) {
   const size_t ne1 = ne > 0 ? ne : 1, nf1 = n_files > 0 ? n_files : 1;
   c.ev_file.ensure(4 * ne1);
   c.ev_op.ensure(ne1);
@@ -146,6 +234,19 @@ void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8
   c.ev_ts.ensure(8 * ne1);
   c.ev_primary.ensure(4 * nf1);
   c.ev_out.ensure(8 * 6 * nf1 + 64);
+}
+
+void features_aggregate_resident(Ctx& c, int64_t ne, int64_t n_files, int64_t* out,
+                                 int64_t* max_ts);
+
+void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8_t* op,
+                        const int32_t* client, const int64_t* ts_us, int64_t n_files,
+                        const int32_t* primary, int64_t* out, int64_t* max_ts) {
+  if (ne < 0 || n_files < 0) CDR_FAIL(CDR_ERR_ARG, "negative sizes");
+  if (n_files >= (1ll << 31)) CDR_FAIL(CDR_ERR_UNSUPPORTED, "n_files >= 2^31");
+  *max_ts = LLONG_MIN;
+  if (n_files == 0 && ne == 0) return;
+  ensure_events(c, ne, n_files);
   if (ne > 0) {
     HIP_CHECK(hipMemcpyAsync(c.ev_file.p, file_idx, 4 * ne, hipMemcpyHostToDevice, c.stream));
     HIP_CHECK(hipMemcpyAsync(c.ev_op.p, op, ne, hipMemcpyHostToDevice, c.stream));
@@ -155,18 +256,31 @@ void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8
   if (n_files > 0)
     HIP_CHECK(hipMemcpyAsync(c.ev_primary.p, primary, 4 * n_files, hipMemcpyHostToDevice,
                              c.stream));
+  features_aggregate_resident(c, ne, n_files, out, max_ts);
+}
+
+// The group-by over the events resident in c.ev_* (uploaded or generated).
+// out: host (n_files, 6) or null (results stay in c.ev_out).
+void features_aggregate_resident(Ctx& c, int64_t ne, int64_t n_files, int64_t* out,
+                                 int64_t* max_ts) {
+  *max_ts = LLONG_MIN;
+  if (n_files == 0 && ne == 0) return;
+  const size_t ne1 = ne > 0 ? ne : 1, nf1 = n_files > 0 ? n_files : 1;
   // timestamp range
   unsigned long long mm_init[2] = {~0ull, 0ull};
   unsigned long long* dmm = reinterpret_cast<unsigned long long*>(c.ev_out.as<char>() + 8 * 6 * nf1);
   HIP_CHECK(hipMemcpyAsync(dmm, mm_init, 16, hipMemcpyHostToDevice, c.stream));
+  int* ts_unordered = reinterpret_cast<int*>(c.ev_out.as<char>() + 8 * 6 * nf1 + 20);
+  HIP_CHECK(hipMemsetAsync(ts_unordered, 0, 4, c.stream));
   if (ne > 0) {
     hipLaunchKernelGGL(ts_minmax, dim3(gcap(ne, 256, 1024)), dim3(256), 0, c.stream,
-                       c.ev_ts.as<long long>(), ne, dmm);
+                       c.ev_ts.as<long long>(), ne, dmm, ts_unordered);
     HIP_CHECK(hipGetLastError());
   }
-  unsigned long long mm[2];
-  HIP_CHECK(hipMemcpyAsync(mm, dmm, 16, hipMemcpyDeviceToHost, c.stream));
+  unsigned long long mm[3];
+  HIP_CHECK(hipMemcpyAsync(mm, dmm, 24, hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
+  const bool time_ordered = (reinterpret_cast<const int*>(&mm[2])[1]) == 0;
   long long sec_min = 0, sec_max = 0;
   if (ne > 0) {
     const long long tmin = (long long)(mm[0] ^ (unsigned long long)LLONG_MIN);
@@ -177,19 +291,80 @@ void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8
     if (sec_max - sec_min >= (1ll << 32))
       CDR_FAIL(CDR_ERR_UNSUPPORTED, "access log spans more than 2^32 seconds");
   }
+  // compact sort keys: file << sbits | (sec - sec_min); invalid events are
+  // all ones and sort after every valid key within end_bit
+  int sbits = 1, fbits = 1;
+  while ((1ll << sbits) <= sec_max - sec_min) ++sbits;
+  while ((1ll << fbits) < n_files) ++fbits;
+  const int end_bit = std::min(64, sbits + fbits + 1);
+  c.fin_red.ensure(16 * nf1);
+  long long* start = c.fin_red.as<long long>();
+  long long* end = start + nf1;
+  int* unsorted = reinterpret_cast<int*>(c.ev_out.as<char>() + 8 * 6 * nf1 + 16);
+  // fast path: time-ordered log, stable 32-bit sort by file only
+  int fb32 = 1;
+  while ((1ll << fb32) <= n_files) ++fb32;  // all ones (invalid) is not a file id
+  if (ne > 1 && time_ordered && fb32 <= 31 && sec_max - sec_min < (1ll << 29)) {
+    const unsigned invalid = (unsigned)((1ull << fb32) - 1);
+    c.ev_scratch.ensure((size_t)24 * ne1 + 64);
+    unsigned long long* v0 = c.ev_scratch.as<unsigned long long>();
+    unsigned long long* v1 = v0 + ne1;
+    unsigned* k0 = reinterpret_cast<unsigned*>(v1 + ne1);
+    unsigned* k1 = k0 + ne1;
+    HIP_CHECK(hipMemsetAsync(unsorted, 0, 4, c.stream));
+    hipLaunchKernelGGL(make_keys32, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream,
+                       c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(), c.ev_client.as<int32_t>(),
+                       c.ev_ts.as<long long>(), ne, n_files, c.ev_primary.as<int32_t>(), sec_min,
+                       invalid, k0, v0);  // primary unused here (per_file32 reads it)
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(check_sorted32, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream, k0,
+                       ne, unsorted);
+    HIP_CHECK(hipGetLastError());
+    int hunsorted = 0;
+    HIP_CHECK(hipMemcpyAsync(&hunsorted, unsorted, 4, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    unsigned* keys = k0;
+    unsigned long long* vals = v0;
+    if (hunsorted) {
+      size_t tmp_bytes = 0;
+      HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, v0, v1, (int)ne,
+                                                   0, fb32, c.stream));
+      c.ev_scratch2.ensure(tmp_bytes + 256);
+      HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c.ev_scratch2.p, tmp_bytes, k0, k1, v0, v1,
+                                                   (int)ne, 0, fb32, c.stream));
+      keys = k1;
+      vals = v1;
+    }
+    HIP_CHECK(hipMemsetAsync(start, 0xFF, 8 * nf1, c.stream));  // -1
+    HIP_CHECK(hipMemsetAsync(end, 0, 8 * nf1, c.stream));
+    hipLaunchKernelGGL(mark_runs32, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream, keys, ne,
+                       invalid, start, end);
+    HIP_CHECK(hipGetLastError());
+    if (n_files > 0) {
+      hipLaunchKernelGGL(per_file32, dim3(gcap(n_files, 256, 8192)), dim3(256), 0, c.stream,
+                         vals, n_files, c.ev_primary.as<int32_t>(), start, end,
+                         c.ev_out.as<long long>());
+      HIP_CHECK(hipGetLastError());
+      if (out)
+        HIP_CHECK(hipMemcpyAsync(out, c.ev_out.p, 8 * 6 * n_files, hipMemcpyDeviceToHost,
+                                 c.stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    return;
+  }
+  // general path: 64-bit (file, second) keys
   // keys + flags
   c.ev_scratch.ensure((8 + 1) * ne1 * 2 + 64);
   unsigned long long* k0 = c.ev_scratch.as<unsigned long long>();
   unsigned long long* k1 = k0 + ne1;
   uint8_t* f0 = reinterpret_cast<uint8_t*>(k1 + ne1);
   uint8_t* f1 = f0 + ne1;
-  int* unsorted = reinterpret_cast<int*>(c.ev_out.as<char>() + 8 * 6 * nf1 + 16);
   HIP_CHECK(hipMemsetAsync(unsorted, 0, 4, c.stream));
   if (ne > 0) {
     hipLaunchKernelGGL(make_keys, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream,
                        c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(), c.ev_client.as<int32_t>(),
                        c.ev_ts.as<long long>(), ne, n_files, c.ev_primary.as<int32_t>(), sec_min,
-                       k0, f0);
+                       sbits, k0, f0);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(check_sorted, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream, k0, ne,
                        unsorted);
@@ -203,31 +378,75 @@ void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8
   if (hunsorted && ne > 1) {
     size_t tmp_bytes = 0;
     HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, f0, f1, (int)ne, 0,
-                                                 64, c.stream));
+                                                 end_bit, c.stream));
     c.ev_scratch2.ensure(tmp_bytes + 256);
     HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c.ev_scratch2.p, tmp_bytes, k0, k1, f0, f1,
-                                                 (int)ne, 0, 64, c.stream));
+                                                 (int)ne, 0, end_bit, c.stream));
     keys = k1;
     flags = f1;
   }
   // runs per file
-  c.fin_red.ensure(16 * nf1);
-  long long* start = c.fin_red.as<long long>();
-  long long* end = start + nf1;
   HIP_CHECK(hipMemsetAsync(start, 0xFF, 8 * nf1, c.stream));  // -1
   HIP_CHECK(hipMemsetAsync(end, 0, 8 * nf1, c.stream));
   if (ne > 0) {
     hipLaunchKernelGGL(mark_runs, dim3(gcap(ne, 256, 8192)), dim3(256), 0, c.stream, keys, ne,
-                       start, end);
+                       sbits, start, end);
     HIP_CHECK(hipGetLastError());
   }
   if (n_files > 0) {
     hipLaunchKernelGGL(per_file, dim3(gcap(n_files, 256, 8192)), dim3(256), 0, c.stream, keys,
-                       flags, n_files, start, end, c.ev_out.as<long long>());
+                       flags, n_files, sbits, start, end, c.ev_out.as<long long>());
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipMemcpyAsync(out, c.ev_out.p, 8 * 6 * n_files, hipMemcpyDeviceToHost, c.stream));
+    if (out)
+      HIP_CHECK(hipMemcpyAsync(out, c.ev_out.p, 8 * 6 * n_files, hipMemcpyDeviceToHost,
+                               c.stream));
   }
   HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+// ---- synthetic access log (device, for the config-4 scale runs) ----------
+// A time-ordered log of ne events over n_files manifest files (counter-based,
+// so any shard regenerates the same events): event e at ts = t0 + e span / ne
+// microseconds, file = uniform over the files (file_begin + ...), op WRITE
+// with probability 1/10 else READ, client uniform over 3 datanodes;
+// primary[f] uniform over the same 3 (access_simulator.py's dn1..dn3).
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void gen_events(int64_t ne, int64_t n_files, unsigned long long seed, long long t0,
+                           long long span, int32_t* __restrict__ file, uint8_t* __restrict__ op,
+                           int32_t* __restrict__ client, long long* __restrict__ ts,
+                           int32_t* __restrict__ primary) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += stride) {
+    const unsigned long long h = mix64(seed ^ ((unsigned long long)e * 0xD1B54A32D192ED03ull));
+    file[e] = (int32_t)(((h >> 32) * (unsigned long long)n_files) >> 32);
+    op[e] = (((h & 0xFFFFull) * 10ull) >> 16) == 0 ? 1 : 2;
+    client[e] = (int32_t)((((h >> 16) & 0xFFFFull) * 3ull) >> 16);
+    ts[e] = t0 + (long long)((e * span) / ne);
+  }
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n_files; f += stride)
+    primary[f] = (int32_t)((((mix64(seed ^ 0x5EEDull ^ ((unsigned long long)f << 1)) >> 48) * 3ull) >> 16));
+}
+
+void features_generate(Ctx& c, int64_t ne, int64_t n_files, unsigned long long seed,
+                       long long t0_us, long long span_us) {
+  if (ne < 0 || n_files < 1) CDR_FAIL(CDR_ERR_ARG, "need n_events >= 0 and n_files >= 1");
+  if (n_files >= (1ll << 31)) CDR_FAIL(CDR_ERR_UNSUPPORTED, "n_files >= 2^31");
+  if (ne > 0 && span_us > (long long)(LLONG_MAX / ne)) CDR_FAIL(CDR_ERR_ARG, "span too large");
+  ensure_events(c, ne, n_files);
+  hipLaunchKernelGGL(gen_events, dim3(8192), dim3(256), 0, c.stream, ne, n_files, seed, t0_us,
+                     span_us, c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(),
+                     c.ev_client.as<int32_t>(), c.ev_ts.as<long long>(),
+                     c.ev_primary.as<int32_t>());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.ev_n = ne;
+  c.ev_nf = n_files;
 }
 
 // ---- K6 -------------------------------------------------------------------
@@ -358,6 +577,46 @@ int cdr_features_aggregate(cdr_ctx* h, int64_t n_events, const int32_t* file_idx
   HIP_CHECK(hipSetDevice(h->c.device));
   features_aggregate(h->c, n_events, file_idx, op, client, ts_us, n_files, primary, out,
                      max_ts_us);
+  CDR_CATCH
+}
+
+int cdr_features_generate(cdr_ctx* h, int64_t n_events, int64_t n_files, uint64_t seed,
+                          int64_t t0_us, int64_t span_us) {
+  CDR_TRY
+  if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  features_generate(h->c, n_events, n_files, seed, t0_us, span_us);
+  CDR_CATCH
+}
+
+int cdr_features_aggregate_resident(cdr_ctx* h, int64_t* out, int64_t* max_ts_us) {
+  CDR_TRY
+  if (!h || !max_ts_us) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  if (c.ev_nf <= 0) CDR_FAIL(CDR_ERR_STATE, "no resident events (cdr_features_generate)");
+  HIP_CHECK(hipSetDevice(c.device));
+  features_aggregate_resident(c, c.ev_n, c.ev_nf, out, max_ts_us);
+  CDR_CATCH
+}
+
+int cdr_features_events_read(cdr_ctx* h, int32_t* file_idx, uint8_t* op, int32_t* client,
+                             int64_t* ts_us, int32_t* primary) {
+  CDR_TRY
+  if (!h || !file_idx || !op || !client || !ts_us || !primary)
+    CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  if (c.ev_nf <= 0) CDR_FAIL(CDR_ERR_STATE, "no resident events (cdr_features_generate)");
+  HIP_CHECK(hipSetDevice(c.device));
+  const int64_t ne = c.ev_n;
+  if (ne > 0) {
+    HIP_CHECK(hipMemcpyAsync(file_idx, c.ev_file.p, 4 * ne, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(op, c.ev_op.p, ne, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(client, c.ev_client.p, 4 * ne, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(ts_us, c.ev_ts.p, 8 * ne, hipMemcpyDeviceToHost, c.stream));
+  }
+  HIP_CHECK(hipMemcpyAsync(primary, c.ev_primary.p, 4 * c.ev_nf, hipMemcpyDeviceToHost,
+                           c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
   CDR_CATCH
 }
 

@@ -154,6 +154,18 @@ int cdr_features_aggregate(cdr_ctx* ctx, int64_t n_events,
                            const int32_t* client, const int64_t* ts_us,
                            int64_t n_files, const int32_t* primary,
                            int64_t* out, int64_t* max_ts_us);
+/* Config-4 scale runs: a synthetic time-ordered access log generated on
+ * the device and kept resident (event e at t0_us + e * span_us / n_events;
+ * file uniform over n_files; op WRITE with p = 1/10 else READ; client and
+ * primary uniform over 3 datanodes).  cdr_features_aggregate_resident runs
+ * the same group-by as cdr_features_aggregate on them (out: host
+ * (n_files, 6) or NULL to keep the result on the device);
+ * cdr_features_events_read copies the events back (parity tests).          */
+int cdr_features_generate(cdr_ctx* ctx, int64_t n_events, int64_t n_files, uint64_t seed,
+                          int64_t t0_us, int64_t span_us);
+int cdr_features_aggregate_resident(cdr_ctx* ctx, int64_t* out, int64_t* max_ts_us);
+int cdr_features_events_read(cdr_ctx* ctx, int32_t* file_idx, uint8_t* op, int32_t* client,
+                             int64_t* ts_us, int32_t* primary);
 /* Finalisation, src/compute_features.py:48-94.  counts: output of
  * cdr_features_aggregate; creation_s: creation_ts_epoch (double seconds, NaN
  * = null -> age 0 as na.fill does); observation_end: max ts in seconds

@@ -96,3 +96,43 @@ def test_main_py_flow_matches_reference(ctx):
     final = pd.read_csv(os.path.join(PDIR, "final_categories.csv"), float_precision="round_trip")
     assert [cats[f"C{i}"] for i in range(4)] == list(final["category"])
     np.testing.assert_array_equal(C, final[feats].to_numpy())
+
+
+def test_generated_log_exact(ctx):
+    """Device-generated, time-ordered log (the config-4 generator): the
+    resident group-by (radix sort on compact (file, second) keys) equals the
+    independent oracle counters and the host-upload path, bit for bit."""
+    ne, nf = 3_000_000, 300_000
+    ctx.features_generate(ne, nf, seed=1234)
+    got, mx = ctx.features_aggregate_resident()
+    f, op, cl, ts, pr = ctx.features_events_read()
+    assert np.all(np.diff(ts) >= 0)  # time-ordered, so the sort path runs
+    want, wmx = features_oracle.counts_from_arrays(f, op, cl, ts, pr, nf)
+    np.testing.assert_array_equal(got, want)
+    assert mx == wmx
+    up, umx = ctx.features_aggregate(f, op, cl, ts, pr)
+    np.testing.assert_array_equal(up, want)
+
+
+def test_generated_log_config4_shard(ctx):
+    """One GPU's share of config 4 (1B events over 8 GPUs): 125M events over
+    12.5M files.  Counters checked exactly with bincount; max_concurrency
+    exactly through unique (file, second) keys."""
+    ne, nf = 125_000_000, 12_500_000
+    ctx.features_generate(ne, nf, seed=99)
+    got, mx = ctx.features_aggregate_resident()
+    f, op, cl, ts, pr = ctx.features_events_read()
+    f64 = f.astype(np.int64)
+    np.testing.assert_array_equal(got[:, 0], np.bincount(f64, minlength=nf))
+    np.testing.assert_array_equal(got[:, 1], np.bincount(f64, weights=(op == 1), minlength=nf))
+    np.testing.assert_array_equal(got[:, 2], np.bincount(f64, weights=(op == 2), minlength=nf))
+    np.testing.assert_array_equal(got[:, 3], np.bincount(f64, weights=(cl == pr[f]), minlength=nf))
+    np.testing.assert_array_equal(got[:, 4], got[:, 0])
+    assert got[:, 0].sum() == ne and mx == int(ts.max())
+    sec = ts // 1_000_000  # ts > 0: floor division == floor(ts / 1e6) here
+    key = f64 * 1024 + (sec - sec.min())
+    del sec
+    uk, cnt = np.unique(key, return_counts=True)
+    conc = np.zeros(nf, dtype=np.int64)
+    np.maximum.at(conc, uk // 1024, cnt)
+    np.testing.assert_array_equal(got[:, 5], conc)
