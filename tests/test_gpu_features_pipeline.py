@@ -136,3 +136,16 @@ def test_generated_log_config4_shard(ctx):
     conc = np.zeros(nf, dtype=np.int64)
     np.maximum.at(conc, uk // 1024, cnt)
     np.testing.assert_array_equal(got[:, 5], conc)
+
+
+@pytest.mark.parametrize("ne,nf", [(0, 5), (1, 1), (2, 3), (70_000, 1)])
+def test_generated_log_edge_sizes(ctx, ne, nf):
+    """Empty and tiny logs, a single manifest file (fbits edge) on the
+    resident path: same counters as the oracle."""
+    ctx.features_generate(ne, nf, seed=ne + nf)
+    got, mx = ctx.features_aggregate_resident()
+    f, op, cl, ts, pr = ctx.features_events_read()
+    want, wmx = features_oracle.counts_from_arrays(f, op, cl, ts, pr, nf)
+    np.testing.assert_array_equal(got, want)
+    if ne:
+        assert mx == wmx

@@ -288,3 +288,19 @@ def test_large_k_path_vs_oracle(ctx, n, d, k):
     C2, lab2 = ko.kmeans(X, k, random_state=42, max_iter=2)
     np.testing.assert_array_equal(lab, lab2)
     np.testing.assert_array_equal(C, C2)
+
+
+@pytest.mark.parametrize("n,d,k", [(50, 64, 300), (1000, 33, 257), (4097, 17, 1500)])
+def test_large_k_ragged_shapes(ctx, n, d, k):
+    """screen_big edge shapes: fewer points than centroids, d not a multiple
+    of 16, k not a multiple of 32 (padding rows and feature slots)."""
+    X = synth.generate(n, 0, n, d, min(k, 64), 11 * n + d)
+    rng = np.random.default_rng(n)
+    C0 = X[rng.integers(0, n, k)] + 0.0
+    C0[::7] += 2.0 ** -20  # centroids off the data points, still on a fine grid
+    ctx.load_points(X)
+    out = ctx.lloyd_step(C0)
+    assert ctx.profile_kernel().startswith("screen_big"), ctx.profile_kernel()
+    want_labels, want = ko.lloyd_partials(X, C0, ctx.info()["scale_bits"])
+    np.testing.assert_array_equal(ctx.labels(), want_labels)
+    np.testing.assert_array_equal(out, want)

@@ -16,8 +16,17 @@ k = int(sys.argv[3]) if len(sys.argv) > 3 else 64
 masks = [int(m) for m in (sys.argv[4].split(",") if len(sys.argv) > 4 else "0,1,2,3,4,8,15".split(","))]
 ctx = _cdr.Context(0)
 ctx.generate_points(n, 0, n, d, k, 0x5EED)
-rng = np.random.default_rng(0)
-C = ctx.get_rows(np.sort(rng.choice(n, k, replace=False)))
+if os.environ.get("ABLATE_RANDOM_C"):
+    rng = np.random.default_rng(0)
+    C = ctx.get_rows(np.sort(rng.choice(n, k, replace=False)))
+else:  # the bench's centroids: k-means++ then a few Lloyd steps
+    from cdr_dist import Comm, ShardedLloyd, seed_sharded
+
+    C = seed_sharded(ctx, Comm(), 0, n, k, random_state=42)
+    lloyd = ShardedLloyd(ctx, Comm(), n, 0)
+    np.random.seed(0)
+    for _ in range(4):
+        C, _ = lloyd.step(C, lloyd.row)
 for _ in range(2):
     ctx.lloyd_step(C)
 res = {m: [] for m in masks}
