@@ -164,6 +164,143 @@ def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> N
         dist.destroy_process_group()
 
 
+INGEST_CFG = (20_000_000, 2_000_000,
+              "config 4 ingest leg: access-log CSV (src/access_simulator.py:61-63 format) -> "
+              "device tokenise + path join + group-by (20M events x 2M files per GPU)")
+
+
+def make_log(ne: int, nf: int, seed: int):
+    """Synthetic time-ordered access log in the simulator's line format,
+    built with NumPy as fixed-width rows: (bytes, manifest paths, primaries)."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    pre = b"2025-11-01T12:00:00.000Z,/user/root/synth/synth_00000000.bin,"
+    rd, wr = b"READ,dn0,00000\n", b"WRITE,dn0,0000\n"
+    width = len(pre) + len(rd)
+    rows = np.empty((ne, width), dtype=np.uint8)
+    rows[:, :len(pre)] = np.frombuffer(pre, dtype=np.uint8)
+    is_w = rng.random(ne) < 0.1
+    rows[:, len(pre):] = np.frombuffer(rd, dtype=np.uint8)
+    rows[is_w, len(pre):] = np.frombuffer(wr, dtype=np.uint8)
+
+    def put(mask, col, ndig, vals):
+        for j in range(ndig):
+            rows[mask, col + ndig - 1 - j] = 48 + (vals // 10 ** j) % 10
+
+    ms_total = (np.arange(ne, dtype=np.int64) * 600_000) // ne
+    allr = slice(None)
+    put(allr, 14, 2, ms_total // 60_000)
+    put(allr, 17, 2, (ms_total // 1000) % 60)
+    put(allr, 20, 3, ms_total % 1000)
+    put(allr, len(pre) - 13, 8, rng.integers(0, nf, ne))
+    cl = rng.integers(1, 4, ne)
+    b = len(pre)
+    put(~is_w, b + 7, 1, cl[~is_w])
+    put(is_w, b + 8, 1, cl[is_w])
+    pid = rng.integers(0, 10000, ne)
+    put(~is_w, b + 9, 5, pid[~is_w])
+    put(is_w, b + 10, 4, pid[is_w])
+    paths = [f"/user/root/synth/synth_{i:08d}.bin" for i in range(nf)]
+    primary = [f"dn{v}" for v in rng.integers(1, 4, nf)]
+    return rows.tobytes(), paths, primary
+
+
+def ingest_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
+    """Config 4, ingest leg: the access-log read + path join of
+    src/compute_features.py:19-41 on the device (csrc/ingest.hip) followed by
+    the group-by, from log bytes resident in HBM.  A step = tokenise + parse
+    + hash-join + aggregate.  Weak scaling: each rank owns its log slice."""
+    import numpy as np
+
+    import _cdr
+    import compute_features as cf
+
+    ne, nf, desc = INGEST_CFG
+    if args.n_total:
+        ne, nf = args.n_total, max(1, args.n_total // 10)
+    data, paths, primary = make_log(ne, nf, args.seed + rank)
+    ctx = _cdr.Context(int(os.environ.get("LOCAL_RANK", "0")))
+    prim, nodes = cf.encode_primary(primary)
+    ctx.ingest_manifest(paths, prim, nodes)
+    st = ctx.ingest_log(data)
+    if st[0] != ne or st[1] != -1 or st[2] != -1:
+        raise RuntimeError(f"ingest status {st.tolist()}")
+
+    def parse_only():
+        ctx.ingest_reparse()
+
+    def step():
+        ctx.ingest_reparse()
+        ctx.features_aggregate_resident(to_host=False)
+
+    def timed(fn, steps):
+        for _ in range(args.warmup):
+            fn()
+        if dist is not None:
+            dist.barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            import torch
+
+            t = torch.tensor([el], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    elapsed = timed(step, args.steps)
+    parse_s = timed(parse_only, args.steps) / max(args.steps, 1)
+    per_step = elapsed / max(args.steps, 1)
+    nbytes = len(data)
+    alg = nbytes + ne * (8 + 4 + 1 + 4 + 8)  # log read once; ends, events written
+    achieved = alg / parse_s / 1e9
+    out = {
+        "metric": "access-log events ingested + aggregated per second (whole node)",
+        "value": world * ne * args.steps / elapsed, "unit": "events/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_step * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic time-ordered CSV log in the simulator's format (NumPy fixed-width rows)",
+        "config": {"workload": desc, "events_per_gpu": ne, "files_per_gpu": nf,
+                   "log_bytes_per_gpu": nbytes,
+                   "parallelism": f"log slices partitioned over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel": "ingest (nl_count + tile_scan + nl_write + parse), log bytes "
+                               "resident", "alg_bytes_per_launch": alg,
+                     "kernel_ms": parse_s * 1e3},
+        "log_GBps": nbytes / parse_s / 1e9,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import tempfile
+
+        s_ne = 300_000
+        s_data = data[: s_ne * (len(data) // ne)]
+        with tempfile.NamedTemporaryFile(suffix=".log", delete=False) as fh:
+            fh.write(s_data)
+        c0 = time.perf_counter()
+        cf.encode(paths, primary, *cf.load_access_log(fh.name))
+        dt = time.perf_counter() - c0
+        os.unlink(fh.name)
+        out["cpu_baseline"] = {"value": s_ne / dt, "unit": "events/s", "cores": 1, "kind": "port",
+                               "sample": f"first {s_ne} lines of the same log: python csv + "
+                                         "ISO regex + dict join (compute_features."
+                                         "load_access_log + encode, the host restatement of "
+                                         "src/compute_features.py:19-41), 1 thread",
+                               "seconds": dt}
+    if rank == 0:
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def pmc_traffic(config: str, n_local: int):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -181,7 +318,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="3", choices=sorted(CONFIGS) + ["4"])
+    ap.add_argument("--config", default="3", choices=sorted(CONFIGS) + ["4", "4-ingest"])
     ap.add_argument("--n-total", type=int, default=0,
                     help="override the per-config point count (testing only)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
@@ -215,6 +352,9 @@ def main() -> None:
 
     if args.config == "4":
         features_bench(args, world, rank, dist, device, json_fd)
+        return
+    if args.config == "4-ingest":
+        ingest_bench(args, world, rank, dist, device, json_fd)
         return
     n_cfg, d, k, desc = CONFIGS[args.config]
     if args.n_total:

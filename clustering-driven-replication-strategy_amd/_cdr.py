@@ -79,6 +79,9 @@ SIGNATURES = {
     "cdr_features_generate": ([_P, _I64, _I64, ctypes.c_uint64, _I64, _I64], None),
     "cdr_features_aggregate_resident": ([_P, _P, _PI64], None),
     "cdr_features_events_read": ([_P, _P, _P, _P, _P, _P], None),
+    "cdr_ingest_manifest": ([_P, _I64, _P, _P, _P, _I32, _P, _P], None),
+    "cdr_ingest_log": ([_P, _P, _I64, _P], None),
+    "cdr_ingest_reparse": ([_P, _P], None),
     "cdr_host_seq_sum": ([_P, _I64, _F64], ctypes.c_double),
 }
 
@@ -338,6 +341,37 @@ class Context:
                                                   _ptr(pr)))
         return f, op, cl, ts, pr
 
+    # -- access-log ingest (csrc/ingest.hip) -------------------------------
+    def ingest_manifest(self, paths, primary, nodes) -> None:
+        """Device dictionaries of the manifest paths and primary node names
+        (None paths never match, like an empty log field)."""
+        pb, po = _pack_strings(paths)
+        nb, no = _pack_strings(nodes)
+        primary = np.ascontiguousarray(primary, dtype=np.int32)
+        if primary.size != len(po) - 1:
+            raise ValueError("primary must have one entry per manifest path")
+        _check(self._lib.cdr_ingest_manifest(self._h, len(po) - 1, _ptr(pb), _ptr(po),
+                                             _ptr(primary), len(no) - 1, _ptr(nb), _ptr(no)))
+        self._ing_nf = len(po) - 1
+
+    def ingest_log(self, data) -> np.ndarray:
+        """Parse the log bytes on the device into the resident events.  Returns
+        status (6,) int64: records, first bad-timestamp record, first record
+        the device tokeniser does not take, bad-timestamp count, byte span of
+        the reported record (include/cdr.h)."""
+        buf = np.frombuffer(memoryview(data), dtype=np.uint8)
+        st = np.zeros(6, dtype=np.int64)
+        _check(self._lib.cdr_ingest_log(self._h, _ptr(buf) if buf.size else None, buf.size,
+                                        _ptr(st)))
+        self._ev = (int(st[0]), self._ing_nf)
+        return st
+
+    def ingest_reparse(self) -> np.ndarray:
+        st = np.zeros(6, dtype=np.int64)
+        _check(self._lib.cdr_ingest_reparse(self._h, _ptr(st)))
+        self._ev = (int(st[0]), self._ing_nf)
+        return st
+
     def features_finalize(self, counts, creation_s, observation_end: float) -> np.ndarray:
         counts = np.ascontiguousarray(counts, dtype=np.int64)
         creation_s = np.ascontiguousarray(creation_s, dtype=np.float64)
@@ -347,6 +381,16 @@ class Context:
             _check(self._lib.cdr_features_finalize(self._h, nf, _ptr(counts), _ptr(creation_s),
                                                    float(observation_end), _ptr(out)))
         return out
+
+
+def _pack_strings(strs):
+    """UTF-8 bytes + int64 offsets (n+1) of a list of str (None -> empty)."""
+    enc = [b"" if v is None else v.encode("utf-8") for v in strs]
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    if enc:
+        np.cumsum([len(b) for b in enc], out=off[1:])
+    data = np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8)
+    return data, off
 
 
 _default_ctx: Context | None = None

@@ -11,10 +11,15 @@ locality, concurrency, access_freq_norm, age_norm, write_ratio_norm,
 locality_norm, concurrency_norm`` (src/compute_features.py:70-96), which
 ``src/main.py:155-168`` globs.
 
-Host side (plumbing): CSV parsing, ISO-8601 timestamps -> microseconds,
-dictionary encoding of paths and client nodes.  Device side (libcdr):
-the group-by counters of :31-46 (``cdr_features_aggregate``) and the
-finalisation / min-max normalisation of :48-94 (``cdr_features_finalize``).
+Host side (plumbing): the manifest CSV and its dictionaries.  Device side
+(libcdr): the access-log read of :19-29 and the path join of :37
+(``cdr_ingest_log``: tokenising, ISO-8601 timestamps -> microseconds, hash
+lookups of paths and client nodes, csrc/ingest.hip), the group-by counters of
+:31-46 (``cdr_features_aggregate_resident``) and the finalisation / min-max
+normalisation of :48-94 (``cdr_features_finalize``).  A log with CSV quoting
+(or NUL bytes, lone CRs, non-ASCII timestamps), which the reference's
+simulator never writes, is tokenised on the host by ``load_access_log`` and
+aggregated on the device the same way.
 
 Spark semantics kept (Spark 3.5, docker/docker-compose.yml:67):
   * ``to_timestamp`` of ISO strings -> microseconds; ``cast(ts as double)`` =
@@ -175,14 +180,51 @@ def encode(paths, primary, log_ts, log_path, log_op, log_client):
     return file_idx, opc, client, ts_us, prim
 
 
+def encode_primary(primary):
+    """Node ids of the primaries (first-appearance order, -2 = null) and the
+    node names in id order: the ids ``encode`` gives them."""
+    nodes = {}
+    prim = np.array([-2 if v is None else nodes.setdefault(v, len(nodes)) for v in primary],
+                    dtype=np.int32)
+    return prim, list(nodes)
+
+
+def _bad_ts_error(data: bytes, status) -> ValueError:
+    # the span starts after the previous record: drop blank lines before it
+    span = bytes(data[int(status[4]):int(status[5])]).rsplit(b"\n", 1)[-1]
+    line = span.decode("utf-8", errors="replace")
+    field = line[:-1] if line.endswith("\r") else line
+    ts = field.split(",")[0] or None
+    return ValueError(f"unparseable access-log timestamp {ts!r} (row {int(status[1])})")
+
+
+def ingest_events(ctx: Context, paths, primary, access_log: str) -> int:
+    """Access log -> resident device events of ``ctx``; returns the count."""
+    prim, nodes = encode_primary(primary)
+    ctx.ingest_manifest(paths, prim, nodes)
+    with open(_strip_scheme(access_log), "rb") as fh:
+        data = fh.read()
+    st = ctx.ingest_log(data)
+    if st[2] >= 0:
+        return -1  # csv syntax the device tokeniser leaves to the host
+    if st[1] >= 0:
+        raise _bad_ts_error(data, st)
+    return int(st[0])
+
+
 def compute_features(manifest: str, access_log: str, ctx: Context | None = None):
     """Returns (paths, table) with table (n_files, 10) float64 in OUT_COLUMNS order."""
     ctx = ctx if ctx is not None else default_context()
     paths, created, primary = load_manifest(manifest)
-    lt, lp, lo, lc = load_access_log(access_log)
-    file_idx, opc, client, ts_us, prim = encode(paths, primary, lt, lp, lo, lc)
-    counts, max_ts_us = ctx.features_aggregate(file_idx, opc, client, ts_us, prim)
-    if ts_us.size:
+    n_events = ingest_events(ctx, paths, primary, access_log) if paths else -1
+    if n_events >= 0:
+        counts, max_ts_us = ctx.features_aggregate_resident()
+    else:
+        lt, lp, lo, lc = load_access_log(access_log)
+        file_idx, opc, client, ts_us, prim = encode(paths, primary, lt, lp, lo, lc)
+        counts, max_ts_us = ctx.features_aggregate(file_idx, opc, client, ts_us, prim)
+        n_events = ts_us.size
+    if n_events:
         observation_end = max_ts_us / 1e6  # max(cast(ts as double)) :48
     else:
         observation_end = time.time()  # :50-51

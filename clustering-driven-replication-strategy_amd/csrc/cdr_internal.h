@@ -161,6 +161,19 @@ struct Ctx {
       ev_scratch2;
   DevBuf fin_counts, fin_creation, fin_out, fin_red;
   int64_t ev_n = 0, ev_nf = 0;  // resident events of cdr_features_generate
+
+  // ---- access-log ingest (ingest.hip) ----
+  DevBuf ing_log;              // log bytes, zero-padded to a whole tile
+  DevBuf ing_blk;              // int64 per tile: record count, then offset
+  DevBuf ing_ends;             // int64 per record: byte index of its terminator
+  DevBuf ing_scalar;           // int64 scratch: totals, error rows, flags
+  DevBuf ing_pbytes, ing_poff; // manifest paths: bytes, int64 offsets (n+1)
+  DevBuf ing_pkey, ing_pidx;   // path hash table: u64 key, int32 first row
+  DevBuf ing_nbytes, ing_noff; // node names
+  DevBuf ing_nkey, ing_nidx;   // node hash table
+  int64_t ing_nbytes_log = 0, ing_nfiles = -1;
+  int32_t ing_nnodes = 0;
+  uint64_t ing_pmask = 0, ing_nmask = 0;
 };
 
 // ---- launchers implemented in the .hip files ----

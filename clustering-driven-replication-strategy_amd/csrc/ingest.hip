@@ -1,0 +1,587 @@
+// ingest.hip — access-log CSV ingest on the device.
+//
+// Replaces the host tokeniser in front of the group-by: the reference reads the
+// header-less log `ts,path,op,client_node,pid` (src/access_simulator.py:61-63)
+// with spark.read.csv + to_timestamp (src/compute_features.py:19-29) and joins
+// `path` against the manifest (:37-41).  The build's host restatement of that
+// read is compute_features.load_access_log + encode (python csv.reader, the
+// ISO regex of parse_ts_us); this file produces the same encoded events,
+// directly into the resident event buffers of features.hip (c.ev_*), so
+// cdr_features_aggregate_resident runs next without a host round trip.
+//
+// Pipeline (all byte work, HBM-bound, no MFMA):
+//   K8a  nl_count   one uint4 per lane, 4 KiB tiles: count record terminators
+//   K8b  tile_scan  one workgroup: exclusive offsets over tiles, tail record
+//   K8c  nl_write   recount, workgroup scan, write each record's end index
+//   K8d  parse      256 records per workgroup: their byte span is staged
+//                   into LDS with coalesced 16-byte loads, then one lane per
+//                   record splits fields, parses the timestamp, and looks the
+//                   path / client up in device hash tables of the manifest.
+// Dictionary build (once per manifest): tab_insert (64-bit CAS, first row
+// wins via atomicMin, like dict.setdefault) + tab_verify (a distinct string
+// with an equal 64-bit hash is reported, never merged silently).
+//
+// Record semantics (python csv.reader, default dialect, on unquoted input):
+//   * records end at '\n'; a '\r' right before it is dropped; a line that is
+//     empty (or only "\r") yields no record (csv gives [] and load_access_log
+//     skips it); a last line without '\n' is still a record;
+//   * fields split at ','; missing fields are empty; an empty field is None:
+//     ts -> error, path -> -1 (no manifest row), op -> 0, client -> -1;
+//   * a '"', a NUL byte, a '\r' elsewhere, or a non-ASCII byte in the ts
+//     field is "unsupported": csv quoting / csv errors / Unicode digits are
+//     left to the host tokeniser (the caller is told, nothing is guessed).
+// Timestamps follow parse_ts_us (the regex in compute_features.py): greedy
+// digit groups are the regex's only possible match, so a left-to-right scan
+// decides it exactly.
+#include <hipcub/hipcub.hpp>
+
+#include <climits>
+#include <cstring>
+
+#include "cdr_internal.h"
+
+namespace cdr {
+
+namespace {
+
+constexpr int kTile = 4096;       // bytes per K8a/K8c workgroup (256 lanes x 16)
+constexpr int kRecPerWG = 256;    // records per K8d workgroup
+constexpr int kStage = 32768;     // LDS bytes staged per K8d workgroup
+constexpr int kNodeMissing = -3;  // a client that is no manifest primary node
+
+__device__ __forceinline__ bool is_rec_end(const uint8_t* b, int64_t p, uint8_t c1, uint8_t c2) {
+  // '\n' at p closes a non-blank line: c1 = b[p-1], c2 = b[p-2] (0 if absent)
+  if (p == 0 || c1 == '\n') return false;
+  if (c1 == '\r' && (p == 1 || c2 == '\n')) return false;
+  return true;
+}
+
+// Terminator mask of the 16 bytes at tile lane t (bit j = record ends at byte j).
+__device__ __forceinline__ unsigned lane_mask(const uint8_t* __restrict__ b, int64_t base,
+                                              uint4 v) {
+  uint8_t by[16];
+  memcpy(by, &v, 16);
+  unsigned m = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (by[j] != '\n') continue;
+    const int64_t p = base + j;
+    const uint8_t c1 = j >= 1 ? by[j - 1] : (p >= 1 ? b[p - 1] : 0);
+    const uint8_t c2 = j >= 2 ? by[j - 2] : (p >= 2 ? b[p - 2] : 0);
+    if (is_rec_end(b, p, c1, c2)) m |= 1u << j;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(256) void nl_count(const uint8_t* __restrict__ b,
+                                                long long* __restrict__ tile_cnt) {
+  const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x * 16;
+  const uint4 v = *reinterpret_cast<const uint4*>(b + base);
+  int cnt = __popc(lane_mask(b, base, v));
+  using R = hipcub::BlockReduce<int, 256>;
+  __shared__ typename R::TempStorage tmp;
+  const int tot = R(tmp).Sum(cnt);
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+// One workgroup: tile counts -> exclusive offsets (in place), then the tail
+// record (a last line without '\n'): sc[0] = records, sc[5] = 1 if the last
+// record is that tail line.
+__global__ __launch_bounds__(1024) void tile_scan(long long* __restrict__ tile, int64_t ntiles,
+                                                  const uint8_t* __restrict__ b, int64_t nbytes,
+                                                  long long* __restrict__ sc) {
+  const int64_t per = (ntiles + 1023) / 1024;
+  const int64_t lo = min<int64_t>(ntiles, threadIdx.x * per), hi = min<int64_t>(ntiles, lo + per);
+  long long s = 0;
+  for (int64_t i = lo; i < hi; ++i) s += tile[i];
+  using S = hipcub::BlockScan<long long, 1024>;
+  __shared__ typename S::TempStorage tmp;
+  long long excl, total;
+  S(tmp).ExclusiveSum(s, excl, total);
+  for (int64_t i = lo; i < hi; ++i) {
+    const long long c = tile[i];
+    tile[i] = excl;
+    excl += c;
+  }
+  if (threadIdx.x == 0) {
+    long long tail = 0;
+    if (nbytes > 0 && b[nbytes - 1] != '\n') {
+      const uint8_t c1 = b[nbytes - 1], c2 = nbytes >= 2 ? b[nbytes - 2] : '\n';
+      tail = !(c1 == '\r' && c2 == '\n');
+    }
+    sc[0] = total + tail;
+    sc[5] = tail;
+  }
+}
+
+__global__ __launch_bounds__(256) void nl_write(const uint8_t* __restrict__ b,
+                                                const long long* __restrict__ tile_off,
+                                                long long* __restrict__ ends) {
+  const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x * 16;
+  const uint4 v = *reinterpret_cast<const uint4*>(b + base);
+  unsigned m = lane_mask(b, base, v);
+  using S = hipcub::BlockScan<int, 256>;
+  __shared__ typename S::TempStorage tmp;
+  int excl;
+  S(tmp).ExclusiveSum(__popc(m), excl);
+  long long o = tile_off[blockIdx.x] + excl;
+  while (m) {
+    const int j = __ffs(m) - 1;
+    m &= m - 1;
+    ends[o++] = base + j;
+  }
+}
+
+// ---- hashing ---------------------------------------------------------------
+__host__ __device__ __forceinline__ unsigned long long fin64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z ? z : 1ull;  // 0 marks an empty slot
+}
+
+__device__ __forceinline__ unsigned long long hash_bytes(const uint8_t* p, int64_t n) {
+  unsigned long long h = 0xCBF29CE484222325ull ^ (unsigned long long)n;  // FNV-1a
+  for (int64_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+  return fin64(h);
+}
+
+__global__ void fill_i32(int32_t* __restrict__ a, int64_t n, int32_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    a[i] = v;
+}
+
+__global__ void tab_insert(const uint8_t* __restrict__ bytes, const long long* __restrict__ off,
+                           int64_t n, unsigned long long* __restrict__ key,
+                           int32_t* __restrict__ idx, unsigned long long mask) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const long long s = off[i], len = off[i + 1] - s;
+    if (len <= 0) continue;  // an empty manifest string never matches a log field
+    const unsigned long long h = hash_bytes(bytes + s, len);
+    for (unsigned long long slot = h & mask;; slot = (slot + 1) & mask) {
+      const unsigned long long old = atomicCAS(&key[slot], 0ull, h);
+      if (old == 0ull || old == h) {
+        atomicMin(&idx[slot], (int32_t)i);
+        break;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// Row j owning string (p, len) in the table, or -1.
+__device__ __forceinline__ int32_t tab_find(const uint8_t* p, int64_t len,
+                                            const unsigned long long* __restrict__ key,
+                                            const int32_t* __restrict__ idx,
+                                            unsigned long long mask,
+                                            const uint8_t* __restrict__ bytes,
+                                            const long long* __restrict__ off) {
+  const unsigned long long h = hash_bytes(p, len);
+  for (unsigned long long slot = h & mask;; slot = (slot + 1) & mask) {
+    const unsigned long long k = key[slot];
+    if (k == 0ull) return -1;
+    if (k == h) {
+      const int32_t j = idx[slot];
+      const long long s = off[j];
+      return (off[j + 1] - s == len && bytes_eq(bytes + s, p, len)) ? j : -1;
+    }
+  }
+}
+
+__global__ void tab_verify(const uint8_t* __restrict__ bytes, const long long* __restrict__ off,
+                           int64_t n, const unsigned long long* __restrict__ key,
+                           const int32_t* __restrict__ idx, unsigned long long mask,
+                           long long* __restrict__ bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const long long s = off[i], len = off[i + 1] - s;
+    if (len <= 0) continue;
+    // -1 here means another string with the same 64-bit hash owns the slot
+    if (tab_find(bytes + s, len, key, idx, mask, bytes, off) < 0) atomicMin(bad, (long long)i);
+  }
+}
+
+// ---- timestamps: compute_features.parse_ts_us ------------------------------
+__device__ __forceinline__ bool dig(uint8_t c) { return c >= '0' && c <= '9'; }
+__device__ __forceinline__ bool wsp(uint8_t c) {
+  // python str \s over ASCII: \t \n \v \f \r, 0x1c-0x1f, space
+  return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f);
+}
+
+// 0 = parsed, 1 = no match / invalid date (None), 2 = unsupported (non-ASCII)
+__device__ int parse_ts(const uint8_t* p, int n, long long* out) {
+  for (int i = 0; i < n; ++i)
+    if (p[i] >= 0x80) return 2;
+  int i = 0;
+  auto num = [&](int lo, int hi, int* v) -> bool {  // greedy lo..hi digits
+    int k = 0, x = 0;
+    while (k < hi && i < n && dig(p[i])) x = x * 10 + (p[i++] - '0'), ++k;
+    *v = x;
+    return k >= lo;
+  };
+  while (i < n && wsp(p[i])) ++i;
+  int y, mo, d, hh = 0, mi = 0, ss = 0, us = 0;
+  if (!num(4, 4, &y)) return 1;
+  if (i >= n || p[i] != '-') return 1;
+  ++i;
+  if (!num(1, 2, &mo)) return 1;
+  if (i >= n || p[i] != '-') return 1;
+  ++i;
+  if (!num(1, 2, &d)) return 1;
+  if (i + 1 < n && (p[i] == 'T' || p[i] == ' ') && dig(p[i + 1])) {
+    ++i;
+    num(1, 2, &hh);
+    if (i >= n || p[i] != ':') return 1;
+    ++i;
+    if (!num(1, 2, &mi)) return 1;
+    if (i + 1 < n && p[i] == ':' && dig(p[i + 1])) {
+      ++i;
+      num(1, 2, &ss);
+      if (i + 1 < n && p[i] == '.' && dig(p[i + 1])) {
+        ++i;
+        int k = 0;
+        while (k < 9 && i < n && dig(p[i])) {
+          if (k < 6) us = us * 10 + (p[i] - '0');
+          ++i, ++k;
+        }
+        for (; k < 6; ++k) us *= 10;
+      }
+    }
+  }
+  while (i < n && wsp(p[i])) ++i;
+  long long off = 0;
+  if (i < n && p[i] == 'Z') {
+    ++i;
+  } else if (i < n && (p[i] == '+' || p[i] == '-')) {
+    const int sign = p[i] == '-' ? -1 : 1;
+    ++i;
+    int zh, zm = 0;
+    if (!num(2, 2, &zh)) return 1;
+    if (i < n && p[i] == ':') {
+      ++i;
+      if (!num(2, 2, &zm)) return 1;
+    } else if (i < n && dig(p[i])) {
+      if (!num(2, 2, &zm)) return 1;
+    }
+    off = sign * (zh * 3600ll + zm * 60ll);
+  }
+  while (i < n && wsp(p[i])) ++i;
+  if (i != n) return 1;
+  // _days_from_civil with its validation
+  if (mo < 1 || mo > 12) return 1;
+  const bool leap = (y % 4 == 0) && (y % 100 != 0 || y % 400 == 0);
+  const int mdays = mo == 2 ? 28 + leap : 30 + ((mo + (mo >> 3)) & 1);
+  if (d < 1 || d > mdays) return 1;
+  if (hh > 23 || mi > 59 || ss > 59) return 1;
+  const long long y2 = y - (mo <= 2);
+  const long long era = (y2 >= 0 ? y2 : y2 - 399) / 400;
+  const long long yoe = y2 - era * 400;
+  const long long doy = (153 * (mo + (mo > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const long long doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  const long long days = era * 146097 + doe - 719468;
+  *out = ((days * 86400 + hh * 3600ll + mi * 60ll + ss) - off) * 1000000ll + us;
+  return 0;
+}
+
+struct Dict {
+  const unsigned long long* key;
+  const int32_t* idx;
+  unsigned long long mask;
+  const uint8_t* bytes;
+  const long long* off;
+};
+
+// sc[1] = first record with an unparseable / null timestamp, sc[2] = first
+// unsupported record, sc[3] = number of unparseable timestamps (all LLONG_MAX /
+// 0 initially).  Unparseable timestamps are stored as LLONG_MIN.
+__global__ __launch_bounds__(256) void parse(const uint8_t* __restrict__ b,
+                                             const long long* __restrict__ ends, int64_t nrec,
+                                             Dict paths, Dict nodes,
+                                             int32_t* __restrict__ o_file,
+                                             uint8_t* __restrict__ o_op,
+                                             int32_t* __restrict__ o_client,
+                                             long long* __restrict__ o_ts,
+                                             long long* __restrict__ sc) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kStage];
+  const int64_t r0 = (int64_t)blockIdx.x * kRecPerWG;
+  const int64_t r1 = min<int64_t>(nrec, r0 + kRecPerWG);
+  const int64_t lo = r0 == 0 ? 0 : ends[r0 - 1] + 1;
+  const int64_t hi = ends[r1 - 1];
+  const int64_t a0 = lo & ~(int64_t)15;
+  // byte positions below are relative to a0 (never form a pointer outside
+  // the LDS stage: an LDS pointer offset by -a0 would wrap in 32 bits)
+  const uint8_t* buf = b + a0;
+  if (hi - a0 <= kStage) {
+    const int nvec = (int)((hi - a0 + 15) >> 4);
+    for (int v = threadIdx.x; v < nvec; v += 256)
+      reinterpret_cast<uint4*>(stage)[v] = reinterpret_cast<const uint4*>(b + a0)[v];
+    __syncthreads();
+    buf = stage;
+  }
+  const int64_t r = r0 + threadIdx.x;
+  if (r >= r1) return;
+  const int64_t e0 = ends[r] - a0, lo_r = lo - a0;
+  int64_t s = e0 - 1;
+  while (s >= lo_r && buf[s] != '\n') --s;
+  ++s;
+  int64_t e = e0;
+  if (e > s && buf[e - 1] == '\r') --e;
+  // field f spans [c_{f-1} + 1, c_f) with c_{-1} = s - 1 and c_f = e past the
+  // last comma (the commas after the fourth one are irrelevant)
+  int64_t c0 = e, c1 = e, c2 = e, c3 = e;
+  int fi = 0;
+  bool unsup = false;
+  for (int64_t k = s; k < e; ++k) {
+    const uint8_t c = buf[k];
+    unsup |= (c == '"') | (c == 0) | (c == '\r');
+    if (c == ',') {
+      if (fi == 0) c0 = k;
+      else if (fi == 1) c1 = k;
+      else if (fi == 2) c2 = k;
+      else if (fi == 3) c3 = k;
+      ++fi;
+    }
+  }
+  const int64_t fs[4] = {s, min(c0 + 1, e), min(c1 + 1, e), min(c2 + 1, e)};
+  const int64_t fe[4] = {c0, c1, c2, c3};
+  long long ts = LLONG_MIN;
+  int st = 1;
+  if (fe[0] > fs[0]) st = parse_ts(buf + fs[0], (int)(fe[0] - fs[0]), &ts);
+  if (st == 2) unsup = true;
+  if (st != 0) ts = LLONG_MIN;
+  int32_t file = -1, client = -1;
+  if (fe[1] > fs[1])
+    file = tab_find(buf + fs[1], fe[1] - fs[1], paths.key, paths.idx, paths.mask, paths.bytes,
+                    paths.off);
+  uint8_t op = 0;
+  const int64_t ol = fe[2] - fs[2];
+  const uint8_t* q = buf + fs[2];
+  if (ol == 5 && q[0] == 'W' && q[1] == 'R' && q[2] == 'I' && q[3] == 'T' && q[4] == 'E') op = 1;
+  if (ol == 4 && q[0] == 'R' && q[1] == 'E' && q[2] == 'A' && q[3] == 'D') op = 2;
+  if (fe[3] > fs[3]) {
+    client = nodes.mask ? tab_find(buf + fs[3], fe[3] - fs[3], nodes.key, nodes.idx, nodes.mask,
+                                   nodes.bytes, nodes.off)
+                        : -1;
+    if (client < 0) client = kNodeMissing;
+  }
+  o_file[r] = file;
+  o_op[r] = op;
+  o_client[r] = client;
+  o_ts[r] = ts;
+  if (st != 0 && !unsup) {
+    atomicMin(&sc[1], (long long)r);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&sc[3]), 1ull);
+  }
+  if (unsup) atomicMin(&sc[2], (long long)r);
+}
+
+int gsz(int64_t work, int threads, int cap) {
+  int64_t g = (work + threads - 1) / threads;
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+uint64_t table_mask(int64_t n) {
+  uint64_t cap = 64;
+  while (cap < (uint64_t)(2 * n)) cap <<= 1;
+  return cap - 1;
+}
+
+// Builds (key, idx) for n strings given as bytes + offsets already on the device.
+void build_table(Ctx& c, DevBuf& key, DevBuf& idx, const uint8_t* bytes, const long long* off,
+                 int64_t n, uint64_t mask, const char* what) {
+  key.ensure(8 * (mask + 1));
+  idx.ensure(4 * (mask + 1));
+  HIP_CHECK(hipMemsetAsync(key.p, 0, 8 * (mask + 1), c.stream));
+  hipLaunchKernelGGL(fill_i32, dim3(gsz(mask + 1, 256, 8192)), dim3(256), 0, c.stream,
+                     idx.as<int32_t>(), (int64_t)(mask + 1), INT_MAX);
+  hipLaunchKernelGGL(tab_insert, dim3(gsz(n, 256, 8192)), dim3(256), 0, c.stream, bytes, off, n,
+                     key.as<unsigned long long>(), idx.as<int32_t>(), (unsigned long long)mask);
+  long long* bad = c.ing_scalar.as<long long>() + 4;
+  const long long init = LLONG_MAX;
+  HIP_CHECK(hipMemcpyAsync(bad, &init, 8, hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(tab_verify, dim3(gsz(n, 256, 8192)), dim3(256), 0, c.stream, bytes, off, n,
+                     key.as<unsigned long long>(), idx.as<int32_t>(), (unsigned long long)mask,
+                     bad);
+  HIP_CHECK(hipGetLastError());
+  long long hb = 0;
+  HIP_CHECK(hipMemcpyAsync(&hb, bad, 8, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (hb != LLONG_MAX)
+    CDR_FAIL(CDR_ERR_UNSUPPORTED, std::string("64-bit hash collision between two distinct ") +
+                                      what + " (row " + std::to_string(hb) + ")");
+}
+
+void upload_strings(Ctx& c, DevBuf& bytes, DevBuf& off, const char* h_bytes,
+                    const int64_t* h_off, int64_t n) {
+  const int64_t nb = h_off[n];
+  if (h_off[0] != 0 || nb < 0) CDR_FAIL(CDR_ERR_ARG, "string offsets must start at 0");
+  for (int64_t i = 0; i < n; ++i)
+    if (h_off[i + 1] < h_off[i]) CDR_FAIL(CDR_ERR_ARG, "string offsets must be non-decreasing");
+  bytes.ensure(nb > 0 ? nb : 1);
+  off.ensure(8 * (n + 1));
+  if (nb > 0) HIP_CHECK(hipMemcpyAsync(bytes.p, h_bytes, nb, hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(off.p, h_off, 8 * (n + 1), hipMemcpyHostToDevice, c.stream));
+}
+
+}  // namespace
+
+void ingest_manifest(Ctx& c, int64_t n_files, const char* pbytes, const int64_t* poff,
+                     const int32_t* primary, int32_t n_nodes, const char* nbytes,
+                     const int64_t* noff) {
+  if (n_files < 1) CDR_FAIL(CDR_ERR_ARG, "need n_files >= 1");
+  if (n_files >= (1ll << 31) - 1) CDR_FAIL(CDR_ERR_UNSUPPORTED, "n_files >= 2^31 - 1");
+  if (n_nodes < 0) CDR_FAIL(CDR_ERR_ARG, "negative n_nodes");
+  c.ing_scalar.ensure(8 * 16);
+  upload_strings(c, c.ing_pbytes, c.ing_poff, pbytes, poff, n_files);
+  c.ing_pmask = table_mask(n_files);
+  build_table(c, c.ing_pkey, c.ing_pidx, c.ing_pbytes.as<uint8_t>(),
+              c.ing_poff.as<long long>(), n_files, c.ing_pmask, "manifest paths");
+  c.ing_nnodes = n_nodes;
+  c.ing_nmask = 0;
+  if (n_nodes > 0) {
+    upload_strings(c, c.ing_nbytes, c.ing_noff, nbytes, noff, n_nodes);
+    c.ing_nmask = table_mask(n_nodes);
+    build_table(c, c.ing_nkey, c.ing_nidx, c.ing_nbytes.as<uint8_t>(),
+                c.ing_noff.as<long long>(), n_nodes, c.ing_nmask, "node names");
+  }
+  c.ev_primary.ensure(4 * n_files);
+  HIP_CHECK(hipMemcpyAsync(c.ev_primary.p, primary, 4 * n_files, hipMemcpyHostToDevice,
+                           c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.ing_nfiles = n_files;
+  c.ev_n = 0;
+  c.ev_nf = 0;
+}
+
+// Parses the resident log bytes (c.ing_log, c.ing_nbytes_log) into c.ev_*.
+// status[0] = records, [1] = first bad-timestamp record (-1 none),
+// [2] = first unsupported record (-1 none), [3] = bad-timestamp count,
+// [4]/[5] = byte span [start, end) of the record in [1] (or [2]).
+void ingest_parse(Ctx& c, int64_t* status) {
+  const int64_t nbytes = c.ing_nbytes_log;
+  const int64_t ntiles = nbytes > 0 ? ceil_div(nbytes, kTile) : 0;
+  long long* sc = c.ing_scalar.as<long long>();
+  const long long init[4] = {0, LLONG_MAX, LLONG_MAX, 0};
+  HIP_CHECK(hipMemcpyAsync(sc, init, sizeof(init), hipMemcpyHostToDevice, c.stream));
+  long long nrec = 0;
+  bool tail = false;
+  if (ntiles > 0) {
+    c.ing_blk.ensure(8 * ntiles);
+    hipLaunchKernelGGL(nl_count, dim3(ntiles), dim3(256), 0, c.stream, c.ing_log.as<uint8_t>(),
+                       c.ing_blk.as<long long>());
+    hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, c.stream, c.ing_blk.as<long long>(),
+                       ntiles, c.ing_log.as<uint8_t>(), nbytes, sc);
+    HIP_CHECK(hipGetLastError());
+    long long r6[6];
+    HIP_CHECK(hipMemcpyAsync(r6, sc, sizeof(r6), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    nrec = r6[0];
+    tail = r6[5] != 0;
+  }
+  const int64_t ne1 = nrec > 0 ? nrec : 1;
+  c.ing_ends.ensure(8 * ne1);
+  c.ev_file.ensure(4 * ne1);
+  c.ev_op.ensure(ne1);
+  c.ev_client.ensure(4 * ne1);
+  c.ev_ts.ensure(8 * ne1);
+  c.ev_out.ensure(8 * 6 * (c.ing_nfiles > 0 ? c.ing_nfiles : 1) + 64);
+  if (nrec > 0) {
+    // tile offsets were scanned in place; the tail record's end goes last
+    hipLaunchKernelGGL(nl_write, dim3(ntiles), dim3(256), 0, c.stream, c.ing_log.as<uint8_t>(),
+                       c.ing_blk.as<long long>(), c.ing_ends.as<long long>());
+    if (tail) {
+      c.h_small.ensure(64);
+      *c.h_small.as<long long>() = nbytes;
+      HIP_CHECK(hipMemcpyAsync(c.ing_ends.as<long long>() + nrec - 1, c.h_small.p, 8,
+                               hipMemcpyHostToDevice, c.stream));
+    }
+    Dict pd{c.ing_pkey.as<unsigned long long>(), c.ing_pidx.as<int32_t>(), c.ing_pmask,
+            c.ing_pbytes.as<uint8_t>(), c.ing_poff.as<long long>()};
+    Dict nd{c.ing_nkey.as<unsigned long long>(), c.ing_nidx.as<int32_t>(), c.ing_nmask,
+            c.ing_nbytes.as<uint8_t>(), c.ing_noff.as<long long>()};
+    hipLaunchKernelGGL(parse, dim3(ceil_div(nrec, kRecPerWG)), dim3(256), 0, c.stream,
+                       c.ing_log.as<uint8_t>(), c.ing_ends.as<long long>(), (int64_t)nrec, pd, nd,
+                       c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(), c.ev_client.as<int32_t>(),
+                       c.ev_ts.as<long long>(), sc);
+    HIP_CHECK(hipGetLastError());
+  }
+  long long r[4];
+  HIP_CHECK(hipMemcpyAsync(r, sc, sizeof(r), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  status[0] = nrec;
+  status[1] = r[1] == LLONG_MAX ? -1 : r[1];
+  status[2] = r[2] == LLONG_MAX ? -1 : r[2];
+  status[3] = r[3];
+  status[4] = status[5] = -1;
+  const long long which = status[2] >= 0 ? status[2] : status[1];
+  if (which >= 0) {
+    long long e[2] = {-1, 0};
+    if (which > 0)
+      HIP_CHECK(hipMemcpyAsync(e, c.ing_ends.as<long long>() + which - 1, 16,
+                               hipMemcpyDeviceToHost, c.stream));
+    else
+      HIP_CHECK(hipMemcpyAsync(e + 1, c.ing_ends.as<long long>(), 8, hipMemcpyDeviceToHost,
+                               c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    status[4] = e[0] + 1;  // the record starts after the last '\n' before it
+    status[5] = e[1];
+  }
+  c.ev_n = nrec;
+  c.ev_nf = c.ing_nfiles;
+}
+
+void ingest_log(Ctx& c, const char* bytes, int64_t nbytes, int64_t* status) {
+  if (c.ing_nfiles < 1) CDR_FAIL(CDR_ERR_STATE, "no manifest (cdr_ingest_manifest)");
+  if (nbytes < 0) CDR_FAIL(CDR_ERR_ARG, "negative nbytes");
+  const int64_t ntiles = nbytes > 0 ? ceil_div(nbytes, kTile) : 0;
+  const size_t padded = (size_t)(ntiles + 1) * kTile;  // a zero tile after the last
+  c.ing_log.ensure(padded);
+  HIP_CHECK(hipMemsetAsync(c.ing_log.as<uint8_t>() + nbytes, 0, padded - nbytes, c.stream));
+  if (nbytes > 0)
+    HIP_CHECK(hipMemcpyAsync(c.ing_log.p, bytes, nbytes, hipMemcpyHostToDevice, c.stream));
+  c.ing_nbytes_log = nbytes;
+  ingest_parse(c, status);
+}
+
+}  // namespace cdr
+
+using namespace cdr;
+
+extern "C" {
+
+int cdr_ingest_manifest(cdr_ctx* h, int64_t n_files, const char* path_bytes,
+                        const int64_t* path_off, const int32_t* primary, int32_t n_nodes,
+                        const char* node_bytes, const int64_t* node_off) {
+  CDR_TRY
+  if (!h || !path_off || !primary || (n_nodes > 0 && !node_off)) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  ingest_manifest(h->c, n_files, path_bytes, path_off, primary, n_nodes, node_bytes, node_off);
+  CDR_CATCH
+}
+
+int cdr_ingest_log(cdr_ctx* h, const char* bytes, int64_t nbytes, int64_t* status) {
+  CDR_TRY
+  if (!h || !status || (nbytes > 0 && !bytes)) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  ingest_log(h->c, bytes, nbytes, status);
+  CDR_CATCH
+}
+
+int cdr_ingest_reparse(cdr_ctx* h, int64_t* status) {
+  CDR_TRY
+  if (!h || !status) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  if (c.ing_nfiles < 1) CDR_FAIL(CDR_ERR_STATE, "no manifest (cdr_ingest_manifest)");
+  HIP_CHECK(hipSetDevice(c.device));
+  ingest_parse(c, status);
+  CDR_CATCH
+}
+
+}  // extern "C"

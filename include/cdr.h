@@ -166,6 +166,31 @@ int cdr_features_generate(cdr_ctx* ctx, int64_t n_events, int64_t n_files, uint6
 int cdr_features_aggregate_resident(cdr_ctx* ctx, int64_t* out, int64_t* max_ts_us);
 int cdr_features_events_read(cdr_ctx* ctx, int32_t* file_idx, uint8_t* op, int32_t* client,
                              int64_t* ts_us, int32_t* primary);
+/* Access-log CSV ingest on the device.  Replaces the
+ * host read of the log (src/compute_features.py:19-29: spark.read.csv of
+ * `ts,path,op,client_node,pid`, to_timestamp; the build's host restatement is
+ * compute_features.load_access_log + encode) and the path join against the
+ * manifest (:37-41).
+ * cdr_ingest_manifest: the manifest's n_files paths (UTF-8 bytes + n_files+1
+ *   int64 offsets; an empty string never matches), primary[f] (node id, -2 =
+ *   null) and the n_nodes node names whose ids primary uses (bytes + offsets).
+ *   Builds device hash tables; CDR_ERR_UNSUPPORTED on a 64-bit hash collision
+ *   between distinct strings.
+ * cdr_ingest_log: uploads the log bytes and parses them into the resident
+ *   events of cdr_features_aggregate_resident (file row or -1, op 1 WRITE /
+ *   2 READ / 0, client id or -1 null or -3 not a primary node, ts in
+ *   microseconds or INT64_MIN when the timestamp does not parse).
+ *   status[6]: records, first bad-timestamp record (-1 none), first record
+ *   the device tokeniser does not take (quotes, NUL, lone CR, non-ASCII
+ *   timestamp; -1 none), bad-timestamp count, byte span [start, end) from
+ *   the end of the previous record to the end of the reported one (blank
+ *   lines before it included).  Bad rows are reported in status, not as an error.
+ * cdr_ingest_reparse: parses the resident bytes again (benchmarks).        */
+int cdr_ingest_manifest(cdr_ctx* ctx, int64_t n_files, const char* path_bytes,
+                        const int64_t* path_off, const int32_t* primary, int32_t n_nodes,
+                        const char* node_bytes, const int64_t* node_off);
+int cdr_ingest_log(cdr_ctx* ctx, const char* bytes, int64_t nbytes, int64_t* status);
+int cdr_ingest_reparse(cdr_ctx* ctx, int64_t* status);
 /* Finalisation, src/compute_features.py:48-94.  counts: output of
  * cdr_features_aggregate; creation_s: creation_ts_epoch (double seconds, NaN
  * = null -> age 0 as na.fill does); observation_end: max ts in seconds

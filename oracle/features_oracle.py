@@ -137,3 +137,78 @@ def finalize(counts, creation_s, obs_end):
 def java_double_check(x: float) -> float:
     """Round trip helper for CSV tests."""
     return float(x) if not math.isnan(x) else x
+
+
+# ---- access-log read (csrc/ingest.hip's checker) ---------------------------
+# The reference reads the log with spark.read.csv + to_timestamp
+# (src/compute_features.py:19-29) and joins path against the manifest (:37).
+# Restated here with python's csv module (the simulator's format,
+# src/access_simulator.py:61-63) and the ISO-8601 grammar the build pins
+# (compute_features.parse_ts_us): regex match, calendar validation, UTC unless
+# a zone is given, fraction truncated to microseconds.
+import re as _re  # noqa: E402
+import datetime as _dt  # noqa: E402
+
+_ISO_RE = _re.compile(
+    r"^\s*(\d{4})-(\d{1,2})-(\d{1,2})(?:[T ](\d{1,2}):(\d{1,2})(?::(\d{1,2})(?:\.(\d{1,9}))?)?)?"
+    r"\s*(Z|[+-]\d{2}(?::?\d{2})?)?\s*$")
+TS_NULL = -(2 ** 63)
+
+
+def iso_to_us(s):
+    """ISO-8601 string -> UTC microseconds, or None (Spark null)."""
+    if s is None:
+        return None
+    m = _ISO_RE.match(s)
+    if not m:
+        return None
+    y, mo, d, hh, mi, ss, frac, zone = m.groups()
+    hh, mi, ss = int(hh or 0), int(mi or 0), int(ss or 0)
+    if hh > 23 or mi > 59 or ss > 59:
+        return None
+    yy = int(y)
+    try:
+        # datetime has no year 0 (1 BCE): it is leap like 2000 and ends 366
+        # days before 0001-01-01 (day -719162 from the epoch)
+        base = _dt.date(yy if yy >= 1 else 2000, int(mo), int(d))
+    except ValueError:
+        return None
+    if yy == 0:
+        days = (base - _dt.date(2000, 1, 1)).days - 719162 - 366
+    else:
+        days = (base - _dt.date(1970, 1, 1)).days
+    us = int((frac or "").ljust(6, "0")[:6] or 0)
+    off = 0
+    if zone and zone != "Z":
+        z = zone[1:].replace(":", "")
+        off = (-1 if zone[0] == "-" else 1) * (int(z[:2]) * 3600 + int(z[2:4] or 0) * 60)
+    return ((days * 86400 + hh * 3600 + mi * 60 + ss) - off) * 1_000_000 + us
+
+
+def encode_log(log_bytes: bytes, paths, primary):
+    """Events of a log as the device ingest encodes them: file row (first
+    manifest row of the path, -1), op (1 WRITE, 2 READ, 0), client (node id
+    of a primary name in first-appearance order, -1 null, -3 other), ts in
+    microseconds (TS_NULL when unparseable)."""
+    import io
+
+    row = {}
+    for i, p in enumerate(paths):
+        if p:
+            row.setdefault(p, i)
+    node = {}
+    for v in primary:
+        if v:
+            node.setdefault(v, len(node))
+    f, o, c, t = [], [], [], []
+    for rec in csv.reader(io.StringIO(log_bytes.decode("utf-8"), newline="")):
+        if not rec:
+            continue
+        rec = rec + [""] * (5 - len(rec))
+        f.append(row.get(rec[1], -1) if rec[1] else -1)
+        o.append(1 if rec[2] == "WRITE" else (2 if rec[2] == "READ" else 0))
+        c.append(-1 if not rec[3] else node.get(rec[3], -3))
+        u = iso_to_us(rec[0] or None)
+        t.append(TS_NULL if u is None else u)
+    return (np.array(f, dtype=np.int32), np.array(o, dtype=np.uint8),
+            np.array(c, dtype=np.int32), np.array(t, dtype=np.int64))
