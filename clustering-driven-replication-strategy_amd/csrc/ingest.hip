@@ -11,7 +11,7 @@
 //
 // Pipeline (all byte work, HBM-bound, no MFMA):
 //   K8a  nl_count   one uint4 per lane, 4 KiB tiles: count record terminators
-//   K8b  tile_scan  one workgroup: exclusive offsets over tiles, tail record
+//   K8b  hipcub exclusive scan of the tile counts + tile_total (tail record)
 //   K8c  nl_write   recount, workgroup scan, write each record's end index
 //   K8d  parse      256 records per workgroup: their byte span is staged
 //                   into LDS with coalesced 16-byte loads, then one lane per
@@ -84,34 +84,19 @@ __global__ __launch_bounds__(256) void nl_count(const uint8_t* __restrict__ b,
   if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
 }
 
-// One workgroup: tile counts -> exclusive offsets (in place), then the tail
-// record (a last line without '\n'): sc[0] = records, sc[5] = 1 if the last
-// record is that tail line.
-__global__ __launch_bounds__(1024) void tile_scan(long long* __restrict__ tile, int64_t ntiles,
-                                                  const uint8_t* __restrict__ b, int64_t nbytes,
-                                                  long long* __restrict__ sc) {
-  const int64_t per = (ntiles + 1023) / 1024;
-  const int64_t lo = min<int64_t>(ntiles, threadIdx.x * per), hi = min<int64_t>(ntiles, lo + per);
-  long long s = 0;
-  for (int64_t i = lo; i < hi; ++i) s += tile[i];
-  using S = hipcub::BlockScan<long long, 1024>;
-  __shared__ typename S::TempStorage tmp;
-  long long excl, total;
-  S(tmp).ExclusiveSum(s, excl, total);
-  for (int64_t i = lo; i < hi; ++i) {
-    const long long c = tile[i];
-    tile[i] = excl;
-    excl += c;
+// Record count after hipcub's scan of the tile counts: sc[0] = records
+// (terminators + the tail record), sc[5] = 1 if the last record is a last
+// line without '\n' (its end index nbytes is then written last).
+__global__ void tile_total(const long long* __restrict__ cnt, const long long* __restrict__ off,
+                           int64_t ntiles, const uint8_t* __restrict__ b, int64_t nbytes,
+                           long long* __restrict__ sc) {
+  long long tail = 0;
+  if (nbytes > 0 && b[nbytes - 1] != '\n') {
+    const uint8_t c1 = b[nbytes - 1], c2 = nbytes >= 2 ? b[nbytes - 2] : '\n';
+    tail = !(c1 == '\r' && c2 == '\n');
   }
-  if (threadIdx.x == 0) {
-    long long tail = 0;
-    if (nbytes > 0 && b[nbytes - 1] != '\n') {
-      const uint8_t c1 = b[nbytes - 1], c2 = nbytes >= 2 ? b[nbytes - 2] : '\n';
-      tail = !(c1 == '\r' && c2 == '\n');
-    }
-    sc[0] = total + tail;
-    sc[5] = tail;
-  }
+  sc[0] = off[ntiles - 1] + cnt[ntiles - 1] + tail;
+  sc[5] = tail;
 }
 
 __global__ __launch_bounds__(256) void nl_write(const uint8_t* __restrict__ b,
@@ -133,6 +118,18 @@ __global__ __launch_bounds__(256) void nl_write(const uint8_t* __restrict__ b,
 }
 
 // ---- hashing ---------------------------------------------------------------
+// Strings are read 4 bytes at a time: two aligned dword loads and a
+// v_alignbyte, so one code path reads the LDS stage (ds_read_b32) and global
+// memory.  Every buffer read this way carries >= 8 bytes past its end.
+__device__ __forceinline__ unsigned ld4(const uint8_t* p) {
+  const unsigned sh = (unsigned)reinterpret_cast<uintptr_t>(p) & 3u;
+  const unsigned* w = reinterpret_cast<const unsigned*>(p - sh);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+}
+__device__ __forceinline__ unsigned tail_mask(int64_t rem) {
+  return rem >= 4 ? ~0u : (1u << (8 * rem)) - 1u;
+}
+
 __host__ __device__ __forceinline__ unsigned long long fin64(unsigned long long z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -140,11 +137,34 @@ __host__ __device__ __forceinline__ unsigned long long fin64(unsigned long long 
   return z ? z : 1ull;  // 0 marks an empty slot
 }
 
+// Word-wise: each step is a bijection of the state for a fixed word and
+// injective in the word, so equal-length strings that differ in one word
+// never collide; the length seeds the state.
 __device__ __forceinline__ unsigned long long hash_bytes(const uint8_t* p, int64_t n) {
-  unsigned long long h = 0xCBF29CE484222325ull ^ (unsigned long long)n;  // FNV-1a
-  for (int64_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+  unsigned long long h = 0x9E3779B97F4A7C15ull ^ (unsigned long long)n;
+  for (int64_t k = 0; k < n; k += 4) {
+    h = (h ^ (ld4(p + k) & tail_mask(n - k))) * 0xFF51AFD7ED558CCDull;
+    h ^= h >> 32;
+  }
   return fin64(h);
 }
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int64_t n) {
+  unsigned diff = 0;
+#pragma unroll 4
+  for (int64_t k = 0; k < n; k += 4) diff |= (ld4(a + k) ^ ld4(b + k)) & tail_mask(n - k);
+  return diff == 0;
+}
+
+// Open-addressing table: slot s = {key, meta} at tab[2s], tab[2s + 1] (one
+// 16-byte load per probe), meta = byte offset << 24 | length of the owning
+// string; idx[s] = its row (the first row with that string).
+struct Dict {
+  const unsigned long long* tab;
+  const int32_t* idx;
+  unsigned long long mask;
+  const uint8_t* bytes;
+};
 
 __global__ void fill_i32(int32_t* __restrict__ a, int64_t n, int32_t v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -153,7 +173,7 @@ __global__ void fill_i32(int32_t* __restrict__ a, int64_t n, int32_t v) {
 }
 
 __global__ void tab_insert(const uint8_t* __restrict__ bytes, const long long* __restrict__ off,
-                           int64_t n, unsigned long long* __restrict__ key,
+                           int64_t n, unsigned long long* __restrict__ tab,
                            int32_t* __restrict__ idx, unsigned long long mask) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -161,7 +181,7 @@ __global__ void tab_insert(const uint8_t* __restrict__ bytes, const long long* _
     if (len <= 0) continue;  // an empty manifest string never matches a log field
     const unsigned long long h = hash_bytes(bytes + s, len);
     for (unsigned long long slot = h & mask;; slot = (slot + 1) & mask) {
-      const unsigned long long old = atomicCAS(&key[slot], 0ull, h);
+      const unsigned long long old = atomicCAS(&tab[2 * slot], 0ull, h);
       if (old == 0ull || old == h) {
         atomicMin(&idx[slot], (int32_t)i);
         break;
@@ -170,41 +190,38 @@ __global__ void tab_insert(const uint8_t* __restrict__ bytes, const long long* _
   }
 }
 
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int64_t n) {
-  for (int64_t i = 0; i < n; ++i)
-    if (a[i] != b[i]) return false;
-  return true;
+__global__ void tab_meta(const long long* __restrict__ off, unsigned long long* __restrict__ tab,
+                         const int32_t* __restrict__ idx, unsigned long long nslots) {
+  for (unsigned long long s = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+       s < nslots; s += (unsigned long long)gridDim.x * blockDim.x) {
+    if (tab[2 * s] == 0ull) continue;
+    const int32_t j = idx[s];
+    tab[2 * s + 1] = ((unsigned long long)off[j] << 24) | (unsigned long long)(off[j + 1] - off[j]);
+  }
 }
 
-// Row j owning string (p, len) in the table, or -1.
-__device__ __forceinline__ int32_t tab_find(const uint8_t* p, int64_t len,
-                                            const unsigned long long* __restrict__ key,
-                                            const int32_t* __restrict__ idx,
-                                            unsigned long long mask,
-                                            const uint8_t* __restrict__ bytes,
-                                            const long long* __restrict__ off) {
+// Row owning string (p, len), or -1.
+__device__ __forceinline__ int32_t tab_find(const uint8_t* p, int64_t len, const Dict& d) {
   const unsigned long long h = hash_bytes(p, len);
-  for (unsigned long long slot = h & mask;; slot = (slot + 1) & mask) {
-    const unsigned long long k = key[slot];
-    if (k == 0ull) return -1;
-    if (k == h) {
-      const int32_t j = idx[slot];
-      const long long s = off[j];
-      return (off[j + 1] - s == len && bytes_eq(bytes + s, p, len)) ? j : -1;
+  for (unsigned long long slot = h & d.mask;; slot = (slot + 1) & d.mask) {
+    const ulonglong2 km = reinterpret_cast<const ulonglong2*>(d.tab)[slot];
+    if (km.x == 0ull) return -1;
+    if (km.x == h) {
+      const int32_t j = d.idx[slot];
+      return ((int64_t)(km.y & 0xFFFFFFull) == len && bytes_eq(d.bytes + (km.y >> 24), p, len))
+                 ? j : -1;
     }
   }
 }
 
 __global__ void tab_verify(const uint8_t* __restrict__ bytes, const long long* __restrict__ off,
-                           int64_t n, const unsigned long long* __restrict__ key,
-                           const int32_t* __restrict__ idx, unsigned long long mask,
-                           long long* __restrict__ bad) {
+                           int64_t n, Dict d, long long* __restrict__ bad) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const long long s = off[i], len = off[i + 1] - s;
     if (len <= 0) continue;
     // -1 here means another string with the same 64-bit hash owns the slot
-    if (tab_find(bytes + s, len, key, idx, mask, bytes, off) < 0) atomicMin(bad, (long long)i);
+    if (tab_find(bytes + s, len, d) < 0) atomicMin(bad, (long long)i);
   }
 }
 
@@ -290,13 +307,73 @@ __device__ int parse_ts(const uint8_t* p, int n, long long* out) {
   return 0;
 }
 
-struct Dict {
-  const unsigned long long* key;
-  const int32_t* idx;
-  unsigned long long mask;
-  const uint8_t* bytes;
-  const long long* off;
-};
+// One record: buf = the bytes from a0 on (LDS stage or global), st = byte
+// position (relative to a0) just after the previous record, e0 = position of
+// this record's terminator.
+__device__ __forceinline__ void parse_record(const uint8_t* buf, int64_t st, int64_t e0,
+                                             const Dict& paths, const Dict& nodes, int64_t r,
+                                             int32_t* __restrict__ o_file,
+                                             uint8_t* __restrict__ o_op,
+                                             int32_t* __restrict__ o_client,
+                                             long long* __restrict__ o_ts,
+                                             long long* __restrict__ sc) {
+  int64_t s = st;  // skip the blank lines before the record ("\n", "\r\n")
+  for (;;) {
+    const uint8_t c = buf[s];
+    if (c == '\n') ++s;
+    else if (c == '\r' && buf[s + 1] == '\n') s += 2;
+    else break;
+  }
+  int64_t e = e0;
+  if (e > s && buf[e - 1] == '\r') --e;
+  // field f spans [c_{f-1} + 1, c_f) with c_{-1} = s - 1 and c_f = e past the
+  // last comma (the commas after the fourth one are irrelevant)
+  int64_t c0 = e, c1 = e, c2 = e, c3 = e;
+  int fi = 0;
+  bool unsup = false;
+  for (int64_t k = s; k < e; k += 4) {
+    const unsigned w = ld4(buf + k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (k + j >= e) break;
+      const unsigned c = (w >> (8 * j)) & 0xFFu;
+      unsup |= (c == '"') | (c == 0) | (c == '\r');
+      if (c == ',') {
+        if (fi == 0) c0 = k + j;
+        else if (fi == 1) c1 = k + j;
+        else if (fi == 2) c2 = k + j;
+        else if (fi == 3) c3 = k + j;
+        ++fi;
+      }
+    }
+  }
+  const int64_t f1 = min(c0 + 1, e), f2 = min(c1 + 1, e), f3 = min(c2 + 1, e);
+  long long ts = LLONG_MIN;
+  int stt = 1;
+  if (c0 > s) stt = parse_ts(buf + s, (int)(c0 - s), &ts);
+  if (stt == 2) unsup = true;
+  if (stt != 0) ts = LLONG_MIN;
+  int32_t file = -1, client = -1;
+  if (c1 > f1) file = tab_find(buf + f1, c1 - f1, paths);
+  uint8_t op = 0;
+  const int64_t ol = c2 - f2;
+  const unsigned ow = ld4(buf + f2);
+  if (ol == 5 && ow == 0x54495257u && buf[f2 + 4] == 'E') op = 1;  // "WRIT" + 'E'
+  if (ol == 4 && ow == 0x44414552u) op = 2;                         // "READ"
+  if (c3 > f3) {
+    client = nodes.mask ? tab_find(buf + f3, c3 - f3, nodes) : -1;
+    if (client < 0) client = kNodeMissing;
+  }
+  o_file[r] = file;
+  o_op[r] = op;
+  o_client[r] = client;
+  o_ts[r] = ts;
+  if (stt != 0 && !unsup) {
+    atomicMin(&sc[1], (long long)r);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&sc[3]), 1ull);
+  }
+  if (unsup) atomicMin(&sc[2], (long long)r);
+}
 
 // sc[1] = first record with an unparseable / null timestamp, sc[2] = first
 // unsupported record, sc[3] = number of unparseable timestamps (all LLONG_MAX /
@@ -309,77 +386,26 @@ __global__ __launch_bounds__(256) void parse(const uint8_t* __restrict__ b,
                                              int32_t* __restrict__ o_client,
                                              long long* __restrict__ o_ts,
                                              long long* __restrict__ sc) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kStage];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kStage + 16];
   const int64_t r0 = (int64_t)blockIdx.x * kRecPerWG;
   const int64_t r1 = min<int64_t>(nrec, r0 + kRecPerWG);
   const int64_t lo = r0 == 0 ? 0 : ends[r0 - 1] + 1;
   const int64_t hi = ends[r1 - 1];
   const int64_t a0 = lo & ~(int64_t)15;
-  // byte positions below are relative to a0 (never form a pointer outside
-  // the LDS stage: an LDS pointer offset by -a0 would wrap in 32 bits)
-  const uint8_t* buf = b + a0;
+  const int64_t r = r0 + threadIdx.x;
+  // byte positions are relative to a0 (an LDS pointer offset by -a0 would
+  // wrap in 32 bits)
+  const int64_t e0 = r < r1 ? ends[r] - a0 : 0;
+  const int64_t st = r < r1 ? (r == r0 ? lo : ends[r - 1] + 1) - a0 : 0;
   if (hi - a0 <= kStage) {
     const int nvec = (int)((hi - a0 + 15) >> 4);
     for (int v = threadIdx.x; v < nvec; v += 256)
       reinterpret_cast<uint4*>(stage)[v] = reinterpret_cast<const uint4*>(b + a0)[v];
     __syncthreads();
-    buf = stage;
+    if (r < r1) parse_record(stage, st, e0, paths, nodes, r, o_file, o_op, o_client, o_ts, sc);
+  } else if (r < r1) {
+    parse_record(b + a0, st, e0, paths, nodes, r, o_file, o_op, o_client, o_ts, sc);
   }
-  const int64_t r = r0 + threadIdx.x;
-  if (r >= r1) return;
-  const int64_t e0 = ends[r] - a0, lo_r = lo - a0;
-  int64_t s = e0 - 1;
-  while (s >= lo_r && buf[s] != '\n') --s;
-  ++s;
-  int64_t e = e0;
-  if (e > s && buf[e - 1] == '\r') --e;
-  // field f spans [c_{f-1} + 1, c_f) with c_{-1} = s - 1 and c_f = e past the
-  // last comma (the commas after the fourth one are irrelevant)
-  int64_t c0 = e, c1 = e, c2 = e, c3 = e;
-  int fi = 0;
-  bool unsup = false;
-  for (int64_t k = s; k < e; ++k) {
-    const uint8_t c = buf[k];
-    unsup |= (c == '"') | (c == 0) | (c == '\r');
-    if (c == ',') {
-      if (fi == 0) c0 = k;
-      else if (fi == 1) c1 = k;
-      else if (fi == 2) c2 = k;
-      else if (fi == 3) c3 = k;
-      ++fi;
-    }
-  }
-  const int64_t fs[4] = {s, min(c0 + 1, e), min(c1 + 1, e), min(c2 + 1, e)};
-  const int64_t fe[4] = {c0, c1, c2, c3};
-  long long ts = LLONG_MIN;
-  int st = 1;
-  if (fe[0] > fs[0]) st = parse_ts(buf + fs[0], (int)(fe[0] - fs[0]), &ts);
-  if (st == 2) unsup = true;
-  if (st != 0) ts = LLONG_MIN;
-  int32_t file = -1, client = -1;
-  if (fe[1] > fs[1])
-    file = tab_find(buf + fs[1], fe[1] - fs[1], paths.key, paths.idx, paths.mask, paths.bytes,
-                    paths.off);
-  uint8_t op = 0;
-  const int64_t ol = fe[2] - fs[2];
-  const uint8_t* q = buf + fs[2];
-  if (ol == 5 && q[0] == 'W' && q[1] == 'R' && q[2] == 'I' && q[3] == 'T' && q[4] == 'E') op = 1;
-  if (ol == 4 && q[0] == 'R' && q[1] == 'E' && q[2] == 'A' && q[3] == 'D') op = 2;
-  if (fe[3] > fs[3]) {
-    client = nodes.mask ? tab_find(buf + fs[3], fe[3] - fs[3], nodes.key, nodes.idx, nodes.mask,
-                                   nodes.bytes, nodes.off)
-                        : -1;
-    if (client < 0) client = kNodeMissing;
-  }
-  o_file[r] = file;
-  o_op[r] = op;
-  o_client[r] = client;
-  o_ts[r] = ts;
-  if (st != 0 && !unsup) {
-    atomicMin(&sc[1], (long long)r);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&sc[3]), 1ull);
-  }
-  if (unsup) atomicMin(&sc[2], (long long)r);
 }
 
 int gsz(int64_t work, int threads, int cap) {
@@ -393,22 +419,25 @@ uint64_t table_mask(int64_t n) {
   return cap - 1;
 }
 
-// Builds (key, idx) for n strings given as bytes + offsets already on the device.
+// Builds (tab, idx) for n strings given as bytes + offsets already on the device.
 void build_table(Ctx& c, DevBuf& key, DevBuf& idx, const uint8_t* bytes, const long long* off,
                  int64_t n, uint64_t mask, const char* what) {
-  key.ensure(8 * (mask + 1));
+  key.ensure(16 * (mask + 1));
   idx.ensure(4 * (mask + 1));
-  HIP_CHECK(hipMemsetAsync(key.p, 0, 8 * (mask + 1), c.stream));
+  HIP_CHECK(hipMemsetAsync(key.p, 0, 16 * (mask + 1), c.stream));
   hipLaunchKernelGGL(fill_i32, dim3(gsz(mask + 1, 256, 8192)), dim3(256), 0, c.stream,
                      idx.as<int32_t>(), (int64_t)(mask + 1), INT_MAX);
   hipLaunchKernelGGL(tab_insert, dim3(gsz(n, 256, 8192)), dim3(256), 0, c.stream, bytes, off, n,
                      key.as<unsigned long long>(), idx.as<int32_t>(), (unsigned long long)mask);
+  hipLaunchKernelGGL(tab_meta, dim3(gsz(mask + 1, 256, 8192)), dim3(256), 0, c.stream, off,
+                     key.as<unsigned long long>(), idx.as<int32_t>(),
+                     (unsigned long long)(mask + 1));
   long long* bad = c.ing_scalar.as<long long>() + 4;
   const long long init = LLONG_MAX;
   HIP_CHECK(hipMemcpyAsync(bad, &init, 8, hipMemcpyHostToDevice, c.stream));
+  const Dict d{key.as<unsigned long long>(), idx.as<int32_t>(), (unsigned long long)mask, bytes};
   hipLaunchKernelGGL(tab_verify, dim3(gsz(n, 256, 8192)), dim3(256), 0, c.stream, bytes, off, n,
-                     key.as<unsigned long long>(), idx.as<int32_t>(), (unsigned long long)mask,
-                     bad);
+                     d, bad);
   HIP_CHECK(hipGetLastError());
   long long hb = 0;
   HIP_CHECK(hipMemcpyAsync(&hb, bad, 8, hipMemcpyDeviceToHost, c.stream));
@@ -422,9 +451,13 @@ void upload_strings(Ctx& c, DevBuf& bytes, DevBuf& off, const char* h_bytes,
                     const int64_t* h_off, int64_t n) {
   const int64_t nb = h_off[n];
   if (h_off[0] != 0 || nb < 0) CDR_FAIL(CDR_ERR_ARG, "string offsets must start at 0");
-  for (int64_t i = 0; i < n; ++i)
+  for (int64_t i = 0; i < n; ++i) {
     if (h_off[i + 1] < h_off[i]) CDR_FAIL(CDR_ERR_ARG, "string offsets must be non-decreasing");
-  bytes.ensure(nb > 0 ? nb : 1);
+    if (h_off[i + 1] - h_off[i] >= (1 << 24))
+      CDR_FAIL(CDR_ERR_UNSUPPORTED, "string of 16 MiB or more in the manifest");
+  }
+  if (nb >= (1ll << 40)) CDR_FAIL(CDR_ERR_UNSUPPORTED, "manifest strings of 1 TiB or more");
+  bytes.ensure(nb + 16);  // ld4 reads up to 7 bytes past a string
   off.ensure(8 * (n + 1));
   if (nb > 0) HIP_CHECK(hipMemcpyAsync(bytes.p, h_bytes, nb, hipMemcpyHostToDevice, c.stream));
   HIP_CHECK(hipMemcpyAsync(off.p, h_off, 8 * (n + 1), hipMemcpyHostToDevice, c.stream));
@@ -473,11 +506,18 @@ void ingest_parse(Ctx& c, int64_t* status) {
   long long nrec = 0;
   bool tail = false;
   if (ntiles > 0) {
-    c.ing_blk.ensure(8 * ntiles);
+    c.ing_blk.ensure(16 * ntiles);
+    long long* cnt = c.ing_blk.as<long long>();
+    long long* toff = cnt + ntiles;
     hipLaunchKernelGGL(nl_count, dim3(ntiles), dim3(256), 0, c.stream, c.ing_log.as<uint8_t>(),
-                       c.ing_blk.as<long long>());
-    hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, c.stream, c.ing_blk.as<long long>(),
-                       ntiles, c.ing_log.as<uint8_t>(), nbytes, sc);
+                       cnt);
+    size_t tmp = 0;
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, toff, (int)ntiles, c.stream));
+    c.ing_tmp.ensure(tmp + 256);
+    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.ing_tmp.p, tmp, cnt, toff, (int)ntiles,
+                                               c.stream));
+    hipLaunchKernelGGL(tile_total, dim3(1), dim3(1), 0, c.stream, cnt, toff, ntiles,
+                       c.ing_log.as<uint8_t>(), nbytes, sc);
     HIP_CHECK(hipGetLastError());
     long long r6[6];
     HIP_CHECK(hipMemcpyAsync(r6, sc, sizeof(r6), hipMemcpyDeviceToHost, c.stream));
@@ -493,19 +533,19 @@ void ingest_parse(Ctx& c, int64_t* status) {
   c.ev_ts.ensure(8 * ne1);
   c.ev_out.ensure(8 * 6 * (c.ing_nfiles > 0 ? c.ing_nfiles : 1) + 64);
   if (nrec > 0) {
-    // tile offsets were scanned in place; the tail record's end goes last
+    // the tail record's end goes last
     hipLaunchKernelGGL(nl_write, dim3(ntiles), dim3(256), 0, c.stream, c.ing_log.as<uint8_t>(),
-                       c.ing_blk.as<long long>(), c.ing_ends.as<long long>());
+                       c.ing_blk.as<long long>() + ntiles, c.ing_ends.as<long long>());
     if (tail) {
       c.h_small.ensure(64);
       *c.h_small.as<long long>() = nbytes;
       HIP_CHECK(hipMemcpyAsync(c.ing_ends.as<long long>() + nrec - 1, c.h_small.p, 8,
                                hipMemcpyHostToDevice, c.stream));
     }
-    Dict pd{c.ing_pkey.as<unsigned long long>(), c.ing_pidx.as<int32_t>(), c.ing_pmask,
-            c.ing_pbytes.as<uint8_t>(), c.ing_poff.as<long long>()};
-    Dict nd{c.ing_nkey.as<unsigned long long>(), c.ing_nidx.as<int32_t>(), c.ing_nmask,
-            c.ing_nbytes.as<uint8_t>(), c.ing_noff.as<long long>()};
+    const Dict pd{c.ing_pkey.as<unsigned long long>(), c.ing_pidx.as<int32_t>(), c.ing_pmask,
+                  c.ing_pbytes.as<uint8_t>()};
+    const Dict nd{c.ing_nkey.as<unsigned long long>(), c.ing_nidx.as<int32_t>(), c.ing_nmask,
+                  c.ing_nbytes.as<uint8_t>()};
     hipLaunchKernelGGL(parse, dim3(ceil_div(nrec, kRecPerWG)), dim3(256), 0, c.stream,
                        c.ing_log.as<uint8_t>(), c.ing_ends.as<long long>(), (int64_t)nrec, pd, nd,
                        c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(), c.ev_client.as<int32_t>(),
