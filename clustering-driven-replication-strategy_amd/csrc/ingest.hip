@@ -13,7 +13,8 @@
 //   K8a  nl_count   one uint4 per lane, 4 KiB tiles: count record terminators
 //   K8b  hipcub exclusive scan of the tile counts + tile_total (tail record)
 //   K8c  nl_write   recount, workgroup scan, write each record's end index
-//   K8d  parse      256 records per workgroup: their byte span is staged
+//   K8d  parse      64 records per workgroup (one wave; measured best of
+//                   64/128/256 at ~96-128 B of LDS per record): their span is staged
 //                   into LDS with coalesced 16-byte loads, then one lane per
 //                   record splits fields, parses the timestamp, and looks the
 //                   path / client up in device hash tables of the manifest.
@@ -45,8 +46,14 @@ namespace cdr {
 namespace {
 
 constexpr int kTile = 4096;       // bytes per K8a/K8c workgroup (256 lanes x 16)
-constexpr int kRecPerWG = 256;    // records per K8d workgroup
-constexpr int kStage = 32768;     // LDS bytes staged per K8d workgroup
+#ifndef CDR_ING_REC
+#define CDR_ING_REC 64
+#endif
+#ifndef CDR_ING_STAGE
+#define CDR_ING_STAGE 8192
+#endif
+constexpr int kRecPerWG = CDR_ING_REC;  // records (lanes) per K8d workgroup
+constexpr int kStage = CDR_ING_STAGE;   // LDS bytes staged per K8d workgroup
 constexpr int kNodeMissing = -3;  // a client that is no manifest primary node
 
 __device__ __forceinline__ bool is_rec_end(const uint8_t* b, int64_t p, uint8_t c1, uint8_t c2) {
@@ -378,7 +385,7 @@ __device__ __forceinline__ void parse_record(const uint8_t* buf, int64_t st, int
 // sc[1] = first record with an unparseable / null timestamp, sc[2] = first
 // unsupported record, sc[3] = number of unparseable timestamps (all LLONG_MAX /
 // 0 initially).  Unparseable timestamps are stored as LLONG_MIN.
-__global__ __launch_bounds__(256) void parse(const uint8_t* __restrict__ b,
+__global__ __launch_bounds__(kRecPerWG) void parse(const uint8_t* __restrict__ b,
                                              const long long* __restrict__ ends, int64_t nrec,
                                              Dict paths, Dict nodes,
                                              int32_t* __restrict__ o_file,
@@ -399,7 +406,7 @@ __global__ __launch_bounds__(256) void parse(const uint8_t* __restrict__ b,
   const int64_t st = r < r1 ? (r == r0 ? lo : ends[r - 1] + 1) - a0 : 0;
   if (hi - a0 <= kStage) {
     const int nvec = (int)((hi - a0 + 15) >> 4);
-    for (int v = threadIdx.x; v < nvec; v += 256)
+    for (int v = threadIdx.x; v < nvec; v += kRecPerWG)
       reinterpret_cast<uint4*>(stage)[v] = reinterpret_cast<const uint4*>(b + a0)[v];
     __syncthreads();
     if (r < r1) parse_record(stage, st, e0, paths, nodes, r, o_file, o_op, o_client, o_ts, sc);
@@ -546,7 +553,7 @@ void ingest_parse(Ctx& c, int64_t* status) {
                   c.ing_pbytes.as<uint8_t>()};
     const Dict nd{c.ing_nkey.as<unsigned long long>(), c.ing_nidx.as<int32_t>(), c.ing_nmask,
                   c.ing_nbytes.as<uint8_t>()};
-    hipLaunchKernelGGL(parse, dim3(ceil_div(nrec, kRecPerWG)), dim3(256), 0, c.stream,
+    hipLaunchKernelGGL(parse, dim3(ceil_div(nrec, kRecPerWG)), dim3(kRecPerWG), 0, c.stream,
                        c.ing_log.as<uint8_t>(), c.ing_ends.as<long long>(), (int64_t)nrec, pd, nd,
                        c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(), c.ev_client.as<int32_t>(),
                        c.ev_ts.as<long long>(), sc);
