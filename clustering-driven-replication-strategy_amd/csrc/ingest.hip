@@ -221,6 +221,30 @@ __device__ __forceinline__ int32_t tab_find(const uint8_t* p, int64_t len, const
   }
 }
 
+// Split lookup: probe_begin hashes and issues the first slot load, so the
+// caller can overlap two lookups and the timestamp parse with its latency.
+struct Probe {
+  unsigned long long h, slot;
+  ulonglong2 km;
+};
+__device__ __forceinline__ void probe_begin(const uint8_t* p, int64_t len, const Dict& d,
+                                            Probe& q) {
+  q.h = hash_bytes(p, len);
+  q.slot = q.h & d.mask;
+  q.km = reinterpret_cast<const ulonglong2*>(d.tab)[q.slot];
+}
+__device__ __forceinline__ int32_t probe_end(const uint8_t* p, int64_t len, const Dict& d,
+                                             Probe& q) {
+  while (q.km.x != 0ull && q.km.x != q.h) {
+    q.slot = (q.slot + 1) & d.mask;
+    q.km = reinterpret_cast<const ulonglong2*>(d.tab)[q.slot];
+  }
+  if (q.km.x == 0ull) return -1;
+  const int32_t j = d.idx[q.slot];
+  return ((int64_t)(q.km.y & 0xFFFFFFull) == len && bytes_eq(d.bytes + (q.km.y >> 24), p, len))
+             ? j : -1;
+}
+
 __global__ void tab_verify(const uint8_t* __restrict__ bytes, const long long* __restrict__ off,
                            int64_t n, Dict d, long long* __restrict__ bad) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -240,7 +264,46 @@ __device__ __forceinline__ bool wsp(uint8_t c) {
 }
 
 // 0 = parsed, 1 = no match / invalid date (None), 2 = unsupported (non-ASCII)
+__device__ __forceinline__ int ts_finish(int y, int mo, int d, int hh, int mi, int ss, int us,
+                                         long long off, long long* out) {
+  // _days_from_civil with its validation
+  if (mo < 1 || mo > 12) return 1;
+  const bool leap = (y % 4 == 0) && (y % 100 != 0 || y % 400 == 0);
+  const int mdays = mo == 2 ? 28 + leap : 30 + ((mo + (mo >> 3)) & 1);
+  if (d < 1 || d > mdays) return 1;
+  if (hh > 23 || mi > 59 || ss > 59) return 1;
+  const long long y2 = y - (mo <= 2);
+  const long long era = (y2 >= 0 ? y2 : y2 - 399) / 400;
+  const long long yoe = y2 - era * 400;
+  const long long doy = (153 * (mo + (mo > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const long long doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  const long long days = era * 146097 + doe - 719468;
+  *out = ((days * 86400 + hh * 3600ll + mi * 60ll + ss) - off) * 1000000ll + us;
+  return 0;
+}
+
 __device__ int parse_ts(const uint8_t* p, int n, long long* out) {
+  if (n == 24) {
+    // fast path for the simulator's own layout "YYYY-MM-DDTHH:MM:SS.fffZ"
+    // (src/access_simulator.py:61): six word loads, straight-line digits;
+    // any other string takes the general scan below (same result).
+    unsigned w[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) w[k] = ld4(p + 4 * k);
+    auto B = [&](int i) -> unsigned { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; };
+    auto D = [&](int i) -> int { return (int)B(i) - '0'; };
+    bool ok = B(4) == '-' && B(7) == '-' && B(10) == 'T' && B(13) == ':' && B(16) == ':' &&
+              B(19) == '.' && B(23) == 'Z';
+#pragma unroll
+    for (int i = 0; i < 23; ++i) {
+      if (i == 4 || i == 7 || i == 10 || i == 13 || i == 16 || i == 19) continue;
+      ok &= (unsigned)D(i) <= 9u;
+    }
+    if (ok)
+      return ts_finish(D(0) * 1000 + D(1) * 100 + D(2) * 10 + D(3), D(5) * 10 + D(6),
+                       D(8) * 10 + D(9), D(11) * 10 + D(12), D(14) * 10 + D(15),
+                       D(17) * 10 + D(18), (D(20) * 100 + D(21) * 10 + D(22)) * 1000, 0, out);
+  }
   for (int i = 0; i < n; ++i)
     if (p[i] >= 0x80) return 2;
   int i = 0;
@@ -298,20 +361,7 @@ __device__ int parse_ts(const uint8_t* p, int n, long long* out) {
   }
   while (i < n && wsp(p[i])) ++i;
   if (i != n) return 1;
-  // _days_from_civil with its validation
-  if (mo < 1 || mo > 12) return 1;
-  const bool leap = (y % 4 == 0) && (y % 100 != 0 || y % 400 == 0);
-  const int mdays = mo == 2 ? 28 + leap : 30 + ((mo + (mo >> 3)) & 1);
-  if (d < 1 || d > mdays) return 1;
-  if (hh > 23 || mi > 59 || ss > 59) return 1;
-  const long long y2 = y - (mo <= 2);
-  const long long era = (y2 >= 0 ? y2 : y2 - 399) / 400;
-  const long long yoe = y2 - era * 400;
-  const long long doy = (153 * (mo + (mo > 2 ? -3 : 9)) + 2) / 5 + d - 1;
-  const long long doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
-  const long long days = era * 146097 + doe - 719468;
-  *out = ((days * 86400 + hh * 3600ll + mi * 60ll + ss) - off) * 1000000ll + us;
-  return 0;
+  return ts_finish(y, mo, d, hh, mi, ss, us, off, out);
 }
 
 // One record: buf = the bytes from a0 on (LDS stage or global), st = byte
@@ -355,20 +405,25 @@ __device__ __forceinline__ void parse_record(const uint8_t* buf, int64_t st, int
     }
   }
   const int64_t f1 = min(c0 + 1, e), f2 = min(c1 + 1, e), f3 = min(c2 + 1, e);
+  // both dictionary probes go out first; the timestamp parse overlaps them
+  const bool has_path = c1 > f1, has_client = c3 > f3 && nodes.mask;
+  Probe qp, qc;
+  if (has_path) probe_begin(buf + f1, c1 - f1, paths, qp);
+  if (has_client) probe_begin(buf + f3, c3 - f3, nodes, qc);
   long long ts = LLONG_MIN;
   int stt = 1;
   if (c0 > s) stt = parse_ts(buf + s, (int)(c0 - s), &ts);
   if (stt == 2) unsup = true;
   if (stt != 0) ts = LLONG_MIN;
-  int32_t file = -1, client = -1;
-  if (c1 > f1) file = tab_find(buf + f1, c1 - f1, paths);
   uint8_t op = 0;
   const int64_t ol = c2 - f2;
   const unsigned ow = ld4(buf + f2);
   if (ol == 5 && ow == 0x54495257u && buf[f2 + 4] == 'E') op = 1;  // "WRIT" + 'E'
   if (ol == 4 && ow == 0x44414552u) op = 2;                         // "READ"
+  const int32_t file = has_path ? probe_end(buf + f1, c1 - f1, paths, qp) : -1;
+  int32_t client = -1;
   if (c3 > f3) {
-    client = nodes.mask ? tab_find(buf + f3, c3 - f3, nodes) : -1;
+    client = has_client ? probe_end(buf + f3, c3 - f3, nodes, qc) : -1;
     if (client < 0) client = kNodeMissing;
   }
   o_file[r] = file;

@@ -132,6 +132,17 @@ def test_timestamp_grammar_fuzz(ctx):
         ts[i] = f"{y:04d}-{mo:02d}-{d:02d}T{int(rng.integers(0, 25)):02d}:" \
                 f"{int(rng.integers(0, 61)):02d}:{int(rng.integers(0, 61)):02d}" \
                 + rng.choice(["", ".5", ".123456", ".1234567", "Z", "+02:00"])
+    # the kernel's fixed-layout fast path: 24-byte "YYYY-MM-DDTHH:MM:SS.fffZ"
+    # strings with random digits (invalid dates and times included) and a
+    # mutated separator or digit now and then
+    for i in range(1, len(ts), 3):
+        s = list(f"{int(rng.integers(0, 10000)):04d}-{int(rng.integers(0, 14)):02d}-"
+                 f"{int(rng.integers(0, 33)):02d}T{int(rng.integers(0, 26)):02d}:"
+                 f"{int(rng.integers(0, 62)):02d}:{int(rng.integers(0, 62)):02d}."
+                 f"{int(rng.integers(0, 1000)):03d}Z")
+        if rng.random() < 0.2:
+            s[int(rng.integers(0, 24))] = str(rng.choice(list("0-T:.Z zx/+")))
+        ts[i] = "".join(s)
     lines = [f"{t},{paths[i % len(paths)]},READ,dn1,{i}" for i, t in enumerate(ts)]
     data = "\n".join(lines).encode()
     st = _ingest_and_check(ctx, data, paths, primary)
