@@ -1,5 +1,6 @@
 # One GPU call: all GPU tests, bench config 3 (with CPU leg) and 2, rocprofv3
-# kernel stats of the config-3 bench, PMC passes for configs 3 and 2.
+# kernel stats of the config-3 bench, PMC passes for configs 3 and 2, config 5,
+# and the config-4 ingest leg with its kernel stats.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -20,4 +21,7 @@ cp profiles/pmc_traffic.json gpurun_out/ || true
 timeout -k 10 300 python -u bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench5.json 2> gpurun_out/bench5.err || { echo BENCH5_FAIL; tail -20 gpurun_out/bench5.err; exit 9; }
 cat gpurun_out/bench5.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof5.log 2>&1 || { echo PROF5_FAIL; tail -20 gpurun_out/prof5.log; exit 10; }
+timeout -k 10 300 python -u bench.py --config 4-ingest --steps 10 --warmup 2 > gpurun_out/bench4i.json 2> gpurun_out/bench4i.err || { echo BENCH4I_FAIL; tail -20 gpurun_out/bench4i.err; exit 12; }
+cat gpurun_out/bench4i.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4i -o run --output-format csv -- python3 bench.py --config 4-ingest --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof4i.log 2>&1 || { echo PROF4I_FAIL; tail -20 gpurun_out/prof4i.log; exit 13; }
 echo ALL_OK
