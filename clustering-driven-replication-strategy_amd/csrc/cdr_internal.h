@@ -166,6 +166,7 @@ struct Ctx {
   DevBuf ing_log;              // log bytes, zero-padded to a whole tile
   DevBuf ing_blk;              // int64 per tile: record counts, then offsets
   DevBuf ing_tmp;              // hipcub scan scratch
+  DevBuf ing_mask;             // uint16 per 16 log bytes: record-terminator mask
   DevBuf ing_ends;             // int64 per record: byte index of its terminator
   DevBuf ing_scalar;           // int64 scratch: totals, error rows, flags
   DevBuf ing_pbytes, ing_poff; // manifest paths: bytes, int64 offsets (n+1)

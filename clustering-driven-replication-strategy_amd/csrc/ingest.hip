@@ -12,7 +12,8 @@
 // Pipeline (all byte work, HBM-bound, no MFMA):
 //   K8a  nl_count   one uint4 per lane, 4 KiB tiles: count record terminators
 //   K8b  hipcub exclusive scan of the tile counts + tile_total (tail record)
-//   K8c  nl_write   recount, workgroup scan, write each record's end index
+//   K8c  nl_write   K8a's per-lane masks (2 B per 16 log bytes), workgroup scan,
+//                   write each record's end index
 //   K8d  parse      64 records per workgroup (one wave; measured best of
 //                   64/128/256 at ~96-128 B of LDS per record): their span is staged
 //                   into LDS with coalesced 16-byte loads, then one lane per
@@ -81,10 +82,13 @@ __device__ __forceinline__ unsigned lane_mask(const uint8_t* __restrict__ b, int
 }
 
 __global__ __launch_bounds__(256) void nl_count(const uint8_t* __restrict__ b,
-                                                long long* __restrict__ tile_cnt) {
+                                                long long* __restrict__ tile_cnt,
+                                                uint16_t* __restrict__ masks) {
   const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x * 16;
   const uint4 v = *reinterpret_cast<const uint4*>(b + base);
-  int cnt = __popc(lane_mask(b, base, v));
+  const unsigned m = lane_mask(b, base, v);
+  masks[(int64_t)blockIdx.x * 256 + threadIdx.x] = (uint16_t)m;  // nl_write reads these
+  int cnt = __popc(m);
   using R = hipcub::BlockReduce<int, 256>;
   __shared__ typename R::TempStorage tmp;
   const int tot = R(tmp).Sum(cnt);
@@ -106,12 +110,13 @@ __global__ void tile_total(const long long* __restrict__ cnt, const long long* _
   sc[5] = tail;
 }
 
-__global__ __launch_bounds__(256) void nl_write(const uint8_t* __restrict__ b,
+// From nl_count's per-lane terminator masks (1/8 of the log's bytes) instead
+// of a second read of the log.
+__global__ __launch_bounds__(256) void nl_write(const uint16_t* __restrict__ masks,
                                                 const long long* __restrict__ tile_off,
                                                 long long* __restrict__ ends) {
   const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x * 16;
-  const uint4 v = *reinterpret_cast<const uint4*>(b + base);
-  unsigned m = lane_mask(b, base, v);
+  unsigned m = masks[(int64_t)blockIdx.x * 256 + threadIdx.x];
   using S = hipcub::BlockScan<int, 256>;
   __shared__ typename S::TempStorage tmp;
   int excl;
@@ -571,8 +576,9 @@ void ingest_parse(Ctx& c, int64_t* status) {
     c.ing_blk.ensure(16 * ntiles);
     long long* cnt = c.ing_blk.as<long long>();
     long long* toff = cnt + ntiles;
+    c.ing_mask.ensure(2 * 256 * ntiles);
     hipLaunchKernelGGL(nl_count, dim3(ntiles), dim3(256), 0, c.stream, c.ing_log.as<uint8_t>(),
-                       cnt);
+                       cnt, c.ing_mask.as<uint16_t>());
     size_t tmp = 0;
     HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, toff, (int)ntiles, c.stream));
     c.ing_tmp.ensure(tmp + 256);
@@ -596,7 +602,7 @@ void ingest_parse(Ctx& c, int64_t* status) {
   c.ev_out.ensure(8 * 6 * (c.ing_nfiles > 0 ? c.ing_nfiles : 1) + 64);
   if (nrec > 0) {
     // the tail record's end goes last
-    hipLaunchKernelGGL(nl_write, dim3(ntiles), dim3(256), 0, c.stream, c.ing_log.as<uint8_t>(),
+    hipLaunchKernelGGL(nl_write, dim3(ntiles), dim3(256), 0, c.stream, c.ing_mask.as<uint16_t>(),
                        c.ing_blk.as<long long>() + ntiles, c.ing_ends.as<long long>());
     if (tail) {
       c.h_small.ensure(64);
