@@ -15,7 +15,7 @@
 //   K8c  nl_write   K8a's per-lane masks (2 B per 16 log bytes), workgroup scan,
 //                   write each record's end index
 //   K8d  parse      64 records per workgroup (one wave; measured best of
-//                   64/128/256 at ~96-128 B of LDS per record): their span is staged
+//                   64/128/256 records and 5/6/8 KiB stages): their span is staged
 //                   into LDS with coalesced 16-byte loads, then one lane per
 //                   record splits fields, parses the timestamp, and looks the
 //                   path / client up in device hash tables of the manifest.
@@ -51,7 +51,7 @@ constexpr int kTile = 4096;       // bytes per K8a/K8c workgroup (256 lanes x 16
 #define CDR_ING_REC 64
 #endif
 #ifndef CDR_ING_STAGE
-#define CDR_ING_STAGE 8192
+#define CDR_ING_STAGE 6144
 #endif
 constexpr int kRecPerWG = CDR_ING_REC;  // records (lanes) per K8d workgroup
 constexpr int kStage = CDR_ING_STAGE;   // LDS bytes staged per K8d workgroup
