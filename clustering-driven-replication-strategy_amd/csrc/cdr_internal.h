@@ -159,6 +159,7 @@ struct Ctx {
   DevBuf med_vals, med_off, med_out, med_tmp, med_tmp2;
   DevBuf ev_file, ev_op, ev_client, ev_ts, ev_primary, ev_out, ev_scratch,
       ev_scratch2;
+  DevBuf ev_part;  // int64 per ts_minmax workgroup: min, max
   DevBuf fin_counts, fin_creation, fin_out, fin_red;
   int64_t ev_n = 0, ev_nf = 0;  // resident events of cdr_features_generate
 
