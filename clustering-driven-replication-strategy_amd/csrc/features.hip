@@ -174,40 +174,72 @@ __global__ void mark_runs32(const unsigned* __restrict__ keys, int64_t n, unsign
   }
 }
 
-__global__ void per_file32(const unsigned long long* __restrict__ vals, int64_t n_files,
-                           const int32_t* __restrict__ primary,
-                           const long long* __restrict__ start, const long long* __restrict__ end,
-                           long long* __restrict__ out) {
-  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n_files;
-       f += (int64_t)gridDim.x * blockDim.x) {
-    long long cnt = 0, w = 0, r = 0, loc = 0, best = 0;
-    const long long s = start[f];
-    if (s >= 0) {
-      const long long e = end[f];
-      const int pr = primary[f];
-      unsigned prev = 0xFFFFFFFFu;
-      long long run = 0;
-      for (long long i = s; i < e; ++i) {
-        const unsigned long long vv = vals[i];
-        const unsigned v = (unsigned)vv;
-        const int cl = (int)(unsigned)(vv >> 32);
-        const unsigned sec = v >> 3;
-        ++cnt;
-        w += v & 1;
-        r += (v >> 1) & 1;
-        loc += (cl >= 0 && pr >= 0 && cl == pr) ? 1 : 0;
-        run = (sec == prev) ? run + 1 : 1;
-        prev = sec;
-        best = run > best ? run : best;
-      }
+// One wave per 64 consecutive files: their events are one contiguous span of
+// the sorted values, staged into LDS with coalesced loads (spans over
+// kPerFileStage values read global memory), then one lane per file walks its
+// run.  Before: a grid-stride thread per file walking global memory (each
+// load instruction touching 64 lines; 0.74 ms at 12.5M files).
+constexpr int kPerFileStage = 768;  // 6 KiB of values per wave
+
+__device__ __forceinline__ void per_file_run(const unsigned long long* src, long long s,
+                                             long long e, int pr, long long* o) {
+  long long cnt = 0, w = 0, r = 0, loc = 0, best = 0, run = 0;
+  unsigned prev = 0xFFFFFFFFu;
+  for (long long i = s; i < e; ++i) {
+    const unsigned long long vv = src[i];
+    const unsigned v = (unsigned)vv;
+    const int cl = (int)(unsigned)(vv >> 32);
+    const unsigned sec = v >> 3;
+    ++cnt;
+    w += v & 1;
+    r += (v >> 1) & 1;
+    loc += (cl >= 0 && pr >= 0 && cl == pr) ? 1 : 0;
+    run = (sec == prev) ? run + 1 : 1;
+    prev = sec;
+    best = run > best ? run : best;
+  }
+  o[0] = cnt;
+  o[1] = w;
+  o[2] = r;
+  o[3] = loc;
+  o[4] = cnt;
+  o[5] = best;
+}
+
+__global__ __launch_bounds__(64) void per_file32(const unsigned long long* __restrict__ vals,
+                                                 int64_t n_files,
+                                                 const int32_t* __restrict__ primary,
+                                                 const long long* __restrict__ start,
+                                                 const long long* __restrict__ end,
+                                                 long long* __restrict__ out) {
+  __shared__ unsigned long long stage[kPerFileStage];
+  const int64_t f = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  long long s = -1, e = -1;
+  if (f < n_files) {
+    s = start[f];
+    if (s >= 0) e = end[f];
+  }
+  long long lo = s >= 0 ? s : LLONG_MAX, hi = e;
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o));
+    hi = max(hi, __shfl_xor(hi, o));
+  }
+  long long o6[6];
+  if (lo != LLONG_MAX && hi - lo <= kPerFileStage) {
+    for (long long i = threadIdx.x; i < hi - lo; i += 64) stage[i] = vals[lo + i];
+    __syncthreads();
+    if (f < n_files) {
+      if (s >= 0) per_file_run(stage, s - lo, e - lo, primary[f], o6);
+      else per_file_run(stage, 0, 0, 0, o6);
     }
+  } else if (f < n_files) {
+    if (s >= 0) per_file_run(vals, s, e, primary[f], o6);
+    else per_file_run(vals, 0, 0, 0, o6);
+  }
+  if (f < n_files) {
     long long* o = out + f * 6;
-    o[0] = cnt;
-    o[1] = w;
-    o[2] = r;
-    o[3] = loc;
-    o[4] = cnt;
-    o[5] = best;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) o[j] = o6[j];
   }
 }
 
@@ -395,7 +427,7 @@ void features_aggregate_resident(Ctx& c, int64_t ne, int64_t n_files, int64_t* o
                        invalid, start, end);
     HIP_CHECK(hipGetLastError());
     if (n_files > 0) {
-      hipLaunchKernelGGL(per_file32, dim3(gcap(n_files, 256, 8192)), dim3(256), 0, c.stream,
+      hipLaunchKernelGGL(per_file32, dim3(ceil_div(n_files, 64)), dim3(64), 0, c.stream,
                          vals, n_files, c.ev_primary.as<int32_t>(), start, end,
                          c.ev_out.as<long long>());
       HIP_CHECK(hipGetLastError());
