@@ -165,12 +165,20 @@ __global__ void check_sorted32(const unsigned* __restrict__ keys, int64_t n,
 
 __global__ void mark_runs32(const unsigned* __restrict__ keys, int64_t n, unsigned invalid,
                             long long* __restrict__ start, long long* __restrict__ end) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const unsigned f = keys[i];
-    if (f == invalid) continue;
-    if (i == 0 || keys[i - 1] != f) start[f] = i;
-    if (i == n - 1 || keys[i + 1] != f) end[f] = i + 1;
+  // neighbours by lane shuffles (one load per key instead of three); the
+  // loop bound is wave-uniform so every lane takes part in the shuffles
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < n;
+       base += stride) {
+    const int64_t i = base + lane;
+    const unsigned f = i < n ? keys[i] : invalid;
+    unsigned prev = __shfl(f, (lane + 63) & 63), next = __shfl(f, (lane + 1) & 63);
+    if (lane == 0 && i > 0 && i - 1 < n) prev = keys[i - 1];
+    if (lane == 63 && i + 1 < n) next = keys[i + 1];
+    if (i >= n || f == invalid) continue;
+    if (i == 0 || prev != f) start[f] = i;
+    if (i == n - 1 || next != f) end[f] = i + 1;
   }
 }
 
