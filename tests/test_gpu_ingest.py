@@ -231,3 +231,20 @@ def test_empty_logs(ctx, data):
     assert st[0] == 0
     counts, mx = ctx.features_aggregate_resident()
     assert not counts.any() and mx == -(2 ** 63)
+
+
+def test_bench_log_generator_events(ctx):
+    """The config-4 ingest leg's fixed-width log (bench.make_log): every event
+    as the checker reads it, then the group-by counts."""
+    import bench
+    import compute_features as cf
+
+    data, paths, primary = bench.make_log(200000, 20000, 7)
+    st = _ingest_and_check(ctx, data, paths, primary)
+    assert st[0] == 200000 and st[1] == -1
+    counts, mx = ctx.features_aggregate_resident()
+    f, o, c, t = fo.encode_log(data, paths, primary)
+    prim, _ = cf.encode_primary(primary)
+    exp, emx = fo.counts_from_arrays(f, o, c, t, prim, len(paths))
+    np.testing.assert_array_equal(counts, exp)
+    assert mx == emx
