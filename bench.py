@@ -7,13 +7,15 @@
 
 A step = one full Lloyd iteration of src/kmeans_plusplus.py:31-48 over the
 whole sharded data set: fused assign+update kernels on every rank, one RCCL
-SUM all-reduce of the k x (d+1) int64 partials, host means / empty-cluster
-reseed / shift — nothing skipped.  Inputs are generated on the device
-(synthetic, oracle/synth.py formula) and resident in HBM before timing; the
-initial centroids come from the sharded k-means++ seeding (timed separately,
-`seed_s`).  Default "scaling": "weak": every rank holds its own 100M-point
-shard of an N x 100M data set (the points partition; the only exchange is
-the k x (d+1) all-reduce).  `--scaling strong` keeps 100M points in total.
+SUM all-reduce of the k x (d+1) int64 partials, then the means, the shift
+and the convergence test on the device (csrc/loop.hip; the host polls once
+per timed region and would take over for an empty cluster) — nothing
+skipped; tol is disabled so exactly K steps run.  Inputs are generated on the
+device (synthetic, oracle/synth.py formula) and resident in HBM before
+timing; the initial centroids come from the sharded k-means++ seeding (timed
+separately, `seed_s`).  Default "scaling": "strong": the config's 100M points
+in total, sharded in 8192-row blocks over the N ranks (`--scaling weak`: N x
+100M).  `--gpus N` without a launcher spawns the N ranks itself.
 
 stdout carries exactly one JSON line (rank 0): native libraries that print
 banners (RCCL) are pointed at stderr.
@@ -313,6 +315,24 @@ def pmc_traffic(config: str, n_local: int):
     return float(r["hbm_bytes_per_launch"])
 
 
+def spawn_ranks(n: int) -> None:
+    """`bench.py --gpus N` without a launcher: start N rank processes with
+    torch.distributed.run (before anything touches the GPU) and exit with its
+    status; rank 0's JSON line reaches this process's stdout."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get(
+        "HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -321,13 +341,16 @@ def main() -> None:
     ap.add_argument("--config", default="3", choices=sorted(CONFIGS) + ["4", "4-ingest"])
     ap.add_argument("--n-total", type=int, default=0,
                     help="override the per-config point count (testing only)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: n points per rank (N x n in total); strong: n in total")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="strong (default): the config's n points in total over the N GPUs; "
+                         "weak: n points per GPU (N x n in total)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
     ap.add_argument("--rccl", action="store_true",
                     help="use torch.distributed (RCCL) even at WORLD_SIZE=1 (path testing)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(args.gpus)
     json_fd = os.dup(1)
     os.dup2(2, 1)  # RCCL prints its banner on stdout; keep stdout for the JSON line
 
@@ -348,7 +371,7 @@ def main() -> None:
     import numpy as np
 
     import _cdr
-    from cdr_dist import Comm, ShardedLloyd, seed_sharded, shard_rows
+    from cdr_dist import Comm, DeviceLloyd, row_fetcher, seed_sharded, shard_rows
 
     if args.config == "4":
         features_bench(args, world, rank, dist, device, json_fd)
@@ -360,8 +383,9 @@ def main() -> None:
     if args.n_total:
         n_cfg = args.n_total
     n_total = n_cfg * world if args.scaling == "weak" else n_cfg
-    if args.scaling == "weak" and world > 1:
-        desc += f" per GPU ({world} x {n_cfg} points in total)"
+    if world > 1:
+        desc += (f" per GPU ({world} x {n_cfg} points in total)" if args.scaling == "weak"
+                 else f", {world} shards of {n_cfg // world}+ points")
     begin, n_local = shard_rows(n_total, world, rank)
     comm = Comm(dist, device)
     ctx = _cdr.Context(local_rank)
@@ -376,25 +400,25 @@ def main() -> None:
     C = seed_sharded(ctx, comm, begin, n_total, k, random_state=42)
     seed_s = time.perf_counter() - t0
 
-    lloyd = ShardedLloyd(ctx, comm, n_total, begin)
+    # tol disabled: exactly warmup + steps Lloyd iterations, every one of them
+    # assign + fused update + all-reduce + means on the device
     np.random.seed(0)
-    for _ in range(args.warmup):
-        C, _ = lloyd.step(C, lloyd.row)
+    run = DeviceLloyd(ctx, C, -1.0, row_fetcher(ctx, comm, begin, d), n_total, comm)
+    if args.warmup:
+        run.advance(args.warmup)
     ctx.profile_reset(True)
     comm.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
-    marks = []
-    for _ in range(args.steps):
-        C, shift = lloyd.step(C, lloyd.row)
-        marks.append(time.perf_counter())
+    done = run.advance(args.steps, chunk=max(args.steps, 1), chunk_max=max(args.steps, 1))
     ctx.synchronize()
-    if os.environ.get("CDR_BENCH_STEP_TIMES"):
-        dts = np.diff([t0] + marks) * 1e3
-        print("step ms:", " ".join(f"{v:.3f}" for v in dts), file=sys.stderr)
     comm.barrier()
     elapsed = time.perf_counter() - t0
+    if done != args.steps:
+        raise RuntimeError(f"ran {done} of {args.steps} steps")
     prof = ctx.profile_read()
+    st = run.status
+    run.finish()
     if dist is not None:
         import torch
 
@@ -438,14 +462,18 @@ def main() -> None:
         "dtype": "f64",
         "data": "synthetic (device generator, oracle/synth.py formula; 2^-24-grid blobs)",
         "config": {"workload": desc, "n_files": n_total, "d": d, "k": k,
-                   "parallelism": f"rows sharded over {world} GPU(s), RCCL all-reduce",
+                   "parallelism": f"rows sharded over {world} GPU(s), RCCL all-reduce of "
+                                  f"k x (d+1) int64 per step",
                    "screen": "fp16 hi/lo split MFMA (certified) + exact fp64 fallback; "
-                             "int64 fixed-point sums (results bit-identical to fp64 NumPy)"},
+                             "int64 fixed-point sums (results bit-identical to fp64 NumPy)",
+                   "loop": "device-resident (means, shift, convergence test on the device; "
+                           "host polls once per timed region)"},
         "roofline": roofline,
         "step_kernels_ms": step_kernel_ms,
         "fallback_frac": fb_frac,
         "seed_s": seed_s,
-        "final_shift": float(shift) if args.steps else None,
+        "final_shift": st["shift"],
+        "final_inertia": st["inertia"],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(d, k, args.seed)

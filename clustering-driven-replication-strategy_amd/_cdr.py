@@ -71,7 +71,15 @@ SIGNATURES = {
     "cdr_profile_reset": ([_P, _I32], None),
     "cdr_profile_read": ([_P, _P], None),
     "cdr_profile_kernel": ([_P, _P, _I32], None),
-    "cdr_debug_screen_ablate": ([_P, _I32], None),
+    "cdr_points_sqdev": ([_P, _P, _PF64], None),
+    "cdr_lloyd_begin": ([_P, _P, _I32, _F64, _I32, _P, _F64], None),
+    "cdr_lloyd_enqueue_assign": ([_P, _P], None),
+    "cdr_lloyd_enqueue_finalize": ([_P, _P], None),
+    "cdr_lloyd_status": ([_P, _P, _P], None),
+    "cdr_lloyd_read": ([_P, _P, _P, _P], None),
+    "cdr_lloyd_resume": ([_P, _P, _I32, _I32], None),
+    "cdr_lloyd_end": ([_P], None),
+    "cdr_build_id": ([], ctypes.c_char_p),
     "cdr_medians_segmented": ([_P, _P, _P, _I64, _P], None),
     "cdr_medians_by_label": ([_P, _I32, _P], None),
     "cdr_features_aggregate": ([_P, _I64, _P, _P, _P, _P, _I64, _P, _P, _PI64], None),
@@ -89,8 +97,27 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+def source_build_id() -> str | None:
+    """Hash of the sources libcdr.so is built from (csrc/Makefile BUILD_ID):
+    the sorted *.hip and *.h of csrc/, then include/cdr.h; None when the
+    sources are not next to the module."""
+    import hashlib
+
+    csrc = os.path.join(_HERE, "csrc")
+    hdr = os.path.join(os.path.dirname(_HERE), "include", "cdr.h")
+    if not (os.path.isdir(csrc) and os.path.exists(hdr)):
+        return None
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h")))
+    h = hashlib.sha256()
+    for f in [os.path.join(csrc, f) for f in names] + [hdr]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libcdr.so once.  Raises ImportError when it has not been built."""
+    """Load libcdr.so once.  Raises ImportError when it has not been built or
+    was built from other sources than the ones next to it (a stale binary)."""
     global _lib
     with _lib_lock:
         if _lib is not None:
@@ -101,6 +128,18 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                 "`make -C clustering-driven-replication-strategy_amd/csrc` "
                 "(or __graft_entry__.build()); there is no CPU fallback")
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        want = source_build_id() if path == LIB_PATH else None
+        if want is not None:
+            fn = getattr(lib, "cdr_build_id", None)
+            got = None
+            if fn is not None:
+                fn.restype = ctypes.c_char_p
+                got = fn().decode()
+            if got != want:
+                raise ImportError(
+                    f"stale libcdr.so at {path}: built from sources {got}, the sources "
+                    f"here are {want}; rebuild with `make -C "
+                    "clustering-driven-replication-strategy_amd/csrc`")
         for name, (argt, rest) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.argtypes = argt
@@ -268,8 +307,52 @@ class Context:
         _check(self._lib.cdr_profile_kernel(self._h, buf, 96))
         return buf.value.decode()
 
-    def debug_ablate(self, mask: int) -> None:
-        _check(self._lib.cdr_debug_screen_ablate(self._h, int(mask)))
+    # -- device-resident Lloyd loop (csrc/loop.hip) ---------------------------
+    LL_RUNNING, LL_CONVERGED, LL_EMPTY, LL_HOST_PLAN, LL_AMBIGUOUS = 0, 1, 2, 3, 4
+
+    def points_sqdev(self, ref) -> float:
+        ref = np.ascontiguousarray(ref, dtype=np.float64)
+        v = _F64()
+        _check(self._lib.cdr_points_sqdev(self._h, _ptr(ref), ctypes.byref(v)))
+        return float(v.value)
+
+    def lloyd_begin(self, C, tol: float, ref, x2_total: float = float("nan"),
+                    round32: bool = False) -> None:
+        C = np.ascontiguousarray(C, dtype=np.float64)
+        ref = np.ascontiguousarray(ref, dtype=np.float64)
+        self._ll_shape = C.shape
+        _check(self._lib.cdr_lloyd_begin(self._h, _ptr(C), C.shape[0], float(tol),
+                                         1 if round32 else 0, _ptr(ref), float(x2_total)))
+
+    def lloyd_enqueue_assign(self, dsums_ptr: int | None = None) -> None:
+        _check(self._lib.cdr_lloyd_enqueue_assign(self._h, _P(dsums_ptr or 0)))
+
+    def lloyd_enqueue_finalize(self, dsums_ptr: int | None = None) -> None:
+        _check(self._lib.cdr_lloyd_enqueue_finalize(self._h, _P(dsums_ptr or 0)))
+
+    def lloyd_status(self) -> dict:
+        st = np.zeros(4, dtype=np.int64)
+        v = np.zeros(2, dtype=np.float64)
+        _check(self._lib.cdr_lloyd_status(self._h, _ptr(st), _ptr(v)))
+        return {"running": bool(st[0]), "steps": int(st[1]), "reason": int(st[2]),
+                "enqueued": int(st[3]), "shift": float(v[0]), "inertia": float(v[1])}
+
+    def lloyd_read(self):
+        k, d = self._ll_shape
+        C = np.empty((k, d), dtype=np.float64)
+        means = np.empty((k, d), dtype=np.float64)
+        counts = np.empty(k, dtype=np.int64)
+        _check(self._lib.cdr_lloyd_read(self._h, _ptr(C), _ptr(means), _ptr(counts)))
+        return C, means, counts
+
+    def lloyd_resume(self, C=None, add_steps: int = 0, host_plan_once: bool = False) -> None:
+        if C is not None:
+            C = np.ascontiguousarray(C, dtype=np.float64)
+        _check(self._lib.cdr_lloyd_resume(self._h, _ptr(C) if C is not None else None,
+                                          int(add_steps), 1 if host_plan_once else 0))
+
+    def lloyd_end(self) -> None:
+        _check(self._lib.cdr_lloyd_end(self._h))
 
     def debug_screen(self, C: np.ndarray):
         C = np.ascontiguousarray(C, dtype=np.float64)

@@ -15,8 +15,13 @@ the single-process run:
   ``searchsorted`` hits and a broadcast of the chosen row by its owner.
 * Lloyd (:33-48) per step: the fused device step writes k x (d+1) int64
   fixed-point sums/counts; one SUM all-reduce (integer, hence exact and
-  order-free) over RCCL; every rank then forms the identical means on host.
-  Empty clusters draw from NumPy's global RNG on every rank (same seed).
+  order-free) over RCCL; every rank then forms the identical means.  With
+  the device-resident loop (``device_lloyd``, csrc/loop.hip) the means, the
+  shift and the convergence test run on the device after the all-reduce, so
+  a step is three enqueues and no host round trip; the host only polls every
+  few steps and takes over exactly when the reference's host logic is needed
+  (empty cluster: np.random.randint on every rank in j order, the row
+  broadcast by its owner; a shift too close to tol: np.linalg.norm).
 
 ``Comm`` hides the backend: NCCL (=RCCL on ROCm) keeps the all-reduced
 tensor on the GPU; gloo (the CPU test backend) uses host tensors.
@@ -83,6 +88,35 @@ class Comm:
         self.dist.all_gather(outs, t)
         return [o.cpu().numpy()[:s] for o, s in zip(outs, sizes)]
 
+    def allreduce_sum_f64(self, v: float) -> float:
+        if not self.dist:
+            return v
+        t = self._t(np.array([v], dtype=np.float64))
+        self.dist.all_reduce(t)
+        return float(t.cpu().numpy()[0])
+
+    def lloyd_buffer(self, n: int):
+        """(buffer, pointer) of the per-step (k, d+1) int64 all-reduce: a
+        device tensor under NCCL (RCCL), a host array otherwise."""
+        if self.device is not None and self.dist:
+            import torch
+
+            t = torch.empty(n, dtype=torch.int64, device=self.device)
+            return t, t.data_ptr()
+        a = np.zeros(n, dtype=np.int64)
+        return a, a
+
+    def allreduce_inplace(self, buf) -> None:
+        if not self.dist:
+            return
+        if self.device is not None:
+            self.dist.all_reduce(buf)
+        else:
+            import torch
+
+            t = torch.from_numpy(buf)
+            self.dist.all_reduce(t)
+
     def bcast(self, arr: np.ndarray, src: int) -> np.ndarray:
         if not self.dist:
             return arr
@@ -94,6 +128,17 @@ class Comm:
 def _fetch_row(ctx, comm: Comm, owner: int, local_idx: int, d: int) -> np.ndarray:
     row = ctx.get_rows([local_idx])[0] if comm.rank == owner else np.zeros(d)
     return comm.bcast(np.asarray(row, dtype=np.float64), owner)
+
+
+def row_fetcher(ctx, comm: Comm, row_begin: int, d: int):
+    """gidx -> X[gidx] over the shards (collective: every rank calls it)."""
+    offs = np.concatenate(comm.allgather(np.array([row_begin], dtype=np.int64)))
+
+    def row(gidx: int) -> np.ndarray:
+        owner = _owner_of(offs, gidx)
+        return _fetch_row(ctx, comm, owner, gidx - int(offs[owner]), d)
+
+    return row
 
 
 def _owner_of(offsets: np.ndarray, gidx: int) -> int:
@@ -130,6 +175,96 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
         owner = int(np.flatnonzero(hits >= 0)[0])
         C[i] = _fetch_row(ctx, comm, owner, int(hits[owner]), d)
     return C
+
+
+LL_CHUNK_MAX = 64  # steps enqueued between two status polls (doubling from 2)
+
+
+class DeviceLloyd:
+    """Lloyd iterations (src/kmeans_plusplus.py:31-48) on the device-resident
+    loop of one context (csrc/loop.hip), optionally sharded over ``comm``.
+
+    ``reseed_row(gidx)`` returns X[gidx] for the reference's empty-cluster
+    reseed (:43); under ``comm`` every rank calls it (the owner broadcasts)."""
+
+    def __init__(self, ctx, C, tol: float, reseed_row, n_total: int, comm: Comm | None = None,
+                 dtype=np.float64):
+        self.ctx, self.tol, self.reseed_row, self.n_total = ctx, tol, reseed_row, n_total
+        self.comm, self.dtype = comm, np.dtype(dtype)
+        self.k, self.d = C.shape
+        ref = np.array(C[0], dtype=np.float64)  # a data row: x - ref is exact
+        x2 = ctx.points_sqdev(ref)
+        if comm is not None:
+            x2 = comm.allreduce_sum_f64(x2)
+        ctx.lloyd_begin(C, tol, ref, x2, round32=self.dtype == np.float32)
+        self.buf, self.ptr = None, None
+        if comm is not None and comm.world > 1:
+            self.buf, self.ptr = comm.lloyd_buffer(self.k * (self.d + 1))
+        self.steps = 0
+        self.converged = False
+        self.status = None
+
+    def enqueue(self, m: int) -> None:
+        for _ in range(m):
+            self.ctx.lloyd_enqueue_assign(self.ptr)
+            if self.buf is not None:
+                self.comm.allreduce_inplace(self.buf)
+            self.ctx.lloyd_enqueue_finalize(self.ptr)
+
+    def advance(self, max_steps: int, chunk: int = 2, chunk_max: int = LL_CHUNK_MAX) -> int:
+        """Run up to max_steps more steps (fewer on convergence); returns the
+        number of steps the reference would have taken."""
+        start = self.steps
+        target = start + max_steps
+        while self.steps < target and not self.converged:
+            self.enqueue(min(chunk, target - self.steps))
+            chunk = min(2 * chunk, chunk_max)
+            st = self.status = self.ctx.lloyd_status()
+            self.steps = st["steps"]
+            if st["running"]:
+                continue
+            if st["reason"] == self.ctx.LL_CONVERGED:
+                self.converged = True
+                break
+            if st["reason"] == self.ctx.LL_HOST_PLAN:
+                self.ctx.lloyd_resume(host_plan_once=True)
+                continue
+            # empty cluster or a shift too close to tol: the reference's host
+            # logic for this one step (kmeans_plusplus.py:37-48)
+            C_cur, means, counts = self.ctx.lloyd_read()
+            new = np.empty((self.k, self.d), dtype=self.dtype)
+            new[...] = means
+            for j in np.flatnonzero(counts == 0):  # j order, as the reference draws
+                new[j] = self.reseed_row(np.random.randint(0, self.n_total))
+            shift = np.linalg.norm(new - C_cur.astype(self.dtype))
+            self.ctx.lloyd_resume(new, add_steps=1)
+            self.steps += 1
+            if shift < self.tol:
+                self.converged = True
+        return self.steps - start
+
+    def finish(self):
+        """(centroids as dtype, status of the last step); ends the loop."""
+        try:
+            C = self.ctx.lloyd_read()[0].astype(self.dtype)
+            st = self.ctx.lloyd_status()
+        finally:
+            self.ctx.lloyd_end()
+        return C, st
+
+
+def device_lloyd(ctx, C, max_iter: int, tol: float, reseed_row, n_total: int,
+                 comm: Comm | None = None, dtype=np.float64):
+    """max_iter Lloyd steps (fewer on convergence) on the device loop:
+    (centroids as ``dtype``, status dict of the last step: steps, shift,
+    inertia)."""
+    run = DeviceLloyd(ctx, C, tol, reseed_row, n_total, comm, dtype)
+    try:
+        run.advance(max_iter)
+    except BaseException:
+        ctx.lloyd_end()
+        raise
+    return run.finish()
 
 
 class ShardedLloyd:
@@ -176,6 +311,13 @@ class ShardedLloyd:
         return _fetch_row(self.ctx, self.comm, owner, gidx - int(offs[owner]), self.d)
 
     def run(self, C: np.ndarray, max_iter: int, tol: float = 1e-4):
+        """max_iter Lloyd steps (fewer on convergence) on the device loop."""
+        C, self.last_status = device_lloyd(self.ctx, C, max_iter, tol, self.row, self.n_total,
+                                           self.comm)
+        return C
+
+    def run_host(self, C: np.ndarray, max_iter: int, tol: float = 1e-4):
+        """The same iterations with the host forming the means every step."""
         for _ in range(max_iter):
             C, shift = self.step(C, self.row)
             if shift < tol:

@@ -1,6 +1,7 @@
 // cdr_internal.h — shared definitions for the libcdr HIP sources (gfx950 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 #include <string>
 #include <vector>
@@ -124,12 +125,17 @@ struct Ctx {
   hipEvent_t up_event = nullptr;  // recorded after that upload
   bool up_pending = false;
   int64_t last_fallback = 0;
-  // profiling (cdr_profile_*): HIP events on the context stream around the
-  // screen kernel and around the whole step (screen + reduce + fallback)
-  bool prof_on = false, prof_pending = false;
-  hipEvent_t pe[3] = {nullptr, nullptr, nullptr};
+  // profiling (cdr_profile_*): per profiled step three HIP events on the
+  // context stream (step start, after the screen kernel, step end), taken
+  // from a pool and only resolved by cdr_profile_read, so that profiling
+  // never makes the host wait inside an enqueued loop
+  bool prof_on = false;
+  std::vector<hipEvent_t> prof_pool;
+  size_t prof_used = 0;  // events of this profiling session (triples)
+  int64_t prof_cur = -1; // first event of the current step's triple, -1 none
   double prof_screen_ms = 0.0, prof_step_ms = 0.0, prof_fb_points = 0.0;
   int64_t prof_launches = 0;
+  DevBuf fb_accum;  // int64: fallback points summed over the steps (publish32)
   char prof_kernel[96] = {0};  // name of the last screen kernel launched
   int fb_layout = -1;     // screen32: nwaves the fb_count buffer was zeroed for
   int fb_total_slot = 0;  // fb_count index holding the last step's fallback total
@@ -142,7 +148,21 @@ struct Ctx {
   bool run_valid = false;
   int32_t run_k = 0;
   bool last_delta = false;
-  int screen_ablate = 0;  // timing experiments only
+#ifdef CDR_EXPERIMENTS
+  int screen_ablate = 0;  // timing experiments only (never in the product build)
+#endif
+
+  // ---- device-resident Lloyd loop (loop.hip) ----
+  // ll_C current centroids (k x d fp64), ll_new last means (k x d) + counts
+  // (k int64), ll_sums the step's (k, d+1) sums when the caller passes no
+  // buffer, ll_ref the inertia reference row + mu (2d fp64), ll_state int64[8]:
+  // [0] active, [1] steps done, [2] stop reason, [3] shift^2 bits,
+  // [4] inertia bits.
+  DevBuf ll_C, ll_new, ll_sums, ll_ref, ll_state;
+  bool ll_on = false, ll_devplan = false, ll_hostplan_once = false;
+  int32_t ll_k = 0, ll_flags = 0;
+  double ll_tol = 0.0, ll_x2 = 0.0, ll_xxmax = 0.0, ll_l1x = 0.0;
+  int64_t ll_enqueued = 0;
 
   // ---- seeding ----
   DevBuf dmin;        // double[n_pad]
@@ -209,6 +229,26 @@ void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
                        double* out);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Profiling (lloyd.hip): prof_step_begin starts a profiled step when
+// profiling is on (false otherwise); prof_mark(c, i) records event i of it
+// (0 start, 1 after the screen kernel, 2 end).
+bool prof_step_begin(Ctx& c);
+void prof_mark(Ctx& c, int i);
+
+// fp64 -> fp16 with one round-to-nearest-even, identical on host and device
+// (the screen fragments are built by both: build_plan32 and plan32_kernel).
+// |v| >= 65520 gives +-inf, NaN stays NaN.
+__host__ __device__ inline _Float16 f64_to_f16(double v) {
+  const double a = fabs(v);
+  if (!(a == a)) return (_Float16)v;
+  if (a >= 65520.0) return v > 0 ? (_Float16)INFINITY : (_Float16)(-INFINITY);
+  int e;
+  (void)frexp(a, &e);                        // a in [2^(e-1), 2^e)
+  const int ue = (e - 1 > -14 ? e - 1 : -14) - 10;  // fp16 spacing of a: 2^ue
+  const double r = ldexp(rint(ldexp(a, -ue)), ue);  // exact: fits fp16
+  return (_Float16)copysign(r, v);
+}
 
 }  // namespace cdr
 

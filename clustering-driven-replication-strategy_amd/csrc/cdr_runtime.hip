@@ -282,6 +282,7 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
   c.d = d;
   c.n_pad = ceil_div(n > 0 ? n : 1, kSeedBlock) * kSeedBlock;
   c.run_valid = false;
+  c.ll_on = false;
   c.labels.ensure(sizeof(int32_t) * c.n_pad);
   HIP_CHECK(hipMemsetAsync(c.labels.p, 0, sizeof(int32_t) * c.n_pad, c.stream));
 }
@@ -377,7 +378,9 @@ int cdr_create(int device, cdr_ctx** out) {
     HIP_CHECK(e);
   }
   h->c.own_stream = true;
+#ifdef CDR_EXPERIMENTS
   if (const char* ab = getenv("CDR_SCREEN_ABLATE")) h->c.screen_ablate = atoi(ab);
+#endif
   *out = h;
   CDR_CATCH
 }
@@ -394,12 +397,14 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.seed_scalar, &c.med_vals, &c.med_off, &c.med_out, &c.med_tmp,
                     &c.med_tmp2, &c.ev_file, &c.ev_op, &c.ev_client, &c.ev_ts,
                     &c.ev_primary, &c.ev_out, &c.ev_scratch, &c.ev_scratch2,
-                    &c.fin_counts, &c.fin_creation, &c.fin_out, &c.fin_red, &c.run_sums};
+                    &c.fin_counts, &c.fin_creation, &c.fin_out, &c.fin_red, &c.run_sums,
+                    &c.fb_accum, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
+                    &c.ll_state};
   for (DevBuf* b : bufs) b->release();
   c.h_small.release();
   c.h_up.release();
   if (c.up_event) (void)hipEventDestroy(c.up_event);
-  for (hipEvent_t& e : c.pe)
+  for (hipEvent_t& e : c.prof_pool)
     if (e) (void)hipEventDestroy(e);
   if (c.own_stream && c.stream) (void)hipStreamDestroy(c.stream);
   delete h;

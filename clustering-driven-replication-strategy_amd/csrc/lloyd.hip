@@ -950,6 +950,7 @@ static int fast_blocks_per_cu(int DCH, int KT, size_t lds) {
 
 static void dispatch_fast(int DCH, int KT, bool nonneg, bool full, dim3 grid, size_t lds,
                           hipStream_t s, const ScreenArgs& a) {
+#ifdef CDR_EXPERIMENTS
   if (a.ablate && DCH == 1 && KT == 4 && nonneg && full) {  // timing experiments
     switch (a.ablate) {
       case 1: hipLaunchKernelGGL((screen_fast<1, 4, true, true, 1>), grid, dim3(256), lds, s, a); return;
@@ -962,6 +963,7 @@ static void dispatch_fast(int DCH, int KT, bool nonneg, bool full, dim3 grid, si
       default: break;
     }
   }
+#endif
   if (DCH == 1 && KT == 1) launch_fast<1, 1>(nonneg, full, grid, lds, s, a);
   else if (DCH == 1 && KT == 2) launch_fast<1, 2>(nonneg, full, grid, lds, s, a);
   else if (DCH == 1 && KT == 3) launch_fast<1, 3>(nonneg, full, grid, lds, s, a);
@@ -1012,19 +1014,46 @@ float g_dbg_thr[2] = {0.f, 0.f};
 bool screen32_supported(const Ctx& c, int k);
 bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof);
 bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* hout, bool prof,
-                   float* dbg, float* thr_out);
+                   float* dbg, float* thr_out, long long* gate);
 
-// Fold the last step's event pair into the profile accumulators.
+// Adds a screen's published fallback total to the profiling accumulator.
+__global__ void fb_accumulate(const int32_t* __restrict__ total, long long* __restrict__ acc) {
+  if (threadIdx.x == 0) acc[0] += total[0];
+}
+
+bool prof_step_begin(Ctx& c) {
+  c.prof_cur = -1;
+  if (!c.prof_on) return false;
+  if (c.prof_used + 3 > (size_t)(3 << 16)) return false;  // session cap: 65536 steps
+  while (c.prof_pool.size() < c.prof_used + 3) {
+    hipEvent_t e = nullptr;
+    HIP_CHECK(hipEventCreate(&e));
+    c.prof_pool.push_back(e);
+  }
+  c.prof_cur = (int64_t)c.prof_used;
+  c.prof_used += 3;
+  return true;
+}
+
+void prof_mark(Ctx& c, int i) {
+  if (c.prof_cur >= 0) HIP_CHECK(hipEventRecord(c.prof_pool[(size_t)c.prof_cur + i], c.stream));
+}
+
+// Fold every recorded step's events into the profile accumulators (waits
+// for the last one).
 void prof_collect(Ctx& c) {
-  if (!c.prof_pending) return;
-  HIP_CHECK(hipEventSynchronize(c.pe[2]));
-  float a = 0.f, b = 0.f;
-  HIP_CHECK(hipEventElapsedTime(&a, c.pe[0], c.pe[1]));
-  HIP_CHECK(hipEventElapsedTime(&b, c.pe[0], c.pe[2]));
-  c.prof_screen_ms += a;
-  c.prof_step_ms += b;
-  c.prof_launches += 1;
-  c.prof_pending = false;
+  if (c.prof_used == 0) return;
+  HIP_CHECK(hipEventSynchronize(c.prof_pool[c.prof_used - 1]));
+  for (size_t t = 0; t + 3 <= c.prof_used; t += 3) {
+    float a = 0.f, b = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&a, c.prof_pool[t], c.prof_pool[t + 1]));
+    HIP_CHECK(hipEventElapsedTime(&b, c.prof_pool[t], c.prof_pool[t + 2]));
+    c.prof_screen_ms += a;
+    c.prof_step_ms += b;
+    c.prof_launches += 1;
+  }
+  c.prof_used = 0;
+  c.prof_cur = -1;
 }
 
 void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_dev) {
@@ -1041,8 +1070,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   const float fx = (float)std::ldexp(1.0, c.scale_bits);
   const int cus = lloyd_num_cus(c.device);
 
-  prof_collect(c);
-  const bool prof = c.prof_on;
+  const bool prof = prof_step_begin(c);
   bool screened = false;
   // screen32 uploads its own operands (one pinned copy) and leaves the totals
   // in c.run_sums; it copies them to a device `out` itself
@@ -1052,7 +1080,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   bool s32 = screen32_supported(c, k) &&
              screen32_step(c, C, k, out_dev ? dout : nullptr,
                            out_dev ? nullptr : c.h_small.as<long long>(), prof, g_dbg_ptr,
-                           g_dbg_ptr ? g_dbg_thr : nullptr);
+                           g_dbg_ptr ? g_dbg_thr : nullptr, nullptr);
   if (!s32) {
     upload_centroids(c, C, k);
     HIP_CHECK(hipMemsetAsync(dout, 0, sizeof(long long) * len, c.stream));
@@ -1108,13 +1136,17 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     a.fb_count = c.fb_count.as<int32_t>();
     a.fb_cap = cap;
     a.dbg = g_dbg_ptr;
+#ifdef CDR_EXPERIMENTS
     a.ablate = c.screen_ablate;
+#else
+    a.ablate = 0;
+#endif
     const bool dbg = g_dbg_ptr != nullptr;
     if (pl.fast)
       snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_fast<%d,%d>", pl.DCH, pl.KT);
     else
       snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_kernel<%d>", pl.DCH);
-    if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
+    if (prof) prof_mark(c, 0);
     if (pl.fast) {
       bool nonneg = true;
       for (int f = 0; f < d; ++f) nonneg = nonneg && c.fmin[f] >= 0.0;
@@ -1128,7 +1160,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
       }
     }
     HIP_CHECK(hipGetLastError());
-    if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
+    if (prof) prof_mark(c, 1);
     // fallback first: it adds into the screen's partial rows
     const size_t fb_lds = (size_t)k * KS * 8;
     const size_t fb_lds_c = fb_lds + (size_t)k * d * 8;
@@ -1170,9 +1202,17 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     HIP_CHECK(hipGetLastError());
   }
   c.last_screened = screened;
-  if (prof && screened) {
-    HIP_CHECK(hipEventRecord(c.pe[2], c.stream));
-    c.prof_pending = true;
+  if (prof) {
+    if (!screened) {  // no screen kernel: an empty triple keeps the pairing
+      prof_mark(c, 0);
+      prof_mark(c, 1);
+    } else if (!s32) {  // screen32's publish32 sums its fallback total itself
+      c.fb_accum.ensure(sizeof(long long));
+      hipLaunchKernelGGL(fb_accumulate, dim3(1), dim3(64), 0, c.stream,
+                         c.fb_count.as<int32_t>() + c.fb_total_slot, c.fb_accum.as<long long>());
+      HIP_CHECK(hipGetLastError());
+    }
+    prof_mark(c, 2);
   }
   c.last_k = k;
   c.have_labels = true;
@@ -1194,8 +1234,6 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     }
     memcpy(out, c.h_small.p, sizeof(long long) * len);
     c.last_fallback = screened ? fb : c.n;
-    if (c.prof_pending) c.prof_fb_points += fb;
-    prof_collect(c);
   } else {
     c.last_fallback = -1;  // unknown until cdr_lloyd_stats synchronises
   }
@@ -1301,25 +1339,31 @@ int cdr_lloyd_stats(cdr_ctx* h, int64_t* n_fallback) {
   CDR_CATCH
 }
 
+#ifdef CDR_EXPERIMENTS
+// Timing experiments only (not in the product build or include/cdr.h): skip
+// parts of the screen kernel; results are garbage while mask != 0.
 int cdr_debug_screen_ablate(cdr_ctx* h, int32_t mask) {
   CDR_TRY
   if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
   h->c.screen_ablate = mask;
   CDR_CATCH
 }
+#endif
 
 int cdr_profile_reset(cdr_ctx* h, int32_t enable) {
   CDR_TRY
   if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
   Ctx& c = h->c;
   HIP_CHECK(hipSetDevice(c.device));
-  for (int i = 0; i < 3; ++i)
-    if (!c.pe[i]) HIP_CHECK(hipEventCreate(&c.pe[i]));
-  if (c.prof_pending) HIP_CHECK(hipEventSynchronize(c.pe[2]));
-  c.prof_pending = false;
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.prof_used = 0;
+  c.prof_cur = -1;
   c.prof_on = enable != 0;
   c.prof_screen_ms = c.prof_step_ms = c.prof_fb_points = 0.0;
   c.prof_launches = 0;
+  c.fb_accum.ensure(sizeof(long long));
+  HIP_CHECK(hipMemsetAsync(c.fb_accum.p, 0, sizeof(long long), c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
   CDR_CATCH
 }
 
@@ -1329,10 +1373,16 @@ int cdr_profile_read(cdr_ctx* h, double* out) {
   Ctx& c = h->c;
   HIP_CHECK(hipSetDevice(c.device));
   prof_collect(c);
+  long long fb = 0;
+  if (c.fb_accum.p) {
+    HIP_CHECK(hipMemcpyAsync(&fb, c.fb_accum.p, sizeof(long long), hipMemcpyDeviceToHost,
+                             c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+  }
   out[0] = c.prof_screen_ms;
   out[1] = (double)c.prof_launches;
   out[2] = c.prof_step_ms;
-  out[3] = c.prof_fb_points;
+  out[3] = c.prof_fb_points + (double)fb;
   CDR_CATCH
 }
 

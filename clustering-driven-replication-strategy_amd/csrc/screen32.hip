@@ -68,6 +68,8 @@ struct S32Args {
   int fb_cap;
   float* dbg;  // tests only: screen values (n_pad x dbg_ld) when non-null
   int dbg_ld;   // ceil(k / 16) * 16 (the cdr_debug_screen layout)
+  const long long* gate;  // device loop: run only while gate[0] != 0 (null: always)
+  const float* thr_dev;   // device loop: thr0 written by plan32_kernel (null: thr0)
 };
 
 __device__ __forceinline__ unsigned pack_h2(float a, float b) {
@@ -227,6 +229,7 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int KP = 32 * MT;
   constexpr int NF = 8 * QH;
+  if (a.gate && a.gate[0] == 0) return;  // device loop stopped: uniform exit
   double* tsum = reinterpret_cast<double*>(smem);                      // [NF][KP]
   int* tcnt = reinterpret_cast<int*>(tsum + (size_t)NF * KP);          // [KP]
   double* cs = reinterpret_cast<double*>(tcnt + KP);                   // [k][17]
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
       ms[u][i] = f < a.d ? a.mu_s[f] : 0.0f;
     }
   }
-  const float sig = a.sig, thr0 = a.thr0, thr_rel = a.thr_rel;
+  const float sig = a.sig, thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
   const f4* Xq = reinterpret_cast<const f4*>(a.X);
   const int wpb = blockDim.x >> 6;
   const int64_t ngroups = a.n_pad >> 6;
@@ -635,8 +638,10 @@ constexpr int kR32Slices = 16;
 __global__ __launch_bounds__(256) void reduce32(const double* __restrict__ part, int nwg, int k,
                                                 int d, int d4, int KP, double fx,
                                                 const long long* __restrict__ muf,
-                                                unsigned long long* __restrict__ out) {
+                                                unsigned long long* __restrict__ out,
+                                                const long long* __restrict__ gate) {
   __shared__ long long red[4][64];
+  if (gate && gate[0] == 0) return;
   const int cells = k * (d + 1);
   const int u = blockIdx.x * 64 + (threadIdx.x & 63);
   const int sub = threadIdx.x >> 6;
@@ -673,7 +678,10 @@ __global__ __launch_bounds__(256) void reduce32(const double* __restrict__ part,
 __global__ __launch_bounds__(256) void publish32(const long long* __restrict__ out, int cells,
                                                  long long* __restrict__ dout,
                                                  long long* __restrict__ hout,
-                                                 int* __restrict__ fbc, int nwaves) {
+                                                 int* __restrict__ fbc, int nwaves,
+                                                 long long* __restrict__ fb_acc,
+                                                 const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
   for (int i = threadIdx.x; i < cells; i += blockDim.x) {
     const long long v = out[i];
     if (dout) dout[i] = v;
@@ -684,7 +692,15 @@ __global__ __launch_bounds__(256) void publish32(const long long* __restrict__ o
     fbc[nwaves] = 0;
     fbc[nwaves + 1] = fb;
     if (hout) hout[cells] = fb;
+    if (fb_acc) fb_acc[0] += fb;
   }
+}
+
+// Zeroes n int64 (the running sums before a full, non-DELTA step) unless
+// the device loop has stopped.
+__global__ void zero_gated(long long* __restrict__ p, int n, const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0;
 }
 
 // xt = (x - mu) 2^sigma = fma(x, 2^sigma, -mu 2^sigma), exact (Ctx::pre_ok).
@@ -709,7 +725,7 @@ __global__ void precenter_kernel(const float* __restrict__ x, int64_t n, int64_t
 struct Plan32 {
   int QH, MT;
   float thr0, thr_rel;
-  std::vector<h8> frag;      // [MT][3][64]
+  std::vector<h8> frag;      // [MT][2][64]
   std::vector<float> cinit;  // [MT][16][64]
 };
 
@@ -732,6 +748,83 @@ bool screen32_supported(const Ctx& c, int k) {
   const int64_t groups = c.n_pad / 64;
   const int64_t per_wg = ceil_div(groups, lloyd_num_cus(c.device)) * 64;
   return per_wg < (int64_t(1) << 23);
+}
+
+// Point side of the bound: |xhat_f| <= max(fmax - mu, mu - fmin) 2^sigma.
+void plan32_point_side(const Ctx& c, double& xxmax, double& l1x) {
+  const double sc = std::ldexp(1.0, c.sigma);
+  xxmax = 0.0;
+  l1x = 0.0;
+  for (int f = 0; f < c.d; ++f) {
+    const double dev =
+        std::fmax(c.fmax[f] - (double)c.mu[f], (double)c.mu[f] - c.fmin[f]) * sc;
+    xxmax += dev * dev;
+    l1x += dev;
+  }
+  xxmax *= 1.0 + 1e-6;
+}
+
+// Certification constants from the centroid side (ccmax =
+// max ||chat||^2, l1c = max ||chat||_1) and the point side.  Shared by the
+// host plan (build_plan32) and the device plan (plan32_kernel): the same
+// fp64 operations in the same order, so both give the same bits.
+__host__ __device__ inline void plan32_bounds(double ccmax, double l1c, double xxmax, double l1x,
+                                              int QH, double& D, float& thr0) {
+  const double u = ldexp(1.0, -24);
+  const int nmfma = QH == 2 ? 3 : 2;
+  const double N = 16.0 * nmfma + 1.0;
+  // fp32 accumulation inside the MFMA chain, order unknown, each addition
+  // erring by at most 2u (no assumption on internal extra precision)
+  const double gamma = 2.0 * u * N / (1.0 - 2.0 * u * N);
+  // D >= max ||xhat||^2 + margin so that every screen value stays >= 0
+  const double E0 = gamma * (2.0 * ccmax + 2.0 * xxmax + 4.0) + 2.4 * ldexp(1.0, -22) *
+                    (ccmax + xxmax) + u * (ccmax + 2.0 * xxmax + 4.0) +
+                    ldexp(1.0, -24) * (l1c + l1x) + ldexp(1.0, -40);
+  D = xxmax + 4.0 * E0 + ldexp(1.0, -20);
+  const double sum_abs = (ccmax + D) * (1.0 + u) + (1.0 + ldexp(1.0, -9)) * (ccmax + xxmax);
+  const double E = gamma * sum_abs + 2.4 * ldexp(1.0, -22) * (ccmax + xxmax) + u * (ccmax + D) +
+                   ldexp(1.0, -24) * (l1c + l1x) + ldexp(1.0, -46) * (ccmax + D);
+  // reference slack: the fp64 distances and roots must not tie or flip
+  const double Wmax = (sqrt(ccmax) + sqrt(xxmax)) * (sqrt(ccmax) + sqrt(xxmax));
+  const double slack = ldexp(Wmax + 1.0, -38);
+  thr0 = (float)((2.0 * E + slack) * 1.001);
+}
+
+// Fragments of one lane of 32-centroid tile m: A1 = -2 chi, A3 = -2 clo (the
+// lane-half quad layout of screen32), and its 16 C-operand values.
+__host__ __device__ inline void plan32_lane(const double* ch, const double* cc, double D, int k,
+                                            int d, int QH, int m, int lane, h8& A1, h8& A3,
+                                            float* cin16) {
+  const int h = lane >> 5;
+  const int j = 32 * m + (lane & 31);  // A row
+  for (int i = 0; i < 8; ++i) {
+    A1[i] = (_Float16)0.0f;
+    A3[i] = (_Float16)0.0f;
+  }
+  for (int uq = 0; uq < QH; ++uq) {
+    const int q = QH * h + uq;
+    for (int i = 0; i < 4; ++i) {
+      const int f = 4 * q + i;
+      if (j >= k || f >= d) continue;
+      const double v = ch[(size_t)j * d + f];
+      const _Float16 hi = f64_to_f16(v);
+      const _Float16 lo = f64_to_f16(v - (double)hi);
+      const _Float16 m2hi = f64_to_f16(-2.0 * (double)hi);
+      const _Float16 m2lo = f64_to_f16(-2.0 * (double)lo);
+      if (QH == 1) {  // H = [hi(q0), lo(q0)]
+        A1[i] = m2hi;
+        A1[4 + i] = m2hi;
+        A3[i] = m2lo;
+      } else {  // H = [hi(q0), hi(q1)], L = [lo(q0), lo(q1)]
+        A1[4 * uq + i] = m2hi;
+        A3[4 * uq + i] = m2lo;
+      }
+    }
+  }
+  for (int i = 0; i < 16; ++i) {
+    const int row = 32 * m + 8 * (i >> 2) + 4 * h + (i & 3);
+    cin16[i] = row < k ? (float)(cc[row] + D) : 1.0e30f;
+  }
 }
 
 // Fragments, C operand and certification constants.
@@ -757,71 +850,93 @@ static bool build_plan32(const Ctx& c, const double* C, int k, Plan32& pl) {
     l1c = std::fmax(l1c, l1);
   }
   if (!(cabs <= 1024.0)) return false;  // fp16 split range (and NaN) guard
-  // point side: |xhat_f| <= max(fmax - mu, mu - fmin) 2^sigma
-  double xxmax = 0.0, l1x = 0.0;
-  for (int f = 0; f < d; ++f) {
-    const double dev =
-        std::fmax(c.fmax[f] - (double)c.mu[f], (double)c.mu[f] - c.fmin[f]) * sc;
-    xxmax += dev * dev;
-    l1x += dev;
-  }
-  xxmax *= 1.0 + 1e-6;
-  const double u = std::ldexp(1.0, -24);
-  const int nmfma = pl.QH == 2 ? 3 : 2;
-  const double N = 16.0 * nmfma + 1.0;
-  // fp32 accumulation inside the MFMA chain, order unknown, each addition
-  // erring by at most 2u (no assumption on internal extra precision)
-  const double gamma = 2.0 * u * N / (1.0 - 2.0 * u * N);
-  // D >= max ||xhat||^2 + margin so that every screen value stays >= 0
-  const double E0 = gamma * (2.0 * ccmax + 2.0 * xxmax + 4.0) + 2.4 * std::ldexp(1.0, -22) *
-                    (ccmax + xxmax) + u * (ccmax + 2.0 * xxmax + 4.0) +
-                    std::ldexp(1.0, -24) * (l1c + l1x) + std::ldexp(1.0, -40);
-  const double D = xxmax + 4.0 * E0 + std::ldexp(1.0, -20);
-  const double sum_abs = (ccmax + D) * (1.0 + u) + (1.0 + std::ldexp(1.0, -9)) * (ccmax + xxmax);
-  const double E = gamma * sum_abs + 2.4 * std::ldexp(1.0, -22) * (ccmax + xxmax) +
-                   u * (ccmax + D) + std::ldexp(1.0, -24) * (l1c + l1x) +
-                   std::ldexp(1.0, -46) * (ccmax + D);
-  // reference slack: the fp64 distances and roots must not tie or flip
-  const double Wmax = (std::sqrt(ccmax) + std::sqrt(xxmax)) * (std::sqrt(ccmax) + std::sqrt(xxmax));
-  const double slack = std::ldexp(Wmax + 1.0, -38);
-  pl.thr0 = (float)((2.0 * E + slack) * 1.001);
+  double xxmax, l1x, D;
+  plan32_point_side(c, xxmax, l1x);
+  plan32_bounds(ccmax, l1c, xxmax, l1x, pl.QH, D, pl.thr0);
   pl.thr_rel = 1.0f + std::ldexp(1.0f, -16);  // the 64-ulp key truncation (2^-18 rel.)
   const int MT = pl.MT;
   pl.frag.assign((size_t)MT * 2 * 64, h8{});
   pl.cinit.assign((size_t)MT * 16 * 64, 0.0f);
   for (int m = 0; m < MT; ++m)
     for (int lane = 0; lane < 64; ++lane) {
-      const int h = lane >> 5;
-      const int j = 32 * m + (lane & 31);  // A row
-      h8 A1 = {}, A3 = {};
-      for (int uq = 0; uq < pl.QH; ++uq) {
-        const int q = pl.QH * h + uq;
-        for (int i = 0; i < 4; ++i) {
-          const int f = 4 * q + i;
-          if (j >= k || f >= d) continue;
-          const double v = ch[(size_t)j * d + f];
-          const _Float16 hi = (_Float16)v;
-          const _Float16 lo = (_Float16)(v - (double)hi);
-          const _Float16 m2hi = (_Float16)(-2.0 * (double)hi);
-          const _Float16 m2lo = (_Float16)(-2.0 * (double)lo);
-          if (pl.QH == 1) {  // H = [hi(q0), lo(q0)]
-            A1[i] = m2hi;
-            A1[4 + i] = m2hi;
-            A3[i] = m2lo;
-          } else {  // H = [hi(q0), hi(q1)], L = [lo(q0), lo(q1)]
-            A1[4 * uq + i] = m2hi;
-            A3[4 * uq + i] = m2lo;
-          }
-        }
-      }
-      pl.frag[(m * 2 + 0) * 64 + lane] = A1;
-      pl.frag[(m * 2 + 1) * 64 + lane] = A3;
-      for (int i = 0; i < 16; ++i) {
-        const int row = 32 * m + 8 * (i >> 2) + 4 * h + (i & 3);
-        pl.cinit[(m * 16 + i) * 64 + lane] = row < k ? (float)(cc[row] + D) : 1.0e30f;
-      }
+      float cin[16];
+      plan32_lane(ch.data(), cc.data(), D, k, d, pl.QH, m, lane, pl.frag[(m * 2 + 0) * 64 + lane],
+                  pl.frag[(m * 2 + 1) * 64 + lane], cin);
+      for (int i = 0; i < 16; ++i) pl.cinit[(m * 16 + i) * 64 + lane] = cin[i];
     }
   return true;
+}
+
+// Device plan for the device-resident loop (loop.hip): one workgroup builds
+// from the current centroids C (k x d fp64, device) exactly what build_plan32
+// builds on the host, into the plan buffer laid out as the host upload:
+// frag [MT][2][64] h8 | cinit [MT][16][64] f32 | C copy k x d f64 | thr0 f32.
+// The fp16 range guard failing (or a NaN) stops the loop with reason
+// kLLHostPlan (the host then takes that step on the host-plan path).
+// k <= 64, d <= 16 (screen32 shapes).
+__global__ __launch_bounds__(256) void plan32_kernel(const double* __restrict__ C, int k, int d,
+                                                     int QH, int MT,
+                                                     const double* __restrict__ mu, double sc,
+                                                     double xxmax, double l1x,
+                                                     long long* __restrict__ state,
+                                                     unsigned char* __restrict__ plan) {
+  if (state[0] == 0) return;
+  __shared__ double ch[64 * 16];
+  __shared__ double cc[64], l1s[64], cas[64];
+  __shared__ double sD;
+  __shared__ int ok;
+  const int t = threadIdx.x;
+  if (t < k) {
+    double s = 0.0, l1 = 0.0, ca = 0.0;
+    for (int f = 0; f < d; ++f) {
+      const double v = (C[(size_t)t * d + f] - mu[f]) * sc;
+      ch[t * d + f] = v;
+      s += v * v;
+      l1 += fabs(v);
+      ca = fmax(ca, fabs(v));
+    }
+    cc[t] = s;
+    l1s[t] = l1;
+    cas[t] = ca;
+  }
+  __syncthreads();
+  const size_t b_frag = (size_t)MT * 2 * 64 * sizeof(h8);
+  const size_t b_cinit = (size_t)MT * 16 * 64 * sizeof(float);
+  const size_t b_cent = sizeof(double) * (size_t)k * d;
+  if (t == 0) {
+    double ccmax = 0.0, l1c = 0.0, cabs = 0.0;
+    for (int j = 0; j < k; ++j) {  // max is exact: same value as the host's loop
+      ccmax = fmax(ccmax, cc[j]);
+      l1c = fmax(l1c, l1s[j]);
+      cabs = fmax(cabs, cas[j]);
+    }
+    ok = cabs <= 1024.0;
+    if (!ok) {
+      state[0] = 0;
+      state[2] = 3;  // kLLHostPlan
+    } else {
+      double D;
+      float thr0;
+      plan32_bounds(ccmax, l1c, xxmax, l1x, QH, D, thr0);
+      sD = D;
+      *reinterpret_cast<float*>(plan + b_frag + b_cinit + b_cent) = thr0;
+    }
+  }
+  __syncthreads();
+  if (!ok) return;
+  h8* frag = reinterpret_cast<h8*>(plan);
+  float* cinit = reinterpret_cast<float*>(plan + b_frag);
+  double* cent = reinterpret_cast<double*>(plan + b_frag + b_cinit);
+  for (int idx = t; idx < MT * 64; idx += blockDim.x) {
+    const int m = idx >> 6, lane = idx & 63;
+    float cin[16];
+    h8 A1, A3;
+    plan32_lane(ch, cc, sD, k, d, QH, m, lane, A1, A3, cin);
+    frag[(m * 2 + 0) * 64 + lane] = A1;
+    frag[(m * 2 + 1) * 64 + lane] = A3;
+    for (int i = 0; i < 16; ++i) cinit[(m * 16 + i) * 64 + lane] = cin[i];
+  }
+  for (int i = t; i < k * d; i += blockDim.x) cent[i] = C[i];
 }
 
 static int s32_blocks_per_cu(int QH, int MT, size_t lds) {
@@ -833,6 +948,15 @@ static int s32_blocks_per_cu(int QH, int MT, size_t lds) {
   if (QH == 2 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 2, true, true, false, true>, 256, lds);
   if (e != hipSuccess || nb < 1) nb = 2;
   return nb > 8 ? 8 : nb;
+}
+
+// Device plan of the loop's current centroids (c.ll_C; mu as fp64 after the
+// d reference values in c.ll_ref) into c.frag.
+void plan32_launch(Ctx& c, int k, int QH, int MT) {
+  hipLaunchKernelGGL(plan32_kernel, dim3(1), dim3(256), 0, c.stream, c.ll_C.as<double>(), k, c.d,
+                     QH, MT, c.ll_ref.as<double>() + c.d, std::ldexp(1.0, c.sigma), c.ll_xxmax,
+                     c.ll_l1x, c.ll_state.as<long long>(), static_cast<unsigned char*>(c.frag.p));
+  HIP_CHECK(hipGetLastError());
 }
 
 // Build the exact pre-centred copy xt = (x - mu) 2^sigma once per point set
@@ -856,16 +980,38 @@ void ensure_precentered(Ctx& c) {
 
 // One F32X Lloyd step through screen32; returns false (nothing launched) when
 // the centroids are out of the fp16 split range.
+// One F32X Lloyd step through screen32.  C != null: host plan (built here,
+// uploaded with the step); returns false (nothing launched) when the
+// centroids are out of the fp16 split range.  C == null: device-resident loop
+// (loop.hip) — plan32_kernel builds the plan from c.ll_C on the device and
+// every kernel of the step runs only while gate[0] != 0.
 bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* hout, bool prof,
-                   float* dbg, float* thr_out) {
+                   float* dbg, float* thr_out, long long* gate) {
+  const bool devplan = C == nullptr;
   Plan32 pl;
-  if (!build_plan32(c, C, k, pl)) return false;
+  if (devplan) {
+    const int Q4 = d4_of(c.d) / 4;
+    pl.QH = Q4 <= 2 ? 1 : 2;
+    pl.MT = k <= 32 ? 1 : 2;
+    pl.thr0 = 0.0f;
+    pl.thr_rel = 1.0f + std::ldexp(1.0f, -16);
+  } else if (!build_plan32(c, C, k, pl)) {
+    return false;
+  }
   // incremental update when the device labels and running sums belong to the
   // previous step of this point set and k
   const bool delta = c.run_valid && c.run_k == k && !dbg && !std::getenv("CDR_NO_DELTA");
   const int len = k * (c.d + 1);
   c.run_sums.ensure(sizeof(long long) * len);
-  if (!delta) HIP_CHECK(hipMemsetAsync(c.run_sums.p, 0, sizeof(long long) * len, c.stream));
+  if (!delta) {
+    if (gate) {
+      hipLaunchKernelGGL(zero_gated, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(),
+                         len, gate);
+      HIP_CHECK(hipGetLastError());
+    } else {
+      HIP_CHECK(hipMemsetAsync(c.run_sums.p, 0, sizeof(long long) * len, c.stream));
+    }
+  }
   c.run_valid = false;
   c.last_delta = delta;
   if (thr_out) {
@@ -874,22 +1020,26 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   }
   const int d = c.d, Q = d4_of(d) / 4;
   const int KP = 32 * pl.MT, NF = 8 * pl.QH;
-  // one pinned upload per step: fragments | C operand | centroids (fp64, for
-  // fallback32); the previous step's copy must have left the staging buffer
-  const size_t b_frag = pl.frag.size() * sizeof(h8);
-  const size_t b_cinit = pl.cinit.size() * sizeof(float);
+  // plan buffer: fragments | C operand | centroids (fp64, for the fused
+  // exact fallback) | thr0 (device plan only)
+  const size_t b_frag = (size_t)pl.MT * 2 * 64 * sizeof(h8);
+  const size_t b_cinit = (size_t)pl.MT * 16 * 64 * sizeof(float);
   const size_t b_cent = sizeof(double) * (size_t)k * c.d;
   const size_t b_all = b_frag + b_cinit + b_cent;
-  if (c.up_pending) HIP_CHECK(hipEventSynchronize(c.up_event));
-  c.h_up.ensure((b_all + 15) / 16 * 16);
-  memcpy(c.h_up.p, pl.frag.data(), b_frag);
-  memcpy(static_cast<char*>(c.h_up.p) + b_frag, pl.cinit.data(), b_cinit);
-  memcpy(static_cast<char*>(c.h_up.p) + b_frag + b_cinit, C, b_cent);
-  c.frag.ensure((b_all + 15) / 16 * 16);
-  // the device pulls the staging buffer itself (pinned, mapped host memory)
-  // with one small kernel on the stream: no DMA-engine copy in the step (a
-  // runtime H2D copy here stalled the host for 7-16 ms once per run)
-  {
+  c.frag.ensure((b_all + 16 + 15) / 16 * 16);
+  if (devplan) {
+    plan32_launch(c, k, pl.QH, pl.MT);
+  } else {
+    // one pinned upload per step; the previous step's copy must have left the
+    // staging buffer
+    if (c.up_pending) HIP_CHECK(hipEventSynchronize(c.up_event));
+    c.h_up.ensure((b_all + 15) / 16 * 16);
+    memcpy(c.h_up.p, pl.frag.data(), b_frag);
+    memcpy(static_cast<char*>(c.h_up.p) + b_frag, pl.cinit.data(), b_cinit);
+    memcpy(static_cast<char*>(c.h_up.p) + b_frag + b_cinit, C, b_cent);
+    // the device pulls the staging buffer itself (pinned, mapped host memory)
+    // with one small kernel on the stream: no DMA-engine copy in the step (a
+    // runtime H2D copy here stalled the host for 7-16 ms once per run)
     void* hdev = nullptr;
     HIP_CHECK(hipHostGetDevicePointer(&hdev, c.h_up.p, 0));
     const int64_t n16 = (int64_t)((b_all + 15) / 16);
@@ -897,14 +1047,16 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
                        c.stream, static_cast<const uint4*>(hdev), static_cast<uint4*>(c.frag.p),
                        n16);
     HIP_CHECK(hipGetLastError());
+    if (!c.up_event) HIP_CHECK(hipEventCreateWithFlags(&c.up_event, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(c.up_event, c.stream));
+    c.up_pending = true;
   }
-  if (!c.up_event) HIP_CHECK(hipEventCreateWithFlags(&c.up_event, hipEventDisableTiming));
-  HIP_CHECK(hipEventRecord(c.up_event, c.stream));
-  c.up_pending = true;
   h8* dfrag = c.frag.as<h8>();
   float* dcinit = reinterpret_cast<float*>(static_cast<char*>(c.frag.p) + b_frag);
   const double* dcent =
       reinterpret_cast<const double*>(static_cast<char*>(c.frag.p) + b_frag + b_cinit);
+  const float* dthr =
+      devplan ? reinterpret_cast<const float*>(static_cast<char*>(c.frag.p) + b_all) : nullptr;
   const size_t lds = (size_t)NF * KP * 8 + (size_t)KP * 4 + (size_t)k * 17 * 8;
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
@@ -950,10 +1102,12 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   a.fb_cap = cap;
   a.dbg = dbg;
   a.dbg_ld = (k + 15) / 16 * 16;
+  a.gate = gate;
+  a.thr_dev = dthr;
   snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32<%d,%d,%s,%s,%s,%s>", pl.QH, pl.MT,
            Q == 2 * pl.QH ? "true" : "false", delta ? "true" : "false", dbg ? "true" : "false",
            pre ? "true" : "false");
-  if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
+  if (prof) prof_mark(c, 0);
   const dim3 grid(nwg), blk(256);
   const bool fullq = Q == 2 * pl.QH;
 #define CDR_S32P(QH_, MT_, P_)                                                                  \
@@ -964,6 +1118,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   else hipLaunchKernelGGL((screen32<QH_, MT_, false, false, false, P_>), grid, blk, lds, c.stream, a);
 #define CDR_S32(QH_, MT_) \
   if (pre) { CDR_S32P(QH_, MT_, true) } else { CDR_S32P(QH_, MT_, false) }
+#ifdef CDR_EXPERIMENTS
   const int abl = c.screen_ablate;
   if (abl && pl.QH == 2 && pl.MT == 2 && fullq && delta && pre) {  // timing experiments only
     switch (abl) {
@@ -976,6 +1131,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
       default: hipLaunchKernelGGL((screen32<2, 2, true, true, false, true, 0>), grid, blk, lds, c.stream, a); break;
     }
   } else
+#endif
   if (pl.QH == 1 && pl.MT == 1) { CDR_S32(1, 1) }
   else if (pl.QH == 1) { CDR_S32(1, 2) }
   else if (pl.MT == 1) { CDR_S32(2, 1) }
@@ -983,7 +1139,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
 #undef CDR_S32P
 #undef CDR_S32
   HIP_CHECK(hipGetLastError());
-  if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));
+  if (prof) prof_mark(c, 1);
   long long* hout_dev = nullptr;
   if (hout) {
     void* hp = nullptr;
@@ -993,10 +1149,13 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   hipLaunchKernelGGL(reduce32, dim3((len + 63) / 64, kR32Slices), dim3(256), 0, c.stream,
                      c.partials.as<double>(), nwg, k, d, NF, KP,
                      std::ldexp(1.0, c.scale_bits - (pre ? c.sigma : 0)),
-                     pre ? c.muf.as<long long>() : nullptr, c.run_sums.as<unsigned long long>());
+                     pre ? c.muf.as<long long>() : nullptr, c.run_sums.as<unsigned long long>(),
+                     gate);
   HIP_CHECK(hipGetLastError());
+  c.fb_accum.ensure(sizeof(long long));
   hipLaunchKernelGGL(publish32, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(), len,
-                     dout, hout_dev, c.fb_count.as<int32_t>(), nwaves);
+                     dout, hout_dev, c.fb_count.as<int32_t>(), nwaves,
+                     c.prof_on ? c.fb_accum.as<long long>() : nullptr, gate);
   c.run_valid = dbg == nullptr;
   c.run_k = k;
   return true;

@@ -661,8 +661,12 @@ static void launch_big_levels(Ctx& c, const BigArgs& a1, const BigArgs& a2, dim3
   }
   hipLaunchKernelGGL((screen_big<DQ, 1, false, true>), g1, dim3(kBigThreads), lds1, c.stream, a1);
   HIP_CHECK(hipGetLastError());
-  if (prof) HIP_CHECK(hipEventRecord(c.pe[1], c.stream));  // the L1 screen alone
+  if (prof) prof_mark(c, 1);  // the L1 screen alone
+#ifdef CDR_EXPERIMENTS
   static const int abl = std::getenv("CDR_BIG_ABL") ? std::atoi(std::getenv("CDR_BIG_ABL")) : 0;
+#else
+  constexpr int abl = 0;
+#endif
   hipLaunchKernelGGL((cand_big<DQ>), g2, dim3(256), 0, c.stream, a2, c.x32.as<float>(), dC, ovf,
                      ovf_count, abl);
   HIP_CHECK(hipGetLastError());
@@ -755,7 +759,7 @@ bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof) {
   a2.in_cap = cap1;
   a2.in_regions = nw1;
   snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_big<%d,1,false,true>", DQ);
-  if (prof) HIP_CHECK(hipEventRecord(c.pe[0], c.stream));
+  if (prof) prof_mark(c, 0);
   switch (DQ) {
     case 1: launch_big_levels<1>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
     case 2: launch_big_levels<2>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;

@@ -106,11 +106,22 @@ def kmeans(X, k, number_of_files=100, tol=1e-4, random_state=None, *,
 
     if max_iter is None:
         max_iter = max(100, number_of_files / 100)
+    iters = range(max_iter)  # the reference's TypeError for a float max_iter (:29-31)
     info = ctx.info()
     mode, scale_bits = info["mode"], info["scale_bits"]
 
+    if mode == MODE_F32X and centroids.dtype in (np.float64, np.float32) and len(iters) > 0:
+        # device-resident loop: means, shift and convergence on the device,
+        # the host only for empty clusters and near-tol shifts (csrc/loop.hip)
+        from cdr_dist import device_lloyd
+
+        centroids, st = device_lloyd(ctx, centroids, len(iters), tol,
+                                     lambda g: X[g], n_samples, dtype=centroids.dtype)
+        ctx.last_inertia = st["inertia"]
+        return centroids, ctx.labels()
+
     ran = False
-    for _ in range(max_iter):
+    for _ in iters:
         ran = True
         calc = np.asarray(centroids, dtype=np.float64)
         means, counts = _cluster_means(ctx, calc, mode, scale_bits)

@@ -118,10 +118,46 @@ int cdr_lloyd_stats(cdr_ctx* ctx, int64_t* n_fallback);
  * out[4] = {screen kernel ms (sum), steps, whole step kernels ms (sum),
  * fallback points (sum)}.                                                    */
 int cdr_profile_reset(cdr_ctx* ctx, int32_t enable);
-/* Timing experiments only: skip parts of the screen kernel (1 update,
- * 2 argmin, 4 MFMA, 8 loads).  Results are garbage while mask != 0.       */
-int cdr_debug_screen_ablate(cdr_ctx* ctx, int32_t mask);
 int cdr_profile_read(cdr_ctx* ctx, double* out);
+
+/* ---- device-resident Lloyd loop: src/kmeans_plusplus.py:31-48 ----------- */
+/* The same iterations as cdr_lloyd_step + the host's means / reseed / shift,
+ * but the means, the shift and the convergence test run on the device
+ * (bit-identical: the same fp64 operations), so steps can be enqueued without
+ * a host round trip.  The device STOPS the loop (later enqueued steps do
+ * nothing) and reports why whenever the reference's host logic is needed:
+ * an empty cluster (np.random.randint reseed, :43), a shift within 1e-9
+ * relative of tol (np.linalg.norm decides, :45-47), or centroids outside the
+ * fp16 screen range.  F32X points only (CDR_ERR_UNSUPPORTED otherwise).
+ *
+ * cdr_points_sqdev: sum_i ||x_i - ref||^2 (fp64) of this shard; with ref a
+ *   data row this is exact per term; it anchors the inertia.
+ * cdr_lloyd_begin: centroids C (k, d); tol (<= 0: never converged); flags bit
+ *   0: round the means to float32 (X is float32); ref (d) and x2_total =
+ *   cdr_points_sqdev summed over every shard (NaN: this shard alone).
+ * cdr_lloyd_enqueue_assign: assignment + fused update of the current
+ *   centroids; the (k, d+1) int64 sums go to dsums (device pointer, e.g. the
+ *   buffer an RCCL all-reduce sums next) or to an internal buffer (NULL).
+ * cdr_lloyd_enqueue_finalize: means / shift / inertia from the (all-reduced)
+ *   sums at dsums (NULL: the internal buffer) and the move to the means.
+ * cdr_lloyd_status (synchronises): status[4] = {running, steps done, stop
+ *   reason (0 running, 1 converged, 2 empty cluster, 3 needs the host plan,
+ *   4 shift too close to tol), steps enqueued}; values[2] = {shift, inertia}
+ *   of the last finalised step.
+ * cdr_lloyd_read: current centroids C (k, d), the last means (k, d, NaN rows
+ *   for empty clusters) and counts (k); any pointer may be NULL.
+ * cdr_lloyd_resume: after the host took a step itself: C (NULL keeps the
+ *   device's), add_steps to the step count, host_plan_once != 0 runs the next
+ *   assignment on the host-plan path.                                      */
+int cdr_points_sqdev(cdr_ctx* ctx, const double* ref, double* out);
+int cdr_lloyd_begin(cdr_ctx* ctx, const double* C, int32_t k, double tol, int32_t flags,
+                    const double* ref, double x2_total);
+int cdr_lloyd_enqueue_assign(cdr_ctx* ctx, int64_t* dsums);
+int cdr_lloyd_enqueue_finalize(cdr_ctx* ctx, const int64_t* dsums);
+int cdr_lloyd_status(cdr_ctx* ctx, int64_t* status, double* values);
+int cdr_lloyd_read(cdr_ctx* ctx, double* C, double* means, int64_t* counts);
+int cdr_lloyd_resume(cdr_ctx* ctx, const double* C, int32_t add_steps, int32_t host_plan_once);
+int cdr_lloyd_end(cdr_ctx* ctx);
 /* Name of the last screen kernel launched (for the bench's roofline line);
  * NUL-terminated, truncated to len.                                          */
 int cdr_profile_kernel(cdr_ctx* ctx, char* buf, int32_t len);

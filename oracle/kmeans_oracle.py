@@ -142,6 +142,32 @@ def kmeans(X, k, number_of_files=100, tol=1e-4, random_state=None, max_iter=None
     return centroids, labels
 
 
+def lloyd(X: np.ndarray, C: np.ndarray, max_iter: int, tol: float = 1e-4):
+    """kmeans_plusplus.py:31-48 from given centroids: (centroids, labels of
+    the last assignment, the centroids that assignment used, steps taken)."""
+    labels, used, steps = None, C, 0
+    for _ in range(max_iter):
+        steps += 1
+        labels = assign(X, C)
+        used = C
+        new = update(X, labels, C, X.shape[0])
+        shift = np.linalg.norm(new - C)
+        C = new
+        if shift < tol:
+            break
+    return C, labels, used, steps
+
+
+def inertia(X: np.ndarray, C: np.ndarray, labels: np.ndarray, chunk: int = 1 << 20) -> float:
+    """sum_i ||x_i - C[labels_i]||^2 in fp64 (north_star's per-step inertia;
+    the reference computes none)."""
+    tot = 0.0
+    for s in range(0, X.shape[0], chunk):
+        diff = X[s:s + chunk] - C[labels[s:s + chunk]]
+        tot += float(np.sum(diff * diff))
+    return tot
+
+
 def lloyd_partials(X: np.ndarray, C: np.ndarray, scale_bits: int):
     """(labels, int64 fixed-point sums (k, d+1)) for grid data — what one
     device step returns; exact when every x * 2^scale_bits is an integer."""

@@ -52,6 +52,61 @@ class OracleShard:
         self._labels, out = ko.lloyd_partials(self.X, C, 24)
         return out
 
+    # host model of the device-resident loop (csrc/loop.hip ll_finalize)
+    LL_RUNNING, LL_CONVERGED, LL_EMPTY, LL_HOST_PLAN, LL_AMBIGUOUS = 0, 1, 2, 3, 4
+
+    def points_sqdev(self, ref):
+        return float(((self.X - ref) ** 2).sum())
+
+    def lloyd_begin(self, C, tol, ref, x2_total, round32=False):
+        self.C, self.tol, self.x2 = np.array(C, dtype=np.float64), tol, x2_total
+        self.ref = np.asarray(ref, dtype=np.float64)
+        self.st = {"running": True, "steps": 0, "reason": 0, "enqueued": 0, "shift": 0.0,
+                   "inertia": 0.0}
+        self.means = self.counts = None
+
+    def lloyd_enqueue_assign(self, buf):
+        self.st["enqueued"] += 1
+        if self.st["running"]:
+            buf[...] = self.lloyd_step(self.C).ravel()
+
+    def lloyd_enqueue_finalize(self, buf):
+        if not self.st["running"]:
+            return
+        k, d = self.C.shape
+        acc = buf.reshape(k, d + 1)
+        self.counts = acc[:, d].copy()
+        S = np.ldexp(acc[:, :d].astype(np.float64), -24)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            self.means = S / self.counts[:, None].astype(np.float64)
+        ct = self.C - self.ref
+        self.st["inertia"] = self.x2 - 2 * (ct * (S - self.counts[:, None] * self.ref)).sum() + \
+            (self.counts[:, None] * ct * ct).sum()
+        if (self.counts == 0).any():
+            self.st.update(running=False, reason=self.LL_EMPTY)
+            return
+        shift = np.linalg.norm(self.means - self.C)
+        self.st["shift"] = shift
+        self.C = self.means.copy()
+        self.st["steps"] += 1
+        if shift < self.tol:
+            self.st.update(running=False, reason=self.LL_CONVERGED)
+
+    def lloyd_status(self):
+        return dict(self.st)
+
+    def lloyd_read(self):
+        return self.C.copy(), self.means.copy(), self.counts.copy()
+
+    def lloyd_resume(self, C=None, add_steps=0, host_plan_once=False):
+        if C is not None:
+            self.C = np.array(C, dtype=np.float64)
+        self.st.update(running=True, reason=0)
+        self.st["steps"] += add_steps
+
+    def lloyd_end(self):
+        pass
+
 
 def _free_port():
     with socket.socket() as s:
@@ -59,7 +114,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, empty):
     import torch.distributed as dist
 
     from cdr_dist import Comm, ShardedLloyd, seed_sharded, shard_rows
@@ -70,8 +125,10 @@ def _worker(rank, world, port, out_dir):
     shard = OracleShard(synth.generate(N_TOTAL, begin, n_local, D, K, 9))
     comm = Comm(dist, None)
     C = seed_sharded(shard, comm, begin, N_TOTAL, K, random_state=42)
+    if empty:
+        C[-1] = 50.0  # far from every point: empty from the first step on
     np.random.seed(0)
-    C = ShardedLloyd(shard, comm, N_TOTAL, begin).run(C, max_iter=4, tol=-1.0)
+    C = ShardedLloyd(shard, comm, N_TOTAL, begin).run(C, max_iter=6, tol=1e-4 if empty else -1.0)
     if rank == 0:
         np.save(os.path.join(out_dir, "C.npy"), C)
     dist.barrier()
@@ -93,10 +150,29 @@ def test_shard_rows_blocks():
                 assert m % 8192 == 0 or begin + m == n  # only the last block is partial
 
 
-def test_two_ranks_match_single_process(tmp_path):
+def _reference_lloyd(X, C, max_iter, tol):
+    """kmeans_plusplus.py:31-48 from given centroids (oracle assign/update)."""
+    for _ in range(max_iter):
+        labels = ko.assign(X, C)
+        new = ko.update(X, labels, C, X.shape[0])
+        shift = np.linalg.norm(new - C)
+        C = new
+        if shift < tol:
+            break
+    return C
+
+
+@pytest.mark.parametrize("empty", [False, True], ids=["fixed-steps", "empty-cluster+tol"])
+def test_two_ranks_match_single_process(tmp_path, empty):
+    """Sharded seeding + the device-loop protocol (enqueue, all-reduce,
+    finalize, host take-over for an empty cluster, convergence stop) on two
+    gloo ranks equals the single-process reference."""
     mp = pytest.importorskip("torch.multiprocessing")
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), empty), nprocs=2, join=True)
     X = synth.generate(N_TOTAL, 0, N_TOTAL, D, K, 9)
+    C0 = ko.kmeans_plusplus_init(X, K, random_state=42)
+    if empty:
+        C0[-1] = 50.0
     np.random.seed(0)
-    C_ref, _ = ko.kmeans(X, K, random_state=42, max_iter=4, tol=-1.0)
+    C_ref = _reference_lloyd(X, C0, 6, 1e-4 if empty else -1.0)
     np.testing.assert_array_equal(np.load(tmp_path / "C.npy"), C_ref)

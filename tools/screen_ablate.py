@@ -1,5 +1,7 @@
 """In-process A/B timing of the screen kernel with parts switched off
-(interleaved rounds, HIP-event timings).  Diagnostic tool, not a test."""
+(interleaved rounds, HIP-event timings).  Diagnostic tool, not a test.
+Needs the experiments build:  make -C .../csrc OUT=../libcdr_exp.so
+OBJDIR=../build_exp EXTRA=-DCDR_EXPERIMENTS  and  CDR_LIB=<that .so>."""
 import os
 import sys
 import time
@@ -25,22 +27,21 @@ else:  # the bench's centroids: k-means++ then a few Lloyd steps
     C = seed_sharded(ctx, Comm(), 0, n, k, random_state=42)
     lloyd = ShardedLloyd(ctx, Comm(), n, 0)
     np.random.seed(0)
-    for _ in range(4):
-        C, _ = lloyd.step(C, lloyd.row)
+    C = lloyd.run_host(C, 4, tol=-1.0)
 for _ in range(2):
     ctx.lloyd_step(C)
 res = {m: [] for m in masks}
 steps = {m: [] for m in masks}
 for rnd in range(5):
     for m in masks:
-        ctx.debug_ablate(m)
+        ctx._lib.cdr_debug_screen_ablate(ctx._h, m)
         ctx.profile_reset(True)
         for _ in range(3):
             ctx.lloyd_step(C)
         p = ctx.profile_read()
         res[m].append(p["screen_ms"] / p["steps"])
         steps[m].append(p["step_ms"] / p["steps"])
-ctx.debug_ablate(0)
+ctx._lib.cdr_debug_screen_ablate(ctx._h, 0)
 alg = n * (4 * d + 4)
 for m in masks:
     med = float(np.median(res[m]))
