@@ -293,8 +293,9 @@ class Context:
         _check(self._lib.cdr_lloyd_stats(self._h, ctypes.byref(v)))
         return int(v.value)
 
-    def profile_reset(self, enable: bool = True) -> None:
-        _check(self._lib.cdr_profile_reset(self._h, 1 if enable else 0))
+    def profile_reset(self, enable: bool = True, every: int = 1) -> None:
+        """Collect HIP-event timings of every ``every``-th following step."""
+        _check(self._lib.cdr_profile_reset(self._h, max(int(every), 1) if enable else 0))
 
     def profile_read(self) -> dict:
         out = np.zeros(4, dtype=np.float64)

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <string.h>
 #include <stdint.h>
 #include <string>
 #include <vector>
@@ -71,6 +72,9 @@ struct HostBuf {
 };
 
 constexpr int kSeedBlock = 8192;  // NumPy reduction buffer (add.reduce chunk)
+// screen32's running sums are kept in kRunSlices copies (workgroup b adds into
+// slice b % kRunSlices: 1/16 of the atomic contention); readers sum them.
+constexpr int kRunSlices = 16;
 
 // Point layout in HBM ("quad-interleaved SoA"): features are grouped in quads;
 // quad q of point i is 4 consecutive values at ((q * n_pad) + i) * 4.  One
@@ -106,8 +110,17 @@ struct Ctx {
   // pre-centred copy for screen32: float [d4/4][n_pad][4] of (x - mu) 2^sigma,
   // exact (pre_ok, decided with the mode); built on the first screen32 step
   DevBuf xt32;
-  DevBuf muf;  // int64[d]: mu_f 2^S (reduce32 restores x sums from xt sums)
+  DevBuf muf;  // int64[d]: mu_f 2^S (screen32 restores x sums from xt sums)
   bool pre_ok = false, xt_valid = false;
+  // split screen copy for the DELTA steps (screen32d): fp16 hi / lo of
+  // xhat = fma(x, 2^sigma, -mu 2^sigma), tiled [n_pad/32][2 halves][32][16 QH B]
+  // (the MFMA B operands as loaded); built once per point set
+  DevBuf xs16;
+  DevBuf xa32;  // the points row-major (float [n_pad][d4]) for fixup32's gathers
+  bool xs_valid = false;
+  int xs_qh = 0;
+  DevBuf mv_list;   // screen32d: per-wave regions of moved points {pt, old | new << 16}
+  DevBuf mv_count;  // int32 per wave
 
   // ---- Lloyd ----
   DevBuf labels;    // int32[n_pad]
@@ -130,6 +143,8 @@ struct Ctx {
   // from a pool and only resolved by cdr_profile_read, so that profiling
   // never makes the host wait inside an enqueued loop
   bool prof_on = false;
+  int prof_period = 1;     // profile every prof_period-th step (event records
+  int64_t prof_seen = 0;   // cost the GPU a few us each)
   std::vector<hipEvent_t> prof_pool;
   size_t prof_used = 0;  // events of this profiling session (triples)
   int64_t prof_cur = -1; // first event of the current step's triple, -1 none
@@ -163,6 +178,9 @@ struct Ctx {
   int32_t ll_k = 0, ll_flags = 0;
   double ll_tol = 0.0, ll_x2 = 0.0, ll_xxmax = 0.0, ll_l1x = 0.0;
   int64_t ll_enqueued = 0;
+  const long long* ll_fin_sums = nullptr;  // what the next finalize reads
+  int ll_fin_slices = 1;
+  bool ll_fin_devstep = false;  // the last assign was a device-plan screen32 step
 
   // ---- seeding ----
   DevBuf dmin;        // double[n_pad]
@@ -237,17 +255,21 @@ bool prof_step_begin(Ctx& c);
 void prof_mark(Ctx& c, int i);
 
 // fp64 -> fp16 with one round-to-nearest-even, identical on host and device
-// (the screen fragments are built by both: build_plan32 and plan32_kernel).
-// |v| >= 65520 gives +-inf, NaN stays NaN.
+// (the screen fragments are built by both: build_plan32 and plan32_build).
+// Branch-free: round to odd into fp32 (truncate, then set the lowest bit when
+// inexact), then one RNE fp32 -> fp16 conversion; fp32 keeps 13 bits more than
+// fp16, so the two roundings give the correctly rounded fp16 (the classic
+// round-to-odd argument).  |v| >= 65520 gives +-inf, NaN stays NaN.
 __host__ __device__ inline _Float16 f64_to_f16(double v) {
-  const double a = fabs(v);
-  if (!(a == a)) return (_Float16)v;
-  if (a >= 65520.0) return v > 0 ? (_Float16)INFINITY : (_Float16)(-INFINITY);
-  int e;
-  (void)frexp(a, &e);                        // a in [2^(e-1), 2^e)
-  const int ue = (e - 1 > -14 ? e - 1 : -14) - 10;  // fp16 spacing of a: 2^ue
-  const double r = ldexp(rint(ldexp(a, -ue)), ue);  // exact: fits fp16
-  return (_Float16)copysign(r, v);
+  const float f = (float)v;  // RNE
+  const double back = (double)f;
+  unsigned b;
+  memcpy(&b, &f, 4);
+  b -= (fabs(back) > fabs(v)) ? 1u : 0u;  // one ulp toward zero: truncation
+  b |= (back != v) ? 1u : 0u;              // sticky bit: round to odd
+  float fo;
+  memcpy(&fo, &b, 4);
+  return (_Float16)fo;
 }
 
 }  // namespace cdr

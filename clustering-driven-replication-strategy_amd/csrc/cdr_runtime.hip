@@ -254,6 +254,7 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
     if ((double)ms[f] != -std::ldexp(mu, c.sigma)) c.pre_ok = false;
   }
   c.xt_valid = false;
+  c.xs_valid = false;
   c.mu_s.ensure(sizeof(float) * (d > 0 ? d : 1));
   HIP_CHECK(hipMemcpyAsync(c.mu_s.p, ms.data(), sizeof(float) * d,
                            hipMemcpyHostToDevice, c.stream));
@@ -277,6 +278,9 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
   c.x64.release();
   c.xt32.release();
   c.xt_valid = false;
+  c.xs16.release();
+  c.xa32.release();
+  c.xs_valid = false;
   c.pre_ok = false;
   c.n = n;
   c.d = d;
@@ -398,7 +402,7 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.med_tmp2, &c.ev_file, &c.ev_op, &c.ev_client, &c.ev_ts,
                     &c.ev_primary, &c.ev_out, &c.ev_scratch, &c.ev_scratch2,
                     &c.fin_counts, &c.fin_creation, &c.fin_out, &c.fin_red, &c.run_sums,
-                    &c.fb_accum, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
+                    &c.fb_accum, &c.xs16, &c.xa32, &c.mv_list, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
                     &c.ll_state};
   for (DevBuf* b : bufs) b->release();
   c.h_small.release();

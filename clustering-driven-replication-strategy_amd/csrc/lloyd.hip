@@ -1024,6 +1024,7 @@ __global__ void fb_accumulate(const int32_t* __restrict__ total, long long* __re
 bool prof_step_begin(Ctx& c) {
   c.prof_cur = -1;
   if (!c.prof_on) return false;
+  if (c.prof_seen++ % c.prof_period != 0) return false;
   if (c.prof_used + 3 > (size_t)(3 << 16)) return false;  // session cap: 65536 steps
   while (c.prof_pool.size() < c.prof_used + 3) {
     hipEvent_t e = nullptr;
@@ -1359,6 +1360,8 @@ int cdr_profile_reset(cdr_ctx* h, int32_t enable) {
   c.prof_used = 0;
   c.prof_cur = -1;
   c.prof_on = enable != 0;
+  c.prof_period = enable > 1 ? enable : 1;
+  c.prof_seen = 0;
   c.prof_screen_ms = c.prof_step_ms = c.prof_fb_points = 0.0;
   c.prof_launches = 0;
   c.fb_accum.ensure(sizeof(long long));

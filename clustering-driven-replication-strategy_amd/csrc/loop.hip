@@ -29,6 +29,7 @@
 #include <cstring>
 
 #include "cdr_internal.h"
+#include "plan32.h"
 
 namespace cdr {
 
@@ -41,39 +42,111 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
 void plan32_point_side(const Ctx& c, double& xxmax, double& l1x);
 void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_dev);
 
-// One workgroup.  sums: (k, d+1) int64 fixed-point sums | counts (after the
-// all-reduce).  Cnew (k*d means, then k counts as int64) is always written;
-// C moves to Cnew unless the loop stops for the host.
-__global__ __launch_bounds__(256) void ll_finalize(const long long* __restrict__ sums, int k,
-                                                   int d, int sbits, int round32, double tol,
-                                                   double margin, double x2,
-                                                   const double* __restrict__ ref,
-                                                   double* __restrict__ C,
-                                                   double* __restrict__ Cnew,
-                                                   long long* __restrict__ state) {
-  if (state[0] == 0) return;
-  __shared__ double r_ss[256], r_cross[256], r_quad[256];
-  __shared__ int r_empty[256];
-  __shared__ int move;
+struct FinArgs {
+  const long long* sums;  // nslices x (k, d+1) int64 fixed-point sums | counts
+  int nslices;
+  int k, d, sbits, round32;
+  double tol, margin, x2;
+  const double* ref;  // inertia reference row (d), then mu (d)
+  double* C;          // current centroids (k x d)
+  double* Cnew;       // k x d means, then k counts (int64)
+  long long* state;
+  // screen32's fallback counter (device plan steps): fbc[nwaves] -> [nwaves+1]
+  int* fbc;
+  int nwaves;
+  long long* fb_acc;
+  // device plan of the next step (null: host plan)
+  unsigned char* plan;
+  int QH, MT;
+  double sc, xxmax, l1x;
+};
+
+constexpr int kFinThreads = 512;
+constexpr int kFinLds = 64 * 17;  // (k, d+1) cells staged in LDS (screen32 shapes)
+
+// One workgroup.  Cnew is always written; C moves to Cnew unless the loop
+// stops for the host, and then the next step's screen plan is built from it.
+// Every global read is issued in independent batches (one workgroup: latency,
+// not bandwidth, sets its time).
+__global__ __launch_bounds__(kFinThreads) void ll_finalize(FinArgs a) {
+  long long* __restrict__ state = a.state;
+  const int k = a.k, d = a.d;
+  double* __restrict__ C = a.C;
+  double* __restrict__ Cnew = a.Cnew;
+  const int cells = k * (d + 1);
+  __shared__ long long lsum[kFinLds];
+  __shared__ double lC[kFinLds];
+  __shared__ double lref[2 * 64];
+  // screen32 shapes: every input of the step is loaded in one batch (state,
+  // all slices of the sums, the centroids, ref / mu) into LDS
+  const bool staged = cells <= kFinLds && d <= 64;
+  const double* __restrict__ ref = staged ? lref : a.ref;
+  const double* __restrict__ Cin = staged ? lC : C;
+  if (staged) {
+    constexpr int PER = (kFinLds + kFinThreads - 1) / kFinThreads;
+    long long p[PER][kRunSlices];
+    double cv[PER];
+    double rv = 0.0;
+    const long long st0 = state[0];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * kFinThreads;
+#pragma unroll
+      for (int sl = 0; sl < kRunSlices; ++sl)
+        p[i][sl] = (c < cells && sl < a.nslices) ? a.sums[(size_t)sl * cells + c] : 0;
+      cv[i] = c < k * d ? C[c] : 0.0;
+    }
+    if (threadIdx.x < 2 * d) rv = a.ref[threadIdx.x];
+    if (st0 == 0) return;  // uniform: the loop has stopped
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * kFinThreads;
+      long long v = 0;
+#pragma unroll
+      for (int sl = 0; sl < kRunSlices; ++sl) v += p[i][sl];
+      if (c < cells) lsum[c] = v;
+      if (c < k * d) lC[c] = cv[i];
+    }
+    if (threadIdx.x < 2 * d) lref[threadIdx.x] = rv;
+    __syncthreads();
+  } else if (state[0] == 0) {
+    return;
+  }
+  auto sum_at = [&](size_t e) -> long long {
+    if (staged) return lsum[e];
+    long long v = 0;
+    for (int sl = 0; sl < a.nslices; ++sl) v += a.sums[(size_t)sl * cells + e];
+    return v;
+  };
+  __shared__ double r_ss[kFinThreads], r_cross[kFinThreads], r_quad[kFinThreads];
+  __shared__ int r_empty[kFinThreads];
+  __shared__ int move, plan_next;
   const int t = threadIdx.x;
   const int d1 = d + 1;
   double ss = 0.0, cross = 0.0, quad = 0.0;
   int empty = 0;
   long long* cnt_out = reinterpret_cast<long long*>(Cnew + (size_t)k * d);
-  for (int j = t; j < k; j += blockDim.x) cnt_out[j] = sums[(size_t)j * d1 + d];
+  for (int j = t; j < k; j += blockDim.x) cnt_out[j] = sum_at((size_t)j * d1 + d);
+  if (t == 0 && a.fbc) {
+    const int fb = a.fbc[a.nwaves];
+    a.fbc[a.nwaves] = 0;
+    a.fbc[a.nwaves + 1] = fb;
+    if (a.fb_acc) a.fb_acc[0] += fb;
+  }
+#pragma unroll 4
   for (int e = t; e < k * d; e += blockDim.x) {
     const int j = e / d, f = e - j * d;
-    const long long cnt = sums[(size_t)j * d1 + d];
+    const long long cnt = sum_at((size_t)j * d1 + d);
     // the host's np.ldexp(acc.astype(float64), -S) / counts (kmeans_plusplus.py)
-    const double sj = ldexp((double)sums[(size_t)j * d1 + f], -sbits);
+    const double sj = ldexp((double)sum_at((size_t)j * d1 + f), -a.sbits);
     double m = sj / (double)cnt;
-    if (round32) m = (double)(float)m;  // new_centroids has X's dtype (float32)
+    if (a.round32) m = (double)(float)m;  // new_centroids has X's dtype (float32)
     Cnew[e] = m;
     if (cnt == 0) {
       empty = 1;
       continue;
     }
-    const double c = C[e];
+    const double c = Cin[e];
     const double df = m - c;
     ss += df * df;
     const double ct = c - ref[f];
@@ -85,7 +158,7 @@ __global__ __launch_bounds__(256) void ll_finalize(const long long* __restrict__
   r_quad[t] = quad;
   r_empty[t] = empty;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {  // fixed tree: deterministic
+  for (int o = kFinThreads / 2; o > 0; o >>= 1) {  // fixed tree: deterministic
     if (t < o) {
       r_ss[t] += r_ss[t + o];
       r_cross[t] += r_cross[t + o];
@@ -96,7 +169,7 @@ __global__ __launch_bounds__(256) void ll_finalize(const long long* __restrict__
   }
   if (t == 0) {
     const double sst = r_ss[0];
-    const double inertia = x2 - 2.0 * r_cross[0] + r_quad[0];
+    const double inertia = a.x2 - 2.0 * r_cross[0] + r_quad[0];
     long long reason = kLLRun;
     int mv = 0;
     if (r_empty[0]) {
@@ -104,8 +177,8 @@ __global__ __launch_bounds__(256) void ll_finalize(const long long* __restrict__
     } else {
       const double sh = sqrt(sst);
       mv = 1;
-      if (tol > 0.0 && !(sh > tol * (1.0 + margin))) {
-        if (sh < tol * (1.0 - margin)) {
+      if (a.tol > 0.0 && !(sh > a.tol * (1.0 + a.margin))) {
+        if (sh < a.tol * (1.0 - a.margin)) {
           reason = kLLConverged;  // shift < tol: the reference breaks after moving
         } else {
           reason = kLLAmbiguous;  // too close to call in fp64: the host decides
@@ -121,10 +194,21 @@ __global__ __launch_bounds__(256) void ll_finalize(const long long* __restrict__
     state[3] = __double_as_longlong(sst);
     state[4] = __double_as_longlong(inertia);
     move = mv;
+    plan_next = mv && reason == kLLRun;  // the loop goes on: plan its next step
   }
   __syncthreads();
-  if (move)
-    for (int e = t; e < k * d; e += blockDim.x) C[e] = Cnew[e];
+  if (!move) return;
+  for (int e = t; e < k * d; e += blockDim.x) {
+    const double m = Cnew[e];  // this thread's own store above
+    C[e] = m;
+    if (staged) lC[e] = m;
+  }
+  // the next step's plan from the new centroids
+  if (a.plan && plan_next) {
+    __syncthreads();
+    plan32_build(staged ? lC : Cnew, k, d, a.QH, a.MT, ref + d, a.sc, a.xxmax, a.l1x, state,
+                 a.plan);
+  }
 }
 
 // Per-block partial sums of ||x_i - r||^2 (features in order, fp64).
@@ -179,6 +263,23 @@ static double points_sqdev(Ctx& c, const double* ref_host) {
   double s = 0.0;
   for (double v : h) s += v;
   return s;
+}
+
+void plan32_launch(Ctx& c, int k, int QH, int MT);  // screen32.hip
+
+static void ll_plan_shape(const Ctx& c, int& QH, int& MT) {
+  QH = d4_of(c.d) / 4 <= 2 ? 1 : 2;
+  MT = c.ll_k <= 32 ? 1 : 2;
+}
+
+// Device plan of the loop's current centroids (begin, resume); the plan
+// buffer is sized for the screen32 layout of (k, d).
+static void ll_plan(Ctx& c) {
+  int QH, MT;
+  ll_plan_shape(c, QH, MT);
+  c.frag.ensure(((size_t)MT * 2 * 64 * 16 + (size_t)MT * 16 * 64 * 4 +
+                 sizeof(double) * (size_t)c.ll_k * c.d + 16 + 15) / 16 * 16);
+  plan32_launch(c, c.ll_k, QH, MT);
 }
 
 static void ll_require(const Ctx& c) {
@@ -243,6 +344,7 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   c.ll_hostplan_once = false;
   // the first step recomputes the running sums from scratch (see resume)
   c.run_valid = false;
+  if (c.ll_devplan) ll_plan(c);
   CDR_CATCH
 }
 
@@ -256,8 +358,12 @@ int cdr_lloyd_enqueue_assign(cdr_ctx* h, int64_t* dsums) {
   long long* state = c.ll_state.as<long long>();
   if (c.ll_devplan && !c.ll_hostplan_once) {
     const bool prof = prof_step_begin(c);
-    screen32_step(c, nullptr, c.ll_k, dout, nullptr, prof, nullptr, nullptr, state);
-    if (prof) prof_mark(c, 2);
+    // single process: no published copy, ll_finalize reads the running sums
+    screen32_step(c, nullptr, c.ll_k, dsums ? dout : nullptr, nullptr, prof, nullptr, nullptr,
+                  state);
+    c.ll_fin_sums = dsums ? dout : c.run_sums.as<long long>();
+    c.ll_fin_slices = dsums ? 1 : kRunSlices;
+    c.ll_fin_devstep = true;
     c.last_k = c.ll_k;
     c.have_labels = true;
     c.last_screened = true;
@@ -268,6 +374,9 @@ int cdr_lloyd_enqueue_assign(cdr_ctx* h, int64_t* dsums) {
     long long st[kLLState];
     ll_read_state(c, st);
     c.ll_hostplan_once = false;
+    c.ll_fin_sums = dout;
+    c.ll_fin_slices = 1;
+    c.ll_fin_devstep = false;
     if (st[0]) {
       std::vector<double> Ch((size_t)c.ll_k * c.d);
       HIP_CHECK(hipMemcpy(Ch.data(), c.ll_C.p, sizeof(double) * Ch.size(), hipMemcpyDeviceToHost));
@@ -284,17 +393,41 @@ int cdr_lloyd_enqueue_finalize(cdr_ctx* h, const int64_t* dsums) {
   Ctx& c = h->c;
   HIP_CHECK(hipSetDevice(c.device));
   ll_require(c);
-  const long long* sums =
-      dsums ? reinterpret_cast<const long long*>(dsums) : c.ll_sums.as<long long>();
+  if (dsums && reinterpret_cast<const long long*>(dsums) != c.ll_fin_sums)
+    CDR_FAIL(CDR_ERR_ARG, "lloyd finalize: pass the buffer given to the assign");
   const int kd = c.ll_k * c.d;
   const bool r32 = (c.ll_flags & 1) != 0;
+  FinArgs a;
+  a.sums = c.ll_fin_sums;
+  a.nslices = c.ll_fin_slices;
+  a.k = c.ll_k;
+  a.d = c.d;
+  a.sbits = c.scale_bits;
+  a.round32 = r32 ? 1 : 0;
+  a.tol = c.ll_tol;
   // fp64 sum of kd squares errs by < kd 2^-53 relative; float32 centroids are
   // compared by NumPy in float32 (kd 2^-23)
-  const double margin = r32 ? std::ldexp((double)(kd + 2), -22) : 1e-9;
-  hipLaunchKernelGGL(ll_finalize, dim3(1), dim3(256), 0, c.stream, sums, c.ll_k, c.d, c.scale_bits,
-                     r32 ? 1 : 0, c.ll_tol, margin, c.ll_x2, c.ll_ref.as<double>(),
-                     c.ll_C.as<double>(), c.ll_new.as<double>(), c.ll_state.as<long long>());
+  a.margin = r32 ? std::ldexp((double)(kd + 2), -22) : 1e-9;
+  a.x2 = c.ll_x2;
+  a.ref = c.ll_ref.as<double>();
+  a.C = c.ll_C.as<double>();
+  a.Cnew = c.ll_new.as<double>();
+  a.state = c.ll_state.as<long long>();
+  a.fbc = c.ll_fin_devstep ? c.fb_count.as<int>() : nullptr;
+  a.nwaves = c.fb_regions;
+  c.fb_accum.ensure(sizeof(long long));
+  a.fb_acc = c.prof_on ? c.fb_accum.as<long long>() : nullptr;
+  a.plan = c.ll_devplan ? static_cast<unsigned char*>(c.frag.p) : nullptr;
+  ll_plan_shape(c, a.QH, a.MT);
+  a.sc = std::ldexp(1.0, c.sigma);
+  a.xxmax = c.ll_xxmax;
+  a.l1x = c.ll_l1x;
+#ifdef CDR_EXPERIMENTS
+  if (std::getenv("CDR_FIN_NOPLAN")) a.plan = nullptr;  // timing experiments only
+#endif
+  hipLaunchKernelGGL(ll_finalize, dim3(1), dim3(kFinThreads), 0, c.stream, a);
   HIP_CHECK(hipGetLastError());
+  if (c.ll_fin_devstep && c.prof_cur >= 0) prof_mark(c, 2);
   CDR_CATCH
 }
 
@@ -348,8 +481,9 @@ int cdr_lloyd_resume(cdr_ctx* h, const double* C, int32_t add_steps, int32_t hos
   hipLaunchKernelGGL(ll_set_state, dim3(1), dim3(64), 0, c.stream, c.ll_state.as<long long>(), 1LL,
                      (long long)add_steps, (long long)kLLRun);
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipStreamSynchronize(c.stream));  // C belongs to the caller
   c.ll_hostplan_once = host_plan_once != 0;
+  if (c.ll_devplan && !c.ll_hostplan_once) ll_plan(c);
+  HIP_CHECK(hipStreamSynchronize(c.stream));  // C belongs to the caller
   // Steps enqueued after the stop did nothing, but the host marked the
   // running sums valid after each of them; a full (non-DELTA) step that was
   // among them never zeroed and rebuilt them.  The next step starts afresh.

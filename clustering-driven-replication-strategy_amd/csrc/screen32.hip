@@ -38,6 +38,7 @@
 
 #include "cdr_internal.h"
 #include "exact_math.h"
+#include "plan32.h"
 
 namespace cdr {
 
@@ -61,7 +62,9 @@ struct S32Args {
   float sig;
   float thr0, thr_rel;
   int32_t* labels;
-  double* partials;  // per workgroup: sums [d4][KP] then counts [KP] (as double)
+  unsigned long long* run_sums;  // kRunSlices x (k, d+1) int64 running sums
+  const long long* muf;          // PRE: int64 mu_f 2^S (null otherwise)
+  double fx;                     // 2^(S - sigma) (PRE) or 2^S: table value -> fixed point
   int KP;
   int32_t* fb_list;
   int32_t* fb_count;
@@ -519,162 +522,35 @@ __global__ __launch_bounds__(256) void screen32(S32Args a) {
     if (fb_used) fallback_tail(a, fb_region, fb_used, tsum, tcnt, cs, KP, DELTA, PRE);
   }
   __syncthreads();
-  double* dst = a.partials + (size_t)blockIdx.x * (NF + 1) * KP;
-  for (int i = threadIdx.x; i < NF * KP; i += blockDim.x) dst[i] = tsum[i];
-  for (int i = threadIdx.x; i < KP; i += blockDim.x) dst[NF * KP + i] = (double)tcnt[i];
-}
-
-// Exact assignment of the points the screen did not certify: 16 lanes per
-// point (the 256 threads of workgroup b share the points of the screen's
-// fallback regions 4b..4b+3, so a crowded region is spread over the whole
-// workgroup).  Lane c of a point's 16 walks centroids c, c + 16, c + 32, ...
-// (rows staged in LDS with a pad double: the 16 rows of a group sit in 16
-// different bank pairs) computing the NumPy-order fp64 squared distance and
-// its correctly rounded sqrt, keeping the first minimum of its roots; the 16
-// candidates are merged on (root, index) — np.argmin of np.linalg.norm, first
-// index on ties (src/kmeans_plusplus.py:33-34).  Changes go into partial
-// table b.  k <= 64, d = D <= 16 (compile time: the point lives in registers).
-template <int D>
-__global__ __launch_bounds__(256) void fallback32(const float* __restrict__ X, int64_t n_pad,
-                                                  int Q, const double* __restrict__ C,
-                                                  int k, const int32_t* __restrict__ list,
-                                                  const int32_t* __restrict__ count, int cap,
-                                                  int KP, int32_t* __restrict__ labels,
-                                                  double* __restrict__ partials, int delta,
-                                                  const float* __restrict__ pre_ms, float sig) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int CS = D + 1;  // staged centroid row stride (doubles)
-  const int d4 = Q;          // table rows (NF of the screen)
-  const int reg0 = blockIdx.x * (blockDim.x >> 6);
-  int cnt[4], tot = 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    cnt[r] = count[reg0 + r];
-    tot += cnt[r];
-  }
-  if (tot == 0) return;  // uniform: nothing to add to this workgroup's table
-  double* tsum = reinterpret_cast<double*>(smem);  // [d4][KP]
-  int* tcnt = reinterpret_cast<int*>(tsum + (size_t)d4 * KP);
-  double* cs = reinterpret_cast<double*>(tcnt + KP + (KP & 1));  // [k][CS]
-  for (int i = threadIdx.x; i < d4 * KP; i += blockDim.x) tsum[i] = 0.0;
-  for (int i = threadIdx.x; i < KP; i += blockDim.x) tcnt[i] = 0;
-  for (int i = threadIdx.x; i < k * D; i += blockDim.x) cs[(i / D) * CS + i % D] = C[i];
-  __syncthreads();
-  const int c16 = threadIdx.x & 15;
-  for (int e0 = 0; e0 < tot; e0 += 16) {
-    const int e = e0 + (threadIdx.x >> 4);
-    const bool live = e < tot;
-    int64_t pt = 0;
-    if (live) {
-      int r = 0, i = e;
-      while (i >= cnt[r]) i -= cnt[r++];
-      pt = list[(size_t)(reg0 + r) * cap + i];
-    }
-    double x[D];
-#pragma unroll
-    for (int f = 0; f < D; ++f) x[f] = live ? (double)X[xidx(f, pt, n_pad)] : 0.0;
-    double sb = INFINITY, rb = INFINITY;
-    int jmin = 0x7fffffff;
-    for (int j = c16; j < k; j += 16) {
-      const double* cj = cs + j * CS;
-      const double s = np_sqdist([&](int f) { return x[f]; }, [&](int f) { return cj[f]; }, D);
-      // sqrt is monotone: a root can only undercut the best root when s < sb,
-      // and then the roots decide (strict: first index on ties of the roots)
-      if (s < sb) {
-        const double r2 = sqrt(s);
-        sb = s;
-        if (r2 < rb) {
-          rb = r2;
-          jmin = j;
-        }
+  // This workgroup's table as exact int64 fixed point, added into slice
+  // (blockIdx % kRunSlices) of the running sums: sum x 2^S = sum xt 2^(S -
+  // sigma) + count mu 2^S (PRE), both exact integers.  Lanes walk the (k,
+  // d+1) output contiguously; zero contributions (clusters no point of this
+  // workgroup entered or left) are skipped.
+  {
+    const int d1 = a.d + 1, cells = a.k * d1;
+    unsigned long long* out = a.run_sums + (size_t)(blockIdx.x % kRunSlices) * cells;
+    for (int e = threadIdx.x; e < cells; e += blockDim.x) {
+      const int j = e / d1, r = e - j * d1;
+      const int cnt = tcnt[j];
+      long long v;
+      if (r < a.d) {
+        v = __double2ll_rn(tsum[r * KP + j] * a.fx);
+        if (PRE) v += (long long)cnt * a.muf[r];
+      } else {
+        v = cnt;
       }
+      if (v) atomicAdd(&out[e], (unsigned long long)v);
     }
-    // merge the 16 lanes of the point: smaller root, then smaller index
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
-      const double ro = __shfl_xor(rb, o, 16);
-      const int jo = __shfl_xor(jmin, o, 16);
-      if (ro < rb || (ro == rb && jo < jmin)) {
-        rb = ro;
-        jmin = jo;
-      }
-    }
-    if (!live || c16 != 0) continue;
-    if (jmin >= k) jmin = 0;  // every root NaN: np.argmin of all-NaN is 0
-    const int old = delta ? labels[pt] : -1;  // not yet overwritten by the screen
-    if (jmin != old) {
-      labels[pt] = jmin;
-      if (pre_ms) {  // the screen's tables hold xt = (x - mu) 2^sigma (exact)
-#pragma unroll
-        for (int f = 0; f < D; ++f) x[f] = (double)fmaf((float)x[f], sig, pre_ms[f]);
-      }
-#pragma unroll
-      for (int f = 0; f < D; ++f) atomicAdd(&tsum[f * KP + jmin], x[f]);
-      atomicAdd(&tcnt[jmin], 1);
-      if (old >= 0) {
-#pragma unroll
-        for (int f = 0; f < D; ++f) atomicAdd(&tsum[f * KP + old], -x[f]);
-        atomicAdd(&tcnt[old], -1);
-      }
-    }
-  }
-  __syncthreads();
-  double* dst = partials + (size_t)blockIdx.x * (d4 + 1) * KP;
-  for (int i = threadIdx.x; i < d4 * KP; i += blockDim.x) {
-    const double v = tsum[i];
-    if (v != 0.0) dst[i] += v;
-  }
-  for (int i = threadIdx.x; i < KP; i += blockDim.x)
-    if (tcnt[i]) dst[d4 * KP + i] += (double)tcnt[i];
-}
-
-// out (k, d+1) int64 += sum over workgroups of the exact fixed-point values
-// (the step's changes).  Block (x, y): 64 consecutive table cells (row r =
-// feature or count, column j: coalesced over j) of the y-th slice of the
-// workgroups.
-// With the pre-centred copy (muf != null) the table sums are of xt = (x - mu)
-// 2^sigma: sum x 2^S = sum xt 2^(S - sigma) + count mu 2^S, both exact.
-constexpr int kR32Slices = 16;
-__global__ __launch_bounds__(256) void reduce32(const double* __restrict__ part, int nwg, int k,
-                                                int d, int d4, int KP, double fx,
-                                                const long long* __restrict__ muf,
-                                                unsigned long long* __restrict__ out,
-                                                const long long* __restrict__ gate) {
-  __shared__ long long red[4][64];
-  if (gate && gate[0] == 0) return;
-  const int cells = k * (d + 1);
-  const int u = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int sub = threadIdx.x >> 6;
-  const int per = (nwg + kR32Slices - 1) / kR32Slices;
-  const int w0 = blockIdx.y * per, w1 = min(nwg, w0 + per);
-  long long s = 0;
-  int e = 0;
-  if (u < cells) {
-    const int r = u / k, j = u - r * k;  // r < d: feature r, r == d: count
-    e = j * (d + 1) + r;
-    const int src = (r < d ? r : d4) * KP + j;
-    const size_t stride = (size_t)(d4 + 1) * KP;
-    const long long mf = (muf && r < d) ? muf[r] : 0;
-    for (int w = w0 + sub; w < w1; w += 4) {
-      const double v = part[(size_t)w * stride + src];
-      s += r < d ? __double2ll_rn(v * fx) : __double2ll_rn(v);
-      if (mf) s += __double2ll_rn(part[(size_t)w * stride + (size_t)d4 * KP + j]) * mf;
-    }
-  }
-  red[sub][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (sub == 0 && u < cells) {
-    const long long t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                        red[3][threadIdx.x];
-    if (t) atomicAdd(&out[e], (unsigned long long)t);
   }
 }
 
-// One block after reduce32 (the kernel boundary orders it after every
-// block's atomics): out -> dout (device, for the all-reduce) and/or hout
-// (mapped pinned host memory, with the fallback total at hout[cells]); the
-// screen's fallback counter fbc[nwaves] moves to fbc[nwaves + 1] and is
-// cleared for the next step — replaces a memset and up to three copies.
+// One block after the screen (the kernel boundary orders it after every
+// workgroup's atomics): the sum of the kRunSlices slices of the running sums
+// -> dout (device, e.g. for the all-reduce) and/or hout (mapped pinned host
+// memory, with the fallback total at hout[cells]); the screen's fallback
+// counter fbc[nwaves] moves to fbc[nwaves + 1] and is cleared for the next
+// step.
 __global__ __launch_bounds__(256) void publish32(const long long* __restrict__ out, int cells,
                                                  long long* __restrict__ dout,
                                                  long long* __restrict__ hout,
@@ -683,11 +559,12 @@ __global__ __launch_bounds__(256) void publish32(const long long* __restrict__ o
                                                  const long long* __restrict__ gate) {
   if (gate && gate[0] == 0) return;
   for (int i = threadIdx.x; i < cells; i += blockDim.x) {
-    const long long v = out[i];
+    long long v = 0;
+    for (int sl = 0; sl < kRunSlices; ++sl) v += out[(size_t)sl * cells + i];
     if (dout) dout[i] = v;
     if (hout) hout[i] = v;
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && fbc) {
     const int fb = fbc[nwaves];
     fbc[nwaves] = 0;
     fbc[nwaves + 1] = fb;
@@ -716,6 +593,458 @@ __global__ void precenter_kernel(const float* __restrict__ x, int64_t n, int64_t
     const int64_t i = r >> 2;
     const int f = (int)(4 * q + (r & 3));
     xt[t] = (f < d && i < n) ? fmaf(x[t], sig, ms[f]) : 0.0f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// DELTA steps without the in-loop update: screen32d + fixup32.
+//
+// screen32's per-group instruction stream is ~260 VALU, and the SIMDs issue
+// back to back (PMC: three waves per SIMD are active / issue-stalled 67 % of
+// their cycles).  After the first step almost every point keeps its label, so
+// the DELTA steps run a leaner pair:
+// * screen32d reads a split screen copy (xs16: the fp16 hi / lo halves the
+//   MFMA B operands consist of, split once per point set with the same
+//   instructions screen32 uses: identical screen values and certification)
+//   with wave-uniform base addresses, and writes only labels and two lists per
+//   wave: certified points whose label changed ({pt, old | new << 16}) and
+//   uncertified points;
+// * fixup32 applies the changes of both lists to the running sums: it
+//   gathers the moved points from x32 (1-2 % of the points), re-does the
+//   uncertified ones in exact fp64 NumPy order, and adds its LDS table into
+//   the int64 slices.  Integer sums, so the result equals a full recompute.
+// ---------------------------------------------------------------------------
+
+// xs16 tile of 32 points: [h = 0, 1][p = 0..31][hi(QH quads) | lo(QH quads)]
+// as fp16, where lane half h owns quads QH h .. QH h + QH - 1 (screen32's
+// layout; QH = 1: [hi(q), lo(q)] is the B operand itself).  Missing features
+// and padding rows are 0.
+template <int QH>
+__global__ void split_copy_kernel(const float* __restrict__ x, int64_t n, int64_t n_pad, int d,
+                                  const float* __restrict__ ms, float sig,
+                                  uint4* __restrict__ xs) {
+  const int64_t total = n_pad * 2;  // (point, half) pairs
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t tile = t >> 6;
+    const int h = (int)((t >> 5) & 1), p = (int)(t & 31);
+    const int64_t i = tile * 32 + p;
+    unsigned hw[2 * QH], lw[2 * QH];
+#pragma unroll
+    for (int u = 0; u < QH; ++u) {
+      f4 xt;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 4 * (QH * h + u) + c;
+        xt[c] = (f < d && i < n) ? fmaf(x[xidx(f, i, n_pad)], sig, ms[f]) : 0.0f;
+      }
+      split4(xt, hw[2 * u], hw[2 * u + 1], lw[2 * u], lw[2 * u + 1]);
+    }
+    uint4* dst = xs + (size_t)t * QH;  // 16 QH bytes per (point, half)
+    if (QH == 1) {
+      dst[0] = uint4{hw[0], hw[1], lw[0], lw[1]};
+    } else {
+      dst[0] = uint4{hw[0], hw[1], hw[2], hw[3]};
+      dst[1] = uint4{lw[0], lw[1], lw[2], lw[3]};
+    }
+  }
+}
+
+struct S32DArgs {
+  const unsigned char* XS;  // split copy (tiles of 32 points, 1024 QH bytes each)
+  int64_t n, n_pad;
+  const h8* frag;
+  const float* cinit;
+  float thr0, thr_rel;
+  const float* thr_dev;
+  const long long* gate;
+  int32_t* labels;
+  int2* fb_list;      // per-wave regions of uncertified points {pt, old label}
+  int32_t* fb_count;  // per-wave counts, then the step total at [nwaves]
+  int2* mv_list;      // per-wave regions of moved points
+  int32_t* mv_count;
+  int cap;
+};
+
+template <int QH, int MT>
+__global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
+  if (a.gate && a.gate[0] == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int p = lane & 31;
+  h8 A[MT][2];
+  f16v Ci[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) A[m][u] = a.frag[(m * 2 + u) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Ci[m][i] = a.cinit[(m * 16 + i) * 64 + lane];
+  }
+  const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
+  const int wpb = blockDim.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+  const int nwaves = gridDim.x * wpb;
+  const int64_t ngroups = a.n_pad >> 6;
+  int2* fb_region = a.fb_list + (size_t)wave * a.cap;
+  int2* mv_region = a.mv_list + (size_t)wave * a.cap;
+  int fb_used = 0, mv_used = 0;
+  // per group: two tiles of 1024 QH bytes; lane (h, p) reads 16 QH bytes at
+  // (h * 32 + p) * 16 QH of each tile
+  constexpr int kTile = 1024 * QH;
+  const unsigned loff = (unsigned)((h * 32 + p) * 16 * QH);
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  struct Buf {
+    u4v v[2][QH];  // [tile][0] = H (QH = 2: hi of both quads; QH = 1: hi | lo), [tile][1] = L
+    int ob;
+  };
+  auto load = [&](Buf& b, int64_t G) {
+    if (G < ngroups) {
+      const unsigned char* base = a.XS + (size_t)G * (2 * kTile);  // wave-uniform
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < QH; ++u)
+          b.v[t][u] = *reinterpret_cast<const u4v*>(base + loff + t * kTile + 16 * u);
+      b.ob = a.labels[G * 64 + lane];
+    }
+  };
+  // (best, runner-up) keys of one 32-point tile, as screen32's tile()
+  auto tile = [&](const u4v (&v)[QH], unsigned& bk, unsigned& sk) {
+    const h8 BH = __builtin_bit_cast(h8, v[0]);
+    f16v acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BH, Ci[m], 0, 0, 0);
+      if constexpr (QH == 2) {
+        const h8 BL = __builtin_bit_cast(h8, v[1]);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BL, acc[m], 0, 0, 0);
+      }
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][1], BH, acc[m], 0, 0, 0);
+    }
+    auto key = [&](int m, int i) {
+      return (__float_as_uint(acc[m][i]) & ~63u) | (unsigned)(32 * m + 8 * (i >> 2) + (i & 3));
+    };
+    unsigned b, s;
+    {
+      const unsigned k0 = key(0, 0), k1 = key(0, 1);
+      b = min(k0, k1);
+      s = max(k0, k1);
+    }
+#pragma unroll
+    for (int q = 2; q < 16 * MT; q += 2) {
+      const unsigned x = key(q >> 4, q & 15), y = key(q >> 4, (q & 15) + 1);
+      unsigned t;
+      asm("v_med3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(b), "v"(x), "v"(y));
+      asm("v_min3_u32 %0, %1, %2, %3" : "=v"(b) : "v"(b), "v"(x), "v"(y));
+      s = min(s, t);
+    }
+    bk = b | ((unsigned)h << 2);
+    sk = s | ((unsigned)h << 2);
+  };
+  auto process = [&](const Buf& b, int64_t G) {
+    const int64_t base = G << 6;
+    if (base >= a.n) return;  // wave-uniform: padding groups have no real points
+    unsigned bA, sA, bB, sB;
+    tile(b.v[0], bA, sA);
+    tile(b.v[1], bB, sB);
+    swap32(bA, bB);
+    swap32(sA, sB);
+    merge_top2(bA, sA, bB, sB);
+    const int64_t pt = base + lane;
+    const int label = (int)(bA & 63u);
+    const float vb = __uint_as_float(bA & ~63u);
+    const float vs = __uint_as_float(sA & ~63u);
+    const bool cert = vs > fmaf(vb, thr_rel, thr0);  // NaN: never certified
+    const bool real = pt < a.n;
+    const bool moved = cert && real && label != b.ob;
+    if (moved) a.labels[pt] = label;
+    const unsigned long long mv = __ballot(moved);
+    if (mv) {
+      const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(mv >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((unsigned)mv, 0u));
+      if (moved) mv_region[mv_used + r] = int2{(int)pt, b.ob | (label << 16)};
+      mv_used += __popcll(mv);
+    }
+    const unsigned long long need = __ballot(real && !cert);
+    if (need) {
+      const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+      if (real && !cert) fb_region[fb_used + r] = int2{(int)pt, b.ob};
+      fb_used += __popcll(need);
+    }
+  };
+  const int64_t gs = nwaves;
+  int64_t G = wave;
+  Buf b0, b1;
+  load(b0, G);
+  for (; G < ngroups; G += 2 * gs) {
+    load(b1, G + gs);
+    process(b0, G);
+    if (G + gs >= ngroups) break;
+    load(b0, G + 2 * gs);
+    process(b1, G + gs);
+  }
+  if (lane == 0) {
+    a.fb_count[wave] = fb_used;
+    a.mv_count[wave] = mv_used;
+    if (fb_used) atomicAdd(a.fb_count + nwaves, fb_used);
+  }
+}
+
+struct FixArgs {
+  const float* XA;     // the points row-major, d4 floats per point (one line each)
+  int64_t n_pad;
+  const double* cent;  // k x d fp64 centroids of the step
+  int k, d;
+  int32_t* labels;
+  const int2* fb_list;  // {pt, old label}
+  const int32_t* fb_count;
+  const int2* mv_list;
+  const int32_t* mv_count;
+  int cap;
+  int regions;  // screen32d waves
+  double fx;    // 2^S
+  unsigned long long* run_sums;  // kRunSlices x (k, d+1)
+  const long long* gate;
+  int abl;  // timing experiments only (0 in the product build): 1 no moves, 2 no fallback,
+           // 4 no flush, 8 first candidate only, 16 no point gather, 32 no label / table change
+  // the step's screen (the uncertified points are screened again)
+  const unsigned char* XS;
+  const h8* frag;
+  const float* cinit;
+  float thr0, thr_rel;
+  const float* thr_dev;
+};
+
+// Workgroup b applies the lists of screen32d waves 4b .. 4b+3 (a region
+// spread over the whole workgroup) to an LDS table (rows padded to 65: the
+// lanes of one point hit different banks).
+// * Moves, 4 lanes per point (lane q: feature quad q): +x into the new
+//   cluster, -x out of the old one.
+// * Uncertified points, 64 per wave: the screen of screen32d is recomputed
+//   for them (the same plan, so the same values), and every centroid whose
+//   key is within the certification threshold of the best key is a candidate
+//   (|S_j - T_j| <= E for all j: the reference's argmin is among them; a point
+//   is certified exactly when the best is the only one).  The lane owning the
+//   point evaluates its candidates in index order in exact fp64 NumPy order
+//   with a correctly rounded sqrt: np.argmin of np.linalg.norm, first index on
+//   ties (src/kmeans_plusplus.py:33-34).
+template <int D, int MT>
+__global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
+  if (a.gate && a.gate[0] == 0) return;
+  constexpr int CS = D + 1;
+  constexpr int Q = (D + 3) / 4;
+  constexpr int TS = 65;  // table row stride
+  __shared__ double tsum[D * TS];
+  __shared__ int tcnt[64];
+  __shared__ double cs[64 * CS];
+  __shared__ int s_mv[5], s_fb[5];
+  const int k = a.k;
+  const int r0 = blockIdx.x * 4;
+  if (threadIdx.x < 4) {
+    const int r = r0 + threadIdx.x;
+    s_mv[threadIdx.x + 1] = r < a.regions ? a.mv_count[r] : 0;
+    s_fb[threadIdx.x + 1] = r < a.regions ? a.fb_count[r] : 0;
+  }
+  // the step's centroids (fp64), loaded by every thread at once
+#pragma unroll 4
+  for (int i = threadIdx.x; i < k * D; i += blockDim.x) {
+    const double v = a.cent[i];
+    cs[(i / D) * CS + i % D] = v;
+  }
+  for (int i = threadIdx.x; i < D * TS; i += blockDim.x) tsum[i] = 0.0;
+  for (int i = threadIdx.x; i < 64; i += blockDim.x) tcnt[i] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s_mv[0] = s_fb[0] = 0;
+    for (int r = 1; r <= 4; ++r) {
+      s_mv[r] += s_mv[r - 1];
+      s_fb[r] += s_fb[r - 1];
+    }
+  }
+  __syncthreads();
+  const int nmv = s_mv[4], nfb = s_fb[4];
+  if (nmv == 0 && nfb == 0) return;  // uniform: nothing changes here
+  const f4* XA4 = reinterpret_cast<const f4*>(a.XA);  // point i: XA4[i * Q + q]
+  auto region_of = [&](const int* pre, int e, int& r, int& i) {
+    r = 0;
+    while (r < 3 && e >= pre[r + 1]) ++r;
+    i = e - pre[r];
+  };
+  const int g = threadIdx.x >> 2, q4 = threadIdx.x & 3;
+  // moved points: 64 per pass, lane q4 adds feature quad q4
+  for (int e0 = 0; e0 < ((a.abl & 1) ? 0 : nmv); e0 += 64) {
+    const int e = e0 + g;
+    if (e < nmv && q4 < Q) {
+      int r, i;
+      region_of(s_mv, e, r, i);
+      const int2 rec = a.mv_list[(size_t)(r0 + r) * a.cap + i];
+      const f4 xq = XA4[(int64_t)rec.x * Q + q4];
+      const int to = rec.y >> 16, from = rec.y & 0xFFFF;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 4 * q4 + c;
+        if (f < D) {
+          atomicAdd(&tsum[f * TS + to], (double)xq[c]);
+          atomicAdd(&tsum[f * TS + from], -(double)xq[c]);
+        }
+      }
+      if (q4 == 0) {
+        atomicAdd(&tcnt[to], 1);
+        atomicAdd(&tcnt[from], -1);
+      }
+    }
+  }
+  if (nfb && !(a.abl & 2)) {
+    constexpr int QH = D <= 8 ? 1 : 2;
+    constexpr int kTile = 1024 * QH;
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int h = lane >> 5, p = lane & 31;
+    h8 A[MT][2];
+    f16v Ci[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) A[m][u] = a.frag[(m * 2 + u) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) Ci[m][i] = a.cinit[(m * 16 + i) * 64 + lane];
+    }
+    const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
+    auto rec_of = [&](int e) -> int2 {
+      int r, i;
+      region_of(s_fb, e, r, i);
+      return a.fb_list[(size_t)(r0 + r) * a.cap + i];
+    };
+    for (int e0 = wv * 64; e0 < nfb; e0 += 256) {
+      // tile t holds list entries e0 + 32 t .. + 31; lane (h, p) the B
+      // operand of entry e0 + 32 t + p (its half h), as screen32d loads it
+      int32_t ptt[2], oldt[2];
+      u4v v[2][QH];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int e = e0 + 32 * t + p;
+        const int2 rec = e < nfb ? rec_of(e) : int2{-1, 0};
+        ptt[t] = rec.x;
+        oldt[t] = rec.y;
+        const int32_t q = ptt[t] < 0 ? 0 : ptt[t];
+        const unsigned char* src = a.XS + (size_t)(q >> 5) * kTile + (h * 32 + (q & 31)) * 16 * QH;
+#pragma unroll
+        for (int u = 0; u < QH; ++u) v[t][u] = *reinterpret_cast<const u4v*>(src + 16 * u);
+      }
+      // this lane's point after the half swap: entry e0 + lane (tile lane >> 5)
+      const int own = ptt[h];  // lane (h, p) owns entry e0 + 32 h + p
+      const int old = oldt[h];
+      const int e_own = e0 + lane;
+      const bool live = e_own < nfb;
+      f4 xq[Q];
+      if (live) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          xq[q] = (a.abl & 16) ? f4{0.f, 0.f, 0.f, 0.f} : XA4[(int64_t)own * Q + q];
+      }
+      // screen values and candidate masks per tile: bit 16 m + i of a lane's
+      // mask = value i of centroid tile m in its half (row 32 m + 8 (i / 4) +
+      // 4 h + i % 4); immediates only, so nothing is hoisted into registers
+      unsigned mine[2], other[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const h8 BH = __builtin_bit_cast(h8, v[t][0]);
+        f16v acc[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BH, Ci[m], 0, 0, 0);
+          if constexpr (QH == 2) {
+            const h8 BL = __builtin_bit_cast(h8, v[t][1]);
+            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BL, acc[m], 0, 0, 0);
+          }
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][1], BH, acc[m], 0, 0, 0);
+        }
+        // best key of the point over both halves (as screen32d forms keys)
+        unsigned bk = 0xFFFFFFFFu;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            bk = min(bk, (__float_as_uint(acc[m][i]) & ~63u) |
+                             (unsigned)(32 * m + 8 * (i >> 2) + (i & 3)));
+        bk |= (unsigned)h << 2;
+        bk = min(bk, (unsigned)__shfl_xor((int)bk, 32));
+        const float tau = fmaf(__uint_as_float(bk & ~63u), thr_rel, thr0);
+        unsigned cm = 0;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            // not excluded: key value <= tau (NaN: a candidate)
+            const float kv = __uint_as_float(__float_as_uint(acc[m][i]) & ~63u);
+            if (!(kv > tau)) cm |= 1u << (16 * m + i);
+          }
+        mine[t] = cm;
+        other[t] = (unsigned)__shfl_xor((int)cm, 32);
+      }
+      // lane (h, p) owns tile h's point p: its rows of half h are in mine[h],
+      // those of half 1 - h in other[h]; as a 64-bit row mask
+      unsigned long long cand = 0;
+      {
+        const unsigned mh[2] = {h == 0 ? mine[0] : other[1], h == 0 ? other[0] : mine[1]};
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          unsigned mm = mh[hh];  // rows of half hh of tile h
+          while (mm) {
+            const int bb = __builtin_ctz(mm);
+            mm &= mm - 1;
+            const int m = bb >> 4, i = bb & 15;
+            cand |= 1ull << (32 * m + 8 * (i >> 2) + 4 * hh + (i & 3));
+          }
+        }
+        if (k < 64) cand &= (1ull << k) - 1;
+      }
+      if (live) {
+        double x[D];
+#pragma unroll
+        for (int f = 0; f < D; ++f) x[f] = (double)xq[f >> 2][f & 3];
+        double sb = INFINITY, rb = INFINITY;
+        int jmin = 0x7fffffff;
+        unsigned long long cmk = (a.abl & 8) ? (cand & (~cand + 1)) : cand;
+        while (cmk) {  // increasing j
+          const int j = __builtin_ctzll(cmk);
+          cmk &= cmk - 1;
+          const double* cj = cs + j * CS;
+          const double sq =
+              np_sqdist([&](int f) { return x[f]; }, [&](int f) { return cj[f]; }, D);
+          if (sq < sb) {  // sqrt is monotone: only a smaller square can give a smaller root
+            const double rt = sqrt(sq);
+            sb = sq;
+            if (rt < rb) {
+              rb = rt;
+              jmin = j;
+            }
+          }
+        }
+        if (jmin >= k) jmin = 0;  // every root NaN: np.argmin of all-NaN is 0
+        if (jmin != old && !(a.abl & 32)) {
+          a.labels[own] = jmin;
+#pragma unroll
+          for (int f = 0; f < D; ++f) {
+            atomicAdd(&tsum[f * TS + jmin], x[f]);
+            atomicAdd(&tsum[f * TS + old], -x[f]);
+          }
+          atomicAdd(&tcnt[jmin], 1);
+          atomicAdd(&tcnt[old], -1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (a.abl & 4) return;
+  const int d1 = a.d + 1, cells = k * d1;
+  unsigned long long* out = a.run_sums + (size_t)(blockIdx.x % kRunSlices) * cells;
+  for (int e = threadIdx.x; e < cells; e += blockDim.x) {
+    const int j = e / d1, r = e - j * d1;
+    const long long v = r < a.d ? __double2ll_rn(tsum[r * TS + j] * a.fx) : (long long)tcnt[j];
+    if (v) atomicAdd(&out[e], (unsigned long long)v);
   }
 }
 
@@ -764,69 +1093,6 @@ void plan32_point_side(const Ctx& c, double& xxmax, double& l1x) {
   xxmax *= 1.0 + 1e-6;
 }
 
-// Certification constants from the centroid side (ccmax =
-// max ||chat||^2, l1c = max ||chat||_1) and the point side.  Shared by the
-// host plan (build_plan32) and the device plan (plan32_kernel): the same
-// fp64 operations in the same order, so both give the same bits.
-__host__ __device__ inline void plan32_bounds(double ccmax, double l1c, double xxmax, double l1x,
-                                              int QH, double& D, float& thr0) {
-  const double u = ldexp(1.0, -24);
-  const int nmfma = QH == 2 ? 3 : 2;
-  const double N = 16.0 * nmfma + 1.0;
-  // fp32 accumulation inside the MFMA chain, order unknown, each addition
-  // erring by at most 2u (no assumption on internal extra precision)
-  const double gamma = 2.0 * u * N / (1.0 - 2.0 * u * N);
-  // D >= max ||xhat||^2 + margin so that every screen value stays >= 0
-  const double E0 = gamma * (2.0 * ccmax + 2.0 * xxmax + 4.0) + 2.4 * ldexp(1.0, -22) *
-                    (ccmax + xxmax) + u * (ccmax + 2.0 * xxmax + 4.0) +
-                    ldexp(1.0, -24) * (l1c + l1x) + ldexp(1.0, -40);
-  D = xxmax + 4.0 * E0 + ldexp(1.0, -20);
-  const double sum_abs = (ccmax + D) * (1.0 + u) + (1.0 + ldexp(1.0, -9)) * (ccmax + xxmax);
-  const double E = gamma * sum_abs + 2.4 * ldexp(1.0, -22) * (ccmax + xxmax) + u * (ccmax + D) +
-                   ldexp(1.0, -24) * (l1c + l1x) + ldexp(1.0, -46) * (ccmax + D);
-  // reference slack: the fp64 distances and roots must not tie or flip
-  const double Wmax = (sqrt(ccmax) + sqrt(xxmax)) * (sqrt(ccmax) + sqrt(xxmax));
-  const double slack = ldexp(Wmax + 1.0, -38);
-  thr0 = (float)((2.0 * E + slack) * 1.001);
-}
-
-// Fragments of one lane of 32-centroid tile m: A1 = -2 chi, A3 = -2 clo (the
-// lane-half quad layout of screen32), and its 16 C-operand values.
-__host__ __device__ inline void plan32_lane(const double* ch, const double* cc, double D, int k,
-                                            int d, int QH, int m, int lane, h8& A1, h8& A3,
-                                            float* cin16) {
-  const int h = lane >> 5;
-  const int j = 32 * m + (lane & 31);  // A row
-  for (int i = 0; i < 8; ++i) {
-    A1[i] = (_Float16)0.0f;
-    A3[i] = (_Float16)0.0f;
-  }
-  for (int uq = 0; uq < QH; ++uq) {
-    const int q = QH * h + uq;
-    for (int i = 0; i < 4; ++i) {
-      const int f = 4 * q + i;
-      if (j >= k || f >= d) continue;
-      const double v = ch[(size_t)j * d + f];
-      const _Float16 hi = f64_to_f16(v);
-      const _Float16 lo = f64_to_f16(v - (double)hi);
-      const _Float16 m2hi = f64_to_f16(-2.0 * (double)hi);
-      const _Float16 m2lo = f64_to_f16(-2.0 * (double)lo);
-      if (QH == 1) {  // H = [hi(q0), lo(q0)]
-        A1[i] = m2hi;
-        A1[4 + i] = m2hi;
-        A3[i] = m2lo;
-      } else {  // H = [hi(q0), hi(q1)], L = [lo(q0), lo(q1)]
-        A1[4 * uq + i] = m2hi;
-        A3[4 * uq + i] = m2lo;
-      }
-    }
-  }
-  for (int i = 0; i < 16; ++i) {
-    const int row = 32 * m + 8 * (i >> 2) + 4 * h + (i & 3);
-    cin16[i] = row < k ? (float)(cc[row] + D) : 1.0e30f;
-  }
-}
-
 // Fragments, C operand and certification constants.
 static bool build_plan32(const Ctx& c, const double* C, int k, Plan32& pl) {
   const int d = c.d;
@@ -867,13 +1133,8 @@ static bool build_plan32(const Ctx& c, const double* C, int k, Plan32& pl) {
   return true;
 }
 
-// Device plan for the device-resident loop (loop.hip): one workgroup builds
-// from the current centroids C (k x d fp64, device) exactly what build_plan32
-// builds on the host, into the plan buffer laid out as the host upload:
-// frag [MT][2][64] h8 | cinit [MT][16][64] f32 | C copy k x d f64 | thr0 f32.
-// The fp16 range guard failing (or a NaN) stops the loop with reason
-// kLLHostPlan (the host then takes that step on the host-plan path).
-// k <= 64, d <= 16 (screen32 shapes).
+// Device plan of the loop's centroids (c.ll_C) at begin / resume; later
+// steps are planned by ll_finalize right after it moves the centroids.
 __global__ __launch_bounds__(256) void plan32_kernel(const double* __restrict__ C, int k, int d,
                                                      int QH, int MT,
                                                      const double* __restrict__ mu, double sc,
@@ -881,62 +1142,7 @@ __global__ __launch_bounds__(256) void plan32_kernel(const double* __restrict__ 
                                                      long long* __restrict__ state,
                                                      unsigned char* __restrict__ plan) {
   if (state[0] == 0) return;
-  __shared__ double ch[64 * 16];
-  __shared__ double cc[64], l1s[64], cas[64];
-  __shared__ double sD;
-  __shared__ int ok;
-  const int t = threadIdx.x;
-  if (t < k) {
-    double s = 0.0, l1 = 0.0, ca = 0.0;
-    for (int f = 0; f < d; ++f) {
-      const double v = (C[(size_t)t * d + f] - mu[f]) * sc;
-      ch[t * d + f] = v;
-      s += v * v;
-      l1 += fabs(v);
-      ca = fmax(ca, fabs(v));
-    }
-    cc[t] = s;
-    l1s[t] = l1;
-    cas[t] = ca;
-  }
-  __syncthreads();
-  const size_t b_frag = (size_t)MT * 2 * 64 * sizeof(h8);
-  const size_t b_cinit = (size_t)MT * 16 * 64 * sizeof(float);
-  const size_t b_cent = sizeof(double) * (size_t)k * d;
-  if (t == 0) {
-    double ccmax = 0.0, l1c = 0.0, cabs = 0.0;
-    for (int j = 0; j < k; ++j) {  // max is exact: same value as the host's loop
-      ccmax = fmax(ccmax, cc[j]);
-      l1c = fmax(l1c, l1s[j]);
-      cabs = fmax(cabs, cas[j]);
-    }
-    ok = cabs <= 1024.0;
-    if (!ok) {
-      state[0] = 0;
-      state[2] = 3;  // kLLHostPlan
-    } else {
-      double D;
-      float thr0;
-      plan32_bounds(ccmax, l1c, xxmax, l1x, QH, D, thr0);
-      sD = D;
-      *reinterpret_cast<float*>(plan + b_frag + b_cinit + b_cent) = thr0;
-    }
-  }
-  __syncthreads();
-  if (!ok) return;
-  h8* frag = reinterpret_cast<h8*>(plan);
-  float* cinit = reinterpret_cast<float*>(plan + b_frag);
-  double* cent = reinterpret_cast<double*>(plan + b_frag + b_cinit);
-  for (int idx = t; idx < MT * 64; idx += blockDim.x) {
-    const int m = idx >> 6, lane = idx & 63;
-    float cin[16];
-    h8 A1, A3;
-    plan32_lane(ch, cc, sD, k, d, QH, m, lane, A1, A3, cin);
-    frag[(m * 2 + 0) * 64 + lane] = A1;
-    frag[(m * 2 + 1) * 64 + lane] = A3;
-    for (int i = 0; i < 16; ++i) cinit[(m * 16 + i) * 64 + lane] = cin[i];
-  }
-  for (int i = t; i < k * d; i += blockDim.x) cent[i] = C[i];
+  plan32_build(C, k, d, QH, MT, mu, sc, xxmax, l1x, state, plan);
 }
 
 static int s32_blocks_per_cu(int QH, int MT, size_t lds) {
@@ -980,6 +1186,159 @@ void ensure_precentered(Ctx& c) {
 
 // One F32X Lloyd step through screen32; returns false (nothing launched) when
 // the centroids are out of the fp16 split range.
+// Row-major copy of the points (d4 floats per point): fixup32's gathers touch
+// one line (and one page) per point instead of one per feature quad.
+__global__ void aos_copy_kernel(const float4* __restrict__ x, int64_t n_pad, int Q,
+                                float4* __restrict__ xa) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_pad * Q;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / Q;
+    const int q = (int)(t - i * Q);
+    xa[t] = x[(int64_t)q * n_pad + i];
+  }
+}
+
+// Split screen copy and row-major copy (screen32d / fixup32), built once per
+// point set.
+static void ensure_split(Ctx& c, int QH) {
+  if (c.xs_valid && c.xs_qh == QH) return;
+  const int Q = d4_of(c.d) / 4;
+  c.xa32.ensure(sizeof(float) * (size_t)c.n_pad * 4 * Q);
+  hipLaunchKernelGGL(aos_copy_kernel, dim3(4096), dim3(256), 0, c.stream, c.x32.as<float4>(),
+                     c.n_pad, Q, c.xa32.as<float4>());
+  HIP_CHECK(hipGetLastError());
+  c.xs16.ensure((size_t)c.n_pad * 32 * QH);
+  const float sig = (float)std::ldexp(1.0, c.sigma);
+  if (QH == 1)
+    hipLaunchKernelGGL(split_copy_kernel<1>, dim3(4096), dim3(256), 0, c.stream, c.x32.as<float>(),
+                       c.n, c.n_pad, c.d, c.mu_s.as<float>(), sig, c.xs16.as<uint4>());
+  else
+    hipLaunchKernelGGL(split_copy_kernel<2>, dim3(4096), dim3(256), 0, c.stream, c.x32.as<float>(),
+                       c.n, c.n_pad, c.d, c.mu_s.as<float>(), sig, c.xs16.as<uint4>());
+  HIP_CHECK(hipGetLastError());
+  c.xs_valid = true;
+  c.xs_qh = QH;
+}
+
+template <int QH, int MT>
+static int s32d_blocks_per_cu() {
+  static int nb = 0;
+  if (!nb) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32d<QH, MT>, 256, 0) != hipSuccess ||
+        nb < 1)
+      nb = 2;
+    if (nb > 8) nb = 8;
+  }
+  return nb;
+}
+
+// A DELTA step on screen32d + fixup32 (labels and running sums as screen32's).
+static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const float* dcinit,
+                           const double* dcent, float thr0, float thr_rel, const float* dthr,
+                           long long* dout, long long* hout, bool prof, long long* gate) {
+  ensure_split(c, QH);
+  const int64_t groups = c.n_pad / 64;
+  const int cus = lloyd_num_cus(c.device);
+  int bpc;
+  if (QH == 1 && MT == 1) bpc = s32d_blocks_per_cu<1, 1>();
+  else if (QH == 1) bpc = s32d_blocks_per_cu<1, 2>();
+  else if (MT == 1) bpc = s32d_blocks_per_cu<2, 1>();
+  else bpc = s32d_blocks_per_cu<2, 2>();
+  int nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * bpc);
+  if (nwg < 1) nwg = 1;
+  const int nwaves = nwg * 4;
+  const int cap = (int)(ceil_div(groups, nwaves) * 64);
+  c.fb_list.ensure(sizeof(int2) * (size_t)nwaves * cap);
+  c.mv_list.ensure(sizeof(int2) * (size_t)nwaves * cap);
+  c.mv_count.ensure(sizeof(int32_t) * (size_t)nwaves);
+  if (c.fb_count.bytes < sizeof(int32_t) * (nwaves + 3) || c.fb_layout != nwaves) {
+    c.fb_count.ensure(sizeof(int32_t) * (nwaves + 3));
+    HIP_CHECK(hipMemsetAsync(c.fb_count.p, 0, sizeof(int32_t) * (nwaves + 3), c.stream));
+    c.fb_layout = nwaves;
+  }
+  c.fb_regions = nwaves;
+  c.fb_total_slot = nwaves + 1;
+  S32DArgs a;
+  a.XS = c.xs16.as<unsigned char>();
+  a.n = c.n;
+  a.n_pad = c.n_pad;
+  a.frag = dfrag;
+  a.cinit = dcinit;
+  a.thr0 = thr0;
+  a.thr_rel = thr_rel;
+  a.thr_dev = dthr;
+  a.gate = gate;
+  a.labels = c.labels.as<int32_t>();
+  a.fb_list = c.fb_list.as<int2>();
+  a.fb_count = c.fb_count.as<int32_t>();
+  a.mv_list = c.mv_list.as<int2>();
+  a.mv_count = c.mv_count.as<int32_t>();
+  a.cap = cap;
+  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32d<%d,%d>", QH, MT);
+  if (prof) prof_mark(c, 0);
+  const dim3 grid(nwg), blk(256);
+  if (QH == 1 && MT == 1) hipLaunchKernelGGL((screen32d<1, 1>), grid, blk, 0, c.stream, a);
+  else if (QH == 1) hipLaunchKernelGGL((screen32d<1, 2>), grid, blk, 0, c.stream, a);
+  else if (MT == 1) hipLaunchKernelGGL((screen32d<2, 1>), grid, blk, 0, c.stream, a);
+  else hipLaunchKernelGGL((screen32d<2, 2>), grid, blk, 0, c.stream, a);
+  HIP_CHECK(hipGetLastError());
+  if (prof) prof_mark(c, 1);
+  FixArgs f;
+  f.XA = c.xa32.as<float>();
+  f.n_pad = c.n_pad;
+  f.cent = dcent;
+  f.k = k;
+  f.d = c.d;
+  f.labels = c.labels.as<int32_t>();
+  f.fb_list = c.fb_list.as<int2>();
+  f.fb_count = c.fb_count.as<int32_t>();
+  f.mv_list = c.mv_list.as<int2>();
+  f.mv_count = c.mv_count.as<int32_t>();
+  f.cap = cap;
+  f.regions = nwaves;
+  f.fx = std::ldexp(1.0, c.scale_bits);
+  f.run_sums = c.run_sums.as<unsigned long long>();
+  f.gate = gate;
+  f.abl = 0;
+  f.XS = c.xs16.as<unsigned char>();
+  f.frag = dfrag;
+  f.cinit = dcinit;
+  f.thr0 = thr0;
+  f.thr_rel = thr_rel;
+  f.thr_dev = dthr;
+#ifdef CDR_EXPERIMENTS
+  if (const char* e = std::getenv("CDR_FIX_ABL")) f.abl = std::atoi(e);
+#endif
+  const dim3 fgrid((nwaves + 3) / 4);
+  switch (c.d) {
+#define CDR_FIX(D_)                                                                  \
+  case D_:                                                                           \
+    if (MT == 1) hipLaunchKernelGGL((fixup32<D_, 1>), fgrid, blk, 0, c.stream, f);    \
+    else hipLaunchKernelGGL((fixup32<D_, 2>), fgrid, blk, 0, c.stream, f);            \
+    break;
+    CDR_FIX(1) CDR_FIX(2) CDR_FIX(3) CDR_FIX(4) CDR_FIX(5) CDR_FIX(6) CDR_FIX(7) CDR_FIX(8)
+    CDR_FIX(9) CDR_FIX(10) CDR_FIX(11) CDR_FIX(12) CDR_FIX(13) CDR_FIX(14) CDR_FIX(15)
+    CDR_FIX(16)
+#undef CDR_FIX
+    default: CDR_FAIL(CDR_ERR_STATE, "screen32d: d > 16");
+  }
+  HIP_CHECK(hipGetLastError());
+  const int len = k * (c.d + 1);
+  long long* hout_dev = nullptr;
+  if (hout) {
+    void* hp = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer(&hp, hout, 0));
+    hout_dev = static_cast<long long*>(hp);
+  }
+  c.fb_accum.ensure(sizeof(long long));
+  if (dout || hout_dev || !gate) {
+    hipLaunchKernelGGL(publish32, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(),
+                       len, dout, hout_dev, gate ? nullptr : c.fb_count.as<int32_t>(), nwaves,
+                       c.prof_on ? c.fb_accum.as<long long>() : nullptr, gate);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
 // One F32X Lloyd step through screen32.  C != null: host plan (built here,
 // uploaded with the step); returns false (nothing launched) when the
 // centroids are out of the fp16 split range.  C == null: device-resident loop
@@ -1002,14 +1361,14 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   // previous step of this point set and k
   const bool delta = c.run_valid && c.run_k == k && !dbg && !std::getenv("CDR_NO_DELTA");
   const int len = k * (c.d + 1);
-  c.run_sums.ensure(sizeof(long long) * len);
+  c.run_sums.ensure(sizeof(long long) * len * kRunSlices);
   if (!delta) {
     if (gate) {
-      hipLaunchKernelGGL(zero_gated, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(),
-                         len, gate);
+      hipLaunchKernelGGL(zero_gated, dim3(4), dim3(256), 0, c.stream, c.run_sums.as<long long>(),
+                         len * kRunSlices, gate);
       HIP_CHECK(hipGetLastError());
     } else {
-      HIP_CHECK(hipMemsetAsync(c.run_sums.p, 0, sizeof(long long) * len, c.stream));
+      HIP_CHECK(hipMemsetAsync(c.run_sums.p, 0, sizeof(long long) * len * kRunSlices, c.stream));
     }
   }
   c.run_valid = false;
@@ -1027,9 +1386,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   const size_t b_cent = sizeof(double) * (size_t)k * c.d;
   const size_t b_all = b_frag + b_cinit + b_cent;
   c.frag.ensure((b_all + 16 + 15) / 16 * 16);
-  if (devplan) {
-    plan32_launch(c, k, pl.QH, pl.MT);
-  } else {
+  if (!devplan) {  // (device plan: built by plan32_kernel / ll_finalize)
     // one pinned upload per step; the previous step's copy must have left the
     // staging buffer
     if (c.up_pending) HIP_CHECK(hipEventSynchronize(c.up_event));
@@ -1057,6 +1414,14 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
       reinterpret_cast<const double*>(static_cast<char*>(c.frag.p) + b_frag + b_cinit);
   const float* dthr =
       devplan ? reinterpret_cast<const float*>(static_cast<char*>(c.frag.p) + b_all) : nullptr;
+  const bool lean = delta && !dbg && !std::getenv("CDR_NO_LEAN");
+  if (lean) {
+    screen32d_step(c, pl.QH, pl.MT, k, dfrag, dcinit, dcent, pl.thr0, pl.thr_rel, dthr, dout,
+                   hout, prof, gate);
+    c.run_valid = true;
+    c.run_k = k;
+    return true;
+  }
   const size_t lds = (size_t)NF * KP * 8 + (size_t)KP * 4 + (size_t)k * 17 * 8;
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
@@ -1065,7 +1430,6 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   if (nwg < 1) nwg = 1;
   const int nwaves = nwg * 4;
   const int cap = (int)(ceil_div(groups, nwaves) * 64);
-  c.partials.ensure(sizeof(double) * (size_t)nwg * (NF + 1) * KP);
   c.fb_list.ensure(sizeof(int32_t) * (size_t)nwaves * cap);
   // per-wave counts | running total (screen) | published total: zeroed once
   // per layout; publish32 clears the running total every step
@@ -1095,7 +1459,9 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   a.thr0 = pl.thr0;
   a.thr_rel = pl.thr_rel;
   a.labels = c.labels.as<int32_t>();
-  a.partials = c.partials.as<double>();
+  a.run_sums = c.run_sums.as<unsigned long long>();
+  a.muf = pre ? c.muf.as<long long>() : nullptr;
+  a.fx = std::ldexp(1.0, c.scale_bits - (pre ? c.sigma : 0));
   a.KP = KP;
   a.fb_list = c.fb_list.as<int32_t>();
   a.fb_count = c.fb_count.as<int32_t>();
@@ -1146,16 +1512,15 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
     HIP_CHECK(hipHostGetDevicePointer(&hp, hout, 0));
     hout_dev = static_cast<long long*>(hp);
   }
-  hipLaunchKernelGGL(reduce32, dim3((len + 63) / 64, kR32Slices), dim3(256), 0, c.stream,
-                     c.partials.as<double>(), nwg, k, d, NF, KP,
-                     std::ldexp(1.0, c.scale_bits - (pre ? c.sigma : 0)),
-                     pre ? c.muf.as<long long>() : nullptr, c.run_sums.as<unsigned long long>(),
-                     gate);
-  HIP_CHECK(hipGetLastError());
   c.fb_accum.ensure(sizeof(long long));
-  hipLaunchKernelGGL(publish32, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(), len,
-                     dout, hout_dev, c.fb_count.as<int32_t>(), nwaves,
-                     c.prof_on ? c.fb_accum.as<long long>() : nullptr, gate);
+  if (dout || hout_dev || !gate) {
+    // (device loop with no all-reduce buffer: ll_finalize reads the slices and
+    // moves the fallback counter itself)
+    hipLaunchKernelGGL(publish32, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(),
+                       len, dout, hout_dev, gate ? nullptr : c.fb_count.as<int32_t>(), nwaves,
+                       c.prof_on ? c.fb_accum.as<long long>() : nullptr, gate);
+    HIP_CHECK(hipGetLastError());
+  }
   c.run_valid = dbg == nullptr;
   c.run_k = k;
   return true;

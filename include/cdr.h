@@ -114,7 +114,8 @@ int cdr_lloyd_labels(cdr_ctx* ctx, int64_t* labels);
  * and that went through the exact fp64 path.                                */
 int cdr_lloyd_stats(cdr_ctx* ctx, int64_t* n_fallback);
 /* Profiling: enable != 0 starts collecting HIP-event timings of every
- * following F32X step (on the context stream); cdr_profile_read returns
+ * enable-th following F32X step (1: every step; the event records cost the GPU
+ * a few microseconds each) on the context stream; cdr_profile_read returns
  * out[4] = {screen kernel ms (sum), steps, whole step kernels ms (sum),
  * fallback points (sum)}.                                                    */
 int cdr_profile_reset(cdr_ctx* ctx, int32_t enable);
