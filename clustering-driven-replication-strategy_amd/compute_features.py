@@ -28,6 +28,16 @@ Spark semantics kept (Spark 3.5, docker/docker-compose.yml:67):
   * ``avg(writes)`` = double(sum) / count; ``long / long`` divides as doubles;
   * rows in manifest order (Spark's order is unspecified; main.py's seed
     depends on row order, so the build pins the manifest order);
+  * an unparseable or empty timestamp is null (non-ANSI ``to_timestamp``): the
+    event still counts (:31-42), the nulls of a file form one more second
+    group (:44-46), and ``max(ts_epoch)`` ignores them (:48; all null ->
+    ``time.time()``, :50-51);
+  * a path listed twice in the manifest is joined as Spark joins it: every
+    event meets every manifest row of its path in the locality join (:37-42),
+    and the age join (:56-59) pairs every manifest row of the path with every
+    row of it again, so m rows give m * m output rows (manifest row order,
+    then age-row order); an empty path is null and joins nothing (age 0).
+    The reference's generators never write either case: parity unpinned.
   * doubles written like Java's ``Double.toString`` (decimal in [1e-3, 1e7),
     otherwise ``d.dddE<exp>``), longs as integers.
 """
@@ -50,6 +60,7 @@ OUT_COLUMNS = ["path", "access_freq", "age_seconds", "write_ratio", "locality", 
                "access_freq_norm", "age_norm", "write_ratio_norm", "locality_norm",
                "concurrency_norm"]
 LONG_COLUMNS = {"access_freq", "concurrency"}
+TS_NULL = -(2 ** 63)  # a null timestamp in the device events (include/cdr.h)
 
 _ISO = re.compile(
     r"^\s*(\d{4})-(\d{1,2})-(\d{1,2})(?:[T ](\d{1,2}):(\d{1,2})(?::(\d{1,2})(?:\.(\d{1,9}))?)?)?"
@@ -131,7 +142,7 @@ def load_manifest(path: str):
         rows = list(csv.DictReader(fh))
     paths = [r.get("path") for r in rows]
     created = np.array([np.nan if (u := parse_ts_us(r.get("creation_ts"))) is None
-                        else float(math.floor(u / 1_000_000)) for r in rows], dtype=np.float64)
+                        else float(u // 1_000_000) for r in rows], dtype=np.float64)
     primary = [r.get("primary_node") or None for r in rows]
     return paths, created, primary
 
@@ -174,9 +185,7 @@ def encode(paths, primary, log_ts, log_path, log_op, log_client):
         c = log_client[i]
         client[i] = -1 if c is None else node_id(c)
         u = parse_ts_us(log_ts[i])
-        if u is None:
-            raise ValueError(f"unparseable access-log timestamp {log_ts[i]!r} (row {i})")
-        ts_us[i] = u
+        ts_us[i] = TS_NULL if u is None else u  # Spark: null timestamp
     return file_idx, opc, client, ts_us, prim
 
 
@@ -189,15 +198,6 @@ def encode_primary(primary):
     return prim, list(nodes)
 
 
-def _bad_ts_error(data: bytes, status) -> ValueError:
-    # the span starts after the previous record: drop blank lines before it
-    span = bytes(data[int(status[4]):int(status[5])]).rsplit(b"\n", 1)[-1]
-    line = span.decode("utf-8", errors="replace")
-    field = line[:-1] if line.endswith("\r") else line
-    ts = field.split(",")[0] or None
-    return ValueError(f"unparseable access-log timestamp {ts!r} (row {int(status[1])})")
-
-
 def ingest_events(ctx: Context, paths, primary, access_log: str) -> int:
     """Access log -> resident device events of ``ctx``; returns the count."""
     prim, nodes = encode_primary(primary)
@@ -207,27 +207,73 @@ def ingest_events(ctx: Context, paths, primary, access_log: str) -> int:
     st = ctx.ingest_log(data)
     if st[2] >= 0:
         return -1  # csv syntax the device tokeniser leaves to the host
-    if st[1] >= 0:
-        raise _bad_ts_error(data, st)
-    return int(st[0])
+    return int(st[0])  # (unparseable timestamps are null events, st[3] of them)
+
+
+def expand_joins(paths, created, primary, counts, events):
+    """Spark's join multiplicity for the manifest (src/compute_features.py:37,
+    :56-59).  ``counts`` (n, 6) has every event of a path on its first
+    manifest row (the device dictionary's row); ``events`` () -> (file, client)
+    arrays of the events, read only when a path repeats.  Returns the output
+    rows: (paths, counts, creation seconds), one row per manifest row, m * m
+    rows for a path listed m times; an empty (null) path joins nothing."""
+    rows_of = {}
+    for i, p in enumerate(paths):
+        if p:
+            rows_of.setdefault(p, []).append(i)
+    created = np.where([bool(p) for p in paths], created, np.nan) if len(paths) else created
+    dup = {p: r for p, r in rows_of.items() if len(r) > 1}
+    if not dup:
+        return list(paths), counts, created
+    f_ev, c_ev = events()
+    prim, _ = encode_primary(primary)
+    local = {}
+    for p, rows in dup.items():
+        cl = c_ev[f_ev == rows[0]]
+        local[p] = sum(int(np.count_nonzero((cl >= 0) & (cl == prim[r]))) for r in rows
+                       if prim[r] >= 0)
+    out_p, out_c, out_t = [], [], []
+    for i, p in enumerate(paths):
+        if p not in dup:
+            out_p.append(p)
+            out_c.append(counts[i])
+            out_t.append(created[i])
+            continue
+        rows = dup[p]
+        c = counts[rows[0]].copy()
+        c[3] = local[p]              # every event meets every manifest row (:37)
+        c[4] = c[4] * len(rows)
+        for j in rows:               # the age join pairs row i with every row j (:56-59)
+            out_p.append(p)
+            out_c.append(c)
+            out_t.append(created[j])
+    return out_p, np.array(out_c, dtype=np.int64).reshape(-1, 6), np.array(out_t)
 
 
 def compute_features(manifest: str, access_log: str, ctx: Context | None = None):
-    """Returns (paths, table) with table (n_files, 10) float64 in OUT_COLUMNS order."""
+    """Returns (paths, table) with table (rows, 10) float64 in OUT_COLUMNS order
+    (one row per manifest row; see expand_joins for repeated paths)."""
     ctx = ctx if ctx is not None else default_context()
     paths, created, primary = load_manifest(manifest)
     n_events = ingest_events(ctx, paths, primary, access_log) if paths else -1
     if n_events >= 0:
         counts, max_ts_us = ctx.features_aggregate_resident()
+
+        def events():
+            f, _, cl, _, _ = ctx.features_events_read()
+            return f, cl
     else:
         lt, lp, lo, lc = load_access_log(access_log)
         file_idx, opc, client, ts_us, prim = encode(paths, primary, lt, lp, lo, lc)
         counts, max_ts_us = ctx.features_aggregate(file_idx, opc, client, ts_us, prim)
-        n_events = ts_us.size
-    if n_events:
+
+        def events():
+            return file_idx, client
+    if max_ts_us != TS_NULL:
         observation_end = max_ts_us / 1e6  # max(cast(ts as double)) :48
     else:
-        observation_end = time.time()  # :50-51
+        observation_end = time.time()  # no events or every timestamp null :50-51
+    paths, counts, created = expand_joins(paths, created, primary, counts, events)
     table = ctx.features_finalize(counts, created, observation_end)
     return paths, table
 

@@ -197,8 +197,10 @@ static void run_stats(Ctx& c, bool f32, std::vector<unsigned long long>& st) {
 }
 
 // Decide the storage mode and the screen transform from the statistics.
+// n_sum: the number of rows a cluster sum can run over (the whole data set:
+// n_total when this context holds one shard of it).
 static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
-                        bool have_f64_copy) {
+                        bool have_f64_copy, int64_t n_sum) {
   const int d = c.d;
   if (st[2 * d + 2])
     CDR_FAIL(CDR_ERR_NAN, "Probabilities contain NaN");  // non-finite input
@@ -217,8 +219,11 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   bool f32x = (st[2 * d + 1] == 0) && S <= 1000;
   if (f32x && c.absmax > 0) {
     const double m = std::ldexp(c.absmax, S);
-    if (!(m < 1073741824.0)) f32x = false;                       // |x|2^S < 2^30
-    if (!(m * (double)(c.n > 0 ? c.n : 1) < 4.0e18)) f32x = false;  // sums < 2^62
+    if (!(m < 1073741824.0)) f32x = false;  // |x|2^S < 2^30
+    // Every partial sum of a cluster stays below 2^53 grid units, so NumPy's
+    // sequential fp64 mean (src/kmeans_plusplus.py:41) never rounds and equals
+    // the exact int64 sum converted once: the F32X promise.
+    if (!(m * (double)(n_sum > 0 ? n_sum : 1) < 9007199254740992.0)) f32x = false;
   }
   c.mode = f32x ? CDR_MODE_F32X : CDR_MODE_F64;
   c.scale_bits = f32x ? S : 0;
@@ -311,7 +316,7 @@ void points_analyze_and_store(Ctx& c, const double* hX) {
   stage.release();
   std::vector<unsigned long long> st;
   run_stats(c, false, st);
-  decide_mode(c, st, true);
+  decide_mode(c, st, true, c.n);
 }
 
 void points_generate(Ctx& c, int64_t n_total, int64_t row_begin, int32_t n_blobs,
@@ -327,7 +332,7 @@ void points_generate(Ctx& c, int64_t n_total, int64_t row_begin, int32_t n_blobs
   HIP_CHECK(hipGetLastError());
   std::vector<unsigned long long> st;
   run_stats(c, true, st);
-  decide_mode(c, st, false);
+  decide_mode(c, st, false, n_total);
   if (c.mode != CDR_MODE_F32X)
     CDR_FAIL(CDR_ERR_STATE, "generate: synthetic data must be F32X");
 }

@@ -36,9 +36,16 @@ __device__ __forceinline__ long long sec_of(long long ts_us) {
   return (long long)floor((double)ts_us / 1000000.0);
 }
 
-// Timestamp range and order check: per-workgroup partials (part[2b], part[2b+1]
-// = min, max), then ts_minmax_fin; one atomic pair per workgroup on the same
-// two words serialised (0.3 ms at 125M events).
+// Null timestamps (Spark's to_timestamp of an unparseable string, :28): the
+// event still counts (:31-42), its second is the null group of its file
+// (:44-46: groupBy(path, sec) keeps a null key), and max(ts_epoch) (:48)
+// ignores it.
+constexpr long long kTsNull = LLONG_MIN;
+
+// Timestamp range (non-null) and order check: per-workgroup partials
+// (part[2b], part[2b+1] = min, max), then ts_minmax_fin; one atomic pair per
+// workgroup on the same two words serialised (0.3 ms at 125M events).  Any
+// null marks the log unordered (the general path groups the nulls).
 __global__ __launch_bounds__(256) void ts_minmax(const long long* __restrict__ ts, int64_t n,
                                                  long long* __restrict__ part,
                                                  int* __restrict__ unordered) {
@@ -47,6 +54,10 @@ __global__ __launch_bounds__(256) void ts_minmax(const long long* __restrict__ t
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const long long t = ts[i];
+    if (t == kTsNull) {
+      bad = 1;
+      continue;
+    }
     lo = min(lo, t);
     hi = max(hi, t);
     if (i + 1 < n) bad |= t > ts[i + 1];
@@ -102,6 +113,8 @@ __global__ __launch_bounds__(256) void ts_minmax_fin(const long long* __restrict
   }
 }
 
+// Null seconds take the all-ones code of sbits (a group of their own, after
+// every real second of the file).
 __global__ void make_keys(const int32_t* __restrict__ file, const uint8_t* __restrict__ op,
                           const int32_t* __restrict__ client, const long long* __restrict__ ts,
                           int64_t n, int64_t n_files, const int32_t* __restrict__ primary,
@@ -113,7 +126,10 @@ __global__ void make_keys(const int32_t* __restrict__ file, const uint8_t* __res
     unsigned long long key = ~0ull;
     uint8_t fl = 0;
     if (f >= 0 && f < n_files) {
-      key = ((unsigned long long)f << sbits) | (unsigned long long)(sec_of(ts[i]) - sec_min);
+      const long long t = ts[i];
+      const unsigned long long so = t == kTsNull ? (1ull << sbits) - 1
+                                                 : (unsigned long long)(sec_of(t) - sec_min);
+      key = ((unsigned long long)f << sbits) | so;
       fl = (op[i] == 1 ? 1 : 0) | (op[i] == 2 ? 2 : 0);
       const int pr = primary[f];
       if (client[i] >= 0 && pr >= 0 && client[i] == pr) fl |= 4;
@@ -376,19 +392,20 @@ void features_aggregate_resident(Ctx& c, int64_t ne, int64_t n_files, int64_t* o
   HIP_CHECK(hipStreamSynchronize(c.stream));
   const bool time_ordered = (reinterpret_cast<const int*>(&mm[2])[1]) == 0;
   long long sec_min = 0, sec_max = 0;
-  if (ne > 0) {
-    const long long tmin = (long long)(mm[0] ^ (unsigned long long)LLONG_MIN);
-    const long long tmax = (long long)(mm[1] ^ (unsigned long long)LLONG_MIN);
+  const long long tmin = (long long)(mm[0] ^ (unsigned long long)LLONG_MIN);
+  const long long tmax = (long long)(mm[1] ^ (unsigned long long)LLONG_MIN);
+  if (ne > 0 && tmin <= tmax) {  // some timestamp is not null
     *max_ts = tmax;
     sec_min = (long long)std::floor((double)tmin / 1000000.0);
     sec_max = (long long)std::floor((double)tmax / 1000000.0);
-    if (sec_max - sec_min >= (1ll << 32))
+    if (sec_max - sec_min >= (1ll << 32) - 1)
       CDR_FAIL(CDR_ERR_UNSUPPORTED, "access log spans more than 2^32 seconds");
   }
-  // compact sort keys: file << sbits | (sec - sec_min); invalid events are
-  // all ones and sort after every valid key within end_bit
+  // compact sort keys: file << sbits | (sec - sec_min), the null second all
+  // ones; invalid events are all ones and sort after every valid key within
+  // end_bit
   int sbits = 1, fbits = 1;
-  while ((1ll << sbits) <= sec_max - sec_min) ++sbits;
+  while ((1ll << sbits) - 1 <= sec_max - sec_min) ++sbits;
   while ((1ll << fbits) < n_files) ++fbits;
   const int end_bit = std::min(64, sbits + fbits + 1);
   c.fin_red.ensure(16 * nf1);

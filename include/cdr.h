@@ -180,12 +180,14 @@ int cdr_medians_by_label(cdr_ctx* ctx, int32_t k, double* out);
 /* ---- access-log group-by: src/compute_features.py:31-54 ---------------- */
 /* Events: file index (row of the manifest, -1 = path not in the manifest),
  * op (1 = WRITE, 2 = READ, other = neither), client id (-1 = null),
- * timestamp in microseconds since the epoch (Spark TimestampType units).
+ * timestamp in microseconds since the epoch (Spark TimestampType units;
+ * INT64_MIN = null: the event counts, the nulls of a file form one more
+ * second group, and the max ignores them).
  * primary[f] = client id of file f's primary node (-2 = null).
  * out (n_files, 6) int64: access_freq, writes, reads, local_accesses,
  * total_accesses, max_concurrency (sec = floor(ts_us / 1e6) in fp64, as
- * F.floor(cast(ts as double))).  *max_ts_us = max event timestamp over all
- * events (INT64_MIN when there are none).                                  */
+ * F.floor(cast(ts as double))).  *max_ts_us = max non-null event timestamp
+ * over all events (INT64_MIN when there is none).                          */
 int cdr_features_aggregate(cdr_ctx* ctx, int64_t n_events,
                            const int32_t* file_idx, const uint8_t* op,
                            const int32_t* client, const int64_t* ts_us,

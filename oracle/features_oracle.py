@@ -1,101 +1,142 @@
 """pandas restatement of the reference PySpark job (TEST INFRASTRUCTURE ONLY).
 
 Follows /root/reference/src/compute_features.py:14-94 with Spark 3.5 value
-semantics (docker/docker-compose.yml:67 pins apache/spark:3.5.2):
+semantics (docker/docker-compose.yml:67 pins apache/spark:3.5.2), one pandas
+step per Spark statement:
 
   :16-17  creation_ts_epoch = double(floorDiv(micros, 1e6))
-  :28-29  ts_epoch = micros / 1e6 (double)
+  :28-29  ts_epoch = micros / 1e6 (double); unparseable / empty -> null
   :31-35  access_freq, writes, reads per path
-  :37-42  local_accesses / total_accesses via the left join on path
-  :44-46  max over floor(ts_epoch) of per-(path, sec) counts
-  :48-54  observation_end = max(ts_epoch); age = end - creation
-  :56-60  manifest-order left joins, nulls -> 0
+  :37-42  local_accesses / total_accesses via the left join on path (an event
+          meets every manifest row of its path; null keys match nothing)
+  :44-46  max over floor(ts_epoch) of per-(path, sec) counts (null sec = group)
+  :48-54  observation_end = max(ts_epoch) skipping nulls (none -> now);
+          age = end - creation
+  :56-60  manifest-order left joins (m rows of a path x m age rows), nulls -> 0
   :62-68  write_ratio = writes / mean(writes) (0 -> 1.0); locality
   :77-94  min-max normalisation (max == min -> 0.0; longs as double(v-min)/...)
 
 PARITY UNPINNED against Spark itself (no PySpark/Java in this image): the
 timestamp parsing is a restatement of Spark's ISO-8601 handling; integer
-counts are pinned by an independent group-by.
+counts are pinned by an independent group-by (counts_from_arrays); the null
+and repeated-path rules are pinned by hand-derived values
+(tests/test_spark_semantics.py).
 """
 from __future__ import annotations
 
 import csv
 import math
+import time
 
 import numpy as np
 import pandas as pd
 
 
-def _ts_us(series: pd.Series) -> pd.Series:
-    t = pd.to_datetime(series, format="ISO8601", utc=True, errors="coerce")
-    return pd.Series(t.astype("int64") // 1000, index=series.index).where(t.notna())
+def _ts_us(series: pd.Series) -> list:
+    """to_timestamp (:17, :28) of each string -> UTC microseconds or None."""
+    t = pd.to_datetime(pd.Series(series, dtype=object), format="ISO8601", utc=True,
+                       errors="coerce")
+    us = t.astype("int64") // 1000
+    return [int(u) if ok else None for u, ok in zip(us, t.notna())]
 
 
-def compute(manifest_csv: str, log_csv: str):
-    man = pd.read_csv(manifest_csv, dtype=str, keep_default_na=False)
-    cr_us = _ts_us(man["creation_ts"])
-    creation = np.floor(cr_us.to_numpy(dtype=np.float64) / 1e6)
+def _keys(paths, tag):
+    """Join keys: Spark's equi-join never matches a null key, pandas merges
+    NaN with NaN -- so a null path gets a per-row key that matches nothing."""
+    return [p if isinstance(p, str) else f"\0{tag}{i}" for i, p in enumerate(paths)]
+
+
+def _nulls(df: pd.DataFrame) -> pd.DataFrame:
+    """spark.read.csv: an empty field is null."""
+    df = df.astype(object)
+    return df.where(df != "", None)
+
+
+def compute(manifest_csv: str, log_csv: str, now=None):
+    """The reference job, one pandas step per Spark statement.  Returns
+    (paths, table (rows, 10), counts (rows, 6): access_freq, writes, reads,
+    local_accesses, total_accesses, max_concurrency, observation_end)."""
+    man = _nulls(pd.read_csv(manifest_csv, dtype=str, keep_default_na=False))
+    cr = _ts_us(man["creation_ts"])                                        # :16-17
+    man["creation_ts_epoch"] = [np.nan if u is None else float(u // 1_000_000) for u in cr]
     rows = []
-    with open(log_csv, newline="") as fh:
+    with open(log_csv, newline="") as fh:                                  # :19-26
         for rec in csv.reader(fh):
             if rec:
                 rows.append((rec + [""] * 5)[:5])
-    log = pd.DataFrame(rows, columns=["ts", "path", "op", "client", "pid"])
-    us = _ts_us(log["ts"]).astype("int64") if len(log) else pd.Series([], dtype="int64")
-    log["sec"] = np.floor(us.to_numpy(dtype=np.int64) / 1e6).astype(np.int64) if len(log) else []
-    log["w"] = (log["op"] == "WRITE").astype(np.int64)
+    log = _nulls(pd.DataFrame(rows, columns=["ts_iso", "path", "op", "client_node", "pid"],
+                              dtype=object))
+    log["ts_epoch"] = [np.nan if u is None else u / 1e6 for u in _ts_us(log["ts_iso"])]  # :28-29
+    log["w"] = (log["op"] == "WRITE").astype(np.int64)                     # :31-35
     log["r"] = (log["op"] == "READ").astype(np.int64)
-    prim = dict(zip(man["path"], man["primary_node"]))
-    log["loc"] = [1 if (c != "" and prim.get(p, None) not in (None, "") and c == prim[p]) else 0
-                  for p, c in zip(log["path"], log["client"])]
-    g = log.groupby("path")
-    agg = pd.DataFrame({"access_freq": g.size(), "writes": g["w"].sum(), "reads": g["r"].sum(),
-                        "local": g["loc"].sum()})
-    conc = log.groupby(["path", "sec"]).size().groupby(level=0).max()
-    agg["conc"] = conc
-    if len(log):
-        obs_end = float(us.max()) / 1e6
-    else:
-        obs_end = None
-    n = len(man)
-    af = np.zeros(n, dtype=np.int64)
-    wr = np.zeros(n, dtype=np.int64)
-    lo = np.zeros(n, dtype=np.int64)
-    co = np.zeros(n, dtype=np.int64)
-    for i, p in enumerate(man["path"]):
-        if p in agg.index:
-            a = agg.loc[p]
-            af[i], wr[i], lo[i], co[i] = a["access_freq"], a["writes"], a["local"], a["conc"]
-    age = np.where(np.isnan(creation), 0.0, (obs_end if obs_end is not None else 0.0) - creation)
-    mean_w = float(wr.sum()) / n if n else 0.0
+    freq = log.groupby("path").agg(access_freq=("w", "size"), writes=("w", "sum"),
+                                   reads=("r", "sum"))
+    lk = log.assign(key=_keys(log["path"], "l"))                           # :37
+    mk = pd.DataFrame({"key": _keys(man["path"], "m"), "primary_node": man["primary_node"]})
+    awp = lk.merge(mk, on="key", how="left")
+    awp["is_local"] = [1 if isinstance(c, str) and isinstance(p, str) and c == p else 0
+                       for c, p in zip(awp["client_node"], awp["primary_node"])]  # :38-39
+    loc = awp.groupby("path").agg(local_accesses=("is_local", "sum"),      # :40-42
+                                  total_accesses=("is_local", "size"))
+    log["sec"] = np.floor(log["ts_epoch"].astype(np.float64))              # :44-46
+    conc = (log.groupby(["path", "sec"], dropna=False).size().groupby(level=0).max()
+            .rename("max_concurrency").to_frame())
+    mx = log["ts_epoch"].astype(np.float64).max() if len(log) else np.nan  # :48-51
+    obs_end = float(mx) if not np.isnan(mx) else (time.time() if now is None else now)
+    age = pd.DataFrame({"key": _keys(man["path"], "a"),                    # :53-54
+                        "age_seconds": float(obs_end) - man["creation_ts_epoch"].astype(np.float64)})
+
+    def keyed(df):
+        df = df.reset_index()
+        return df.assign(key=df["path"]).drop(columns="path")
+
+    j = pd.DataFrame({"key": _keys(man["path"], "j"), "path": man["path"]})  # :56-59
+    j = (j.merge(keyed(freq), on="key", how="left").merge(keyed(loc), on="key", how="left")
+         .merge(keyed(conc), on="key", how="left").merge(age, on="key", how="left"))
+    longs = ["access_freq", "writes", "reads", "local_accesses", "total_accesses",
+             "max_concurrency"]
+    for cname in longs:                                                    # :60
+        j[cname] = j[cname].fillna(0).astype(np.int64)
+    j["age_seconds"] = j["age_seconds"].fillna(0.0).astype(np.float64)
+    n = len(j)
+    mean_w = float(j["writes"].sum()) / n if n else 0.0                    # :62-65
     if mean_w == 0:
         mean_w = 1.0
-    write_ratio = wr / mean_w
-    locality = np.where(af > 0, lo / np.maximum(af, 1), 1.0)
+    af, co = j["access_freq"].to_numpy(), j["max_concurrency"].to_numpy()
+    lo, tot = j["local_accesses"].to_numpy(), j["total_accesses"].to_numpy()
+    age_s = j["age_seconds"].to_numpy()
+    write_ratio = j["writes"].to_numpy() / mean_w                          # :66
+    locality = np.where(tot > 0, lo / np.maximum(tot, 1), 1.0)             # :68
 
-    def norm_long(v):
-        mn, mx = int(v.min()), int(v.max())
-        return np.zeros(n) if mx == mn else (v - mn).astype(np.float64) / float(mx - mn)
+    def norm_long(v):                                                      # :77-94
+        if n == 0:
+            return np.zeros(0)
+        mn, mx_ = int(v.min()), int(v.max())
+        return np.zeros(n) if mx_ == mn else (v - mn).astype(np.float64) / float(mx_ - mn)
 
     def norm_dbl(v):
-        mn, mx = float(v.min()), float(v.max())
-        return np.zeros(n) if mx == mn else (v - mn) / (mx - mn)
+        if n == 0:
+            return np.zeros(0)
+        mn, mx_ = float(v.min()), float(v.max())
+        return np.zeros(n) if mx_ == mn else (v - mn) / (mx_ - mn)
 
-    table = np.column_stack([af.astype(np.float64), age, write_ratio, locality,
-                             co.astype(np.float64), norm_long(af), norm_dbl(age),
+    table = np.column_stack([af.astype(np.float64), age_s, write_ratio, locality,
+                             co.astype(np.float64), norm_long(af), norm_dbl(age_s),
                              norm_dbl(write_ratio), norm_dbl(locality), norm_long(co)])
-    counts = np.column_stack([af, wr, np.zeros(n, dtype=np.int64), lo, af, co])
-    return list(man["path"]), table, counts, obs_end
+    counts = j[longs].to_numpy(dtype=np.int64).reshape(-1, 6)
+    return list(j["path"]), table.reshape(-1, 10), counts, obs_end
 
 
 def counts_from_arrays(file_idx, op, client, ts_us, primary, n_files):
-    """Independent per-file counters from encoded arrays (for the device K5)."""
+    """Independent per-file counters from encoded arrays (for the device K5);
+    ts TS_NULL is a null timestamp (its own second group, not in the max)."""
     out = np.zeros((n_files, 6), dtype=np.int64)
     ok = (file_idx >= 0) & (file_idx < n_files)
     f = file_idx[ok].astype(np.int64)
     o = op[ok]
     c = client[ok]
-    sec = np.floor(ts_us[ok] / 1e6).astype(np.int64)
+    t = ts_us[ok]
+    null = t == TS_NULL
     np.add.at(out[:, 0], f, 1)
     np.add.at(out[:, 1], f, (o == 1).astype(np.int64))
     np.add.at(out[:, 2], f, (o == 2).astype(np.int64))
@@ -103,11 +144,14 @@ def counts_from_arrays(file_idx, op, client, ts_us, primary, n_files):
     np.add.at(out[:, 3], f, ((c >= 0) & (pr >= 0) & (c == pr)).astype(np.int64))
     out[:, 4] = out[:, 0]
     if f.size:
-        key = f * (1 << 33) + (sec - sec.min())
+        sec = np.where(null, 0, np.floor(np.where(null, 0, t) / 1e6)).astype(np.int64)
+        s0 = sec[~null].min() if (~null).any() else 0
+        so = np.where(null, (1 << 33) - 1, sec - s0)
+        key = f * (1 << 33) + so
         uk, cnt = np.unique(key, return_counts=True)
-        files = uk // (1 << 33)
-        np.maximum.at(out[:, 5], files, cnt)
-    mx = int(ts_us.max()) if ts_us.size else None
+        np.maximum.at(out[:, 5], uk // (1 << 33), cnt)
+    real = ts_us[ts_us != TS_NULL]
+    mx = int(real.max()) if real.size else None
     return out, mx
 
 

@@ -149,21 +149,28 @@ def test_timestamp_grammar_fuzz(ctx):
     assert 0 < st[3] < st[0]
 
 
-def test_bad_timestamp_raises_like_host_path(ctx, tmp_path):
+def test_bad_timestamp_is_null_like_host_path(ctx, tmp_path):
+    """An unparseable timestamp is a null event (Spark's non-ANSI
+    to_timestamp): device ingest, host tokeniser and the oracle agree."""
     import compute_features as cf
 
     log = tmp_path / "bad.log"
-    lines = list(EDGE_LINES[:1]) + ["", "2025-13-01T00:00:00Z,/user/root/synth/synth_1.bin,READ,dn1,1"]
+    lines = list(EDGE_LINES[:1]) + ["", "2025-13-01T00:00:00Z,/user/root/synth/synth_1.bin,READ,dn1,1",
+                                    "x,/user/root/synth/synth_1.bin,WRITE,dn2,1"]
     log.write_bytes(("\n".join(lines) + "\n").encode())
     man = os.path.join(PDIR, "metadata.csv")
     paths, _, primary = cf.load_manifest(man)
+    st = _ingest_and_check(ctx, log.read_bytes(), paths, primary)
+    assert st[0] == 3 and st[3] == 2
+    _, table = cf.compute_features(man, str(log), ctx=ctx)
     lt, lp, lo, lc = cf.load_access_log(str(log))
-    with pytest.raises(ValueError) as host:
-        cf.encode(paths, primary, lt, lp, lo, lc)
-    with pytest.raises(ValueError) as dev:
-        cf.compute_features(man, str(log), ctx=ctx)
-    assert str(dev.value) == str(host.value)
-    assert "(row 1)" in str(dev.value)
+    fidx, opc, client, ts, prim = cf.encode(paths, primary, lt, lp, lo, lc)
+    counts, mx = ctx.features_aggregate(fidx, opc, client, ts, prim)
+    _, exp_table, exp_counts, obs = fo.compute(man, str(log))
+    np.testing.assert_array_equal(counts, exp_counts)
+    assert mx / 1e6 == obs
+    np.testing.assert_array_equal(table, exp_table)
+    assert exp_counts[1, 5] == 2  # synth_1: the two null events are one second group
 
 
 def test_quoted_log_goes_to_host_tokeniser(ctx, tmp_path):

@@ -304,3 +304,15 @@ def test_large_k_ragged_shapes(ctx, n, d, k):
     want_labels, want = ko.lloyd_partials(X, C0, ctx.info()["scale_bits"])
     np.testing.assert_array_equal(ctx.labels(), want_labels)
     np.testing.assert_array_equal(out, want)
+
+
+def test_f32x_gate_keeps_numpy_mean_exact(ctx):
+    """F32X (exact int64 sums) only while every cluster partial sum stays below
+    2^53 grid units: absmax * 2^S * n < 2^53, else F64 mode."""
+    v = float(2 ** 29 - 32)  # fp32-exact, integer grid (S = 0), |x| 2^S < 2^30
+    for n, want in ((2 ** 23, 1), (2 ** 24 + 8, 2)):
+        X = np.full((n, 1), v)
+        X[::3] = 1.0
+        ctx.load_points(X)
+        inf = ctx.info()
+        assert inf["mode"] == want, (n, inf)

@@ -102,3 +102,18 @@ def test_scoring_oracle_matches_reference_golden():
         assert res == c["result"], c["name"]
     demo = cases[0]
     assert demo["result"] == {"C1": "Hot", "C2": "Archival", "C3": "Archival", "C4": "Hot"}
+
+
+def test_int64_mean_equals_numpy_mean_only_below_2_53():
+    """Why the F32X gate sits at 2^53 grid units: below it NumPy's sequential
+    fp64 sum of grid values is exact (so the exact int64 sum converted once is
+    the same number); past it the running sum rounds and the two differ."""
+    import numpy as np
+
+    small = np.array([2.0 ** 52, 1.0, 1.0, 1.0])  # partial sums < 2^53: exact
+    assert np.add.accumulate(small)[-1] == float(int(2 ** 52) + 3)
+    big = np.array([2.0 ** 53, 1.0, 1.0])  # past 2^53: each + 1 rounds away
+    seq = 0.0
+    for v in big:
+        seq = seq + v
+    assert seq == 2.0 ** 53 and float(int(2 ** 53) + 2) == 2.0 ** 53 + 2
