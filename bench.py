@@ -51,10 +51,13 @@ CONFIGS = {
     "3": (100_000_000, 16, 64, "config 3: 100M files x d=16, k=64"),
     "5": (50_000_000, 64, 1024, "config 5: 50M files x d=64, k=1024"),
 }
-# config 4 (features): events and manifest files per GPU (1B events over 8 GPUs)
-FEATURES_CFG = (125_000_000, 12_500_000,
+# config 4 (features): the reference simulator's model (src/access_simulator.py
+# with the Makefile's 600 s and 3 datanodes, src/generator.py's category mix:
+# ~168 events per file), sized so that 8 GPUs hold ~1B events
+FEATURES_CFG = (744_000, 600.0, 3,
                 "config 4: 1B access-log events over 8 GPUs -> per-file features "
-                "(125M events x 12.5M files per GPU)")
+                "(simulator model: 744K files x 600 s x 3 datanodes = ~125M events per GPU)")
+EVENTS_PER_FILE = 168.1  # mean of the simulator model (sum of category rates x 600 s)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense
 METRIC = "Lloyd point-iters/sec (whole node) + achieved HBM GB/s, 100M files d=16 k=64"
@@ -82,23 +85,24 @@ def cpu_baseline(d: int, k: int, seed: int, rows: int = 1_000_000, iters: int = 
 
 def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
     """Config 4: the compute_features group-by (src/compute_features.py:31-54)
-    over a device-resident, time-ordered synthetic log.  A step = one full
-    group-by of this rank's events (timestamp range, compact (file, second)
-    keys, radix sort, per-file runs) plus the MAX all-reduce of the log's
-    last timestamp (:48).  Weak scaling: each rank owns its files and events."""
+    over a device-resident, time-ordered log from the device access simulator
+    (csrc/simulate.hip, the model of src/access_simulator.py).  A step = one
+    full group-by of this rank's events (csrc/groupby.hip: partition by file
+    id, per-bucket LDS hash) plus the MAX all-reduce of the log's last
+    timestamp (:48).  Weak scaling: each rank simulates and owns its files."""
     import numpy as np
 
     import _cdr
 
-    ne, nf, desc = FEATURES_CFG
+    nf, duration, nclients, desc = FEATURES_CFG
     if args.n_total:
-        ne, nf = args.n_total, max(1, args.n_total // 10)
+        nf = max(1, int(args.n_total / EVENTS_PER_FILE))
     ctx = _cdr.Context(int(os.environ.get("LOCAL_RANK", "0")))
     if dist is not None:
         import torch
 
         ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-    ctx.features_generate(ne, nf, seed=args.seed ^ (rank * 0x9E3779B97F4A7C15 & (2**64 - 1)))
+    ne = ctx.features_simulate(nf, duration, nclients, seed=args.seed, file_begin=rank * nf)
 
     def step():
         _, mx = ctx.features_aggregate_resident(to_host=False)
@@ -115,6 +119,7 @@ def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> N
     if dist is not None:
         dist.barrier()
     ctx.synchronize()
+    ctx.profile_reset(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -122,6 +127,9 @@ def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> N
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile_reset(False)
+    info = ctx.features_groupby_info()
     if dist is not None:
         import torch
 
@@ -129,27 +137,32 @@ def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> N
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     per_step = elapsed / max(args.steps, 1)
+    gb_ms = prof["step_ms"] / max(prof["steps"], 1)  # HIP events around the group-by
     alg_bytes = ne * (4 + 1 + 4 + 8) + nf * (4 + 6 * 8)  # events read once, counters written
-    achieved = alg_bytes / per_step / 1e9
+    achieved = alg_bytes / (gb_ms / 1e3) / 1e9
     out = {
         "metric": "access-log events aggregated per second (whole node), compute_features group-by",
         "value": world * ne * args.steps / elapsed, "unit": "events/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_step * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-        "data": "synthetic time-ordered access log generated on the device (counter-based)",
+        "data": "synthetic time-ordered access log from the device access simulator "
+                "(per-file Poisson arrivals at jittered category rates, locality bias)",
         "config": {"workload": desc, "events_per_gpu": ne, "files_per_gpu": nf,
                    "parallelism": f"files and events partitioned over {world} GPU(s), "
                                   "RCCL MAX all-reduce of the last timestamp"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": "features group-by (keys + hipCUB radix sort + runs), whole step",
-                     "alg_bytes_per_launch": alg_bytes, "kernel_ms": per_step * 1e3},
+                     "kernel": "features group-by (csrc/groupby.hip: file-id partition + "
+                               "per-bucket LDS hash), all kernels of one step",
+                     "alg_bytes_per_launch": alg_bytes, "kernel_ms": gb_ms,
+                     "partition_ms": prof["screen_ms"] / max(prof["steps"], 1)},
+        "groupby": info,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import features_oracle
 
-        s_ne, s_nf = 10_000_000, 1_000_000
-        ctx.features_generate(s_ne, s_nf, seed=args.seed)
+        s_nf = 60_000
+        s_ne = ctx.features_simulate(s_nf, duration, nclients, seed=args.seed)
         f, op, cl, ts, pr = ctx.features_events_read()
         c0 = time.perf_counter()
         features_oracle.counts_from_arrays(f, op, cl, ts, pr, s_nf)

@@ -87,6 +87,15 @@ SIGNATURES = {
     "cdr_features_generate": ([_P, _I64, _I64, ctypes.c_uint64, _I64, _I64], None),
     "cdr_features_aggregate_resident": ([_P, _P, _PI64], None),
     "cdr_features_events_read": ([_P, _P, _P, _P, _P, _P], None),
+    "cdr_features_groupby_info": ([_P, _P], None),
+    "cdr_features_exchange_pack": ([_P, _I32, _P, _P, _P, _PI64], None),
+    "cdr_features_exchange_unpack": ([_P, _P, _I64, _I64, _I64], None),
+    "cdr_features_load_events": ([_P, _I64, _P, _P, _P, _P, _I64, _P], None),
+    "cdr_features_finalize_stats": ([_P, _I64, _P, _P, ctypes.c_double, _P, _P], None),
+    "cdr_features_finalize_apply": ([_P, _I64, _P, _P, ctypes.c_double, _P, _P, _I64, _P],
+                                    None),
+    "cdr_features_simulate": ([_P, _I64, _I64, ctypes.c_double, _I32, ctypes.c_uint64, _I64,
+                               _PI64], None),
     "cdr_ingest_manifest": ([_P, _I64, _P, _P, _P, _I32, _P, _P], None),
     "cdr_ingest_log": ([_P, _P, _I64, _P], None),
     "cdr_ingest_reparse": ([_P, _P], None),
@@ -406,6 +415,19 @@ class Context:
                                                int(span_us)))
         self._ev = (int(n_events), int(n_files))
 
+    def features_simulate(self, n_files: int, duration_s: float = 600.0, n_clients: int = 3,
+                          seed: int = 0x5EED, t0_us: int = 1_761_998_400_000_000,
+                          file_begin: int = 0) -> int:
+        """Device access simulator (include/cdr.h cdr_features_simulate);
+        returns the number of events left resident."""
+        ne = _I64()
+        _check(self._lib.cdr_features_simulate(self._h, int(n_files), int(file_begin),
+                                               float(duration_s), int(n_clients),
+                                               int(seed) & 0xFFFFFFFFFFFFFFFF, int(t0_us),
+                                               ctypes.byref(ne)))
+        self._ev = (int(ne.value), int(n_files))
+        return int(ne.value)
+
     def features_aggregate_resident(self, to_host: bool = True):
         ne, nf = self._ev
         out = np.zeros((nf, 6), dtype=np.int64) if to_host else None
@@ -413,6 +435,14 @@ class Context:
         _check(self._lib.cdr_features_aggregate_resident(
             self._h, _ptr(out) if to_host else None, ctypes.byref(mx)))
         return out, int(mx.value)
+
+    def features_groupby_info(self) -> dict:
+        """What the last group-by ran (include/cdr.h cdr_features_groupby_info)."""
+        info = np.zeros(7, dtype=np.int64)
+        _check(self._lib.cdr_features_groupby_info(self._h, _ptr(info)))
+        return {"hand": int(info[0]), "L": int(info[1]), "passes": int(info[2]),
+                "payload_bytes": int(info[3]), "big_buckets": int(info[4]),
+                "dense": int(info[5]), "bucket_grid": int(info[6])}
 
     def features_events_read(self):
         ne, nf = self._ev
@@ -455,6 +485,65 @@ class Context:
         _check(self._lib.cdr_ingest_reparse(self._h, _ptr(st)))
         self._ev = (int(st[0]), self._ing_nf)
         return st
+
+    # -- sharded aggregation (csrc/exchange.hip) ----------------------------
+    XREC_BYTES = 16
+
+    def features_exchange_pack(self, bounds, send=None):
+        """Resident events grouped by owner rank of bounds (nranks + 1 rows).
+        `send`: a host uint8 array or (device pointer) int with room for
+        16 bytes per resident event; None -> a host array is allocated.
+        Returns (send, counts (nranks,), max_ts_us)."""
+        bounds = np.ascontiguousarray(bounds, dtype=np.int64)
+        nr = bounds.size - 1
+        ne = self._ev[0]
+        if send is None:
+            send = np.zeros(max(ne, 1) * self.XREC_BYTES, dtype=np.uint8)
+        counts = np.zeros(nr, dtype=np.int64)
+        mx = _I64()
+        ptr = send if isinstance(send, int) else _ptr(send)
+        _check(self._lib.cdr_features_exchange_pack(self._h, nr, _ptr(bounds), ptr,
+                                                    _ptr(counts), ctypes.byref(mx)))
+        return send, counts, int(mx.value)
+
+    def features_exchange_unpack(self, recv, n: int, file_begin: int, file_end: int) -> None:
+        ptr = recv if isinstance(recv, int) else (_ptr(recv) if n else None)
+        _check(self._lib.cdr_features_exchange_unpack(self._h, ptr, int(n), int(file_begin),
+                                                      int(file_end)))
+        self._ev = (int(n), int(file_end - file_begin))
+
+    def features_load_events(self, file_idx, op, client, ts_us, primary) -> None:
+        f = np.ascontiguousarray(file_idx, dtype=np.int32)
+        o = np.ascontiguousarray(op, dtype=np.uint8)
+        c = np.ascontiguousarray(client, dtype=np.int32)
+        t = np.ascontiguousarray(ts_us, dtype=np.int64)
+        p = np.ascontiguousarray(primary, dtype=np.int32)
+        _check(self._lib.cdr_features_load_events(self._h, f.size, _ptr(f), _ptr(o), _ptr(c),
+                                                  _ptr(t), p.size, _ptr(p)))
+        self._ev = (int(f.size), int(p.size))
+
+    def features_finalize_stats(self, counts, creation_s, observation_end: float):
+        counts = np.ascontiguousarray(counts, dtype=np.int64)
+        creation_s = np.ascontiguousarray(creation_s, dtype=np.float64)
+        ist = np.zeros(7, dtype=np.int64)
+        dst = np.zeros(4, dtype=np.float64)
+        _check(self._lib.cdr_features_finalize_stats(self._h, creation_s.size, _ptr(counts),
+                                                     _ptr(creation_s), float(observation_end),
+                                                     _ptr(ist), _ptr(dst)))
+        return ist, dst
+
+    def features_finalize_apply(self, counts, creation_s, observation_end: float, istats,
+                                dstats, n_rows_total: int) -> np.ndarray:
+        counts = np.ascontiguousarray(counts, dtype=np.int64)
+        creation_s = np.ascontiguousarray(creation_s, dtype=np.float64)
+        ist = np.ascontiguousarray(istats, dtype=np.int64)
+        dst = np.ascontiguousarray(dstats, dtype=np.float64)
+        n = creation_s.size
+        out = np.zeros((n, 10), dtype=np.float64)
+        _check(self._lib.cdr_features_finalize_apply(self._h, n, _ptr(counts), _ptr(creation_s),
+                                                     float(observation_end), _ptr(ist),
+                                                     _ptr(dst), int(n_rows_total), _ptr(out)))
+        return out
 
     def features_finalize(self, counts, creation_s, observation_end: float) -> np.ndarray:
         counts = np.ascontiguousarray(counts, dtype=np.int64)

@@ -200,6 +200,15 @@ struct Ctx {
   DevBuf ev_part;  // int64 per ts_minmax workgroup: min, max
   DevBuf fin_counts, fin_creation, fin_out, fin_red;
   int64_t ev_n = 0, ev_nf = 0;  // resident events of cdr_features_generate
+  int32_t ev_cmax = 0;          // largest client id among them (payload width)
+  // hand-written group-by (groupby.hip) scratch and what its last run did
+  DevBuf gb_tilepref, gb_chunk, gb_rsum, gb_part, gb_small, gb_res, gb_bbase, gb_p1, gb_p2, gb_hist2,
+      gb_list, gb_slots;
+  DevBuf sim_cnt, sim_off, sim_tmp, sim_ms, sim_mbase;  // simulate.hip scratch
+  DevBuf x_small, x_buf, x_prim;                        // exchange.hip scratch
+  int gb_last_hand = 0, gb_last_L = 0, gb_last_passes = 0, gb_last_pbytes = 0, gb_last_big = 0,
+      gb_last_dense = 0;
+  int64_t gb_last_grid = 0;
 
   // ---- access-log ingest (ingest.hip) ----
   DevBuf ing_log;              // log bytes, zero-padded to a whole tile
@@ -242,6 +251,9 @@ void features_aggregate(Ctx& c, int64_t n_events, const int32_t* file_idx,
                         const int64_t* ts_ms, int64_t n_files,
                         const int32_t* primary, int64_t* out,
                         int64_t* max_ts_ms);
+// hand-written group-by of the resident events; false = shape not supported
+// (nothing computed, the caller takes the sort-based path)
+bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max_ts);
 void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
                        const double* creation_s, double observation_end,
                        double* out);

@@ -407,6 +407,9 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.med_tmp2, &c.ev_file, &c.ev_op, &c.ev_client, &c.ev_ts,
                     &c.ev_primary, &c.ev_out, &c.ev_scratch, &c.ev_scratch2,
                     &c.fin_counts, &c.fin_creation, &c.fin_out, &c.fin_red, &c.run_sums,
+                    &c.gb_tilepref, &c.gb_chunk, &c.gb_rsum, &c.gb_part, &c.gb_small, &c.gb_res, &c.gb_bbase,
+                    &c.gb_p1, &c.gb_p2, &c.gb_hist2, &c.gb_list, &c.gb_slots, &c.sim_cnt, &c.sim_off,
+                    &c.sim_tmp, &c.sim_ms, &c.sim_mbase, &c.x_small, &c.x_buf, &c.x_prim,
                     &c.fb_accum, &c.xs16, &c.xa32, &c.mv_list, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
                     &c.ll_state};
   for (DevBuf* b : bufs) b->release();

@@ -362,6 +362,9 @@ void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8
   if (n_files > 0)
     HIP_CHECK(hipMemcpyAsync(c.ev_primary.p, primary, 4 * n_files, hipMemcpyHostToDevice,
                              c.stream));
+  int cmax = 0;
+  for (int64_t i = 0; i < ne; ++i) cmax = std::max(cmax, (int)client[i]);
+  c.ev_cmax = cmax;
   features_aggregate_resident(c, ne, n_files, out, max_ts);
 }
 
@@ -371,6 +374,8 @@ void features_aggregate_resident(Ctx& c, int64_t ne, int64_t n_files, int64_t* o
                                  int64_t* max_ts) {
   *max_ts = LLONG_MIN;
   if (n_files == 0 && ne == 0) return;
+  if (groupby_resident(c, ne, n_files, out, max_ts)) return;  // groupby.hip
+  // sort-based path: shapes the packed payload cannot hold
   const size_t ne1 = ne > 0 ? ne : 1, nf1 = n_files > 0 ? n_files : 1;
   // timestamp range
   unsigned long long mm_init[2] = {~0ull, 0ull};
@@ -558,6 +563,7 @@ void features_generate(Ctx& c, int64_t ne, int64_t n_files, unsigned long long s
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.ev_n = ne;
   c.ev_nf = n_files;
+  c.ev_cmax = 2;
 }
 
 // ---- K6 -------------------------------------------------------------------
@@ -626,49 +632,87 @@ __global__ void fin_apply(const long long* __restrict__ cnt, const double* __res
   }
 }
 
-void features_finalize(Ctx& c, int64_t n, const int64_t* counts, const double* creation,
-                       double obs_end, double* out) {
-  if (n < 0) CDR_FAIL(CDR_ERR_ARG, "negative n_files");
-  if (n == 0) return;
-  c.fin_counts.ensure(8 * 6 * n);
-  c.fin_creation.ensure(8 * n);
-  c.fin_out.ensure(8 * 10 * n);
-  c.fin_red.ensure(8 * 16);
-  HIP_CHECK(hipMemcpyAsync(c.fin_counts.p, counts, 8 * 6 * n, hipMemcpyHostToDevice, c.stream));
-  HIP_CHECK(hipMemcpyAsync(c.fin_creation.p, creation, 8 * n, hipMemcpyHostToDevice, c.stream));
+// Uploads counts / creation and reduces them: istats = {sum writes, min/max
+// access_freq, min/max writes, min/max concurrency}, dstats = {min/max age,
+// min/max locality} (identities when n == 0), the inputs of :62-83.
+static void fin_stats(Ctx& c, int64_t n, const int64_t* counts, const double* creation,
+                      double obs_end, int64_t* istats, double* dstats) {
+  auto sx = [](unsigned long long v) { return (long long)(v ^ (unsigned long long)LLONG_MIN); };
   unsigned long long init[11] = {0, ~0ull, 0, ~0ull, 0, ~0ull, 0, ~0ull, 0, ~0ull, 0};
-  HIP_CHECK(hipMemcpyAsync(c.fin_red.p, init, sizeof(init), hipMemcpyHostToDevice, c.stream));
-  hipLaunchKernelGGL(fin_reduce, dim3(gcap(n, 256, 4096)), dim3(256), 0, c.stream,
-                     c.fin_counts.as<long long>(), c.fin_creation.as<double>(), n, obs_end,
-                     c.fin_red.as<unsigned long long>());
-  HIP_CHECK(hipGetLastError());
   unsigned long long r[11];
-  HIP_CHECK(hipMemcpyAsync(r, c.fin_red.p, sizeof(r), hipMemcpyDeviceToHost, c.stream));
-  HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (n > 0) {
+    c.fin_counts.ensure(8 * 6 * n);
+    c.fin_creation.ensure(8 * n);
+    c.fin_red.ensure(8 * 16);
+    HIP_CHECK(hipMemcpyAsync(c.fin_counts.p, counts, 8 * 6 * n, hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(c.fin_creation.p, creation, 8 * n, hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(c.fin_red.p, init, sizeof(init), hipMemcpyHostToDevice, c.stream));
+    hipLaunchKernelGGL(fin_reduce, dim3(gcap(n, 256, 4096)), dim3(256), 0, c.stream,
+                       c.fin_counts.as<long long>(), c.fin_creation.as<double>(), n, obs_end,
+                       c.fin_red.as<unsigned long long>());
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(r, c.fin_red.p, sizeof(r), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    istats[0] = (long long)r[0];
+    for (int i = 1; i <= 6; ++i) istats[i] = sx(r[i]);
+    for (int i = 0; i < 4; ++i) dstats[i] = fkey_val(r[7 + i]);
+  } else {
+    istats[0] = 0;
+    for (int i = 1; i <= 5; i += 2) {
+      istats[i] = LLONG_MAX;
+      istats[i + 1] = LLONG_MIN;
+    }
+    for (int i = 0; i < 4; i += 2) {
+      dstats[i] = INFINITY;
+      dstats[i + 1] = -INFINITY;
+    }
+  }
+}
+
+// The table of n rows (counts / creation already on the device when
+// uploaded is true) from global statistics over n_rows rows.
+static void fin_apply(Ctx& c, int64_t n, const int64_t* counts, const double* creation,
+                      double obs_end, const int64_t* istats, const double* dstats,
+                      int64_t n_rows, bool uploaded, double* out) {
+  if (n == 0) return;
+  if (!uploaded) {
+    c.fin_counts.ensure(8 * 6 * n);
+    c.fin_creation.ensure(8 * n);
+    HIP_CHECK(hipMemcpyAsync(c.fin_counts.p, counts, 8 * 6 * n, hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(c.fin_creation.p, creation, 8 * n, hipMemcpyHostToDevice, c.stream));
+  }
+  c.fin_out.ensure(8 * 10 * n);
   FinConst k;
   k.obs_end = obs_end;
-  const long long sumw = (long long)r[0];
-  double mean = (double)sumw / (double)n;  // Spark avg: double sum / count
+  double mean = (double)istats[0] / (double)n_rows;  // Spark avg: double sum / count
   if (mean == 0.0) mean = 1.0;
   k.mean_w = mean;
-  auto sx = [](unsigned long long v) { return (long long)(v ^ (unsigned long long)LLONG_MIN); };
-  k.af_min = sx(r[1]);
-  k.af_max = sx(r[2]);
-  const long long wmin = sx(r[3]), wmax = sx(r[4]);
-  k.con_min = sx(r[5]);
-  k.con_max = sx(r[6]);
-  k.age_min = fkey_val(r[7]);
-  k.age_max = fkey_val(r[8]);
-  k.wr_min = (double)wmin / mean;  // x -> x / mean is monotone
-  k.wr_max = (double)wmax / mean;
-  k.loc_min = fkey_val(r[9]);
-  k.loc_max = fkey_val(r[10]);
+  k.af_min = istats[1];
+  k.af_max = istats[2];
+  k.con_min = istats[5];
+  k.con_max = istats[6];
+  k.age_min = dstats[0];
+  k.age_max = dstats[1];
+  k.wr_min = (double)istats[3] / mean;  // x -> x / mean is monotone
+  k.wr_max = (double)istats[4] / mean;
+  k.loc_min = dstats[2];
+  k.loc_max = dstats[3];
   hipLaunchKernelGGL(fin_apply, dim3(gcap(n, 256, 4096)), dim3(256), 0, c.stream,
                      c.fin_counts.as<long long>(), c.fin_creation.as<double>(), n, k,
                      c.fin_out.as<double>());
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipMemcpyAsync(out, c.fin_out.p, 8 * 10 * n, hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+void features_finalize(Ctx& c, int64_t n, const int64_t* counts, const double* creation,
+                       double obs_end, double* out) {
+  if (n < 0) CDR_FAIL(CDR_ERR_ARG, "negative n_files");
+  if (n == 0) return;
+  int64_t is[7];
+  double ds[4];
+  fin_stats(c, n, counts, creation, obs_end, is, ds);
+  fin_apply(c, n, counts, creation, obs_end, is, ds, n, true, out);
 }
 
 }  // namespace cdr
@@ -710,6 +754,20 @@ int cdr_features_aggregate_resident(cdr_ctx* h, int64_t* out, int64_t* max_ts_us
   CDR_CATCH
 }
 
+int cdr_features_groupby_info(cdr_ctx* h, int64_t* info) {
+  CDR_TRY
+  if (!h || !info) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  const Ctx& c = h->c;
+  info[0] = c.gb_last_hand;
+  info[1] = c.gb_last_L;
+  info[2] = c.gb_last_passes;
+  info[3] = c.gb_last_pbytes;
+  info[4] = c.gb_last_big;
+  info[5] = c.gb_last_dense;
+  info[6] = c.gb_last_grid;
+  CDR_CATCH
+}
+
 int cdr_features_events_read(cdr_ctx* h, int32_t* file_idx, uint8_t* op, int32_t* client,
                              int64_t* ts_us, int32_t* primary) {
   CDR_TRY
@@ -728,6 +786,33 @@ int cdr_features_events_read(cdr_ctx* h, int32_t* file_idx, uint8_t* op, int32_t
   HIP_CHECK(hipMemcpyAsync(primary, c.ev_primary.p, 4 * c.ev_nf, hipMemcpyDeviceToHost,
                            c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
+  CDR_CATCH
+}
+
+int cdr_features_finalize_stats(cdr_ctx* h, int64_t n_rows, const int64_t* counts,
+                                const double* creation_s, double observation_end,
+                                int64_t* istats, double* dstats) {
+  CDR_TRY
+  if (!h || !istats || !dstats || (n_rows > 0 && (!counts || !creation_s)))
+    CDR_FAIL(CDR_ERR_ARG, "null argument");
+  if (n_rows < 0) CDR_FAIL(CDR_ERR_ARG, "negative n_rows");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  fin_stats(h->c, n_rows, counts, creation_s, observation_end, istats, dstats);
+  CDR_CATCH
+}
+
+int cdr_features_finalize_apply(cdr_ctx* h, int64_t n_rows, const int64_t* counts,
+                                const double* creation_s, double observation_end,
+                                const int64_t* istats, const double* dstats,
+                                int64_t n_rows_total, double* out) {
+  CDR_TRY
+  if (!h || !istats || !dstats || (n_rows > 0 && (!counts || !creation_s || !out)))
+    CDR_FAIL(CDR_ERR_ARG, "null argument");
+  if (n_rows < 0 || n_rows_total < n_rows || n_rows_total < 1)
+    CDR_FAIL(CDR_ERR_ARG, "need 0 <= n_rows <= n_rows_total, n_rows_total >= 1");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  fin_apply(h->c, n_rows, counts, creation_s, observation_end, istats, dstats, n_rows_total,
+            false, out);
   CDR_CATCH
 }
 

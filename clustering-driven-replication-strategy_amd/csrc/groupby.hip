@@ -1,0 +1,1111 @@
+// groupby.hip — the access-log group-by of src/compute_features.py:31-46 as a
+// two-level MSD partition of the events by file id followed by one LDS hash
+// group-by per bucket of 2^L consecutive files.  No library sort.
+//
+// Per event the counters are (:31-42) count, WRITE, READ, local (client ==
+// primary node of its file); max_concurrency (:44-46) is the largest count of
+// one (file, second) pair, the null second (unparseable timestamp) being a
+// pair of its own.  All of them are order-independent sums and maxima, so the
+// partition may place events of one bucket in any order.
+//
+//   K1  gb_hist1    per 8192-event tile: histogram of the pass-1 digit (the
+//                   top B1 bits of the file id), in-chunk prefix per tile;
+//                   timestamp min / max / null flag (file 4 B + ts 8 B read)
+//   S1  gb_scan1    chunk bases, digit bases, pass-2 tile starts, ts range
+//   --- host reads the ts range (the payload layout depends on it) ---
+//   P1  gb_scatter1 tile -> LDS-ranked by digit -> coalesced runs into the
+//                   digit regions; builds the packed payload
+//                   [file low bits | second code | op | client code]
+//                   (17 B read, 4 or 8 B written)
+//   H2  gb_hist2    per pass-2 tile (a slice of one digit region): histogram
+//                   of the pass-2 digit (payload read)
+//   S2  gb_scan2    one workgroup per pass-1 digit: tile offsets and bucket
+//                   bases
+//   P2  gb_scatter2 like P1 within each digit region (payload read + written)
+//   K4  gb_bucket   one workgroup per bucket: LDS hash of (file, second) ->
+//                   count (one 64-bit slot = key << CB | count), per-file
+//                   count / write / read / local sums and the concurrency
+//                   maximum in LDS, then the (files, 6) int64 rows; buckets
+//                   over the LDS capacity are listed and redone by
+//                   gb_bucket_big with the hash in global memory.
+// With B <= 9 bucket bits one partition pass suffices (H2/S2/P2 skipped).
+#include <algorithm>
+#include <cmath>
+
+#include "cdr_internal.h"
+
+namespace cdr {
+
+int lloyd_num_cus(int device);
+
+namespace {
+
+constexpr int kGbTile = 8192;                   // events per partition tile
+constexpr int kGbThreads = 512;                 // partition / histogram workgroups
+constexpr int kGbPer = kGbTile / kGbThreads;    // events per thread in a tile
+constexpr int kGbChunkTiles = 8;                // tiles per gb_hist1 workgroup
+constexpr int kGbRange = 16;                    // chunks per gb_scan1a/c workgroup
+constexpr int kGbMaxDigit = 9;                  // bits per partition pass
+constexpr int kGbMaxBins = 1 << kGbMaxDigit;
+constexpr int kGbBThreads = 256;                // bucket workgroups
+constexpr int kGbSlots = 4096;                  // LDS hash slots per bucket
+constexpr int kGbLdsCap = 3072;                 // events per bucket in LDS (load <= 3/4)
+constexpr int kGbReg = kGbLdsCap / kGbBThreads; // payloads per bucket thread
+constexpr int kGbMaxL = 10;                     // files per bucket <= 1024
+constexpr long long kTsNullG = LLONG_MIN;
+constexpr unsigned long long kEmpty = ~0ull;
+
+__device__ __forceinline__ long long sec_of_g(long long ts_us) {
+  // Spark floor(cast(ts as double)); see features.hip sec_of
+  if (ts_us >= 0 && ts_us < 9000000000000000ll) return ts_us / 1000000;
+  return (long long)floor((double)ts_us / 1000000.0);
+}
+
+// Payload layout (host-computed, passed by value).
+struct GbPay {
+  int fshift;   // bit position of the file-low field
+  int sshift;   // bit position of the second code (= 2 + cbits)
+  int cbits;    // client code bits (code 0 = not a node id, else client + 1)
+  int sbits;    // second code bits (all ones = null)
+  int L;        // file-local bits (files per bucket = 2^L)
+  long long sec_min;
+  unsigned long long low_mask;  // file-low field mask (fbits - B1 bits)
+};
+
+template <typename T>
+__device__ __forceinline__ T gb_make(const GbPay& p, unsigned flow, long long ts, uint8_t op,
+                                     int client) {
+  const unsigned long long sc = ts == kTsNullG ? ((1ull << p.sbits) - 1)
+                                               : (unsigned long long)(sec_of_g(ts) - p.sec_min);
+  const unsigned long long oc = op == 1 ? 1ull : (op == 2 ? 2ull : 0ull);
+  const unsigned long long cc = client >= 0 ? (unsigned long long)client + 1ull : 0ull;
+  return (T)(((unsigned long long)flow << p.fshift) | (sc << p.sshift) | (oc << p.cbits) | cc);
+}
+
+// Exclusive scan of n <= 512 LDS counters by a 512-thread workgroup (one
+// counter per thread).
+__device__ __forceinline__ void lds_scan(const unsigned* cnt, unsigned* lp, int n,
+                                         unsigned* wsum) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const unsigned v = t < n ? cnt[t] : 0u;
+  unsigned inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  unsigned base = 0;
+  for (int i = 0; i < w; ++i) base += wsum[i];
+  if (t < n) lp[t] = base + inc - v;
+  __syncthreads();
+}
+
+// ---- K1 --------------------------------------------------------------------
+__global__ __launch_bounds__(kGbThreads) void gb_hist1(
+    const int32_t* __restrict__ file, const long long* __restrict__ ts, int64_t ne, int64_t nf,
+    int shift1, int R1, unsigned* __restrict__ tilepref, unsigned* __restrict__ chunksum,
+    long long* __restrict__ part) {
+  __shared__ unsigned hist[kGbMaxBins];
+  __shared__ long long red[3][kGbThreads / 64];
+  const int tid = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  unsigned run = 0;  // thread r owns digit r
+  long long lo = LLONG_MAX, hi = LLONG_MIN;
+  long long nul = 0;
+  for (int tt = 0; tt < kGbChunkTiles; ++tt) {
+    const int64_t t = c * kGbChunkTiles + tt;
+    const int64_t base = t * kGbTile;
+    if (base >= ne) break;
+    if (tid < R1) hist[tid] = 0;
+    int fr[kGbPer];
+    long long tv[kGbPer];
+#pragma unroll
+    for (int j = 0; j < kGbPer; ++j) {
+      const int64_t e = base + j * kGbThreads + tid;
+      fr[j] = e < ne ? file[e] : -1;
+      tv[j] = e < ne ? ts[e] : kTsNullG;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kGbPer; ++j) {
+      const int64_t e = base + j * kGbThreads + tid;
+      if (tv[j] == kTsNullG) {
+        nul |= e < ne;
+      } else {
+        lo = min(lo, tv[j]);
+        hi = max(hi, tv[j]);
+      }
+      if (fr[j] >= 0 && fr[j] < nf) atomicAdd(&hist[(unsigned)fr[j] >> shift1], 1u);
+    }
+    __syncthreads();
+    if (tid < R1) {
+      tilepref[t * R1 + tid] = run;
+      run += hist[tid];
+    }
+  }
+  if (tid < R1) chunksum[c * R1 + tid] = run;
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o));
+    hi = max(hi, __shfl_xor(hi, o));
+    nul |= __shfl_xor(nul, o);
+  }
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    red[0][w] = lo;
+    red[1][w] = hi;
+    red[2][w] = nul;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int i = 1; i < kGbThreads / 64; ++i) {
+      lo = min(lo, red[0][i]);
+      hi = max(hi, red[1][i]);
+      nul |= red[2][i];
+    }
+    part[3 * c] = lo;
+    part[3 * c + 1] = hi;
+    part[3 * c + 2] = nul;
+  }
+}
+
+// ---- S1: chunk bases in three small kernels ---------------------------------
+// a: per range of kGbRange chunks, the digit sums; b (one workgroup): range
+// bases per digit, digit bases, pass-2 tile starts, the timestamp range;
+// c: absolute chunk bases (digit base + range base + in-range prefix).
+__global__ __launch_bounds__(kGbMaxBins) void gb_scan1a(const unsigned* __restrict__ chunk,
+                                                        int64_t C, int R1,
+                                                        unsigned* __restrict__ rsum) {
+  const int r = threadIdx.x;
+  if (r >= R1) return;
+  const int64_t c0 = (int64_t)blockIdx.x * kGbRange;
+  unsigned v[kGbRange];
+#pragma unroll
+  for (int j = 0; j < kGbRange; ++j) v[j] = c0 + j < C ? chunk[(c0 + j) * R1 + r] : 0u;
+  unsigned s = 0;
+#pragma unroll
+  for (int j = 0; j < kGbRange; ++j) s += v[j];
+  rsum[(int64_t)blockIdx.x * R1 + r] = s;
+}
+
+__global__ __launch_bounds__(kGbMaxBins) void gb_scan1b(unsigned* __restrict__ rsum, int64_t G,
+                                                        int R1, const long long* __restrict__ part,
+                                                        int64_t C, unsigned* __restrict__ binbase,
+                                                        int* __restrict__ tile2start,
+                                                        long long* __restrict__ res) {
+  __shared__ long long wred[3][8];
+  __shared__ unsigned wsum[8], wt[8];
+  const int tid = threadIdx.x;
+  unsigned run = 0;
+  if (tid < R1) {
+    for (int64_t g0 = 0; g0 < G; g0 += 16) {
+      unsigned v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = g0 + j < G ? rsum[(g0 + j) * R1 + tid] : 0u;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (g0 + j < G) rsum[(g0 + j) * R1 + tid] = run;
+        run += v[j];
+      }
+    }
+  }
+  long long lo = LLONG_MAX, hi = LLONG_MIN, nul = 0;
+  for (int64_t c = tid; c < C; c += kGbMaxBins) {
+    lo = min(lo, part[3 * c]);
+    hi = max(hi, part[3 * c + 1]);
+    nul |= part[3 * c + 2];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o));
+    hi = max(hi, __shfl_xor(hi, o));
+    nul |= __shfl_xor(nul, o);
+  }
+  const int lane = tid & 63, w = tid >> 6;
+  if (lane == 0) {
+    wred[0][w] = lo;
+    wred[1][w] = hi;
+    wred[2][w] = nul;
+  }
+  // exclusive scans over the digits (events and pass-2 tile counts)
+  const unsigned v = tid < R1 ? run : 0u;
+  const unsigned tl = (unsigned)((v + kGbTile - 1) / kGbTile);
+  unsigned iv = v, it = tl;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned a = __shfl_up(iv, o), b = __shfl_up(it, o);
+    if (lane >= o) {
+      iv += a;
+      it += b;
+    }
+  }
+  if (lane == 63) {
+    wsum[w] = iv;
+    wt[w] = it;
+  }
+  __syncthreads();
+  unsigned bv = 0, bt = 0;
+  for (int i = 0; i < w; ++i) {
+    bv += wsum[i];
+    bt += wt[i];
+  }
+  if (tid < R1) {
+    binbase[tid] = bv + iv - v;
+    tile2start[tid] = (int)(bt + it - tl);
+  }
+  if (tid == kGbMaxBins - 1) {
+    binbase[R1] = bv + iv;
+    tile2start[R1] = (int)(bt + it);
+    res[3] = bt + it;
+    res[4] = bv + iv;
+  }
+  if (tid == 0) {
+    for (int i = 1; i < 8; ++i) {
+      lo = min(lo, wred[0][i]);
+      hi = max(hi, wred[1][i]);
+      nul |= wred[2][i];
+    }
+    res[0] = lo;
+    res[1] = hi;
+    res[2] = nul;
+  }
+}
+
+__global__ __launch_bounds__(kGbMaxBins) void gb_scan1c(unsigned* __restrict__ chunk, int64_t C,
+                                                        int R1, const unsigned* __restrict__ rbase,
+                                                        const unsigned* __restrict__ binbase) {
+  const int r = threadIdx.x;
+  if (r >= R1) return;
+  const int64_t c0 = (int64_t)blockIdx.x * kGbRange;
+  unsigned v[kGbRange];
+#pragma unroll
+  for (int j = 0; j < kGbRange; ++j) v[j] = c0 + j < C ? chunk[(c0 + j) * R1 + r] : 0u;
+  unsigned run = binbase[r] + rbase[(int64_t)blockIdx.x * R1 + r];
+#pragma unroll
+  for (int j = 0; j < kGbRange; ++j) {
+    if (c0 + j < C) chunk[(c0 + j) * R1 + r] = run;
+    run += v[j];
+  }
+}
+
+// ---- P1 / P2 ----------------------------------------------------------------
+// Tile order: blocks are dealt round-robin over the 8 XCDs, so block b works
+// on tile (b % 8) * per + b / 8: each XCD walks one contiguous range of tiles
+// and a digit's consecutive runs are written from one L2.
+__device__ __forceinline__ int64_t xcd_tile(int64_t per) {
+  return (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+}
+
+template <typename T>
+struct GbStage {
+  T val[kGbTile];
+  uint16_t dig[kGbTile];
+  unsigned cnt[kGbMaxBins], lp[kGbMaxBins], goff[kGbMaxBins];
+  unsigned wsum[8];
+};
+
+// Rank the tile's events by digit in LDS, stage them digit-contiguous, and
+// write each digit's run to its region (goff[d] = the run's first position).
+// dr[j] = digit of event j, or ~0u when the event is not placed.
+template <typename T>
+__device__ __forceinline__ void gb_place(GbStage<T>& s, const T* val, unsigned* dr, int R,
+                                         T* __restrict__ out) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < kGbPer; ++j)
+    if (dr[j] != ~0u) dr[j] = (dr[j] << 16) | atomicAdd(&s.cnt[dr[j]], 1u);
+  __syncthreads();
+  lds_scan(s.cnt, s.lp, R, s.wsum);
+#pragma unroll
+  for (int j = 0; j < kGbPer; ++j) {
+    if (dr[j] != ~0u) {
+      const unsigned d = dr[j] >> 16;
+      const unsigned slot = s.lp[d] + (dr[j] & 0xFFFFu);
+      s.val[slot] = val[j];
+      s.dig[slot] = (uint16_t)d;
+    }
+  }
+  __syncthreads();
+  const unsigned nv = s.lp[R - 1] + s.cnt[R - 1];
+  for (unsigned i = tid; i < nv; i += kGbThreads) {
+    const unsigned d = s.dig[i];
+    out[s.goff[d] + (i - s.lp[d])] = s.val[i];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(4))) void gb_scatter1(
+    const int32_t* __restrict__ file, const uint8_t* __restrict__ op,
+    const int32_t* __restrict__ client, const long long* __restrict__ ts, int64_t ne, int64_t nf,
+    GbPay p, int shift1, int R1, int64_t T1, int64_t per, const unsigned* __restrict__ tilepref,
+    const unsigned* __restrict__ chunkbase, T* __restrict__ out) {
+  __shared__ GbStage<T> s;
+  const int64_t t = xcd_tile(per);
+  if (t >= T1) return;
+  const int tid = threadIdx.x;
+  const int64_t base = t * kGbTile;
+  const int64_t c = t / kGbChunkTiles;
+  if (tid < R1) {
+    s.cnt[tid] = 0;
+    s.goff[tid] = chunkbase[c * R1 + tid] + tilepref[t * R1 + tid];
+  }
+  // thread tid takes the tile's events base + 16 tid .. + 15 in two halves of
+  // 8: 16-byte loads (a wave reads 2 KiB of file ids contiguously), and the
+  // packed payload of a half is built before the next half is loaded
+  T val[kGbPer];
+  unsigned dr[kGbPer];
+  const int64_t e0 = base + (int64_t)tid * kGbPer;
+  const bool full = e0 + kGbPer <= ne;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    constexpr int H = kGbPer / 2;
+    const int64_t eh = e0 + hf * H;
+    int fr[H], cv[H];
+    long long tv[H];
+    uint8_t ov[H];
+    if (full) {
+      const int4* f4 = reinterpret_cast<const int4*>(file + eh);
+      const int4* c4 = reinterpret_cast<const int4*>(client + eh);
+      const longlong2* t2 = reinterpret_cast<const longlong2*>(ts + eh);
+      const uint2 o2 = *reinterpret_cast<const uint2*>(op + eh);
+#pragma unroll
+      for (int q = 0; q < H / 4; ++q) {
+        const int4 a = f4[q], b = c4[q];
+        fr[4 * q] = a.x, fr[4 * q + 1] = a.y, fr[4 * q + 2] = a.z, fr[4 * q + 3] = a.w;
+        cv[4 * q] = b.x, cv[4 * q + 1] = b.y, cv[4 * q + 2] = b.z, cv[4 * q + 3] = b.w;
+      }
+#pragma unroll
+      for (int q = 0; q < H / 2; ++q) {
+        const longlong2 a = t2[q];
+        tv[2 * q] = a.x, tv[2 * q + 1] = a.y;
+      }
+#pragma unroll
+      for (int j = 0; j < H; ++j) ov[j] = (uint8_t)((j < 4 ? o2.x : o2.y) >> (8 * (j & 3)));
+    } else {
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        const int64_t e = eh + j;
+        const bool in = e < ne;
+        fr[j] = in ? file[e] : -1;
+        tv[j] = in ? ts[e] : 0;
+        ov[j] = in ? op[e] : 0;
+        cv[j] = in ? client[e] : -1;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const int o = hf * H + j;
+      dr[o] = (fr[j] >= 0 && fr[j] < nf) ? (unsigned)fr[j] >> shift1 : ~0u;
+      val[o] = gb_make<T>(p, (unsigned)((unsigned long long)(unsigned)fr[j] & p.low_mask), tv[j],
+                          ov[j], cv[j]);
+    }
+  }
+  __syncthreads();
+  gb_place<T>(s, val, dr, R1, out);
+}
+
+__device__ __forceinline__ int find_digit(const int* __restrict__ start, int R1, int64_t t2) {
+  int lo = 0, hi = R1;  // start[lo] <= t2 < start[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (start[mid] <= t2) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kGbThreads) void gb_hist2(const T* __restrict__ in,
+                                                      const unsigned* __restrict__ binbase,
+                                                      const int* __restrict__ tile2start, int R1,
+                                                      int R2, int shift2,
+                                                      unsigned* __restrict__ hist2) {
+  __shared__ unsigned h[kGbMaxBins];
+  const int64_t t2 = blockIdx.x;
+  const int sd = find_digit(tile2start, R1, t2);
+  const int64_t beg = binbase[sd] + (t2 - tile2start[sd]) * (int64_t)kGbTile;
+  const int64_t end = min((int64_t)binbase[sd + 1], beg + kGbTile);
+  if (threadIdx.x < R2) h[threadIdx.x] = 0;
+  T v[kGbPer];
+#pragma unroll
+  for (int j = 0; j < kGbPer; ++j) {
+    const int64_t i = beg + j * kGbThreads + threadIdx.x;
+    v[j] = i < end ? in[i] : (T)0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kGbPer; ++j)
+    if (beg + j * kGbThreads + threadIdx.x < end)
+      atomicAdd(&h[(unsigned)((unsigned long long)v[j] >> shift2) & (R2 - 1)], 1u);
+  __syncthreads();
+  if (threadIdx.x < R2) hist2[t2 * R2 + threadIdx.x] = h[threadIdx.x];
+}
+
+// One workgroup per pass-1 digit sd, thread r = pass-2 digit: running offsets
+// over the digit's tiles, then the bucket bases bbase[sd * R2 + r].
+__global__ __launch_bounds__(kGbMaxBins) void gb_scan2(unsigned* __restrict__ hist2,
+                                                       const int* __restrict__ tile2start,
+                                                       const unsigned* __restrict__ binbase,
+                                                       int R1, int R2,
+                                                       unsigned* __restrict__ bbase) {
+  __shared__ unsigned cnt[kGbMaxBins], lp[kGbMaxBins], wsum[8];
+  const int sd = blockIdx.x, r = threadIdx.x;
+  const int t0 = tile2start[sd], t1 = tile2start[sd + 1];
+  unsigned run = 0;
+  if (r < R2) {
+    for (int tb = t0; tb < t1; tb += 16) {
+      unsigned v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = tb + j < t1 ? hist2[(int64_t)(tb + j) * R2 + r] : 0u;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (tb + j < t1) hist2[(int64_t)(tb + j) * R2 + r] = run;
+        run += v[j];
+      }
+    }
+    cnt[r] = run;
+  }
+  __syncthreads();
+  lds_scan(cnt, lp, R2, wsum);
+  if (r < R2) bbase[(int64_t)sd * R2 + r] = binbase[sd] + lp[r];
+  if (sd == R1 - 1 && r == 0) bbase[(int64_t)R1 * R2] = binbase[R1];
+}
+
+template <typename T>
+__global__ __launch_bounds__(kGbThreads) void gb_scatter2(
+    const T* __restrict__ in, const unsigned* __restrict__ binbase,
+    const int* __restrict__ tile2start, int R1, int R2, int shift2, int64_t T2, int64_t per,
+    const unsigned* __restrict__ off2, const unsigned* __restrict__ bbase, T* __restrict__ out) {
+  __shared__ GbStage<T> s;
+  const int64_t t2 = xcd_tile(per);
+  if (t2 >= T2) return;
+  const int tid = threadIdx.x;
+  const int sd = find_digit(tile2start, R1, t2);
+  const int64_t beg = binbase[sd] + (t2 - tile2start[sd]) * (int64_t)kGbTile;
+  const int64_t end = min((int64_t)binbase[sd + 1], beg + kGbTile);
+  if (tid < R2) {
+    s.cnt[tid] = 0;
+    s.goff[tid] = bbase[(int64_t)sd * R2 + tid] + off2[t2 * R2 + tid];
+  }
+  T val[kGbPer];
+  unsigned dr[kGbPer];
+#pragma unroll
+  for (int j = 0; j < kGbPer; ++j) {
+    const int64_t i = beg + j * kGbThreads + tid;
+    val[j] = i < end ? in[i] : (T)0;
+  }
+#pragma unroll
+  for (int j = 0; j < kGbPer; ++j)
+    dr[j] = beg + j * kGbThreads + tid < end
+                ? (unsigned)((unsigned long long)val[j] >> shift2) & (R2 - 1)
+                : ~0u;
+  __syncthreads();
+  gb_place<T>(s, val, dr, R2, out);
+}
+
+// ---- K4 --------------------------------------------------------------------
+struct GbKey {
+  int CB;                   // count bits of a hash slot (slot = key << CB | count)
+  unsigned long long cmask;
+};
+
+__device__ __forceinline__ unsigned gb_hash(unsigned long long key) {
+  return (unsigned)((key * 0x9E3779B97F4A7C15ull) >> 32);
+}
+
+// Insert one event of (file-local fl, second code sc) into an open-addressing
+// table; returns the pair's count after this event.
+template <bool LDS>
+__device__ __forceinline__ unsigned long long gb_insert(unsigned long long* slots, unsigned size,
+                                                        bool pow2, unsigned long long key,
+                                                        const GbKey& k) {
+  unsigned h = gb_hash(key);
+  h = pow2 ? (h & (size - 1)) : (h % size);
+  const unsigned long long fresh = (key << k.CB) | 1ull;
+  while (true) {
+    // one CAS claims an empty slot (the common case: a new (file, second)
+    // pair) or returns the occupant
+    const unsigned long long v = atomicCAS(&slots[h], kEmpty, fresh);
+    if (v == kEmpty) return 1;
+    if ((v >> k.CB) == key) return (atomicAdd(&slots[h], 1ull) & k.cmask) + 1;
+    h = h + 1 == size ? 0 : h + 1;
+  }
+}
+
+// Per-file LDS state of a bucket (F = 2^L files), after the hash slots.
+struct GbFiles {
+  unsigned long long* cw;   // count | writes << 32
+  unsigned long long* rl;   // reads | local << 32
+  unsigned* conc;
+  int* prim;
+};
+
+__device__ __forceinline__ GbFiles gb_files(unsigned long long* base, int F) {
+  GbFiles g;
+  g.cw = base;
+  g.rl = base + F;
+  g.conc = reinterpret_cast<unsigned*>(base + 2 * F);
+  g.prim = reinterpret_cast<int*>(g.conc + F);
+  return g;
+}
+
+// One event: hash insert, concurrency maximum, and the per-file sums added
+// once per group of lanes of one file (ballots over the file-local bits), so
+// a bucket's few files do not serialise the LDS atomics.
+template <bool LDS>
+__device__ __forceinline__ void gb_event(bool act, unsigned long long v, const GbPay& p,
+                                         const GbKey& k, unsigned long long* slots,
+                                         unsigned size, bool pow2, GbFiles& g) {
+  const unsigned fl = (unsigned)(v >> p.fshift) & ((1u << p.L) - 1);
+  const unsigned long long sc = (v >> p.sshift) & ((1ull << p.sbits) - 1);
+  const unsigned oc = (unsigned)(v >> p.cbits) & 3u;
+  const int cl = (int)((unsigned)v & ((1u << p.cbits) - 1)) - 1;
+  bool loc = false;
+  if (act) {
+    const unsigned long long cnt =
+        gb_insert<LDS>(slots, size, pow2, ((unsigned long long)fl << p.sbits) | sc, k);
+    const unsigned c32 = (unsigned)min(cnt, 0xFFFFFFFFull);
+    if (c32 > g.conc[fl]) atomicMax(&g.conc[fl], c32);
+    const int pr = g.prim[fl];
+    loc = cl >= 0 && pr >= 0 && cl == pr;
+  }
+  unsigned long long peers = __ballot(act);
+  for (int b = 0; b < p.L; ++b) {
+    const bool bit = (fl >> b) & 1u;
+    const unsigned long long bb = __ballot(act && bit);
+    peers &= bit ? bb : ~bb;
+  }
+  const unsigned long long mw = __ballot(act && oc == 1), mr = __ballot(act && oc == 2);
+  const unsigned long long ml = __ballot(act && loc);
+  const int lane = threadIdx.x & 63;
+  if (act && lane == __ffsll((long long)peers) - 1) {
+    atomicAdd(&g.cw[fl], (unsigned long long)__popcll(peers) |
+                             ((unsigned long long)__popcll(peers & mw) << 32));
+    atomicAdd(&g.rl[fl], (unsigned long long)__popcll(peers & mr) |
+                             ((unsigned long long)__popcll(peers & ml) << 32));
+  }
+}
+
+__device__ __forceinline__ void gb_write_files(const GbFiles& g, int nfl, int64_t f0,
+                                               long long* __restrict__ out) {
+  for (int f = threadIdx.x; f < nfl; f += kGbBThreads) {
+    long long* o = out + (f0 + f) * 6;
+    const unsigned long long cw = g.cw[f], rl = g.rl[f];
+    o[0] = (long long)(cw & 0xFFFFFFFFull);
+    o[1] = (long long)(cw >> 32);
+    o[2] = (long long)(rl & 0xFFFFFFFFull);
+    o[3] = (long long)(rl >> 32);
+    o[4] = (long long)(cw & 0xFFFFFFFFull);
+    o[5] = (long long)g.conc[f];
+  }
+}
+
+// Persistent: workgroup w takes buckets w, w + G, w + 2G, ...; the next
+// bucket's payloads and primaries are loaded while the current one is hashed
+// (a bucket holds ~1k events, so one global round trip per bucket would
+// otherwise dominate).  LDS: kGbSlots hash slots, then the per-file state of
+// F = 2^L files.
+template <typename T>
+__global__ __launch_bounds__(kGbBThreads) void gb_bucket(const T* __restrict__ pb,
+                                                        const unsigned* __restrict__ bbase,
+                                                        int64_t nbuckets, int64_t nf, GbPay p,
+                                                        GbKey k,
+                                                        const int32_t* __restrict__ primary,
+                                                        long long* __restrict__ out,
+                                                        int* __restrict__ big_list,
+                                                        int* __restrict__ big_count) {
+  extern __shared__ unsigned long long lds[];
+  const int tid = threadIdx.x;
+  const int F = 1 << p.L;
+  constexpr int kPrimReg = (1 << kGbMaxL) / kGbBThreads;
+  unsigned long long* slots = lds;
+  GbFiles g = gb_files(lds + kGbSlots, F);
+  const int64_t G = gridDim.x;
+  int64_t b = blockIdx.x;
+  if (b >= nbuckets) return;
+  // bucket b's bounds, payloads (in registers) and primaries
+  int64_t s0 = bbase[b], n = (int64_t)bbase[b + 1] - s0;
+  T v[kGbReg];
+  int pr[kPrimReg];
+  auto fetch = [&](int64_t bb, int64_t ss, int64_t nn, T* vv, int* pp) {
+    const bool small = nn <= kGbLdsCap;
+#pragma unroll
+    for (int j = 0; j < kGbReg; ++j) {
+      const int64_t i = tid + j * kGbBThreads;
+      vv[j] = small && i < nn ? pb[ss + i] : (T)0;
+    }
+    const int64_t f0 = bb << p.L;
+#pragma unroll
+    for (int j = 0; j < kPrimReg; ++j) {
+      const int64_t f = tid + j * kGbBThreads;
+      pp[j] = f < F && f0 + f < nf ? primary[f0 + f] : -2;
+    }
+  };
+  fetch(b, s0, n, v, pr);
+  int64_t s0n = 0, nn = 0;
+  if (b + G < nbuckets) {
+    s0n = bbase[b + G];
+    nn = (int64_t)bbase[b + G + 1] - s0n;
+  }
+  T v2[kGbReg];
+  int pr2[kPrimReg];
+  // One bucket: cur holds it (its loads are waited for at the empty asm,
+  // before the next bucket's loads go out into nxt); ping-pong buffers
+  // instead of copies, so no copy of an in-flight register forces a wait.
+  auto step = [&](T (&cur)[kGbReg], int (&cpr)[kPrimReg], T (&nxt)[kGbReg],
+                  int (&npr)[kPrimReg]) {
+#pragma unroll
+    for (int j = 0; j < kGbReg; ++j) asm volatile("" : "+v"(cur[j]));
+#pragma unroll
+    for (int j = 0; j < kPrimReg; ++j) asm volatile("" : "+v"(cpr[j]));
+    const int64_t bn = b + G;
+    const int64_t f0 = b << p.L;
+    const int nfl = (int)min((int64_t)F, nf - f0);
+    const bool over = n > kGbLdsCap;
+    unsigned size = 64;
+    if (!over) {
+      while (size < 2 * n && size < kGbSlots) size <<= 1;
+      for (unsigned i = tid; i < size; i += kGbBThreads) slots[i] = kEmpty;
+#pragma unroll
+      for (int j = 0; j < kPrimReg; ++j) {
+        const int f = tid + j * kGbBThreads;
+        if (f < nfl) {
+          g.cw[f] = 0;
+          g.rl[f] = 0;
+          g.conc[f] = 0;
+          g.prim[f] = cpr[j];
+        }
+      }
+    }
+    __syncthreads();
+    int64_t s0nn = 0, nnn = 0;
+    if (bn < nbuckets) {
+      fetch(bn, s0n, nn, nxt, npr);
+      if (bn + G < nbuckets) {
+        s0nn = bbase[bn + G];
+        nnn = (int64_t)bbase[bn + G + 1] - s0nn;
+      }
+    }
+    if (over) {
+      if (tid == 0) big_list[atomicAdd(big_count, 1)] = (int)b;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kGbReg; ++j) {
+        const bool act = tid + j * kGbBThreads < n;
+        if (__ballot(act) == 0) break;
+        gb_event<true>(act, (unsigned long long)cur[j], p, k, slots, size, true, g);
+      }
+      __syncthreads();
+      gb_write_files(g, nfl, f0, out);
+    }
+    __syncthreads();  // the LDS is cleared for the next bucket
+    s0 = s0n;
+    n = nn;
+    s0n = s0nn;
+    nn = nnn;
+    b = bn;
+  };
+  while (true) {
+    step(v, pr, v2, pr2);
+    if (b >= nbuckets) break;
+    step(v2, pr2, v, pr);
+    if (b >= nbuckets) break;
+  }
+}
+
+// Dense variant (2^(L + sbits) <= kGbDenseKeys): the bucket's (file, second)
+// grid itself is the table, one u64 per pair = count | writes << 16 |
+// reads << 32 | local << 48 (bucket events < 2^16), one non-returning LDS add
+// per event; the per-file sums and the concurrency maximum are a reduction of
+// the file's row at the end.  Persistent like gb_bucket.
+constexpr int kGbDenseBits = 12;
+constexpr int kGbDenseCap = 65535;
+
+template <typename T>
+__global__ __launch_bounds__(kGbBThreads) void gb_bucket_dense(
+    const T* __restrict__ pb, const unsigned* __restrict__ bbase, int64_t nbuckets, int64_t nf,
+    GbPay p, const int32_t* __restrict__ primary, long long* __restrict__ out,
+    int* __restrict__ big_list, int* __restrict__ big_count) {
+  extern __shared__ unsigned long long lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int F = 1 << p.L;
+  const int S = 1 << p.sbits;
+  const int KS = F * S;
+  constexpr int kPrimReg = (1 << kGbMaxL) / kGbBThreads;
+  unsigned long long* grid = lds;
+  int* prim = reinterpret_cast<int*>(lds + KS);
+  const int64_t G = gridDim.x;
+  int64_t b = blockIdx.x;
+  if (b >= nbuckets) return;
+  const unsigned lmask = (1u << p.L) - 1;
+  const unsigned smask = (1u << p.sbits) - 1;
+  const unsigned ccmask = (1u << p.cbits) - 1;
+  int64_t s0 = bbase[b], n = (int64_t)bbase[b + 1] - s0;
+  T v[kGbReg];
+  int pr[kPrimReg];
+  auto fetch = [&](int64_t bb, int64_t ss, int64_t nn, T* vv, int* pp) {
+    const bool ok = nn <= kGbDenseCap;
+#pragma unroll
+    for (int j = 0; j < kGbReg; ++j) {
+      const int64_t i = tid + j * kGbBThreads;
+      vv[j] = ok && i < nn ? pb[ss + i] : (T)0;
+    }
+    const int64_t f0 = bb << p.L;
+#pragma unroll
+    for (int j = 0; j < kPrimReg; ++j) {
+      const int64_t f = tid + j * kGbBThreads;
+      pp[j] = f < F && f0 + f < nf ? primary[f0 + f] : -2;
+    }
+  };
+  auto add = [&](unsigned long long x) {
+    const unsigned fl = (unsigned)(x >> p.fshift) & lmask;
+    const unsigned sc = (unsigned)(x >> p.sshift) & smask;
+    const unsigned oc = (unsigned)(x >> p.cbits) & 3u;
+    const int cl = (int)((unsigned)x & ccmask) - 1;
+    const int pf = prim[fl];
+    const unsigned long long loc = (cl >= 0 && pf >= 0 && cl == pf) ? 1ull : 0ull;
+    atomicAdd(&grid[(fl << p.sbits) | sc], 1ull | ((unsigned long long)(oc & 1u) << 16) |
+                                               ((unsigned long long)(oc >> 1) << 32) | (loc << 48));
+  };
+  fetch(b, s0, n, v, pr);
+  int64_t s0n = 0, nn = 0;
+  if (b + G < nbuckets) {
+    s0n = bbase[b + G];
+    nn = (int64_t)bbase[b + G + 1] - s0n;
+  }
+  T v2[kGbReg];
+  int pr2[kPrimReg];
+  // ping-pong like gb_bucket
+  auto step = [&](T (&cur)[kGbReg], int (&cpr)[kPrimReg], T (&nxt)[kGbReg],
+                  int (&npr)[kPrimReg]) {
+#pragma unroll
+    for (int j = 0; j < kGbReg; ++j) asm volatile("" : "+v"(cur[j]));
+#pragma unroll
+    for (int j = 0; j < kPrimReg; ++j) asm volatile("" : "+v"(cpr[j]));
+    const int64_t bn = b + G;
+    const int64_t f0 = b << p.L;
+    const int nfl = (int)min((int64_t)F, nf - f0);
+    const bool over = n > kGbDenseCap;
+    if (!over) {
+      for (int i = tid; i < KS; i += kGbBThreads) grid[i] = 0;
+#pragma unroll
+      for (int j = 0; j < kPrimReg; ++j) {
+        const int f = tid + j * kGbBThreads;
+        if (f < F) prim[f] = cpr[j];
+      }
+    }
+    __syncthreads();
+    // the next bucket's loads fly while this one is counted
+    int64_t s0nn = 0, nnn = 0;
+    if (bn < nbuckets) {
+      fetch(bn, s0n, nn, nxt, npr);
+      if (bn + G < nbuckets) {
+        s0nn = bbase[bn + G];
+        nnn = (int64_t)bbase[bn + G + 1] - s0nn;
+      }
+    }
+    if (over) {
+      if (tid == 0) big_list[atomicAdd(big_count, 1)] = (int)b;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kGbReg; ++j)
+        if (tid + j * kGbBThreads < n) add((unsigned long long)cur[j]);
+      for (int64_t i = kGbReg * kGbBThreads + tid; i < n; i += kGbBThreads)
+        add((unsigned long long)pb[s0 + i]);
+      __syncthreads();
+      // one wave per file: sums and maximum over the file's seconds
+      for (int f = wv; f < nfl; f += kGbBThreads / 64) {
+        unsigned long long cnt = 0, w = 0, r = 0, lc = 0, mx = 0;
+        for (int sc = lane; sc < S; sc += 64) {
+          const unsigned long long e = grid[(f << p.sbits) | sc];
+          const unsigned long long c1 = e & 0xFFFFull;
+          cnt += c1;
+          w += (e >> 16) & 0xFFFFull;
+          r += (e >> 32) & 0xFFFFull;
+          lc += e >> 48;
+          mx = c1 > mx ? c1 : mx;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          cnt += __shfl_xor(cnt, o);
+          w += __shfl_xor(w, o);
+          r += __shfl_xor(r, o);
+          lc += __shfl_xor(lc, o);
+          const unsigned long long m2 = __shfl_xor(mx, o);
+          mx = m2 > mx ? m2 : mx;
+        }
+        if (lane < 6) {
+          const unsigned long long val[6] = {cnt, w, r, lc, cnt, mx};
+          out[(f0 + f) * 6 + lane] = (long long)val[lane];
+        }
+      }
+    }
+    __syncthreads();  // the grid is cleared for the next bucket
+    s0 = s0n;
+    n = nn;
+    s0n = s0nn;
+    nn = nnn;
+    b = bn;
+  };
+  while (true) {
+    step(v, pr, v2, pr2);
+    if (b >= nbuckets) break;
+    step(v2, pr2, v, pr);
+    if (b >= nbuckets) break;
+  }
+}
+
+// Buckets over the LDS capacity: the hash lives in global memory (2 n slots
+// from gslots + 2 * s0, so buckets never overlap).
+template <typename T>
+__global__ __launch_bounds__(kGbBThreads) void gb_bucket_big(
+    const T* __restrict__ pb, const unsigned* __restrict__ bbase, const int* __restrict__ list,
+    int64_t nf, GbPay p, GbKey k, const int32_t* __restrict__ primary,
+    unsigned long long* __restrict__ gslots, long long* __restrict__ out) {
+  extern __shared__ unsigned long long lds[];
+  const int64_t b = list[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int64_t s0 = bbase[b], n = (int64_t)bbase[b + 1] - s0;
+  const int F = 1 << p.L;
+  const int64_t f0 = b << p.L;
+  const int nfl = (int)min((int64_t)F, nf - f0);
+  unsigned long long* slots = gslots + 2 * s0;
+  const unsigned size = (unsigned)(2 * n);
+  GbFiles g = gb_files(lds, F);
+  for (unsigned i = tid; i < size; i += kGbBThreads) slots[i] = kEmpty;
+  for (int f = tid; f < nfl; f += kGbBThreads) {
+    g.cw[f] = 0;
+    g.rl[f] = 0;
+    g.conc[f] = 0;
+    g.prim[f] = primary[f0 + f];
+  }
+  __syncthreads();
+  for (int64_t i0 = 0; i0 < n; i0 += kGbBThreads) {
+    const int64_t i = i0 + tid;
+    const bool act = i < n;
+    gb_event<false>(act, act ? (unsigned long long)pb[s0 + i] : 0ull, p, k, slots, size, false,
+                    g);
+  }
+  __syncthreads();
+  gb_write_files(g, nfl, f0, out);
+}
+
+// forget the profile triple of a step that returns before its last event
+void prof_drop(Ctx& c) {
+  if (c.prof_cur >= 0) {
+    c.prof_used -= 3;
+    c.prof_cur = -1;
+  }
+}
+
+int bitlen(unsigned long long v) {  // bits to hold v (0 -> 0)
+  int b = 0;
+  while (b < 64 && (v >> b) != 0) ++b;
+  return b;
+}
+
+template <typename T>
+void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, bool dense,
+            GbPay p, int64_t T1, int64_t* out, const long long* res) {
+  const int R1 = 1 << B1, R2 = 1 << B2;
+  const int shift1 = fbits - B1;
+  const int64_t nb = ceil_div(nf, (int64_t)1 << L);
+  const int64_t nvalid = res[4];
+  T* p1 = c.gb_p1.as<T>();
+  unsigned* binbase = c.gb_small.as<unsigned>();
+  int* tile2start = reinterpret_cast<int*>(binbase + kGbMaxBins + 1);
+  unsigned* tilepref = c.gb_tilepref.as<unsigned>();
+  unsigned* chunkbase = c.gb_chunk.as<unsigned>();
+  const int64_t per1 = ceil_div(T1, 8);
+  if (nvalid > 0) {
+    hipLaunchKernelGGL(gb_scatter1<T>, dim3(8 * per1), dim3(kGbThreads), 0, c.stream,
+                       c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(), c.ev_client.as<int32_t>(),
+                       c.ev_ts.as<long long>(), ne, nf, p, shift1, R1, T1, per1, tilepref,
+                       chunkbase, p1);
+    HIP_CHECK(hipGetLastError());
+  }
+  const T* pb = p1;
+  unsigned* bbase = binbase;  // one pass: the buckets are the pass-1 digits
+  if (B2 > 0) {
+    const int64_t T2 = res[3];
+    bbase = c.gb_bbase.as<unsigned>();
+    c.gb_hist2.ensure(sizeof(unsigned) * (size_t)std::max<int64_t>(T2, 1) * R2);
+    unsigned* hist2 = c.gb_hist2.as<unsigned>();
+    const int shift2 = p.fshift + L;
+    if (T2 > 0)
+      hipLaunchKernelGGL(gb_hist2<T>, dim3(T2), dim3(kGbThreads), 0, c.stream, p1, binbase,
+                         tile2start, R1, R2, shift2, hist2);
+    hipLaunchKernelGGL(gb_scan2, dim3(R1), dim3(kGbMaxBins), 0, c.stream, hist2, tile2start,
+                       binbase, R1, R2, bbase);
+    HIP_CHECK(hipGetLastError());
+    if (T2 > 0) {
+      const int64_t per2 = ceil_div(T2, 8);
+      hipLaunchKernelGGL(gb_scatter2<T>, dim3(8 * per2), dim3(kGbThreads), 0, c.stream, p1,
+                         binbase, tile2start, R1, R2, shift2, T2, per2, hist2, bbase,
+                         c.gb_p2.as<T>());
+      HIP_CHECK(hipGetLastError());
+    }
+    pb = c.gb_p2.as<T>();
+  }
+  prof_mark(c, 1);  // partition done
+  GbKey k;
+  k.CB = 64 - (L + p.sbits);
+  k.cmask = k.CB >= 64 ? ~0ull : ((1ull << k.CB) - 1);
+  int* big = reinterpret_cast<int*>(tile2start + kGbMaxBins + 1);  // count, then the list
+  HIP_CHECK(hipMemsetAsync(big, 0, 4, c.stream));
+  c.gb_list.ensure(sizeof(int) * (size_t)std::max<int64_t>(nb, 1));
+  const size_t files_lds = (size_t)24 << L;
+  // persistent grids: exactly the workgroups that stay resident together (a
+  // second round of late workgroups would double the tail)
+  const size_t lds_b = dense ? (8u << (L + p.sbits)) + (4u << L) : 8 * kGbSlots + files_lds;
+  int per_cu = 0;
+  if (dense)
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(gb_bucket_dense<T>), kGbBThreads, lds_b));
+  else
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(gb_bucket<T>), kGbBThreads, lds_b));
+  per_cu = std::max(1, per_cu);
+  const int64_t gb_grid = std::min<int64_t>(nb, (int64_t)lloyd_num_cus(c.device) * per_cu);
+  c.gb_last_grid = gb_grid;
+  if (dense)
+    hipLaunchKernelGGL(gb_bucket_dense<T>, dim3(gb_grid), dim3(kGbBThreads), lds_b, c.stream, pb,
+                       bbase, nb, nf, p, c.ev_primary.as<int32_t>(), c.ev_out.as<long long>(),
+                       c.gb_list.as<int>(), big);
+  else
+    hipLaunchKernelGGL(gb_bucket<T>, dim3(gb_grid), dim3(kGbBThreads), lds_b, c.stream, pb,
+                       bbase, nb, nf, p, k, c.ev_primary.as<int32_t>(), c.ev_out.as<long long>(),
+                       c.gb_list.as<int>(), big);
+  HIP_CHECK(hipGetLastError());
+  prof_mark(c, 2);
+  int nbig = 0;
+  HIP_CHECK(hipMemcpyAsync(&nbig, big, 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (nbig > 0) {
+    c.gb_slots.ensure(sizeof(unsigned long long) * 2 * (size_t)std::max<int64_t>(nvalid, 1));
+    hipLaunchKernelGGL(gb_bucket_big<T>, dim3(nbig), dim3(kGbBThreads), files_lds, c.stream, pb,
+                       bbase, c.gb_list.as<int>(), nf, p, k, c.ev_primary.as<int32_t>(),
+                       c.gb_slots.as<unsigned long long>(), c.ev_out.as<long long>());
+    HIP_CHECK(hipGetLastError());
+    prof_mark(c, 2);
+  }
+  c.gb_last_big = nbig;
+  if (out)
+    HIP_CHECK(hipMemcpyAsync(out, c.ev_out.p, 8 * 6 * nf, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+}  // namespace
+
+// The group-by of the events resident in c.ev_* (features_aggregate_resident's
+// hand-written path).  Returns false (nothing computed) when the shape is
+// outside what the packed payload and bucket tables can hold; the caller then
+// takes the sort-based path.
+//
+// Layout: fbits = bits of the file id; the top B1 = min(9, fbits) bits are the
+// pass-1 digit; the remaining rem bits split into the pass-2 digit (B2 <= 9)
+// and the file-local bits L (2^L files per bucket), chosen once the second
+// range is known: the dense (file, second) grid when 2^(L + sbits) <= 4096,
+// else the hash with about 1024 events per bucket.
+bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max_ts) {
+  c.gb_last_hand = 0;
+  if (nf < 1 || ne < 0 || ne >= (1ll << 31) || nf >= (1ll << 31)) return false;
+  if (getenv("CDR_GROUPBY_SORT")) return false;  // the sort-based path, for comparisons
+  const int cmax = c.ev_cmax;
+  const int cbits = std::max(1, bitlen((unsigned long long)std::max(cmax, 0) + 1));
+  const int fbits = bitlen((unsigned long long)(nf - 1));
+  const int B1 = std::min(kGbMaxDigit, fbits);
+  const int rem = fbits - B1;
+  const int Lmin = std::max(0, rem - kGbMaxDigit), Lmax = std::min(rem, kGbMaxL);
+  if (Lmin > Lmax) return false;
+  const int R1 = 1 << B1;
+  const int64_t T1 = std::max<int64_t>(1, ceil_div(ne, kGbTile));
+  const int64_t C = ceil_div(T1, kGbChunkTiles);
+  // K1 + S1
+  c.gb_tilepref.ensure(sizeof(unsigned) * (size_t)T1 * R1);
+  c.gb_chunk.ensure(sizeof(unsigned) * (size_t)C * R1);
+  c.gb_part.ensure(sizeof(long long) * 3 * (size_t)C + 64);
+  c.gb_small.ensure(sizeof(int) * (3 * (kGbMaxBins + 1) + 8));
+  c.gb_res.ensure(sizeof(long long) * 8);
+  c.gb_bbase.ensure(sizeof(unsigned) * ((size_t)R1 << kGbMaxDigit) + 64);
+  const size_t ne1 = ne > 0 ? (size_t)ne : 1;
+  c.ev_out.ensure(8 * 6 * (size_t)nf + 64);
+  // profiling: events 0 (start), 1 (partition done), 2 (buckets done)
+  prof_step_begin(c);
+  prof_mark(c, 0);
+  hipLaunchKernelGGL(gb_hist1, dim3(C), dim3(kGbThreads), 0, c.stream, c.ev_file.as<int32_t>(),
+                     c.ev_ts.as<long long>(), ne, nf, fbits - B1, R1,
+                     c.gb_tilepref.as<unsigned>(), c.gb_chunk.as<unsigned>(),
+                     c.gb_part.as<long long>());
+  HIP_CHECK(hipGetLastError());
+  unsigned* binbase = c.gb_small.as<unsigned>();
+  int* tile2start = reinterpret_cast<int*>(binbase + kGbMaxBins + 1);
+  const int64_t G = ceil_div(C, kGbRange);
+  c.gb_rsum.ensure(sizeof(unsigned) * (size_t)G * R1);
+  hipLaunchKernelGGL(gb_scan1a, dim3(G), dim3(kGbMaxBins), 0, c.stream, c.gb_chunk.as<unsigned>(),
+                     C, R1, c.gb_rsum.as<unsigned>());
+  hipLaunchKernelGGL(gb_scan1b, dim3(1), dim3(kGbMaxBins), 0, c.stream, c.gb_rsum.as<unsigned>(),
+                     G, R1, c.gb_part.as<long long>(), C, binbase, tile2start,
+                     c.gb_res.as<long long>());
+  hipLaunchKernelGGL(gb_scan1c, dim3(G), dim3(kGbMaxBins), 0, c.stream, c.gb_chunk.as<unsigned>(),
+                     C, R1, c.gb_rsum.as<unsigned>(), binbase);
+  HIP_CHECK(hipGetLastError());
+  long long res[5];
+  HIP_CHECK(hipMemcpyAsync(res, c.gb_res.p, sizeof(res), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  // payload layout from the timestamp range
+  *max_ts = LLONG_MIN;
+  long long sec_min = 0, sec_max = 0;
+  if (ne > 0 && res[0] <= res[1]) {
+    *max_ts = res[1];
+    sec_min = (long long)std::floor((double)res[0] / 1000000.0);
+    sec_max = (long long)std::floor((double)res[1] / 1000000.0);
+  }
+  if (sec_max - sec_min >= (1ll << 40)) {
+    prof_drop(c);
+    return false;
+  }
+  const int sbits = std::max(1, bitlen((unsigned long long)(sec_max - sec_min) + 1));
+  const double a = (double)std::max<int64_t>(res[4], 1) / (double)nf;  // events per file
+  const bool dense = sbits + Lmin <= kGbDenseBits && !getenv("CDR_GB_HASH");
+  int L;
+  if (dense) {
+    const int Lt = (int)std::floor(std::log2(2048.0 / a));
+    L = std::max(Lmin, std::min({Lt, Lmax, kGbDenseBits - sbits}));
+  } else {
+    const int Lt = (int)std::floor(std::log2(1024.0 / a));
+    L = std::max(Lmin, std::min(Lt, Lmax));
+    if (L + sbits > 40) {  // hash key + count in 64 bits
+      prof_drop(c);
+      return false;
+    }
+  }
+  const int B2 = rem - L;
+  GbPay p;
+  p.cbits = cbits;
+  p.sshift = 2 + cbits;
+  p.sbits = sbits;
+  p.fshift = p.sshift + sbits;
+  p.L = L;
+  p.sec_min = sec_min;
+  const int lowbits = fbits - B1;
+  p.low_mask = lowbits >= 64 ? ~0ull : ((1ull << lowbits) - 1);
+  const int pbits = p.fshift + lowbits;
+  if (pbits > 64) {
+    prof_drop(c);
+    return false;
+  }
+  // pass-2 tiles per digit were counted by S1 for the same tile size
+  c.gb_last_hand = 1;
+  c.gb_last_L = L;
+  c.gb_last_passes = B2 > 0 ? 2 : 1;
+  c.gb_last_pbytes = pbits <= 32 ? 4 : 8;
+  c.gb_last_dense = dense ? 1 : 0;
+  const size_t pay = pbits <= 32 ? 4 : 8;
+  c.gb_p1.ensure(pay * ne1);
+  if (B2 > 0) c.gb_p2.ensure(pay * ne1);
+  if (pbits <= 32)
+    gb_run<unsigned>(c, ne, nf, fbits, L, B1, B2, dense, p, T1, out, res);
+  else
+    gb_run<unsigned long long>(c, ne, nf, fbits, L, B1, B2, dense, p, T1, out, res);
+  return true;
+}
+
+}  // namespace cdr

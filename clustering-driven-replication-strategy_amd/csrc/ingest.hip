@@ -643,6 +643,7 @@ void ingest_parse(Ctx& c, int64_t* status) {
   }
   c.ev_n = nrec;
   c.ev_nf = c.ing_nfiles;
+  c.ev_cmax = std::max(0, c.ing_nnodes - 1);  // client ids are node ids (or < 0)
 }
 
 void ingest_log(Ctx& c, const char* bytes, int64_t nbytes, int64_t* status) {

@@ -203,8 +203,58 @@ int cdr_features_aggregate(cdr_ctx* ctx, int64_t n_events,
 int cdr_features_generate(cdr_ctx* ctx, int64_t n_events, int64_t n_files, uint64_t seed,
                           int64_t t0_us, int64_t span_us);
 int cdr_features_aggregate_resident(cdr_ctx* ctx, int64_t* out, int64_t* max_ts_us);
+/* The reference's access simulator on the device (src/access_simulator.py:
+ * 16-60 with src/generator.py:44-45's category weights and primary nodes):
+ * files file_begin .. file_begin + n_files - 1 of a manifest, each with a
+ * category, jittered read / write rates and locality bias, Poisson arrivals
+ * over duration_s seconds from t0_us, timestamps with millisecond precision,
+ * clients 0 .. n_clients - 1; the log is left resident sorted by timestamp
+ * (file ids local, 0 .. n_files - 1).  *n_events = the events generated.  */
+int cdr_features_simulate(cdr_ctx* ctx, int64_t n_files, int64_t file_begin, double duration_s,
+                          int32_t n_clients, uint64_t seed, int64_t t0_us, int64_t* n_events);
 int cdr_features_events_read(cdr_ctx* ctx, int32_t* file_idx, uint8_t* op, int32_t* client,
                              int64_t* ts_us, int32_t* primary);
+/* What the last group-by did: info[0] 1 = hand-written partition + bucket
+ * hash path (csrc/groupby.hip), 0 = sort-based path; [1] file-local bits L
+ * (2^L files per bucket); [2] partition passes; [3] payload bytes; [4]
+ * buckets redone with the global-memory hash; [5] 1 = dense (file, second)
+ * grid per bucket, 0 = hash; [6] workgroups of the persistent bucket grid.
+ * (info has 7 entries.)                                                    */
+int cdr_features_groupby_info(cdr_ctx* ctx, int64_t* info);
+/* ---- sharded feature aggregation ------------------ */
+/* Rank r owns manifest rows [bounds[r], bounds[r+1]) (nranks + 1 entries,
+ * non-decreasing).  cdr_features_exchange_pack: the resident events, grouped
+ * by owner rank, as 16-byte records {ts int64, file int32 (global row),
+ * client << 8 | op int32} written to `send` (host or device memory, room for
+ * every resident event); counts[r] = records for rank r; events outside the
+ * manifest are not sent; *max_ts_us = max non-null timestamp over ALL
+ * resident events (INT64_MIN if none) for the MAX all-reduce of :48.
+ * cdr_features_exchange_unpack: the n records received (host or device
+ * memory), all of files [file_begin, file_end), become the resident events
+ * with local file ids (and the primaries of those rows move to the front).
+ * cdr_features_load_events: host events made resident (the host-tokenised
+ * log of a shard).                                                         */
+int cdr_features_exchange_pack(cdr_ctx* ctx, int32_t nranks, const int64_t* bounds, void* send,
+                               int64_t* counts, int64_t* max_ts_us);
+int cdr_features_exchange_unpack(cdr_ctx* ctx, const void* recv, int64_t n, int64_t file_begin,
+                                 int64_t file_end);
+int cdr_features_load_events(cdr_ctx* ctx, int64_t n, const int32_t* file_idx, const uint8_t* op,
+                             const int32_t* client, const int64_t* ts_us, int64_t n_files,
+                             const int32_t* primary);
+/* Finalisation over sharded rows (:53-94): cdr_features_finalize_stats
+ * reduces this rank's n_rows rows to istats[7] = {sum writes, min / max
+ * access_freq, min / max writes, min / max concurrency} and dstats[4] = {min /
+ * max age, min / max locality} (identities for n_rows == 0); after the SUM /
+ * MIN / MAX all-reduce, cdr_features_finalize_apply writes the rows' table
+ * with mean(writes) = sum / n_rows_total.  cdr_features_finalize ==
+ * stats + apply on one rank.                                               */
+int cdr_features_finalize_stats(cdr_ctx* ctx, int64_t n_rows, const int64_t* counts,
+                                const double* creation_s, double observation_end,
+                                int64_t* istats, double* dstats);
+int cdr_features_finalize_apply(cdr_ctx* ctx, int64_t n_rows, const int64_t* counts,
+                                const double* creation_s, double observation_end,
+                                const int64_t* istats, const double* dstats,
+                                int64_t n_rows_total, double* out);
 /* Access-log CSV ingest on the device.  Replaces the
  * host read of the log (src/compute_features.py:19-29: spark.read.csv of
  * `ts,path,op,client_node,pid`, to_timestamp; the build's host restatement is

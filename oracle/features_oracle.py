@@ -144,12 +144,15 @@ def counts_from_arrays(file_idx, op, client, ts_us, primary, n_files):
     np.add.at(out[:, 3], f, ((c >= 0) & (pr >= 0) & (c == pr)).astype(np.int64))
     out[:, 4] = out[:, 0]
     if f.size:
-        sec = np.where(null, 0, np.floor(np.where(null, 0, t) / 1e6)).astype(np.int64)
-        s0 = sec[~null].min() if (~null).any() else 0
-        so = np.where(null, (1 << 33) - 1, sec - s0)
-        key = f * (1 << 33) + so
-        uk, cnt = np.unique(key, return_counts=True)
-        np.maximum.at(out[:, 5], uk // (1 << 33), cnt)
+        sec = np.floor(np.where(null, 0, t) / 1e6).astype(np.int64)
+        sec[null] = np.iinfo(np.int64).max  # the null second: one more group per file
+        order = np.lexsort((sec, f))
+        fs, ss = f[order], sec[order]
+        start = np.ones(fs.size, dtype=bool)
+        start[1:] = (fs[1:] != fs[:-1]) | (ss[1:] != ss[:-1])
+        idx = np.flatnonzero(start)
+        cnt = np.diff(np.append(idx, fs.size))
+        np.maximum.at(out[:, 5], fs[idx], cnt)
     real = ts_us[ts_us != TS_NULL]
     mx = int(real.max()) if real.size else None
     return out, mx

@@ -1,0 +1,138 @@
+"""The hand-written group-by (csrc/groupby.hip: two-level file-id partition +
+per-bucket dense (file, second) grid or LDS hash) against the independent NumPy group-by of the oracle
+(oracle/features_oracle.counts_from_arrays, src/compute_features.py:31-48),
+over the shapes its layout logic distinguishes: one or two partition passes,
+dense grid or hash buckets, 4- or 8-byte payloads, buckets over the LDS
+capacity of either kind (redone with the global-memory hash),
+null timestamps, timestamps before the epoch, files without events, events
+outside the manifest, and a hot (file, second) pair."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import features_oracle as fo
+
+pytestmark = pytest.mark.gpu
+NULL = fo.TS_NULL
+T0 = 1_700_000_000_000_000
+
+
+def _events(rng, ne, nf, span_s=600, t0=T0, nclients=4, null_frac=0.01, bad_frac=0.02):
+    f = rng.integers(0, nf, ne).astype(np.int32)
+    f[rng.random(ne) < bad_frac] = -1
+    op = rng.integers(0, 3, ne).astype(np.uint8)
+    cl = rng.integers(-1, nclients, ne).astype(np.int32)
+    ts = (t0 + rng.integers(0, span_s * 1_000_000, ne)).astype(np.int64)
+    ts[rng.random(ne) < null_frac] = NULL
+    prim = rng.integers(-2, nclients, nf).astype(np.int32)
+    return f, op, cl, ts, prim
+
+
+def _check(ctx, f, op, cl, ts, prim, **want):
+    nf = prim.size
+    got, mx = ctx.features_aggregate(f, op, cl, ts, prim)
+    info = ctx.features_groupby_info()
+    exp, emx = fo.counts_from_arrays(f, op, cl, ts, prim, nf)
+    np.testing.assert_array_equal(got, exp)
+    assert mx == (emx if emx is not None else NULL)
+    assert info["hand"] == 1, info
+    for k, v in want.items():
+        if k == "big":
+            assert (info["big_buckets"] > 0) == v, info
+        else:
+            assert info[k] == v, info
+    return got, info
+
+
+def test_empty_log(ctx):
+    prim = np.array([0, 1, -2, 0, 1, 2, 0, 0, 1, 0], dtype=np.int32)
+    e = np.zeros(0, dtype=np.int32)
+    got, mx = ctx.features_aggregate(e, e.astype(np.uint8), e, e.astype(np.int64), prim)
+    assert not got.any() and mx == NULL
+    assert ctx.features_groupby_info()["hand"] == 1
+
+
+def test_one_file(ctx):
+    rng = np.random.default_rng(1)
+    f, op, cl, ts, prim = _events(rng, 5000, 1, span_s=3)
+    _check(ctx, f, op, cl, ts, prim, passes=1, dense=1, big=False)
+
+
+def test_few_files_long_span_hash_buckets_over_lds(ctx):
+    rng = np.random.default_rng(2)
+    f, op, cl, ts, prim = _events(rng, 1_000_000, 50, span_s=100_000)
+    got, _ = _check(ctx, f, op, cl, ts, prim, L=0, passes=1, dense=0, big=True)
+    assert got[:, 5].max() > 1
+
+
+def test_dense_bucket_over_cap(ctx):
+    rng = np.random.default_rng(12)
+    f, op, cl, ts, prim = _events(rng, 300_000, 4, span_s=60)
+    _check(ctx, f, op, cl, ts, prim, dense=1, big=True)
+
+
+def test_one_pass(ctx):
+    rng = np.random.default_rng(3)
+    f, op, cl, ts, prim = _events(rng, 200_000, 2000)
+    _check(ctx, f, op, cl, ts, prim, passes=1, payload_bytes=4, dense=1, big=False)
+
+
+def test_two_passes(ctx):
+    rng = np.random.default_rng(4)
+    f, op, cl, ts, prim = _events(rng, 3_000_000, 300_000)
+    _check(ctx, f, op, cl, ts, prim, passes=2, payload_bytes=4, dense=1, big=False)
+
+
+def test_two_passes_hash(ctx):
+    rng = np.random.default_rng(14)
+    f, op, cl, ts, prim = _events(rng, 3_000_000, 300_000, span_s=86_400)
+    _check(ctx, f, op, cl, ts, prim, passes=2, dense=0, big=False)
+
+
+def test_many_files_sparse_events(ctx):
+    rng = np.random.default_rng(5)
+    f, op, cl, ts, prim = _events(rng, 100_000, (1 << 20) + 3)
+    got, info = _check(ctx, f, op, cl, ts, prim, L=10, passes=2, dense=0)
+    assert (got[:, 0] == 0).sum() > 900_000
+
+
+def test_wide_time_range_and_many_nodes_use_8_byte_payload(ctx):
+    rng = np.random.default_rng(6)
+    f, op, cl, ts, prim = _events(rng, 400_000, 40_000, nclients=5000)
+    # seconds from before the epoch to ~2^33 s later (floor of negatives)
+    ts = np.where(ts == NULL, NULL,
+                  rng.integers(-(2 ** 31) * 10**6, (2 ** 33) * 10**6, ts.size)).astype(np.int64)
+    ts[:1000] = -1  # -1 us floors to second -1
+    _check(ctx, f, op, cl, ts, prim, payload_bytes=8)
+
+
+def test_hot_pair_and_null_seconds(ctx):
+    rng = np.random.default_rng(7)
+    f, op, cl, ts, prim = _events(rng, 300_000, 20_000, null_frac=0.0)
+    f[:20_000] = 17                       # one file, one second: concurrency 20000
+    ts[:20_000] = T0 + 5_000_000 + rng.integers(0, 1_000_000, 20_000)
+    f[20_000:20_500] = 18                 # 500 null timestamps of one file: one group
+    ts[20_000:20_500] = NULL
+    got, _ = _check(ctx, f, op, cl, ts, prim)
+    assert got[17, 5] >= 20_000
+    assert got[18, 5] >= 500
+
+
+def test_all_null_timestamps(ctx):
+    rng = np.random.default_rng(8)
+    f, op, cl, ts, prim = _events(rng, 50_000, 3000)
+    ts[:] = NULL
+    got, _ = _check(ctx, f, op, cl, ts, prim)
+    np.testing.assert_array_equal(got[:, 5][got[:, 0] > 0], got[:, 0][got[:, 0] > 0])
+
+
+def test_sort_path_agrees(ctx, monkeypatch):
+    rng = np.random.default_rng(9)
+    f, op, cl, ts, prim = _events(rng, 500_000, 60_000)
+    a, ma = ctx.features_aggregate(f, op, cl, ts, prim)
+    monkeypatch.setenv("CDR_GROUPBY_SORT", "1")
+    b, mb = ctx.features_aggregate(f, op, cl, ts, prim)
+    assert ctx.features_groupby_info()["hand"] == 0
+    np.testing.assert_array_equal(a, b)
+    assert ma == mb

@@ -1,0 +1,87 @@
+"""The device access simulator (csrc/simulate.hip) against the model of
+src/access_simulator.py:16-60 and src/generator.py:44-45, and the group-by on
+its log against the oracle.
+
+The simulator draws its own counter-based random numbers, so the checks are
+the log's format invariants (sorted timestamps with millisecond precision
+inside [t0, t0 + duration], op / client / file ranges) and its statistics
+against a NumPy Monte Carlo of the same model (mean events per file, READ
+share, share of events at the primary node, per-category event rates), plus
+determinism and shard-independence."""
+import numpy as np
+import pytest
+
+from oracle import features_oracle as fo
+
+pytestmark = pytest.mark.gpu
+T0 = 1_761_998_400_123_456
+CATS = {  # access_simulator.py:42-47 (read, write, locality), generator.py:45 weights
+    "hot": (0.8, 0.2, 0.7, 0.10), "shared": (0.6, 0.02, 0.3, 0.20),
+    "moderate": (0.1, 0.01, 0.5, 0.50), "archival": (0.005, 0.001, 0.9, 0.20)}
+
+
+def _model(n=400_000, duration=600.0, nclients=3, seed=0):
+    """Expected per-file event count, READ share and primary share of the
+    simulator model (Monte Carlo over the jittered per-file rates)."""
+    rng = np.random.default_rng(seed)
+    cat = rng.choice(4, n, p=[v[3] for v in CATS.values()])
+    R = np.array([v[0] for v in CATS.values()])[cat]
+    W = np.array([v[1] for v in CATS.values()])[cat]
+    B = np.array([v[2] for v in CATS.values()])[cat]
+    r = np.maximum(0, rng.normal(R, np.maximum(1e-4, 0.2 * R)))
+    w = np.maximum(0, rng.normal(W, np.maximum(1e-4, 0.5 * W)))
+    b = np.clip(rng.normal(B, 0.2), 0, 1)
+    lam = r + w
+    per_file = lam.mean() * duration
+    read_share = (r).sum() / lam.sum()
+    prim_share = (lam * (b + (1 - b) / nclients)).sum() / lam.sum()
+    return per_file, read_share, prim_share
+
+
+def test_log_format_and_model_statistics(ctx):
+    nf, dur = 40_000, 600.0
+    ne = ctx.features_simulate(nf, dur, 3, seed=11, t0_us=T0)
+    f, op, cl, ts, pr = ctx.features_events_read()
+    assert ne == f.size and ne > 0
+    # format: time-ordered, millisecond precision, within the simulated period
+    assert np.all(np.diff(ts) >= 0)
+    assert np.all(ts % 1000 == 0)
+    assert ts[0] >= (T0 // 1000) * 1000 and ts[-1] <= T0 + int(dur * 1e6)
+    assert f.min() >= 0 and f.max() < nf
+    assert set(np.unique(op)) <= {1, 2}
+    assert cl.min() >= 0 and cl.max() < 3 and pr.min() >= 0 and pr.max() < 3
+    # statistics of the model (tolerances ~5 sigma of the sampling noise)
+    per_file, read_share, prim_share = _model(duration=dur)
+    assert abs(ne / nf - per_file) / per_file < 0.03, (ne / nf, per_file)
+    assert abs((op == 2).mean() - read_share) < 0.01
+    assert abs((cl == pr[f]).mean() - prim_share) < 0.01
+    counts = np.bincount(f, minlength=nf)
+    # hot files (~600 events) and archival files (~3.6) are both there
+    assert (counts > 400).mean() > 0.05 and (counts < 10).mean() > 0.1
+
+
+def test_deterministic_and_shard_independent(ctx):
+    nf = 20_000
+    ctx.features_simulate(nf, 120.0, 3, seed=5, t0_us=T0)
+    a, _ = ctx.features_aggregate_resident()
+    ctx.features_simulate(nf, 120.0, 3, seed=5, t0_us=T0)
+    b, _ = ctx.features_aggregate_resident()
+    np.testing.assert_array_equal(a, b)
+    # files 0..nf-1 simulated as two shards give the same per-file counters
+    ctx.features_simulate(nf // 2, 120.0, 3, seed=5, t0_us=T0, file_begin=0)
+    lo, _ = ctx.features_aggregate_resident()
+    ctx.features_simulate(nf - nf // 2, 120.0, 3, seed=5, t0_us=T0, file_begin=nf // 2)
+    hi, _ = ctx.features_aggregate_resident()
+    np.testing.assert_array_equal(np.vstack([lo, hi]), a)
+
+
+def test_groupby_of_simulated_log_matches_oracle(ctx):
+    nf = 50_000
+    ctx.features_simulate(nf, 600.0, 3, seed=3, t0_us=T0)
+    got, mx = ctx.features_aggregate_resident()
+    assert ctx.features_groupby_info()["hand"] == 1
+    f, op, cl, ts, pr = ctx.features_events_read()
+    exp, emx = fo.counts_from_arrays(f, op, cl, ts, pr, nf)
+    np.testing.assert_array_equal(got, exp)
+    assert mx == emx
+    assert got[:, 5].max() >= 3  # hot files have seconds with several events
