@@ -95,6 +95,63 @@ class Comm:
         self.dist.all_reduce(t)
         return float(t.cpu().numpy()[0])
 
+    def allreduce_i64(self, arr: np.ndarray, op: str = "sum") -> np.ndarray:
+        """Element-wise SUM / MIN / MAX of an int64 vector over the ranks."""
+        if not self.dist:
+            return np.asarray(arr, dtype=np.int64)
+        t = self._t(np.asarray(arr, dtype=np.int64))
+        red = {"sum": self.dist.ReduceOp.SUM, "min": self.dist.ReduceOp.MIN,
+               "max": self.dist.ReduceOp.MAX}[op]
+        self.dist.all_reduce(t, op=red)
+        return t.cpu().numpy()
+
+    def allreduce_f64(self, arr: np.ndarray, op: str = "sum") -> np.ndarray:
+        if not self.dist:
+            return np.asarray(arr, dtype=np.float64)
+        t = self._t(np.asarray(arr, dtype=np.float64))
+        red = {"sum": self.dist.ReduceOp.SUM, "min": self.dist.ReduceOp.MIN,
+               "max": self.dist.ReduceOp.MAX}[op]
+        self.dist.all_reduce(t, op=red)
+        return t.cpu().numpy()
+
+    def exchange_buffer(self, nbytes: int):
+        """(buffer, pointer-or-array) for the feature exchange: a device
+        uint8 tensor under NCCL (RCCL all-to-all), a host array otherwise."""
+        nbytes = max(int(nbytes), 1)
+        if self.device is not None and self.dist:
+            import torch
+
+            t = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            return t, t.data_ptr()
+        a = np.zeros(nbytes, dtype=np.uint8)
+        return a, a
+
+    def all_to_all_bytes(self, send, send_bytes: np.ndarray):
+        """Variable all-to-all: send_bytes[r] bytes of `send` (the regions in
+        rank order) go to rank r.  Returns (recv buffer, pointer-or-array,
+        received bytes per source rank)."""
+        send_bytes = np.asarray(send_bytes, dtype=np.int64)
+        if not self.dist:
+            return send, send, send_bytes
+        import torch
+
+        sb = self._t(send_bytes)
+        rb = torch.empty_like(sb)
+        self.dist.all_to_all_single(rb, sb)
+        recv_bytes = rb.cpu().numpy()
+        recv, handle = self.exchange_buffer(int(recv_bytes.sum()))
+        if self.device is not None:
+            sendt = send
+            recvt = recv
+        else:
+            sendt = torch.from_numpy(send)
+            recvt = torch.from_numpy(recv)
+        total_send = int(send_bytes.sum())
+        self.dist.all_to_all_single(recvt[: int(recv_bytes.sum())], sendt[:total_send],
+                                    output_split_sizes=[int(x) for x in recv_bytes],
+                                    input_split_sizes=[int(x) for x in send_bytes])
+        return recv, handle, recv_bytes
+
     def lloyd_buffer(self, n: int):
         """(buffer, pointer) of the per-step (k, d+1) int64 all-reduce: a
         device tensor under NCCL (RCCL), a host array otherwise."""

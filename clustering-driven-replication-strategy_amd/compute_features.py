@@ -300,11 +300,35 @@ def write_spark_csv(out_dir: str, paths, table) -> str:
 
 
 def main(argv=None):
+    """Single process, or one rank per GPU under torch.distributed.run
+    (WORLD_SIZE > 1: features_dist.sharded_compute_features over RCCL; rank 0
+    writes the CSV)."""
     parser = argparse.ArgumentParser()
     parser.add_argument("--manifest", required=True)
     parser.add_argument("--access_log", required=True)
     parser.add_argument("--out", default="features_out")
     args = parser.parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        from cdr_dist import Comm
+        from features_dist import sharded_compute_features
+
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+        ctx = Context(local)
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        paths, table = sharded_compute_features(args.manifest, args.access_log, ctx,
+                                                Comm(dist, torch.device("cuda", local)))
+        if dist.get_rank() == 0:
+            write_spark_csv(args.out, paths, table)
+            print("Wrote features to", args.out)
+        ctx.close()
+        dist.destroy_process_group()
+        return
     paths, table = compute_features(args.manifest, args.access_log)
     write_spark_csv(args.out, paths, table)
     print("Wrote features to", args.out)

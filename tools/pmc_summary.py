@@ -13,19 +13,26 @@ import glob
 import os
 import sys
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+roots = [a for a in sys.argv[1:] if not a.startswith("--") and os.path.isdir(a)] or ["gpurun_out/pmc"]
+root = roots[0]
 json_cfg = None
+want_arg = None
+if "--want" in sys.argv:
+    want_arg = sys.argv[sys.argv.index("--want") + 1].split(",")
 if "--json" in sys.argv:
     i = sys.argv.index("--json")
     json_cfg, json_n = sys.argv[i + 1], int(sys.argv[i + 2])
 agg = collections.defaultdict(dict)
 names = {}
-for f in sorted(glob.glob(os.path.join(root, "*", "*_counter_collection.csv"))):
+files = [f for r0 in roots for f in sorted(glob.glob(os.path.join(r0, "*", "*_counter_collection.csv")))]
+for f in files:
     for r in csv.DictReader(open(f)):
-        key = (os.path.basename(os.path.dirname(f)), int(r["Dispatch_Id"]))
+        # passes of one command line pair up by dispatch id (same launch order)
+        key = ("+".join(os.path.basename(r0) for r0 in roots), int(r["Dispatch_Id"]))
         names[key] = r["Kernel_Name"]
         agg[key][r["Counter_Name"]] = agg[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-want = ("screen32", "fallback32", "reduce32", "screen_fast", "screen_kernel")
+want = tuple(want_arg) if want_arg else ("screen32", "fallback32", "reduce32", "screen_fast",
+                                         "screen_kernel")
 for key in sorted(agg):
     nm = names[key]
     if not any(w in nm for w in want):
