@@ -88,6 +88,7 @@ SIGNATURES = {
     "cdr_features_aggregate_resident": ([_P, _P, _PI64], None),
     "cdr_features_events_read": ([_P, _P, _P, _P, _P, _P], None),
     "cdr_features_groupby_info": ([_P, _P], None),
+    "cdr_lloyd_f64_walked": ([_P, _PI64], None),
     "cdr_features_exchange_pack": ([_P, _I32, _P, _P, _P, _PI64], None),
     "cdr_features_exchange_unpack": ([_P, _P, _I64, _I64, _I64], None),
     "cdr_features_load_events": ([_P, _I64, _P, _P, _P, _P, _I64, _P], None),
@@ -291,6 +292,12 @@ class Context:
         counts = np.empty(k, dtype=np.int64)
         _check(self._lib.cdr_lloyd_step_f64(self._h, _ptr(C), k, _ptr(sums), _ptr(counts)))
         return sums, counts
+
+    def f64_walked(self) -> int:
+        """Blocks the last F64 step re-added element-wise (-1: serial kernel)."""
+        v = _I64()
+        _check(self._lib.cdr_lloyd_f64_walked(self._h, ctypes.byref(v)))
+        return int(v.value)
 
     def labels(self) -> np.ndarray:
         out = np.empty(self.info()["n"], dtype=np.int64)

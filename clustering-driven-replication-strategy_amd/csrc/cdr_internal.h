@@ -133,6 +133,9 @@ struct Ctx {
   int fb_regions = 0;
   DevBuf f64_sums;  // double k*d
   DevBuf f64_counts;  // int64 k
+  // f64sum.hip: block sums, counts, predicted binades, transfers, walk counts
+  DevBuf f64x_A, f64x_cnt, f64x_E, f64x_T, f64x_walk;
+  int64_t f64x_walked = -1;  // blocks re-added element-wise in the last F64 step (-1: serial)
   HostBuf h_small;  // pinned scratch for small D2H
   HostBuf h_up;     // pinned staging of the per-step screen32 upload
   hipEvent_t up_event = nullptr;  // recorded after that upload
@@ -254,6 +257,9 @@ void features_aggregate(Ctx& c, int64_t n_events, const int32_t* file_idx,
 // hand-written group-by of the resident events; false = shape not supported
 // (nothing computed, the caller takes the sort-based path)
 bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max_ts);
+// exact sequential-order F64 centroid sums in parallel (f64sum.hip); false =
+// shape not covered (d < 2 or k > 64)
+bool f64_sums_parallel(Ctx& c, int k, double* d_sums);
 void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
                        const double* creation_s, double observation_end,
                        double* out);

@@ -1,0 +1,238 @@
+// f64sum.hip — exact, parallel F64-mode centroid sums (src/kmeans_plusplus.py:
+// 41, `X[labels == j].mean(axis=0)`): for d >= 2 NumPy adds the selected rows
+// one after another, so sums[j][f] is the SEQUENTIAL fp64 sum of the column in
+// row order.  Floating-point addition is not associative; this reproduces the
+// sequential result bit for bit without a serial pass over n.
+//
+// While the running value s stays inside one binade [2^e, 2^(e+1)) it is
+// m * g with g = 2^(e-52) and 2^52 <= m < 2^53, and adding x >= 0 gives
+// m + q + (rounding of the fraction r of x / g: up when r > 1/2, down when
+// r < 1/2, to even when r == 1/2).  Only the tie depends on m, through its
+// parity, so a run of additions inside one binade is an integer transfer that
+// depends only on the parity of m when the run starts: (D0, P0) for an even
+// entry and (D1, P1) for an odd one (the same idea as the seeding cumsum,
+// csrc/seed.hip).
+//
+//   A  f64_blocksum   per 256-row block: approximate per-(cluster, feature)
+//                     sums (any order) and member counts
+//   B  f64_predict    per (cluster, feature): running approximate prefix ->
+//                     the binade the exact running value is expected to be in
+//                     when each block starts
+//   C  f64_transfer   per (block, feature): the block's transfer for every
+//                     cluster in its predicted binade (flagged when an addend
+//                     is negative or not below the binade's top)
+//   D  f64_walk       per (cluster, feature), sequential over the blocks: the
+//                     exact running value; a block whose prediction missed,
+//                     whose transfer is flagged or would leave the binade is
+//                     re-added element by element in real fp64 (so the result
+//                     is exact whatever the data; the prediction only decides
+//                     how often that happens: about once per binade crossing,
+//                     ~log2(n) times per sequence for non-negative data).
+#include <algorithm>
+#include <cmath>
+
+#include "cdr_internal.h"
+
+namespace cdr {
+
+namespace {
+
+constexpr int kFB = 256;               // rows per block
+constexpr int kFMaxK = 64;             // clusters handled here (LDS state)
+constexpr int kENone = -100000;        // no prediction (no member before the block)
+
+struct Xfer {
+  long long d0;  // grid steps added for an even entry
+  int dd;        // d1 - d0
+  int flags;     // bit0 P0, bit1 P1 (exit parities), bit2 invalid, bit3 members
+};
+
+__global__ __launch_bounds__(kFB) void f64_blocksum(const double* __restrict__ X, int64_t n,
+                                                    int64_t n_pad, int d, int k,
+                                                    const int32_t* __restrict__ labels,
+                                                    double* __restrict__ A,
+                                                    unsigned* __restrict__ cnt) {
+  extern __shared__ double sh[];
+  double* tab = sh;                                   // [k][d]
+  unsigned* c = reinterpret_cast<unsigned*>(sh + k * d);  // [k]
+  const int64_t b = blockIdx.x;
+  for (int i = threadIdx.x; i < k * d; i += kFB) tab[i] = 0.0;
+  for (int i = threadIdx.x; i < k; i += kFB) c[i] = 0;
+  __syncthreads();
+  const int64_t row = b * kFB + threadIdx.x;
+  if (row < n) {
+    const int j = labels[row];
+    atomicAdd(&c[j], 1u);
+    for (int f = 0; f < d; ++f) atomicAdd(&tab[j * d + f], X[xidx(f, row, n_pad)]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k * d; i += kFB) A[b * k * d + i] = tab[i];
+  for (int i = threadIdx.x; i < k; i += kFB) cnt[b * k + i] = c[i];
+}
+
+__global__ void f64_predict(const double* __restrict__ A, const unsigned* __restrict__ cnt,
+                            int64_t nb, int d, int k, int* __restrict__ E) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= k * d) return;
+  const int j = t / d;
+  double P = 0.0;
+  for (int64_t b = 0; b < nb; ++b) {
+    int e = kENone;
+    if (P > 0.0 && isfinite(P)) {
+      int ex;
+      frexp(P, &ex);  // P in [2^(ex-1), 2^ex)
+      e = ex - 1;
+    }
+    E[b * k * d + t] = e;
+    if (cnt[b * k + j]) P += A[b * k * d + t];
+  }
+}
+
+// One thread per (block, feature); the per-cluster transfer states live in
+// LDS ([thread][cluster]).
+__global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_pad, int d,
+                             int k, int64_t nb, const int32_t* __restrict__ labels,
+                             const int* __restrict__ E, Xfer* __restrict__ T) {
+  extern __shared__ unsigned char smem[];
+  const int nt = blockDim.x;
+  long long* s0 = reinterpret_cast<long long*>(smem);   // [nt][k]
+  int* sdd = reinterpret_cast<int*>(s0 + (size_t)nt * k);  // [nt][k]
+  int* sfl = sdd + (size_t)nt * k;                        // [nt][k]
+  int* se = sfl + (size_t)nt * k;                         // [nt][k]
+  const int64_t t = (int64_t)blockIdx.x * nt + threadIdx.x;
+  const bool live = t < nb * d;
+  const int64_t b = live ? t / d : 0;
+  const int f = live ? (int)(t % d) : 0;
+  long long* m0 = s0 + (size_t)threadIdx.x * k;
+  int* mdd = sdd + (size_t)threadIdx.x * k;
+  int* mfl = sfl + (size_t)threadIdx.x * k;
+  int* me = se + (size_t)threadIdx.x * k;
+  if (!live) return;
+  for (int j = 0; j < k; ++j) {
+    m0[j] = 0;
+    mdd[j] = 0;
+    mfl[j] = 2;  // P0 = 0, P1 = 1
+    me[j] = E[b * k * d + (int64_t)j * d + f];
+  }
+  const int64_t r0 = b * kFB, r1 = min(n, r0 + kFB);
+  for (int64_t row = r0; row < r1; ++row) {
+    const int j = labels[row];
+    const double x = X[xidx(f, row, n_pad)];
+    int fl = mfl[j] | 8;
+    const int e = me[j];
+    if (e == kENone || !(x >= 0.0)) {
+      mfl[j] = fl | 4;
+      continue;
+    }
+    const double y = ldexp(x, 52 - e);  // exact: a power-of-two scaling
+    if (!(y < 9007199254740992.0)) {    // x not below the binade's top
+      mfl[j] = fl | 4;
+      continue;
+    }
+    const double q = floor(y);
+    const double r = y - q;
+    const long long qi = (long long)q;
+    const bool up = r > 0.5, tie = r == 0.5;
+    // even-entry path
+    const int p0 = fl & 1;
+    const long long i0 = qi + (up ? 1 : (tie ? ((p0 + qi) & 1) : 0));
+    // odd-entry path
+    const int p1 = (fl >> 1) & 1;
+    const long long i1 = qi + (up ? 1 : (tie ? ((p1 + qi) & 1) : 0));
+    m0[j] += i0;
+    mdd[j] += (int)(i1 - i0);
+    fl = (fl & ~3) | (int)((p0 + i0) & 1) | ((int)((p1 + i1) & 1) << 1);
+    mfl[j] = fl;
+  }
+  for (int j = 0; j < k; ++j) {
+    Xfer x;
+    x.d0 = m0[j];
+    x.dd = mdd[j];
+    x.flags = mfl[j];
+    T[b * k * d + (int64_t)j * d + f] = x;
+  }
+}
+
+__global__ void f64_walk(const double* __restrict__ X, int64_t n, int64_t n_pad, int d, int k,
+                         int64_t nb, const int32_t* __restrict__ labels,
+                         const unsigned* __restrict__ cnt, const int* __restrict__ E,
+                         const Xfer* __restrict__ T, double* __restrict__ sums,
+                         long long* __restrict__ walked) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= k * d) return;
+  const int j = t / d, f = t % d;
+  double s = 0.0;
+  bool any = false;  // NumPy's reduce starts from the first selected row
+  long long nwalk = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    if (!cnt[b * k + j]) continue;
+    const int64_t at = b * k * d + t;
+    const Xfer x = T[at];
+    const int e = E[at];
+    bool ok = false;
+    if (!(x.flags & 4) && s > 0.0) {
+      int ex;
+      const double fr = frexp(s, &ex);
+      (void)fr;
+      if (ex - 1 == e) {
+        const long long m = (long long)ldexp(s, 52 - e);  // exact: s is on the grid
+        const long long m2 = m + ((m & 1) ? x.d0 + x.dd : x.d0);
+        if (m2 < (1ll << 53)) {
+          s = ldexp((double)m2, e - 52);
+          ok = true;
+        }
+      }
+    }
+    if (!ok) {  // element by element, in real fp64 (row order)
+      ++nwalk;
+      const int64_t r1 = min(n, (b + 1) * kFB);
+      for (int64_t row = b * kFB; row < r1; ++row)
+        if (labels[row] == j) {
+          const double v = X[xidx(f, row, n_pad)];
+          s = any ? s + v : v;
+          any = true;
+        }
+    }
+  }
+  sums[(int64_t)j * d + f] = s;
+  walked[t] = nwalk;
+}
+
+}  // namespace
+
+// sums (k, d) on the device, exact sequential row-order fp64 sums; returns
+// false when the shape is not covered (d < 2, k > 64): the caller runs the
+// serial kernel.
+bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
+  const int d = c.d;
+  if (d < 2 || k < 1 || k > kFMaxK || c.n < 1) return false;
+  const int64_t n = c.n, nb = ceil_div(n, kFB);
+  const size_t kd = (size_t)k * d;
+  c.f64x_A.ensure(sizeof(double) * nb * kd);
+  c.f64x_cnt.ensure(sizeof(unsigned) * nb * k);
+  c.f64x_E.ensure(sizeof(int) * nb * kd);
+  c.f64x_T.ensure(sizeof(Xfer) * nb * kd);
+  c.f64x_walk.ensure(sizeof(long long) * kd);
+  hipLaunchKernelGGL(f64_blocksum, dim3(nb), dim3(kFB), sizeof(double) * kd + 4 * k, c.stream,
+                     c.x64.as<double>(), n, c.n_pad, d, k, c.labels.as<int32_t>(),
+                     c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>());
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(f64_predict, dim3(ceil_div((int64_t)kd, 64)), dim3(64), 0, c.stream,
+                     c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), nb, d, k,
+                     c.f64x_E.as<int>());
+  HIP_CHECK(hipGetLastError());
+  const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
+  const size_t lds = (size_t)nt * k * (8 + 4 + 4 + 4);
+  hipLaunchKernelGGL(f64_transfer, dim3(ceil_div(nb * d, nt)), dim3(nt), lds, c.stream,
+                     c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
+                     c.f64x_E.as<int>(), c.f64x_T.as<Xfer>());
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(f64_walk, dim3(ceil_div((int64_t)kd, 64)), dim3(64), 0, c.stream,
+                     c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
+                     c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(), d_sums,
+                     c.f64x_walk.as<long long>());
+  HIP_CHECK(hipGetLastError());
+  return true;
+}
+
+}  // namespace cdr

@@ -711,11 +711,12 @@ __global__ __launch_bounds__(kGbBThreads) void gb_bucket(const T* __restrict__ p
   }
 }
 
-// Dense variant (2^(L + sbits) <= kGbDenseKeys): the bucket's (file, second)
-// grid itself is the table, one u64 per pair = count | writes << 16 |
-// reads << 32 | local << 48 (bucket events < 2^16), one non-returning LDS add
-// per event; the per-file sums and the concurrency maximum are a reduction of
-// the file's row at the end.  Persistent like gb_bucket.
+// Dense variant (2^(L + sbits) <= 2^kGbDenseBits): the bucket's (file, second)
+// grid of u16 counts is the table (two per u32 word; bucket events < 2^16, so
+// no count overflows), one non-returning LDS add per event; count / writes /
+// reads / local per file are added once per group of lanes of one file
+// (ballots, as gb_event), and the concurrency maximum is a max over the file's
+// row at the end.  Persistent like gb_bucket.
 constexpr int kGbDenseBits = 12;
 constexpr int kGbDenseCap = 65535;
 
@@ -728,10 +729,10 @@ __global__ __launch_bounds__(kGbBThreads) void gb_bucket_dense(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int F = 1 << p.L;
   const int S = 1 << p.sbits;
-  const int KS = F * S;
+  const int KW = (F * S + 1) >> 1;  // u32 words of the count grid
   constexpr int kPrimReg = (1 << kGbMaxL) / kGbBThreads;
-  unsigned long long* grid = lds;
-  int* prim = reinterpret_cast<int*>(lds + KS);
+  GbFiles g = gb_files(lds, F);
+  unsigned* grid = reinterpret_cast<unsigned*>(g.prim + F);
   const int64_t G = gridDim.x;
   int64_t b = blockIdx.x;
   if (b >= nbuckets) return;
@@ -755,15 +756,39 @@ __global__ __launch_bounds__(kGbBThreads) void gb_bucket_dense(
       pp[j] = f < F && f0 + f < nf ? primary[f0 + f] : -2;
     }
   };
-  auto add = [&](unsigned long long x) {
-    const unsigned fl = (unsigned)(x >> p.fshift) & lmask;
+  // the file's sums once per group of lanes of one file (ballots over the
+  // file-local bits); fl / oc / loc of this lane's event, act: it holds one
+  auto file_sums = [&](bool act, unsigned fl, unsigned oc, bool loc) {
+    unsigned long long peers = __ballot(act);
+    for (int bt = 0; bt < p.L; ++bt) {
+      const bool bit = (fl >> bt) & 1u;
+      const unsigned long long bb = __ballot(act && bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const unsigned long long mw = __ballot(act && oc == 1), mr = __ballot(act && oc == 2);
+    const unsigned long long ml = __ballot(act && loc);
+    if (act && lane == __ffsll((long long)peers) - 1) {
+      atomicAdd(&g.cw[fl], (unsigned long long)__popcll(peers) |
+                               ((unsigned long long)__popcll(peers & mw) << 32));
+      atomicAdd(&g.rl[fl], (unsigned long long)__popcll(peers & mr) |
+                               ((unsigned long long)__popcll(peers & ml) << 32));
+    }
+  };
+  // one event's pair count (a non-returning add) and its fields
+  auto pair = [&](unsigned long long x, int pf_sel_unused, unsigned& fl, unsigned& oc, int& cl) {
+    fl = (unsigned)(x >> p.fshift) & lmask;
     const unsigned sc = (unsigned)(x >> p.sshift) & smask;
-    const unsigned oc = (unsigned)(x >> p.cbits) & 3u;
-    const int cl = (int)((unsigned)x & ccmask) - 1;
-    const int pf = prim[fl];
-    const unsigned long long loc = (cl >= 0 && pf >= 0 && cl == pf) ? 1ull : 0ull;
-    atomicAdd(&grid[(fl << p.sbits) | sc], 1ull | ((unsigned long long)(oc & 1u) << 16) |
-                                               ((unsigned long long)(oc >> 1) << 32) | (loc << 48));
+    oc = (unsigned)(x >> p.cbits) & 3u;
+    cl = (int)((unsigned)x & ccmask) - 1;
+    const unsigned key = (fl << p.sbits) | sc;
+    atomicAdd(&grid[key >> 1], 1u << ((key & 1u) << 4));
+  };
+  auto add = [&](bool act, unsigned long long x) {
+    unsigned fl = 0, oc = 0;
+    int cl = -1;
+    if (act) pair(x, 0, fl, oc, cl);
+    const int pf = g.prim[fl];
+    file_sums(act, fl, oc, act && cl >= 0 && pf >= 0 && cl == pf);
   };
   fetch(b, s0, n, v, pr);
   int64_t s0n = 0, nn = 0;
@@ -785,11 +810,15 @@ __global__ __launch_bounds__(kGbBThreads) void gb_bucket_dense(
     const int nfl = (int)min((int64_t)F, nf - f0);
     const bool over = n > kGbDenseCap;
     if (!over) {
-      for (int i = tid; i < KS; i += kGbBThreads) grid[i] = 0;
+      for (int i = tid; i < KW; i += kGbBThreads) grid[i] = 0;
 #pragma unroll
       for (int j = 0; j < kPrimReg; ++j) {
         const int f = tid + j * kGbBThreads;
-        if (f < F) prim[f] = cpr[j];
+        if (f < F) {
+          g.cw[f] = 0;
+          g.rl[f] = 0;
+          g.prim[f] = cpr[j];
+        }
       }
     }
     __syncthreads();
@@ -806,36 +835,32 @@ __global__ __launch_bounds__(kGbBThreads) void gb_bucket_dense(
       if (tid == 0) big_list[atomicAdd(big_count, 1)] = (int)b;
     } else {
 #pragma unroll
-      for (int j = 0; j < kGbReg; ++j)
-        if (tid + j * kGbBThreads < n) add((unsigned long long)cur[j]);
-      for (int64_t i = kGbReg * kGbBThreads + tid; i < n; i += kGbBThreads)
-        add((unsigned long long)pb[s0 + i]);
-      __syncthreads();
-      // one wave per file: sums and maximum over the file's seconds
-      for (int f = wv; f < nfl; f += kGbBThreads / 64) {
-        unsigned long long cnt = 0, w = 0, r = 0, lc = 0, mx = 0;
-        for (int sc = lane; sc < S; sc += 64) {
-          const unsigned long long e = grid[(f << p.sbits) | sc];
-          const unsigned long long c1 = e & 0xFFFFull;
-          cnt += c1;
-          w += (e >> 16) & 0xFFFFull;
-          r += (e >> 32) & 0xFFFFull;
-          lc += e >> 48;
-          mx = c1 > mx ? c1 : mx;
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-          cnt += __shfl_xor(cnt, o);
-          w += __shfl_xor(w, o);
-          r += __shfl_xor(r, o);
-          lc += __shfl_xor(lc, o);
-          const unsigned long long m2 = __shfl_xor(mx, o);
-          mx = m2 > mx ? m2 : mx;
-        }
-        if (lane < 6) {
-          const unsigned long long val[6] = {cnt, w, r, lc, cnt, mx};
-          out[(f0 + f) * 6 + lane] = (long long)val[lane];
-        }
+      for (int j = 0; j < kGbReg; ++j) {
+        const bool act = tid + j * kGbBThreads < n;
+        if (__ballot(act) == 0) break;
+        add(act, (unsigned long long)cur[j]);
       }
+      for (int64_t i0 = kGbReg * kGbBThreads; i0 < n; i0 += kGbBThreads) {
+        const int64_t i = i0 + tid;
+        add(i < n, i < n ? (unsigned long long)pb[s0 + i] : 0ull);
+      }
+      __syncthreads();
+      // one wave per file: the maximum count over the file's seconds
+      for (int f = wv; f < nfl; f += kGbBThreads / 64) {
+        const unsigned* row = grid + (((unsigned)f << p.sbits) >> 1);
+        const int words = S >= 2 ? S >> 1 : 1;
+        unsigned mx = 0;
+        for (int w = lane; w < words; w += 64) {
+          const unsigned e = row[w];
+          const unsigned lo = S >= 2 ? (e & 0xFFFFu) : ((f & 1) ? (e >> 16) : (e & 0xFFFFu));
+          const unsigned hi = S >= 2 ? (e >> 16) : 0u;
+          mx = max(mx, max(lo, hi));
+        }
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+        if (lane == 0) g.conc[f] = mx;
+      }
+      __syncthreads();
+      gb_write_files(g, nfl, f0, out);
     }
     __syncthreads();  // the grid is cleared for the next bucket
     s0 = s0n;
@@ -954,7 +979,8 @@ void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, bo
   const size_t files_lds = (size_t)24 << L;
   // persistent grids: exactly the workgroups that stay resident together (a
   // second round of late workgroups would double the tail)
-  const size_t lds_b = dense ? (8u << (L + p.sbits)) + (4u << L) : 8 * kGbSlots + files_lds;
+  const size_t lds_b = dense ? files_lds + ((size_t)4 << std::max(0, L + p.sbits - 1)) + 16
+                             : 8 * kGbSlots + files_lds;
   int per_cu = 0;
   if (dense)
     HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -1260,11 +1260,24 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
                      dim3(256), 0, c.stream, c.labels.as<int32_t>(), c.n, k,
                      reinterpret_cast<unsigned long long*>(cnt_pre));
   HIP_CHECK(hipGetLastError());
-  const int threads = k * (d + 1);
-  hipLaunchKernelGGL(seq_sums_f64, dim3((threads + 63) / 64), dim3(64), 0, c.stream,
-                     c.x64.as<double>(), c.n, c.n_pad, d, k, c.labels.as<int32_t>(), cnt_pre,
-                     c.f64_sums.as<double>(), c.f64_counts.as<long long>());
-  HIP_CHECK(hipGetLastError());
+  if (!getenv("CDR_F64_SERIAL") && f64_sums_parallel(c, k, c.f64_sums.as<double>())) {
+    // f64sum.hip: exact row-order sums in parallel; counts from count_labels
+    HIP_CHECK(hipMemcpyAsync(c.f64_counts.p, cnt_pre, sizeof(long long) * k,
+                             hipMemcpyDeviceToDevice, c.stream));
+    std::vector<long long> w((size_t)k * d);
+    HIP_CHECK(hipMemcpyAsync(w.data(), c.f64x_walk.p, sizeof(long long) * w.size(),
+                             hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    c.f64x_walked = 0;
+    for (long long v : w) c.f64x_walked += v;
+  } else {
+    const int threads = k * (d + 1);
+    hipLaunchKernelGGL(seq_sums_f64, dim3((threads + 63) / 64), dim3(64), 0, c.stream,
+                       c.x64.as<double>(), c.n, c.n_pad, d, k, c.labels.as<int32_t>(), cnt_pre,
+                       c.f64_sums.as<double>(), c.f64_counts.as<long long>());
+    HIP_CHECK(hipGetLastError());
+    c.f64x_walked = -1;
+  }
   HIP_CHECK(hipMemcpyAsync(sums, c.f64_sums.p, sizeof(double) * (size_t)k * d,
                            hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipMemcpyAsync(counts, c.f64_counts.p, sizeof(long long) * k,
@@ -1320,6 +1333,13 @@ int cdr_lloyd_labels(cdr_ctx* h, int64_t* labels) {
   HIP_CHECK(hipMemcpyAsync(labels, tmp.p, sizeof(long long) * c.n, hipMemcpyDeviceToHost,
                            c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
+  CDR_CATCH
+}
+
+int cdr_lloyd_f64_walked(cdr_ctx* h, int64_t* walked) {
+  CDR_TRY
+  if (!h || !walked) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  *walked = h->c.f64x_walked;
   CDR_CATCH
 }
 

@@ -108,6 +108,11 @@ int cdr_lloyd_step(cdr_ctx* ctx, const double* C, int32_t k, int64_t* out,
  * order exactly like X[labels == j].mean(axis=0)'s sum; counts (k).        */
 int cdr_lloyd_step_f64(cdr_ctx* ctx, const double* C, int32_t k, double* sums,
                        int64_t* counts);
+/* F64 mode, d >= 2, k <= 64: the sums are formed in parallel (csrc/f64sum.hip:
+ * per-block parity transfers inside one binade, exact); *walked = blocks of
+ * (cluster, feature) sequences re-added element by element in the last step,
+ * or -1 when the step used the serial kernel.                               */
+int cdr_lloyd_f64_walked(cdr_ctx* ctx, int64_t* walked);
 /* Labels of the last assignment as int64 (np.argmin dtype, :34).           */
 int cdr_lloyd_labels(cdr_ctx* ctx, int64_t* labels);
 /* Diagnostics of the last step: points the fast screen could not certify

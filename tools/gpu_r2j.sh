@@ -1,0 +1,7 @@
+# F64 parallel sums, sharded features on the device, PMC of the group-by.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu tests/test_gpu_f64_update.py tests/test_gpu_features_dist.py > gpurun_out/pytest_r2j.log 2>&1 || { echo PYTEST_FAIL; tail -60 gpurun_out/pytest_r2j.log; exit 2; }
+grep -E "PASSED|FAILED|F64 2M|passed|failed" gpurun_out/pytest_r2j.log | tail -12
+bash tools/gpu_pmc4.sh

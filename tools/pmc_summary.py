@@ -24,7 +24,7 @@ if "--json" in sys.argv:
     json_cfg, json_n = sys.argv[i + 1], int(sys.argv[i + 2])
 agg = collections.defaultdict(dict)
 names = {}
-files = [f for r0 in roots for f in sorted(glob.glob(os.path.join(r0, "*", "*_counter_collection.csv")))]
+files = [f for r0 in roots for f in sorted(glob.glob(os.path.join(r0, "*", "*_counter_collection.csv")) + glob.glob(os.path.join(r0, "*_counter_collection.csv")))]
 for f in files:
     for r in csv.DictReader(open(f)):
         # passes of one command line pair up by dispatch id (same launch order)
