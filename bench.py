@@ -434,6 +434,29 @@ def main() -> None:
     prof = ctx.profile_read()
     st = run.status
     run.finish()
+    scoring_ms = None
+    if args.config == "5":
+        # the config's "+ replica scoring per cluster" (src/main.py:96-107,
+        # src/scoring.py:40-130): medians of every cluster's columns over all
+        # ranks' points, then the category scores, after the timed Lloyd steps
+        from cdr_dist import sharded_medians
+        from scoring import ClusterClassifier
+
+        names = [f"f{i}" for i in range(d)]
+        cats = ("Hot", "Shared", "Moderate", "Archival")
+        clf = ClusterClassifier({nm: 0.5 for nm in names},
+                                {c: {nm: 1.0 for nm in names} for c in cats},
+                                {c: {nm: (1, 1, 0, -1)[i] for nm in names}
+                                 for i, c in enumerate(cats)},
+                                {"Hot": 3, "Shared": 2, "Moderate": 1, "Archival": 4},
+                                context=ctx)
+        comm.barrier()
+        ctx.synchronize()
+        s0 = time.perf_counter()
+        med = sharded_medians(ctx, comm, k)
+        clf.classify_medians(med, names)
+        comm.barrier()
+        scoring_ms = (time.perf_counter() - s0) * 1e3
     if dist is not None:
         import torch
 
@@ -491,6 +514,8 @@ def main() -> None:
         "final_shift": st["shift"],
         "final_inertia": st["inertia"],
     }
+    if scoring_ms is not None:
+        out["replica_scoring_ms"] = scoring_ms
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(d, k, args.seed)
     if rank == 0:

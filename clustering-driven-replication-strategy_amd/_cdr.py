@@ -89,6 +89,11 @@ SIGNATURES = {
     "cdr_features_events_read": ([_P, _P, _P, _P, _P, _P], None),
     "cdr_features_groupby_info": ([_P, _P], None),
     "cdr_lloyd_f64_walked": ([_P, _PI64], None),
+    "cdr_medians_group": ([_P, _I32, _P], None),
+    "cdr_medians_begin": ([_P, _P, ctypes.POINTER(ctypes.c_int32), _PI64], None),
+    "cdr_medians_pass_hist": ([_P, _I32, _P], None),
+    "cdr_medians_pass_select": ([_P, _I32, _P], None),
+    "cdr_medians_finish": ([_P, _P], None),
     "cdr_features_exchange_pack": ([_P, _I32, _P, _P, _P, _PI64], None),
     "cdr_features_exchange_unpack": ([_P, _P, _I64, _I64, _I64], None),
     "cdr_features_load_events": ([_P, _I64, _P, _P, _P, _P, _I64, _P], None),
@@ -397,6 +402,34 @@ class Context:
         d = self.info()["d"]
         out = np.empty((k, d), dtype=np.float64)
         _check(self._lib.cdr_medians_by_label(self._h, int(k), _ptr(out)))
+        return out
+
+    def medians_group(self, k: int) -> np.ndarray:
+        counts = np.zeros(int(k), dtype=np.int64)
+        _check(self._lib.cdr_medians_group(self._h, int(k), _ptr(counts)))
+        self._med_k = int(k)
+        return counts
+
+    def medians_begin(self, global_counts):
+        g = np.ascontiguousarray(global_counts, dtype=np.int64)
+        passes = ctypes.c_int32()
+        words = _I64()
+        _check(self._lib.cdr_medians_begin(self._h, _ptr(g), ctypes.byref(passes),
+                                           ctypes.byref(words)))
+        return int(passes.value), int(words.value)
+
+    def medians_pass_hist(self, p: int, hist) -> None:
+        """hist: a uint32 host array or a device pointer (int)."""
+        _check(self._lib.cdr_medians_pass_hist(self._h, int(p),
+                                               hist if isinstance(hist, int) else _ptr(hist)))
+
+    def medians_pass_select(self, p: int, hist) -> None:
+        _check(self._lib.cdr_medians_pass_select(self._h, int(p),
+                                                 hist if isinstance(hist, int) else _ptr(hist)))
+
+    def medians_finish(self) -> np.ndarray:
+        out = np.empty((self._med_k, self.info()["d"]), dtype=np.float64)
+        _check(self._lib.cdr_medians_finish(self._h, _ptr(out)))
         return out
 
     # -- features --------------------------------------------------------

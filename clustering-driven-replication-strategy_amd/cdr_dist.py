@@ -380,3 +380,36 @@ class ShardedLloyd:
             if shift < tol:
                 break
         return C
+
+
+def sharded_medians(ctx, comm: Comm, k: int) -> np.ndarray:
+    """Per-cluster, per-feature medians (src/scoring.py:50-54, np.median of
+    each cluster's column) of points sharded over the ranks, from the labels
+    of the last Lloyd step: one SUM all-reduce of the cluster sizes, then per
+    radix pass one SUM all-reduce of the k x d x 2 x 256 digit histograms
+    (RCCL on the device buffer under NCCL).  Every rank returns the same
+    (k, d) array, equal to the single-process medians."""
+    local = ctx.medians_group(k)
+    counts = comm.allreduce_i64(local, "sum")
+    passes, words = ctx.medians_begin(counts)
+    if comm.device is not None and comm.dist:
+        import torch
+
+        buf = torch.empty(words, dtype=torch.int32, device=comm.device)
+        handle = buf.data_ptr()
+    else:
+        buf = np.zeros(words, dtype=np.uint32)
+        handle = buf
+    for p in range(passes):
+        ctx.medians_pass_hist(p, handle)
+        if comm.dist:
+            if comm.device is not None:
+                comm.dist.all_reduce(buf)
+            else:
+                import torch
+
+                t = torch.from_numpy(buf.view(np.int32))
+                comm.dist.all_reduce(t)
+        ctx.medians_pass_select(p, handle)
+    return ctx.medians_finish()
+

@@ -197,7 +197,8 @@ struct Ctx {
   int64_t nblocks() const { return (n + kSeedBlock - 1) / kSeedBlock; }
 
   // ---- medians / features scratch ----
-  DevBuf med_vals, med_off, med_out, med_tmp, med_tmp2;
+  DevBuf med_vals, med_off, med_out, med_tmp, med_tmp2, med_hist;
+  int32_t med_k = 0;  // clusters of the grouped rows (cdr_medians_group)
   DevBuf ev_file, ev_op, ev_client, ev_ts, ev_primary, ev_out, ev_scratch,
       ev_scratch2;
   DevBuf ev_part;  // int64 per ts_minmax workgroup: min, max

@@ -70,21 +70,33 @@ __global__ __launch_bounds__(kFB) void f64_blocksum(const double* __restrict__ X
   for (int i = threadIdx.x; i < k; i += kFB) cnt[b * k + i] = c[i];
 }
 
-__global__ void f64_predict(const double* __restrict__ A, const unsigned* __restrict__ cnt,
-                            int64_t nb, int d, int k, int* __restrict__ E) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per (cluster, feature): an exclusive prefix of the approximate
+// block sums, 64 blocks per round (any order is fine: it only predicts).
+__global__ __launch_bounds__(256) void f64_predict(const double* __restrict__ A,
+                                                   const unsigned* __restrict__ cnt, int64_t nb,
+                                                   int d, int k, int* __restrict__ E) {
+  const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   if (t >= k * d) return;
   const int j = t / d;
-  double P = 0.0;
-  for (int64_t b = 0; b < nb; ++b) {
+  double carry = 0.0;
+  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+    const int64_t b = b0 + lane;
+    const double v = (b < nb && cnt[b * k + j]) ? A[b * k * d + t] : 0.0;
+    double inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const double u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    const double P = carry + (inc - v);
     int e = kENone;
     if (P > 0.0 && isfinite(P)) {
       int ex;
       frexp(P, &ex);  // P in [2^(ex-1), 2^ex)
       e = ex - 1;
     }
-    E[b * k * d + t] = e;
-    if (cnt[b * k + j]) P += A[b * k * d + t];
+    if (b < nb) E[b * k * d + t] = e;
+    carry += __shfl(inc, 63);
   }
 }
 
@@ -153,49 +165,80 @@ __global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_
   }
 }
 
-__global__ void f64_walk(const double* __restrict__ X, int64_t n, int64_t n_pad, int d, int k,
-                         int64_t nb, const int32_t* __restrict__ labels,
-                         const unsigned* __restrict__ cnt, const int* __restrict__ E,
-                         const Xfer* __restrict__ T, double* __restrict__ sums,
-                         long long* __restrict__ walked) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per (cluster, feature), the running value uniform across it: the
+// lanes load 64 blocks' (count, prediction, transfer) per round and the wave
+// steps through them (v_readlane); a block that must be re-added is loaded by
+// all lanes (4 rows each) and its members added in row order.
+__global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, int64_t n,
+                                                int64_t n_pad, int d, int k, int64_t nb,
+                                                const int32_t* __restrict__ labels,
+                                                const unsigned* __restrict__ cnt,
+                                                const int* __restrict__ E,
+                                                const Xfer* __restrict__ T,
+                                                double* __restrict__ sums,
+                                                long long* __restrict__ walked) {
+  const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   if (t >= k * d) return;
   const int j = t / d, f = t % d;
   double s = 0.0;
   bool any = false;  // NumPy's reduce starts from the first selected row
   long long nwalk = 0;
-  for (int64_t b = 0; b < nb; ++b) {
-    if (!cnt[b * k + j]) continue;
-    const int64_t at = b * k * d + t;
-    const Xfer x = T[at];
-    const int e = E[at];
-    bool ok = false;
-    if (!(x.flags & 4) && s > 0.0) {
-      int ex;
-      const double fr = frexp(s, &ex);
-      (void)fr;
-      if (ex - 1 == e) {
-        const long long m = (long long)ldexp(s, 52 - e);  // exact: s is on the grid
-        const long long m2 = m + ((m & 1) ? x.d0 + x.dd : x.d0);
-        if (m2 < (1ll << 53)) {
-          s = ldexp((double)m2, e - 52);
-          ok = true;
+  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+    const int64_t bl = b0 + lane;
+    const bool in = bl < nb;
+    const unsigned c = in ? cnt[bl * k + j] : 0u;
+    const int el = in ? E[bl * k * d + t] : kENone;
+    Xfer xl;
+    xl.d0 = 0;
+    xl.dd = 0;
+    xl.flags = 4;
+    if (in && c) xl = T[bl * k * d + t];
+    unsigned long long live = __ballot(c != 0);
+    while (live) {
+      const int i = __ffsll((long long)live) - 1;
+      live &= live - 1;
+      const int64_t b = b0 + i;
+      const int e = __shfl(el, i);
+      const int flags = __shfl(xl.flags, i);
+      const long long d0 = __shfl(xl.d0, i);
+      const int dd = __shfl(xl.dd, i);
+      bool ok = false;
+      if (!(flags & 4) && s > 0.0) {
+        int ex;
+        frexp(s, &ex);
+        if (ex - 1 == e) {
+          const long long m = (long long)ldexp(s, 52 - e);  // exact: s is on the grid
+          const long long m2 = m + ((m & 1) ? d0 + dd : d0);
+          if (m2 < (1ll << 53)) {
+            s = ldexp((double)m2, e - 52);
+            ok = true;
+          }
+        }
+      }
+      if (!ok) {  // element by element, in real fp64 (row order)
+        ++nwalk;
+        const int64_t r0 = b * kFB;
+        for (int q = 0; q < kFB; q += 64) {
+          const int64_t row = r0 + q + lane;
+          const bool mine = row < n && labels[row] == j;
+          const double x = mine ? X[xidx(f, row, n_pad)] : 0.0;
+          unsigned long long m = __ballot(mine);
+          while (m) {
+            const int l = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const double v = __shfl(x, l);
+            s = any ? s + v : v;
+            any = true;
+          }
         }
       }
     }
-    if (!ok) {  // element by element, in real fp64 (row order)
-      ++nwalk;
-      const int64_t r1 = min(n, (b + 1) * kFB);
-      for (int64_t row = b * kFB; row < r1; ++row)
-        if (labels[row] == j) {
-          const double v = X[xidx(f, row, n_pad)];
-          s = any ? s + v : v;
-          any = true;
-        }
-    }
   }
-  sums[(int64_t)j * d + f] = s;
-  walked[t] = nwalk;
+  if (lane == 0) {
+    sums[(int64_t)j * d + f] = s;
+    walked[t] = nwalk;
+  }
 }
 
 }  // namespace
@@ -217,7 +260,7 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
                      c.x64.as<double>(), n, c.n_pad, d, k, c.labels.as<int32_t>(),
                      c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>());
   HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(f64_predict, dim3(ceil_div((int64_t)kd, 64)), dim3(64), 0, c.stream,
+  hipLaunchKernelGGL(f64_predict, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
                      c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), nb, d, k,
                      c.f64x_E.as<int>());
   HIP_CHECK(hipGetLastError());
@@ -227,7 +270,7 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
                      c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
                      c.f64x_E.as<int>(), c.f64x_T.as<Xfer>());
   HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(f64_walk, dim3(ceil_div((int64_t)kd, 64)), dim3(64), 0, c.stream,
+  hipLaunchKernelGGL(f64_walk, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
                      c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
                      c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(), d_sums,
                      c.f64x_walk.as<long long>());

@@ -9,6 +9,7 @@
 // workgroup per segment: each pass histograms (in LDS) the 8-bit digit of the
 // elements that still match the prefix found so far, for both target ranks.
 // 64-bit keys (fp64 values) take 8 passes, 32-bit keys (F32X points) take 4.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -132,40 +133,210 @@ __global__ __launch_bounds__(256) void seg_median_kernel(const V* __restrict__ v
   }
 }
 
-// Group the points of an F32X/F64 shard by label: counts, offsets, scatter.
-__global__ void label_hist(const int32_t* __restrict__ labels, int64_t n,
-                           unsigned long long* __restrict__ cnt) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&cnt[labels[i]], 1ull);
+// ---- medians of the resident points grouped by label (main.py:96-107) ----
+// The rows of each cluster are gathered once into a point-major copy (a
+// two-pass counting sort: per-block LDS label counts, a column scan for the
+// block offsets, a scatter with LDS ranks: no global cursor atomics), then
+// every (cluster, feature) pair is selected by an MSB radix select over
+// order-preserving keys, 8 bits per pass, for both middle ranks at once: one
+// workgroup per cluster and 64-feature chunk histograms its rows in LDS
+// ([64][2][256] counters), the histograms go to global memory (where a
+// sharded run all-reduces them), and one thread per pair
+// picks the next digit of each rank.  Ranks are of the global cluster sizes.
+constexpr int kMgBlock = 4096;   // points per counting-sort block
+constexpr int kMgRange = 64;     // blocks per column-scan range
+constexpr int kMgMaxK = 8192;
+constexpr int kMgFeat = 64;      // features per histogram workgroup
+
+__global__ __launch_bounds__(256) void mg_count(const int32_t* __restrict__ labels, int64_t n,
+                                                int k, unsigned* __restrict__ cnt) {
+  extern __shared__ unsigned hc[];
+  for (int j = threadIdx.x; j < k; j += 256) hc[j] = 0;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kMgBlock;
+  for (int i = threadIdx.x; i < kMgBlock; i += 256)
+    if (i0 + i < n) atomicAdd(&hc[labels[i0 + i]], 1u);
+  __syncthreads();
+  for (int j = threadIdx.x; j < k; j += 256) cnt[(int64_t)blockIdx.x * k + j] = hc[j];
+}
+
+// column scan of cnt [nblk][k]: a) range sums, b) range bases + label totals
+// and bases (one workgroup), c) absolute block offsets in place
+__global__ __launch_bounds__(256) void mg_scan_a(const unsigned* __restrict__ cnt, int64_t nblk,
+                                                 int k, unsigned long long* __restrict__ rsum) {
+  const int64_t r0 = (int64_t)blockIdx.x * kMgRange;
+  for (int j = threadIdx.x; j < k; j += 256) {
+    unsigned long long s = 0;
+    for (int r = 0; r < kMgRange && r0 + r < nblk; ++r) s += cnt[(r0 + r) * k + j];
+    rsum[(int64_t)blockIdx.x * k + j] = s;
+  }
+}
+
+__global__ __launch_bounds__(1024) void mg_scan_b(unsigned long long* __restrict__ rsum,
+                                                  int64_t nr, int k,
+                                                  long long* __restrict__ base,
+                                                  long long* __restrict__ total) {
+  __shared__ long long wsum[16];
+  __shared__ long long carry;
+  for (int j = threadIdx.x; j < k; j += 1024) {
+    unsigned long long run = 0;
+    for (int64_t r = 0; r < nr; ++r) {
+      const unsigned long long v = rsum[r * k + j];
+      rsum[r * k + j] = run;
+      run += v;
+    }
+    total[j] = (long long)run;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int j0 = 0; j0 < k; j0 += 1024) {
+    const int j = j0 + threadIdx.x;
+    const long long v = j < k ? total[j] : 0;
+    long long inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    long long pre = carry;
+    for (int q = 0; q < w; ++q) pre += wsum[q];
+    if (j < k) base[j] = pre + inc - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = pre + inc;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void mg_scan_c(unsigned* __restrict__ cnt, int64_t nblk, int k,
+                                                 const unsigned long long* __restrict__ rbase,
+                                                 const long long* __restrict__ base) {
+  const int64_t r0 = (int64_t)blockIdx.x * kMgRange;
+  for (int j = threadIdx.x; j < k; j += 256) {
+    unsigned long long run = (unsigned long long)base[j] + rbase[(int64_t)blockIdx.x * k + j];
+    for (int r = 0; r < kMgRange && r0 + r < nblk; ++r) {
+      const unsigned v = cnt[(r0 + r) * k + j];
+      cnt[(r0 + r) * k + j] = (unsigned)run;
+      run += v;
+    }
+  }
 }
 
 template <typename V>
-__global__ void scatter_by_label(const V* __restrict__ X, int64_t n, int64_t n_pad, int d,
-                                 const int32_t* __restrict__ labels, int k,
-                                 unsigned long long* __restrict__ cursor,
-                                 const int64_t* __restrict__ seg_off, V* __restrict__ dst) {
-  // dst layout: feature-major segments: segment (f, j) = dst[f * n + off[j] ..]
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int j = labels[i];
-    const unsigned long long pos = atomicAdd(&cursor[j], 1ull);
-    for (int f = 0; f < d; ++f) dst[(int64_t)f * n + seg_off[j] + (int64_t)pos] = X[xidx(f, i, n_pad)];
+__global__ __launch_bounds__(256) void mg_scatter(const V* __restrict__ X, int64_t n,
+                                                  int64_t n_pad, int d,
+                                                  const int32_t* __restrict__ labels, int k,
+                                                  const unsigned* __restrict__ off,
+                                                  V* __restrict__ rows) {
+  extern __shared__ unsigned cur[];
+  for (int j = threadIdx.x; j < k; j += 256) cur[j] = off[(int64_t)blockIdx.x * k + j];
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kMgBlock;
+  for (int i = threadIdx.x; i < kMgBlock; i += 256) {
+    const int64_t pt = i0 + i;
+    if (pt >= n) break;
+    const unsigned pos = atomicAdd(&cur[labels[pt]], 1u);
+    V* dst = rows + (int64_t)pos * d;
+    for (int f = 0; f < d; ++f) dst[f] = X[xidx(f, pt, n_pad)];
   }
 }
 
-__global__ void make_feature_offsets(const int64_t* __restrict__ seg_off, int k, int d, int64_t n,
-                                     int64_t* __restrict__ off2) {
-  // segment order (j, f) -> out index j*d + f; values live at f*n + seg_off[j]
-  // we emit offsets per (f, j) in f-major order: off2[f*k + j] .. + count
+// Pass p (digit shift sh) for cluster j = blockIdx.x, features [f0, f0 + 64):
+// counts of the digit among the rows whose key matches each rank's prefix.
+// Both ranks share one histogram while their prefixes are equal (flag in
+// two[]), as the selection step reads it.
+template <typename V>
+__global__ __launch_bounds__(256) void mg_hist(const V* __restrict__ rows, int d, int k,
+                                               const long long* __restrict__ base,
+                                               const long long* __restrict__ cnt_local,
+                                               const unsigned long long* __restrict__ pref,
+                                               int sh, unsigned* __restrict__ H) {
+  typedef typename KeyOf<V>::K K;
+  __shared__ unsigned h[kMgFeat][2][256];
+  __shared__ K sp[kMgFeat][2];
+  const int j = blockIdx.x;
+  const int f0 = blockIdx.y * kMgFeat;
+  const int nfc = min(kMgFeat, d - f0);
+  for (int i = threadIdx.x; i < kMgFeat * 512; i += 256) (&h[0][0][0])[i] = 0;
+  for (int i = threadIdx.x; i < 2 * nfc; i += 256)
+    sp[i >> 1][i & 1] = (K)pref[((int64_t)j * d + f0) * 2 + i];
+  __syncthreads();
+  const K mask = sh + 8 >= KeyOf<V>::BITS ? (K)0 : (K)(~(K)0 << (sh + 8));
+  const int64_t lo = base[j], m = cnt_local[j];
+  for (int64_t r = threadIdx.x; r < m; r += 256) {
+    const V* row = rows + (lo + r) * d + f0;
+    for (int f = 0; f < nfc; ++f) {
+      const K key = KeyOf<V>::key(row[f]);
+      const unsigned dig = (unsigned)((key >> sh) & 0xFF);
+      const K p0 = sp[f][0], p1 = sp[f][1];
+      if ((key & mask) == p0) atomicAdd(&h[f][0][dig], 1u);
+      if (p1 != p0 && (key & mask) == p1) atomicAdd(&h[f][1][dig], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nfc * 512; i += 256)
+    H[((int64_t)j * d + f0) * 512 + i] = (&h[0][0][0])[i];
+}
+
+// One thread per (cluster, feature): the next digit of both ranks.
+template <typename V>
+__global__ void mg_select(const unsigned* __restrict__ H, int d, int k,
+                          const long long* __restrict__ cnt_global, int sh,
+                          unsigned long long* __restrict__ pref, long long* __restrict__ rank) {
+  typedef typename KeyOf<V>::K K;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > k * d) return;
-  if (t == k * d) {
-    off2[t] = (int64_t)d * n;
+  if (t >= k * d) return;
+  if (cnt_global[t / d] <= 0) return;
+  const K p0 = (K)pref[2 * t], p1 = (K)pref[2 * t + 1];
+  const bool two = p0 != p1;
+  for (int w = 0; w < 2; ++w) {
+    const unsigned* hist = H + (int64_t)t * 512 + ((w == 1 && two) ? 256 : 0);
+    long long r = rank[2 * t + w];
+    unsigned dsel = 255;
+    for (unsigned g = 0; g < 256; ++g) {
+      const long long c = hist[g];
+      if (r < c) {
+        dsel = g;
+        break;
+      }
+      r -= c;
+    }
+    rank[2 * t + w] = r;
+    pref[2 * t + w] = (unsigned long long)((w == 0 ? p0 : p1) | ((K)dsel << sh));
+  }
+}
+
+template <typename V>
+__global__ void mg_finish(const long long* __restrict__ cnt_global, int d, int k,
+                          const unsigned long long* __restrict__ pref, double* __restrict__ out) {
+  typedef typename KeyOf<V>::K K;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= k * d) return;
+  const long long m = cnt_global[t / d];
+  if (m <= 0) {
+    out[t] = NAN;
     return;
   }
-  const int f = t / k, j = t % k;
-  off2[t] = (int64_t)f * n + seg_off[j];
+  const double a = KeyOf<V>::val((K)pref[2 * t]);
+  if (m & 1) {
+    out[t] = (0.0 + a) / 1.0;
+  } else {
+    const double b = KeyOf<V>::val((K)pref[2 * t + 1]);
+    out[t] = ((0.0 + a) + b) / 2.0;
+  }
+}
+
+__global__ void mg_begin(const long long* __restrict__ cnt_global, int d, int k,
+                         unsigned long long* __restrict__ pref, long long* __restrict__ rank) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= k * d) return;
+  const long long m = cnt_global[t / d];
+  pref[2 * t] = 0;
+  pref[2 * t + 1] = 0;
+  rank[2 * t] = m > 0 ? (m - 1) / 2 : 0;
+  rank[2 * t + 1] = m > 0 ? m / 2 : 0;
 }
 
 static int grid_cap(int64_t work, int threads, int cap) {
@@ -202,62 +373,147 @@ void medians_segmented(Ctx& c, const double* values, const int64_t* offsets, int
   HIP_CHECK(hipStreamSynchronize(c.stream));
 }
 
-void medians_by_label(Ctx& c, int32_t k, double* out) {
+// ---- host side of the label medians (single shard or one rank of several) --
+static int mg_passes(const Ctx& c) { return c.mode == CDR_MODE_F32X ? 4 : 8; }
+
+void medians_group(Ctx& c, int32_t k, int64_t* counts) {
   if (!c.have_labels) CDR_FAIL(CDR_ERR_STATE, "no Lloyd labels: run cdr_lloyd_step first");
   if (k < 1 || k < c.last_k) CDR_FAIL(CDR_ERR_ARG, "k smaller than the labels' k");
+  if (k > kMgMaxK) CDR_FAIL(CDR_ERR_UNSUPPORTED, "medians: k > 8192");
   const int d = c.d;
   const int64_t n = c.n;
+  if (n >= (1ll << 32)) CDR_FAIL(CDR_ERR_UNSUPPORTED, "medians: 2^32 points or more per shard");
   const bool f32 = c.mode == CDR_MODE_F32X;
   const size_t vsz = f32 ? 4 : 8;
-  c.med_tmp.ensure(sizeof(unsigned long long) * k * 2);
-  unsigned long long* cnt = c.med_tmp.as<unsigned long long>();
-  HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * k * 2, c.stream));
-  hipLaunchKernelGGL(label_hist, dim3(grid_cap(n, 256, 4096)), dim3(256), 0, c.stream,
-                     c.labels.as<int32_t>(), n, cnt);
+  const int64_t nblk = std::max<int64_t>(1, ceil_div(n, kMgBlock));
+  const int64_t nr = ceil_div(nblk, kMgRange);
+  c.med_tmp.ensure(sizeof(unsigned) * (size_t)nblk * k);
+  c.med_tmp2.ensure(sizeof(unsigned long long) * (size_t)nr * k);
+  c.med_off.ensure(sizeof(long long) * 2 * (size_t)k);
+  unsigned* cnt = c.med_tmp.as<unsigned>();
+  long long* base = c.med_off.as<long long>();
+  long long* total = base + k;
+  const size_t lds = sizeof(unsigned) * k;
+  hipLaunchKernelGGL(mg_count, dim3(nblk), dim3(256), lds, c.stream, c.labels.as<int32_t>(), n,
+                     k, cnt);
+  hipLaunchKernelGGL(mg_scan_a, dim3(nr), dim3(256), 0, c.stream, cnt, nblk, k,
+                     c.med_tmp2.as<unsigned long long>());
+  hipLaunchKernelGGL(mg_scan_b, dim3(1), dim3(1024), 0, c.stream,
+                     c.med_tmp2.as<unsigned long long>(), nr, k, base, total);
+  hipLaunchKernelGGL(mg_scan_c, dim3(nr), dim3(256), 0, c.stream, cnt, nblk, k,
+                     c.med_tmp2.as<unsigned long long>(), base);
   HIP_CHECK(hipGetLastError());
-  std::vector<unsigned long long> hc(k);
-  HIP_CHECK(hipMemcpyAsync(hc.data(), cnt, sizeof(unsigned long long) * k,
-                           hipMemcpyDeviceToHost, c.stream));
-  HIP_CHECK(hipStreamSynchronize(c.stream));
-  std::vector<int64_t> seg(k + 1, 0);
-  for (int j = 0; j < k; ++j) seg[j + 1] = seg[j] + (int64_t)hc[j];
-  c.med_off.ensure(sizeof(int64_t) * ((size_t)k * d + 1 + k + 1));
-  int64_t* dseg = c.med_off.as<int64_t>() + (size_t)k * d + 1;
-  HIP_CHECK(hipMemcpyAsync(dseg, seg.data(), sizeof(int64_t) * (k + 1), hipMemcpyHostToDevice,
-                           c.stream));
   c.med_vals.ensure(vsz * (size_t)d * (n > 0 ? n : 1));
-  unsigned long long* cursor = cnt + k;
   if (n > 0) {
     if (f32)
-      hipLaunchKernelGGL(scatter_by_label<float>, dim3(grid_cap(n, 256, 4096)), dim3(256), 0,
-                         c.stream, c.x32.as<float>(), n, c.n_pad, d, c.labels.as<int32_t>(), k,
-                         cursor, dseg, c.med_vals.as<float>());
+      hipLaunchKernelGGL(mg_scatter<float>, dim3(nblk), dim3(256), lds, c.stream,
+                         c.x32.as<float>(), n, c.n_pad, d, c.labels.as<int32_t>(), k, cnt,
+                         c.med_vals.as<float>());
     else
-      hipLaunchKernelGGL(scatter_by_label<double>, dim3(grid_cap(n, 256, 4096)), dim3(256), 0,
-                         c.stream, c.x64.as<double>(), n, c.n_pad, d, c.labels.as<int32_t>(),
-                         k, cursor, dseg, c.med_vals.as<double>());
+      hipLaunchKernelGGL(mg_scatter<double>, dim3(nblk), dim3(256), lds, c.stream,
+                         c.x64.as<double>(), n, c.n_pad, d, c.labels.as<int32_t>(), k, cnt,
+                         c.med_vals.as<double>());
     HIP_CHECK(hipGetLastError());
   }
-  int64_t* off2 = c.med_off.as<int64_t>();
-  hipLaunchKernelGGL(make_feature_offsets, dim3((k * d + 256) / 256), dim3(256), 0, c.stream,
-                     dseg, k, d, n, off2);
-  HIP_CHECK(hipGetLastError());
-  // (f, j) segments are contiguous in f-major order; compute them all.
-  const int64_t nseg = (int64_t)k * d;
-  c.med_out.ensure(sizeof(double) * nseg);
-  if (f32)
-    hipLaunchKernelGGL(seg_median_kernel<float>, dim3(grid_cap(nseg, 1, 65536)), dim3(256), 0,
-                       c.stream, c.med_vals.as<float>(), off2, nseg, c.med_out.as<double>());
-  else
-    hipLaunchKernelGGL(seg_median_kernel<double>, dim3(grid_cap(nseg, 1, 65536)), dim3(256), 0,
-                       c.stream, c.med_vals.as<double>(), off2, nseg, c.med_out.as<double>());
-  HIP_CHECK(hipGetLastError());
-  std::vector<double> fm(nseg);
-  HIP_CHECK(hipMemcpyAsync(fm.data(), c.med_out.p, sizeof(double) * nseg, hipMemcpyDeviceToHost,
+  HIP_CHECK(hipMemcpyAsync(counts, total, sizeof(long long) * k, hipMemcpyDeviceToHost,
                            c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.med_k = k;
+}
+
+int medians_begin(Ctx& c, const int64_t* global_counts) {
+  const int k = c.med_k, d = c.d;
+  if (k <= 0) CDR_FAIL(CDR_ERR_STATE, "medians: group the rows first (cdr_medians_group)");
   for (int j = 0; j < k; ++j)
-    for (int f = 0; f < d; ++f) out[(size_t)j * d + f] = fm[(size_t)f * k + j];
+    if (global_counts[j] >= (1ll << 32))
+      CDR_FAIL(CDR_ERR_UNSUPPORTED, "medians: a cluster of 2^32 points or more");
+  const size_t kd = (size_t)k * d;
+  c.med_out.ensure(sizeof(long long) * k + sizeof(unsigned long long) * 2 * kd +
+                   sizeof(long long) * 2 * kd + sizeof(double) * kd);
+  long long* gcnt = c.med_out.as<long long>();
+  unsigned long long* pref = reinterpret_cast<unsigned long long*>(gcnt + k);
+  long long* rank = reinterpret_cast<long long*>(pref + 2 * kd);
+  HIP_CHECK(hipMemcpyAsync(gcnt, global_counts, sizeof(long long) * k, hipMemcpyHostToDevice,
+                           c.stream));
+  hipLaunchKernelGGL(mg_begin, dim3(ceil_div((int64_t)kd, 256)), dim3(256), 0, c.stream, gcnt, d,
+                     k, pref, rank);
+  HIP_CHECK(hipGetLastError());
+  c.med_hist.ensure(sizeof(unsigned) * 512 * kd);
+  return mg_passes(c);
+}
+
+// hist: where the pass's histograms go ([k][d][2][256] u32; host or device
+// memory; nullptr = leave them in the context for the select step)
+void medians_pass_hist(Ctx& c, int pass, void* hist) {
+  const int k = c.med_k, d = c.d, P = mg_passes(c);
+  if (pass < 0 || pass >= P) CDR_FAIL(CDR_ERR_ARG, "medians: pass out of range");
+  const size_t kd = (size_t)k * d;
+  long long* gcnt = c.med_out.as<long long>();
+  unsigned long long* pref = reinterpret_cast<unsigned long long*>(gcnt + k);
+  const int sh = (P - 1 - pass) * 8;
+  const long long* base = c.med_off.as<long long>();
+  const long long* total = base + k;
+  dim3 grid(k, (unsigned)ceil_div(d, kMgFeat));
+  if (c.mode == CDR_MODE_F32X)
+    hipLaunchKernelGGL(mg_hist<float>, grid, dim3(256), 0, c.stream, c.med_vals.as<float>(), d, k,
+                       base, total, pref, sh, c.med_hist.as<unsigned>());
+  else
+    hipLaunchKernelGGL(mg_hist<double>, grid, dim3(256), 0, c.stream, c.med_vals.as<double>(), d,
+                       k, base, total, pref, sh, c.med_hist.as<unsigned>());
+  HIP_CHECK(hipGetLastError());
+  if (hist) {
+    HIP_CHECK(hipMemcpyAsync(hist, c.med_hist.p, sizeof(unsigned) * 512 * kd, hipMemcpyDefault,
+                             c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+  }
+}
+
+void medians_pass_select(Ctx& c, int pass, const void* hist) {
+  const int k = c.med_k, d = c.d, P = mg_passes(c);
+  if (pass < 0 || pass >= P) CDR_FAIL(CDR_ERR_ARG, "medians: pass out of range");
+  const size_t kd = (size_t)k * d;
+  long long* gcnt = c.med_out.as<long long>();
+  unsigned long long* pref = reinterpret_cast<unsigned long long*>(gcnt + k);
+  long long* rank = reinterpret_cast<long long*>(pref + 2 * kd);
+  if (hist)
+    HIP_CHECK(hipMemcpyAsync(c.med_hist.p, hist, sizeof(unsigned) * 512 * kd, hipMemcpyDefault,
+                             c.stream));
+  const int sh = (P - 1 - pass) * 8;
+  if (c.mode == CDR_MODE_F32X)
+    hipLaunchKernelGGL(mg_select<float>, dim3(ceil_div((int64_t)kd, 256)), dim3(256), 0, c.stream,
+                       c.med_hist.as<unsigned>(), d, k, gcnt, sh, pref, rank);
+  else
+    hipLaunchKernelGGL(mg_select<double>, dim3(ceil_div((int64_t)kd, 256)), dim3(256), 0,
+                       c.stream, c.med_hist.as<unsigned>(), d, k, gcnt, sh, pref, rank);
+  HIP_CHECK(hipGetLastError());
+}
+
+void medians_finish(Ctx& c, double* out) {
+  const int k = c.med_k, d = c.d;
+  const size_t kd = (size_t)k * d;
+  long long* gcnt = c.med_out.as<long long>();
+  unsigned long long* pref = reinterpret_cast<unsigned long long*>(gcnt + k);
+  double* res = reinterpret_cast<double*>(reinterpret_cast<long long*>(pref + 2 * kd) + 2 * kd);
+  if (c.mode == CDR_MODE_F32X)
+    hipLaunchKernelGGL(mg_finish<float>, dim3(ceil_div((int64_t)kd, 256)), dim3(256), 0, c.stream,
+                       gcnt, d, k, pref, res);
+  else
+    hipLaunchKernelGGL(mg_finish<double>, dim3(ceil_div((int64_t)kd, 256)), dim3(256), 0,
+                       c.stream, gcnt, d, k, pref, res);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpyAsync(out, res, sizeof(double) * kd, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+void medians_by_label(Ctx& c, int32_t k, double* out) {
+  std::vector<int64_t> counts(k);
+  medians_group(c, k, counts.data());
+  const int P = medians_begin(c, counts.data());
+  for (int p = 0; p < P; ++p) {
+    medians_pass_hist(c, p, nullptr);
+    medians_pass_select(c, p, nullptr);
+  }
+  medians_finish(c, out);
 }
 
 }  // namespace cdr
@@ -272,6 +528,48 @@ int cdr_medians_segmented(cdr_ctx* h, const double* values, const int64_t* offse
   if (!h || !offsets || (n_segments > 0 && !out)) CDR_FAIL(CDR_ERR_ARG, "null argument");
   HIP_CHECK(hipSetDevice(h->c.device));
   medians_segmented(h->c, values, offsets, n_segments, out);
+  CDR_CATCH
+}
+
+int cdr_medians_group(cdr_ctx* h, int32_t k, int64_t* counts) {
+  CDR_TRY
+  if (!h || !counts) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  medians_group(h->c, k, counts);
+  CDR_CATCH
+}
+
+int cdr_medians_begin(cdr_ctx* h, const int64_t* global_counts, int32_t* passes,
+                      int64_t* hist_words) {
+  CDR_TRY
+  if (!h || !global_counts || !passes || !hist_words) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  *passes = medians_begin(h->c, global_counts);
+  *hist_words = (int64_t)h->c.med_k * h->c.d * 512;
+  CDR_CATCH
+}
+
+int cdr_medians_pass_hist(cdr_ctx* h, int32_t pass, void* hist) {
+  CDR_TRY
+  if (!h || !hist) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  medians_pass_hist(h->c, pass, hist);
+  CDR_CATCH
+}
+
+int cdr_medians_pass_select(cdr_ctx* h, int32_t pass, const void* hist) {
+  CDR_TRY
+  if (!h || !hist) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  medians_pass_select(h->c, pass, hist);
+  CDR_CATCH
+}
+
+int cdr_medians_finish(cdr_ctx* h, double* out) {
+  CDR_TRY
+  if (!h || !out) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  medians_finish(h->c, out);
   CDR_CATCH
 }
 

@@ -122,17 +122,31 @@ class ClusterClassifier:
         return {cname: self.classify_cluster(m) for cname, m in medians.items()}
 
     # -- array-native extension ------------------------------------------
-    def classify_labels(self, k, feature_names, *, prefix="C", context: Context | None = None):
+    def classify_labels(self, k, feature_names, *, prefix="C", context: Context | None = None,
+                        comm=None):
         """Classify clusters 0..k-1 from the labels of the last Lloyd step on
         ``context`` (default: the process context ``kmeans`` used).  Same
         result as building ``{f"C{i}": {feature: list}}`` as src/main.py:96-102
-        does and calling ``classify``; medians are computed on the device."""
+        does and calling ``classify``; medians are computed on the device.
+        With ``comm`` (cdr_dist.Comm over several ranks, each holding a shard
+        of the points) the medians are those of the whole point set
+        (cdr_dist.sharded_medians)."""
         ctx = context if context is not None else self._ctx()
-        med = ctx.medians_by_label(int(k))
+        if comm is not None and comm.world > 1:
+            from cdr_dist import sharded_medians
+
+            med = sharded_medians(ctx, comm, int(k))
+        else:
+            med = ctx.medians_by_label(int(k))
+        return self.classify_medians(med, feature_names, prefix=prefix)
+
+    def classify_medians(self, med, feature_names, *, prefix="C"):
+        """{prefix + j: category} from a (k, d) array of cluster medians."""
+        med = np.asarray(med, dtype=np.float64)
         if med.shape[1] != len(feature_names):
             raise ValueError("feature_names must name every column of X")
         out = {}
-        for j in range(int(k)):
+        for j in range(med.shape[0]):
             cm = {name: np.float64(med[j, i]) for i, name in enumerate(feature_names)}
             if any(np.isnan(v) for v in cm.values()):
                 _warn_empty_median()

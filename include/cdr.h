@@ -181,6 +181,21 @@ int cdr_medians_segmented(cdr_ctx* ctx, const double* values,
 /* Array-native form: median of every feature of the local
  * points grouped by the labels of the last Lloyd step; out (k, d).          */
 int cdr_medians_by_label(cdr_ctx* ctx, int32_t k, double* out);
+/* The same in steps, for points sharded over ranks:
+ * cdr_medians_group groups this shard's rows by label (counts[k] = local
+ * cluster sizes); after a SUM all-reduce of the counts, cdr_medians_begin
+ * takes the global sizes and returns the number of radix passes (4 for F32X
+ * points, 8 for F64) and the histogram size in uint32 words (k * d * 512);
+ * per pass, cdr_medians_pass_hist writes this shard's digit histograms to
+ * `hist` (host or device memory), the caller SUM-all-reduces them, and
+ * cdr_medians_pass_select consumes the global histograms; cdr_medians_finish
+ * writes out (k, d).  Every rank gets the medians of the whole data set.    */
+int cdr_medians_group(cdr_ctx* ctx, int32_t k, int64_t* counts);
+int cdr_medians_begin(cdr_ctx* ctx, const int64_t* global_counts, int32_t* passes,
+                      int64_t* hist_words);
+int cdr_medians_pass_hist(cdr_ctx* ctx, int32_t pass, void* hist);
+int cdr_medians_pass_select(cdr_ctx* ctx, int32_t pass, const void* hist);
+int cdr_medians_finish(cdr_ctx* ctx, double* out);
 
 /* ---- access-log group-by: src/compute_features.py:31-54 ---------------- */
 /* Events: file index (row of the manifest, -1 = path not in the manifest),

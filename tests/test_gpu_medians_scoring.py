@@ -83,3 +83,81 @@ def test_medians_by_label_matches_list_path(ctx):
     lists = {f"C{j}": {nm: X[lab == j, i].tolist() for i, nm in enumerate(names)}
              for j in range(k)}
     assert a == clf.classify(lists)
+
+
+def _label_medians(X, lab, k):
+    out = np.full((k, X.shape[1]), np.nan)
+    for j in range(k):
+        m = lab == j
+        if m.any():
+            out[j] = np.median(X[m], axis=0)
+    return out
+
+
+@pytest.mark.parametrize("mode", ["f32x", "f64"])
+def test_medians_by_label_shapes(ctx, mode):
+    """k = 40 with empty clusters, d = 70 (two 64-feature chunks), repeated
+    values, negatives and signed zeros; F32X and F64 points."""
+    rng = np.random.default_rng(5 if mode == "f32x" else 6)
+    n, d, k = 40_000, 70, 40
+    if mode == "f32x":
+        X = np.round(rng.normal(0, 4, (n, d)) * 64) / 64  # a 2^-6 grid
+    else:
+        X = rng.normal(0, 4, (n, d)) * np.pi
+    X[::7, 3] = X[0, 3]          # many ties in one column
+    X[::11, 5] = -0.0
+    X[1::11, 5] = 0.0
+    ctx.load_points(X)
+    assert ctx.info()["mode"] == (1 if mode == "f32x" else 2)
+    C = X[rng.choice(n, k, replace=False)].copy()
+    C[-5:] = 1e6                  # empty clusters
+    if mode == "f32x":
+        ctx.lloyd_step(C)
+    else:
+        ctx.lloyd_step_f64(C)
+    lab = ctx.labels()
+    got = ctx.medians_by_label(k)
+    exp = _label_medians(X, lab, k)
+    np.testing.assert_array_equal(got, exp)
+    assert np.isnan(got[-1]).all()
+
+
+def _med_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    from _cdr import Context
+    from cdr_dist import Comm, sharded_medians
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X = np.load(os.path.join(out_dir, "X.npy"))
+    C = np.load(os.path.join(out_dir, "C.npy"))
+    lo, hi = (X.shape[0] * rank) // world, (X.shape[0] * (rank + 1)) // world
+    ctx = Context(0)
+    ctx.load_points(X[lo:hi])
+    ctx.lloyd_step(C)
+    med = sharded_medians(ctx, Comm(dist, None), C.shape[0])
+    np.save(os.path.join(out_dir, f"med{rank}.npy"), med)
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_medians_two_ranks(ctx, tmp_path):
+    """Two processes on the one GPU, gloo collectives: every rank's medians
+    equal the single-process medians of the whole point set (e4)."""
+    from test_features_dist import _free_port
+
+    mp = pytest.importorskip("torch.multiprocessing")
+    rng = np.random.default_rng(9)
+    X = np.round(rng.normal(0, 3, (60_001, 6)) * 256) / 256
+    C = X[rng.choice(X.shape[0], 12, replace=False)].copy()
+    np.save(tmp_path / "X.npy", X)
+    np.save(tmp_path / "C.npy", C)
+    mp.spawn(_med_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    ctx.load_points(X)
+    ctx.lloyd_step(C)
+    single = ctx.medians_by_label(12)
+    np.testing.assert_array_equal(single, _label_medians(X, ctx.labels(), 12))
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"med{r}.npy"), single)
