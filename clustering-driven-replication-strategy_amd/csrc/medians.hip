@@ -224,6 +224,9 @@ __global__ __launch_bounds__(256) void mg_scan_c(unsigned* __restrict__ cnt, int
   }
 }
 
+// Ranks first (one thread per point, LDS cursors), then the rows copied with
+// the lanes of a wave over (point, feature): each point's row is written as
+// one contiguous run.
 template <typename V>
 __global__ __launch_bounds__(256) void mg_scatter(const V* __restrict__ X, int64_t n,
                                                   int64_t n_pad, int d,
@@ -231,15 +234,23 @@ __global__ __launch_bounds__(256) void mg_scatter(const V* __restrict__ X, int64
                                                   const unsigned* __restrict__ off,
                                                   V* __restrict__ rows) {
   extern __shared__ unsigned cur[];
+  __shared__ unsigned pos[kMgBlock];
   for (int j = threadIdx.x; j < k; j += 256) cur[j] = off[(int64_t)blockIdx.x * k + j];
   __syncthreads();
   const int64_t i0 = (int64_t)blockIdx.x * kMgBlock;
-  for (int i = threadIdx.x; i < kMgBlock; i += 256) {
-    const int64_t pt = i0 + i;
-    if (pt >= n) break;
-    const unsigned pos = atomicAdd(&cur[labels[pt]], 1u);
-    V* dst = rows + (int64_t)pos * d;
-    for (int f = 0; f < d; ++f) dst[f] = X[xidx(f, pt, n_pad)];
+  const int np = (int)min((int64_t)kMgBlock, n - i0);
+  for (int i = threadIdx.x; i < np; i += 256) pos[i] = atomicAdd(&cur[labels[i0 + i]], 1u);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int D2 = 1;
+  while (D2 < d && D2 < 64) D2 <<= 1;
+  const int rpw = 64 / D2;                    // points per wave step
+  const int sub = lane / D2, fl = lane % D2;
+  for (int p0 = w * rpw; p0 < np; p0 += 4 * rpw) {
+    const int pi = p0 + sub;
+    if (pi >= np) continue;
+    V* dst = rows + (int64_t)pos[pi] * d;
+    for (int f = fl; f < d; f += D2) dst[f] = X[xidx(f, i0 + pi, n_pad)];
   }
 }
 
@@ -254,30 +265,43 @@ __global__ __launch_bounds__(256) void mg_hist(const V* __restrict__ rows, int d
                                                const unsigned long long* __restrict__ pref,
                                                int sh, unsigned* __restrict__ H) {
   typedef typename KeyOf<V>::K K;
-  __shared__ unsigned h[kMgFeat][2][256];
+  // counters of feature f, rank t, digit g at f * kMgHs + t * 257 + g: the
+  // odd strides put the lanes of a wave (different features, often the same
+  // digit) in different banks
+  constexpr int kMgHs = 515;
+  __shared__ unsigned h[kMgFeat * kMgHs];
   __shared__ K sp[kMgFeat][2];
   const int j = blockIdx.x;
   const int f0 = blockIdx.y * kMgFeat;
   const int nfc = min(kMgFeat, d - f0);
-  for (int i = threadIdx.x; i < kMgFeat * 512; i += 256) (&h[0][0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kMgFeat * kMgHs; i += 256) h[i] = 0;
   for (int i = threadIdx.x; i < 2 * nfc; i += 256)
     sp[i >> 1][i & 1] = (K)pref[((int64_t)j * d + f0) * 2 + i];
   __syncthreads();
   const K mask = sh + 8 >= KeyOf<V>::BITS ? (K)0 : (K)(~(K)0 << (sh + 8));
   const int64_t lo = base[j], m = cnt_local[j];
-  for (int64_t r = threadIdx.x; r < m; r += 256) {
-    const V* row = rows + (lo + r) * d + f0;
-    for (int f = 0; f < nfc; ++f) {
-      const K key = KeyOf<V>::key(row[f]);
+  // lanes over (row, feature): a wave reads whole rows (contiguous) and, for
+  // d >= 64, its lanes count different features (no counter shared in a wave)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int D2 = 1;
+  while (D2 < nfc) D2 <<= 1;
+  const int rpw = 64 / D2;
+  const int sub = lane / D2, f = lane % D2;
+  if (f < nfc) {
+    const K p0 = sp[f][0], p1 = sp[f][1];
+    const bool two = p1 != p0;
+    for (int64_t r = (int64_t)w * rpw + sub; r < m; r += 4 * rpw) {
+      const K key = KeyOf<V>::key(rows[(lo + r) * d + f0 + f]);
       const unsigned dig = (unsigned)((key >> sh) & 0xFF);
-      const K p0 = sp[f][0], p1 = sp[f][1];
-      if ((key & mask) == p0) atomicAdd(&h[f][0][dig], 1u);
-      if (p1 != p0 && (key & mask) == p1) atomicAdd(&h[f][1][dig], 1u);
+      if ((key & mask) == p0) atomicAdd(&h[f * kMgHs + dig], 1u);
+      if (two && (key & mask) == p1) atomicAdd(&h[f * kMgHs + 257 + dig], 1u);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nfc * 512; i += 256)
-    H[((int64_t)j * d + f0) * 512 + i] = (&h[0][0][0])[i];
+  for (int i = threadIdx.x; i < nfc * 512; i += 256) {
+    const int ff = i >> 9, t = (i >> 8) & 1, g = i & 255;
+    H[((int64_t)j * d + f0) * 512 + i] = h[ff * kMgHs + t * 257 + g];
+  }
 }
 
 // One thread per (cluster, feature): the next digit of both ranks.

@@ -141,16 +141,49 @@ class ClusterClassifier:
         return self.classify_medians(med, feature_names, prefix=prefix)
 
     def classify_medians(self, med, feature_names, *, prefix="C"):
-        """{prefix + j: category} from a (k, d) array of cluster medians."""
+        """{prefix + j: category} from a (k, d) array of cluster medians.
+
+        Vectorised over the clusters with the reference's float order kept:
+        each category's total is accumulated feature by feature exactly as
+        score_category does (a skipped term leaves the total unchanged), and
+        ties go to the larger factor, then the earlier category.  Clusters
+        with a NaN median take the per-cluster path (Python's max over NaN
+        scores depends on order)."""
         med = np.asarray(med, dtype=np.float64)
         if med.shape[1] != len(feature_names):
             raise ValueError("feature_names must name every column of X")
+        k = med.shape[0]
+        bad = np.isnan(med).any(axis=1)
+        scores = np.zeros((k, len(CATEGORIES)))
+        for ci, cat in enumerate(CATEGORIES):
+            w, dirs = self.weights[cat], self.directions[cat]
+            total = np.zeros(k)
+            for i, name in enumerate(feature_names):
+                dev = med[:, i] - self.global_medians[name]
+                if cat == "Moderate":
+                    add = np.abs(dev) < 0.1
+                    term = w[name] * self.f(1 - np.abs(dev))
+                else:
+                    want = dirs[name]
+                    add = (want == 0) | (np.sign(dev) == want)
+                    term = w[name] * self.f(np.abs(dev))
+                total = np.where(add, total + term, total)
+            scores[:, ci] = total
+        best = scores.max(axis=1)
+        factors = np.array([self.replication_factors[c] for c in CATEGORIES])
+        order = sorted(range(len(CATEGORIES)), key=lambda c: -factors[c])  # stable
         out = {}
-        for j in range(med.shape[0]):
-            cm = {name: np.float64(med[j, i]) for i, name in enumerate(feature_names)}
-            if any(np.isnan(v) for v in cm.values()):
+        for j in range(k):
+            if bad[j]:
+                cm = {name: np.float64(med[j, i]) for i, name in enumerate(feature_names)}
                 _warn_empty_median()
-            out[f"{prefix}{j}"] = self.classify_cluster(cm)
+                out[f"{prefix}{j}"] = self.classify_cluster(cm)
+                continue
+            leaders = scores[j] == best[j]
+            if leaders.sum() > 1:
+                out[f"{prefix}{j}"] = CATEGORIES[next(c for c in order if leaders[c])]
+            else:
+                out[f"{prefix}{j}"] = CATEGORIES[int(np.argmax(scores[j]))]
         return out
 
 

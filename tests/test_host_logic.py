@@ -98,3 +98,33 @@ def test_kmeans_keeps_reference_max_iter_formula():
     assert sig.parameters["max_iter"].kind is inspect.Parameter.KEYWORD_ONLY
     with pytest.raises(TypeError, match="cannot be interpreted as an integer"):
         range(max(100, 10001 / 100))
+
+
+def test_classify_medians_vectorised_equals_per_cluster():
+    """classify_medians (vectorised over clusters) = classify_cluster on each
+    row: random medians, exact score ties (zero deviations, equal factors) and
+    NaN rows."""
+    import warnings
+
+    from scoring import CATEGORIES, ClusterClassifier
+
+    rng = np.random.default_rng(0)
+    names = [f"f{i}" for i in range(7)]
+    for trial in range(4):
+        gm = {nm: float(rng.random()) for nm in names}
+        w = {c: {nm: float(rng.choice([0.0, 0.5, 1.0, rng.random()])) for nm in names}
+             for c in CATEGORIES}
+        dirs = {c: {nm: int(rng.integers(-1, 2)) for nm in names} for c in CATEGORIES}
+        rf = {c: int(rng.integers(1, 3)) for c in CATEGORIES}
+        clf = ClusterClassifier(gm, w, dirs, rf)
+        med = rng.random((500, 7))
+        med[:50] = [gm[nm] for nm in names]            # zero deviation: ties
+        med[50:60, 2] = gm["f2"] + 0.05                 # Moderate band
+        med[60:63, 4] = np.nan
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            got = clf.classify_medians(med, names)
+            exp = {f"C{j}": clf.classify_cluster({nm: np.float64(med[j, i])
+                                                  for i, nm in enumerate(names)})
+                   for j in range(500)}
+        assert got == exp, trial

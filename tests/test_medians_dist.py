@@ -72,6 +72,14 @@ class NumpyMedians:
                     self.rank[j, f, w] = r - (c[g - 1] if g else 0)
                     self.pref[j, f, w] = (p0, p1)[w] | np.uint64(g << sh)
 
+    def medians_by_label(self, k):
+        passes, words = self.medians_begin(self.medians_group(k))
+        h = np.zeros(words, dtype=np.uint32)
+        for q in range(passes):
+            self.medians_pass_hist(q, h)
+            self.medians_pass_select(q, h)
+        return self.medians_finish()
+
     def medians_finish(self):
         out = np.full((self.k, self.X.shape[1]), np.nan)
         for j in range(self.k):
