@@ -124,6 +124,20 @@ def java_double(x: float) -> str:
     t = Decimal(repr(abs(x))).as_tuple()
     digits = "".join(map(str, t.digits)).rstrip("0") or "0"
     exp10 = len(t.digits) + t.exponent - 1  # position of the leading digit
+    if len(digits) == 1:
+        # JDK 19+ Double.toString: when the shortest decimal has one digit,
+        # two-digit decimals that round to x compete and the closest to x
+        # wins (only subnormals near 4.9E-324 have one): Double.MIN_VALUE
+        # prints as 4.9E-324, not 5.0E-324
+        exact = Decimal(abs(x))
+        best, bd = None, abs(Decimal(digits + "E" + str(exp10)) - exact)
+        for lead in (exp10, exp10 - 1):  # two-digit decimals of this decade or the one below
+            for c in range(10, 100):
+                cand = Decimal(f"{c}E{lead - 1}")
+                if float(cand) == abs(x) and abs(cand - exact) < bd:
+                    best, bd = (str(c), lead), abs(cand - exact)
+        if best is not None:
+            digits, exp10 = best[0].rstrip("0"), best[1]
     if 1e-3 <= abs(x) < 1e7:
         if exp10 >= 0:
             ip = digits[: exp10 + 1].ljust(exp10 + 1, "0")

@@ -259,29 +259,31 @@ __global__ __launch_bounds__(256) void mg_scatter(const V* __restrict__ X, int64
 // Both ranks share one histogram while their prefixes are equal (flag in
 // two[]), as the selection step reads it.
 template <typename V>
-__global__ __launch_bounds__(256) void mg_hist(const V* __restrict__ rows, int d, int k,
-                                               const long long* __restrict__ base,
-                                               const long long* __restrict__ cnt_local,
-                                               const unsigned long long* __restrict__ pref,
-                                               int sh, unsigned* __restrict__ H) {
+__global__ __launch_bounds__(1024) void mg_hist(const V* __restrict__ rows, int d, int k,
+                                                const long long* __restrict__ base,
+                                                const long long* __restrict__ cnt_local,
+                                                const unsigned long long* __restrict__ pref,
+                                                int sh, unsigned* __restrict__ H) {
   typedef typename KeyOf<V>::K K;
   // counters of feature f, rank t, digit g at f * kMgHs + t * 257 + g: the
   // odd strides put the lanes of a wave (different features, often the same
   // digit) in different banks
   constexpr int kMgHs = 515;
+  constexpr int kU = 8;  // rows in flight per lane
   __shared__ unsigned h[kMgFeat * kMgHs];
   __shared__ K sp[kMgFeat][2];
   const int j = blockIdx.x;
   const int f0 = blockIdx.y * kMgFeat;
   const int nfc = min(kMgFeat, d - f0);
-  for (int i = threadIdx.x; i < kMgFeat * kMgHs; i += 256) h[i] = 0;
-  for (int i = threadIdx.x; i < 2 * nfc; i += 256)
+  for (int i = threadIdx.x; i < kMgFeat * kMgHs; i += 1024) h[i] = 0;
+  for (int i = threadIdx.x; i < 2 * nfc; i += 1024)
     sp[i >> 1][i & 1] = (K)pref[((int64_t)j * d + f0) * 2 + i];
   __syncthreads();
   const K mask = sh + 8 >= KeyOf<V>::BITS ? (K)0 : (K)(~(K)0 << (sh + 8));
   const int64_t lo = base[j], m = cnt_local[j];
   // lanes over (row, feature): a wave reads whole rows (contiguous) and, for
-  // d >= 64, its lanes count different features (no counter shared in a wave)
+  // d >= 64, its lanes count different features (no counter shared in a
+  // wave); kU rows per lane are loaded before any is counted
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int D2 = 1;
   while (D2 < nfc) D2 <<= 1;
@@ -290,15 +292,26 @@ __global__ __launch_bounds__(256) void mg_hist(const V* __restrict__ rows, int d
   if (f < nfc) {
     const K p0 = sp[f][0], p1 = sp[f][1];
     const bool two = p1 != p0;
-    for (int64_t r = (int64_t)w * rpw + sub; r < m; r += 4 * rpw) {
-      const K key = KeyOf<V>::key(rows[(lo + r) * d + f0 + f]);
-      const unsigned dig = (unsigned)((key >> sh) & 0xFF);
-      if ((key & mask) == p0) atomicAdd(&h[f * kMgHs + dig], 1u);
-      if (two && (key & mask) == p1) atomicAdd(&h[f * kMgHs + 257 + dig], 1u);
+    const int64_t step = (int64_t)16 * rpw;  // 16 waves
+    for (int64_t r0 = (int64_t)w * rpw + sub; r0 < m; r0 += kU * step) {
+      V v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t r = r0 + u * step;
+        v[u] = r < m ? rows[(lo + r) * d + f0 + f] : (V)0;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (r0 + u * step >= m) break;
+        const K key = KeyOf<V>::key(v[u]);
+        const unsigned dig = (unsigned)((key >> sh) & 0xFF);
+        if ((key & mask) == p0) atomicAdd(&h[f * kMgHs + dig], 1u);
+        if (two && (key & mask) == p1) atomicAdd(&h[f * kMgHs + 257 + dig], 1u);
+      }
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nfc * 512; i += 256) {
+  for (int i = threadIdx.x; i < nfc * 512; i += 1024) {
     const int ff = i >> 9, t = (i >> 8) & 1, g = i & 255;
     H[((int64_t)j * d + f0) * 512 + i] = h[ff * kMgHs + t * 257 + g];
   }
@@ -479,10 +492,10 @@ void medians_pass_hist(Ctx& c, int pass, void* hist) {
   const long long* total = base + k;
   dim3 grid(k, (unsigned)ceil_div(d, kMgFeat));
   if (c.mode == CDR_MODE_F32X)
-    hipLaunchKernelGGL(mg_hist<float>, grid, dim3(256), 0, c.stream, c.med_vals.as<float>(), d, k,
+    hipLaunchKernelGGL(mg_hist<float>, grid, dim3(1024), 0, c.stream, c.med_vals.as<float>(), d, k,
                        base, total, pref, sh, c.med_hist.as<unsigned>());
   else
-    hipLaunchKernelGGL(mg_hist<double>, grid, dim3(256), 0, c.stream, c.med_vals.as<double>(), d,
+    hipLaunchKernelGGL(mg_hist<double>, grid, dim3(1024), 0, c.stream, c.med_vals.as<double>(), d,
                        k, base, total, pref, sh, c.med_hist.as<unsigned>());
   HIP_CHECK(hipGetLastError());
   if (hist) {

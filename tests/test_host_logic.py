@@ -19,7 +19,11 @@ def test_java_double_layout():
              (9.99e-4, "9.99E-4"), (1e-5, "1.0E-5"), (123.456, "123.456"),
              (9999999.5, "9999999.5"), (0.1 + 0.2, "0.30000000000000004"),
              (-2.5e-7, "-2.5E-7"), (1e300, "1.0E300"), (float("nan"), "NaN"),
-             (float("inf"), "Infinity")]
+             (float("inf"), "Infinity"), (float("-inf"), "-Infinity"),
+             (5e-324, "4.9E-324"), (1e-323, "9.9E-324"), (1.7976931348623157e308, "1.7976931348623157E308"),
+             (1.0 / 3, "0.3333333333333333"), (2.0 / 3, "0.6666666666666666"),
+             (123456789.0, "1.23456789E8"), (1e21, "1.0E21"), (0.001, "0.001"),
+             (1234567.0, "1234567.0")]
     for v, s in cases:
         assert java_double(v) == s, (v, java_double(v))
     rng = random.Random(1)
