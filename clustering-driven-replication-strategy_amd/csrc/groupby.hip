@@ -877,6 +877,141 @@ __global__ __launch_bounds__(kGbBThreads) void gb_bucket_dense(
   }
 }
 
+// Dense variant, one WAVE per bucket (2^L <= 2^kGwMaxL files): each wave of
+// the workgroup owns a private LDS slice [u16 grid of F x S counts | per-file
+// state] and takes every (grid waves)-th bucket, so no workgroup barrier
+// and no end-of-bucket row scan sits between two buckets: the wave clears
+// its grid (ds_write_b128), adds each event with a RETURNING u16 add (the
+// returned count + 1 is the pair's running count, so the concurrency
+// maximum is tracked as it grows; counts of 1 need no atomic since every
+// file with an event has concurrency >= 1), sums count / writes / reads /
+// local per group of lanes of one file (ballots), and writes the bucket's
+// (F, 6) int64 rows as one contiguous run.  LDS instructions of one wave run
+// in order, so the clear, the adds and the reads need no barrier.
+constexpr int kGwMaxL = 8;
+constexpr int kGwWaves = 4;   // waves per workgroup
+constexpr int kGwUnroll = 8;  // payload loads in flight per lane
+
+__host__ __device__ inline int gw_grid_words(int L, int sbits) {
+  return ((((1 << (L + sbits)) + 1) >> 1) + 3) & ~3;  // u32 words, multiple of 4
+}
+__host__ __device__ inline int gw_wave_bytes(int L, int sbits) {
+  return (4 * gw_grid_words(L, sbits) + 24 * (1 << L) + 15) & ~15;  // 16-byte aligned slices
+}
+
+template <typename T>
+__global__ __launch_bounds__(64 * kGwWaves) void gb_bucket_wave(
+    const T* __restrict__ pb, const unsigned* __restrict__ bbase, int64_t nbuckets, int64_t nf,
+    GbPay p, const int32_t* __restrict__ primary, long long* __restrict__ out,
+    int* __restrict__ big_list, int* __restrict__ big_count) {
+  extern __shared__ unsigned long long lds[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int F = 1 << p.L;
+  const int KW = gw_grid_words(p.L, p.sbits);
+  unsigned char* mine =
+      reinterpret_cast<unsigned char*>(lds) + (size_t)wv * gw_wave_bytes(p.L, p.sbits);
+  unsigned* grid = reinterpret_cast<unsigned*>(mine);
+  GbFiles g = gb_files(reinterpret_cast<unsigned long long*>(mine + 4 * KW), F);
+  const unsigned lmask = (1u << p.L) - 1;
+  const unsigned smask = (1u << p.sbits) - 1;
+  const unsigned ccmask = (1u << p.cbits) - 1;
+  // buckets strided over the waves of the grid (a dynamic atomic counter
+  // here miscompiled into a loop that never exits)
+  const int64_t nw = (int64_t)gridDim.x * kGwWaves;
+  for (int64_t b = (int64_t)blockIdx.x * kGwWaves + wv; b < nbuckets; b += nw) {
+    const int b32 = (int)b;
+    const int64_t s0 = bbase[b], n = (int64_t)bbase[b + 1] - s0;
+    if (n > kGbDenseCap) {
+      if (lane == 0) big_list[atomicAdd(big_count, 1)] = b32;
+    } else {
+      const int64_t f0 = b << p.L;
+      const int nfl = (int)min((int64_t)F, nf - f0);
+      // the first payloads go out before the clear
+      T v[kGwUnroll];
+  #pragma unroll
+      for (int u = 0; u < kGwUnroll; ++u) {
+        const int64_t i = u * 64 + lane;
+        v[u] = i < n ? pb[s0 + i] : (T)0;
+      }
+      const uint4 z = {0u, 0u, 0u, 0u};
+      for (int i = lane * 4; i < KW; i += 256) *reinterpret_cast<uint4*>(grid + i) = z;
+      for (int f = lane; f < F; f += 64) {
+        g.cw[f] = 0;
+        g.rl[f] = 0;
+        g.conc[f] = 0;
+        g.prim[f] = f < nfl ? primary[f0 + f] : -2;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int64_t i0 = 0; i0 < n; i0 += 64 * kGwUnroll) {
+        if (i0 > 0) {
+  #pragma unroll
+          for (int u = 0; u < kGwUnroll; ++u) {
+            const int64_t i = i0 + u * 64 + lane;
+            v[u] = i < n ? pb[s0 + i] : (T)0;
+          }
+        }
+  #pragma unroll
+        for (int u = 0; u < kGwUnroll; ++u) {
+          const bool act = i0 + u * 64 + lane < n;
+          if (__ballot(act) == 0) break;
+          const unsigned long long x = (unsigned long long)v[u];
+          unsigned fl = 0, oc = 0;
+          bool loc = false;
+          if (act) {
+            fl = (unsigned)(x >> p.fshift) & lmask;
+            const unsigned sc = (unsigned)(x >> p.sshift) & smask;
+            oc = (unsigned)(x >> p.cbits) & 3u;
+            const int cl = (int)((unsigned)x & ccmask) - 1;
+            const unsigned key = (fl << p.sbits) | sc;
+            const unsigned sh = (key & 1u) << 4;
+            const unsigned old = atomicAdd(&grid[key >> 1], 1u << sh);
+            const unsigned cnt = ((old >> sh) & 0xFFFFu) + 1u;
+            if (cnt > 1u && cnt > g.conc[fl]) atomicMax(&g.conc[fl], cnt);
+            const int pf = g.prim[fl];
+            loc = cl >= 0 && pf >= 0 && cl == pf;
+          }
+          unsigned long long peers = __ballot(act);
+          for (int bt = 0; bt < p.L; ++bt) {
+            const bool bit = (fl >> bt) & 1u;
+            const unsigned long long bb = __ballot(act && bit);
+            peers &= bit ? bb : ~bb;
+          }
+          const unsigned long long mw = __ballot(act && oc == 1), mr = __ballot(act && oc == 2);
+          const unsigned long long ml = __ballot(act && loc);
+          if (act && lane == __ffsll((long long)peers) - 1) {
+            atomicAdd(&g.cw[fl], (unsigned long long)__popcll(peers) |
+                                     ((unsigned long long)__popcll(peers & mw) << 32));
+            atomicAdd(&g.rl[fl], (unsigned long long)__popcll(peers & mr) |
+                                     ((unsigned long long)__popcll(peers & ml) << 32));
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // rows f0 .. f0 + nfl, six fields each: one contiguous run of the output
+      long long* o = out + f0 * 6;
+      for (int t = lane; t < 6 * nfl; t += 64) {
+        const int f = t / 6, fld = t - 6 * f;
+        const unsigned long long cw = g.cw[f], rl = g.rl[f];
+        const long long cntf = (long long)(cw & 0xFFFFFFFFull);
+        long long val;
+        switch (fld) {
+          case 0: val = cntf; break;
+          case 1: val = (long long)(cw >> 32); break;
+          case 2: val = (long long)(rl & 0xFFFFFFFFull); break;
+          case 3: val = (long long)(rl >> 32); break;
+          case 4: val = cntf; break;
+          default: val = cntf > 0 ? (long long)max(g.conc[f], 1u) : 0; break;
+        }
+        o[t] = val;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
 // Buckets over the LDS capacity: the hash lives in global memory (2 n slots
 // from gslots + 2 * s0, so buckets never overlap).
 template <typename T>
@@ -981,24 +1116,38 @@ void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, bo
   // second round of late workgroups would double the tail)
   const size_t lds_b = dense ? files_lds + ((size_t)4 << std::max(0, L + p.sbits - 1)) + 16
                              : 8 * kGbSlots + files_lds;
+  const bool wave = dense && L <= kGwMaxL && !getenv("CDR_GB_BLOCK");
   int per_cu = 0;
-  if (dense)
+  if (wave) {
+    const size_t lds_w = (size_t)kGwWaves * gw_wave_bytes(L, p.sbits);
     HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(gb_bucket_dense<T>), kGbBThreads, lds_b));
-  else
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(gb_bucket<T>), kGbBThreads, lds_b));
-  per_cu = std::max(1, per_cu);
-  const int64_t gb_grid = std::min<int64_t>(nb, (int64_t)lloyd_num_cus(c.device) * per_cu);
-  c.gb_last_grid = gb_grid;
-  if (dense)
-    hipLaunchKernelGGL(gb_bucket_dense<T>, dim3(gb_grid), dim3(kGbBThreads), lds_b, c.stream, pb,
+        &per_cu, reinterpret_cast<const void*>(gb_bucket_wave<T>), 64 * kGwWaves, lds_w));
+    per_cu = std::max(1, per_cu);
+    const int64_t wgrid = std::min<int64_t>(ceil_div(nb, (int64_t)kGwWaves),
+                                            (int64_t)lloyd_num_cus(c.device) * per_cu);
+    c.gb_last_grid = wgrid;
+    hipLaunchKernelGGL(gb_bucket_wave<T>, dim3(wgrid), dim3(64 * kGwWaves), lds_w, c.stream, pb,
                        bbase, nb, nf, p, c.ev_primary.as<int32_t>(), c.ev_out.as<long long>(),
                        c.gb_list.as<int>(), big);
-  else
-    hipLaunchKernelGGL(gb_bucket<T>, dim3(gb_grid), dim3(kGbBThreads), lds_b, c.stream, pb,
-                       bbase, nb, nf, p, k, c.ev_primary.as<int32_t>(), c.ev_out.as<long long>(),
-                       c.gb_list.as<int>(), big);
+  } else {
+    if (dense)
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void*>(gb_bucket_dense<T>), kGbBThreads, lds_b));
+    else
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void*>(gb_bucket<T>), kGbBThreads, lds_b));
+    per_cu = std::max(1, per_cu);
+    const int64_t gb_grid = std::min<int64_t>(nb, (int64_t)lloyd_num_cus(c.device) * per_cu);
+    c.gb_last_grid = gb_grid;
+    if (dense)
+      hipLaunchKernelGGL(gb_bucket_dense<T>, dim3(gb_grid), dim3(kGbBThreads), lds_b, c.stream,
+                         pb, bbase, nb, nf, p, c.ev_primary.as<int32_t>(),
+                         c.ev_out.as<long long>(), c.gb_list.as<int>(), big);
+    else
+      hipLaunchKernelGGL(gb_bucket<T>, dim3(gb_grid), dim3(kGbBThreads), lds_b, c.stream, pb,
+                         bbase, nb, nf, p, k, c.ev_primary.as<int32_t>(),
+                         c.ev_out.as<long long>(), c.gb_list.as<int>(), big);
+  }
   HIP_CHECK(hipGetLastError());
   prof_mark(c, 2);
   int nbig = 0;

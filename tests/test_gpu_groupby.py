@@ -136,3 +136,18 @@ def test_sort_path_agrees(ctx, monkeypatch):
     assert ctx.features_groupby_info()["hand"] == 0
     np.testing.assert_array_equal(a, b)
     assert ma == mb
+
+
+@pytest.mark.parametrize("nf,span", [(300_000, 600), (20_000, 200), (3, 1000)])
+def test_block_dense_kernel_agrees_with_wave_kernel(ctx, monkeypatch, nf, span):
+    """The dense grid's one-wave-per-bucket kernel (default) and the
+    one-workgroup-per-bucket kernel (CDR_GB_BLOCK=1) give the oracle's counts."""
+    rng = np.random.default_rng(21 + nf)
+    f, op, cl, ts, prim = _events(rng, 2_000_000, nf, span_s=span)
+    f[:3000] = nf - 1  # one hot file
+    ts[:3000] = T0 + 7_000_000 + rng.integers(0, 1_000_000, 3000)
+    a, _ = _check(ctx, f, op, cl, ts, prim, dense=1)
+    monkeypatch.setenv("CDR_GB_BLOCK", "1")
+    b, _ = _check(ctx, f, op, cl, ts, prim, dense=1)
+    np.testing.assert_array_equal(a, b)
+    assert a[nf - 1, 5] >= 3000

@@ -1,0 +1,13 @@
+# groupby wave-bucket kernel: tests, config-4 bench + kernel stats; config-5 PMC passes.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 90 --timeout-method thread -m gpu tests/test_gpu_groupby.py tests/test_gpu_features_pipeline.py tests/test_gpu_simulate.py > gpurun_out/pytest_gb.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest_gb.log; exit 1; }
+tail -1 gpurun_out/pytest_gb.log
+timeout -k 10 300 python -u bench.py --config 4 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench4.json 2> gpurun_out/bench4.err || { echo BENCH4_FAIL; tail -20 gpurun_out/bench4.err; exit 5; }
+cat gpurun_out/bench4.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python3 bench.py --config 4 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof4.log 2>&1 || { echo PROF4_FAIL; tail -20 gpurun_out/prof4.log; exit 6; }
+python3 tools/kstats.py gpurun_out/prof4/run_kernel_stats.csv gb_ > gpurun_out/prof4_gb.txt; cat gpurun_out/prof4_gb.txt
+bash tools/pmc_big.sh c5 || exit 7
+python3 tools/pmc_summary.py gpurun_out/pmc_c5 --want screen_big,cand_big,update_big > gpurun_out/pmc_c5.txt; cat gpurun_out/pmc_c5.txt
+echo ALL_OK
