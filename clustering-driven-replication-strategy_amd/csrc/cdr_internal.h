@@ -117,6 +117,10 @@ struct Ctx {
   // (the MFMA B operands as loaded); built once per point set
   DevBuf xs16;
   DevBuf xa32;  // the points row-major (float [n_pad][d4]) for fixup32's gathers
+  // large-k screen copy (screen_big_sp): fp16 of the pre-centred points as the
+  // MFMA B fragments are loaded, [n_pad/64][2 tiles][DQ chunks][64 lanes] x 16 B
+  DevBuf xb16;
+  bool xb_valid = false;
   bool xs_valid = false;
   int xs_qh = 0;
   DevBuf mv_list;   // screen32d: per-wave regions of moved points {pt, old | new << 16}
@@ -178,6 +182,7 @@ struct Ctx {
   // [4] inertia bits.
   DevBuf ll_C, ll_new, ll_sums, ll_ref, ll_state;
   bool ll_on = false, ll_devplan = false, ll_hostplan_once = false;
+  bool ll_devbig = false;  // large-k shapes: screen_big steps on a device-built plan
   int32_t ll_k = 0, ll_flags = 0;
   double ll_tol = 0.0, ll_x2 = 0.0, ll_xxmax = 0.0, ll_l1x = 0.0;
   int64_t ll_enqueued = 0;

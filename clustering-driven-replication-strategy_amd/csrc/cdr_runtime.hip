@@ -260,6 +260,7 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   }
   c.xt_valid = false;
   c.xs_valid = false;
+  c.xb_valid = false;
   c.mu_s.ensure(sizeof(float) * (d > 0 ? d : 1));
   HIP_CHECK(hipMemcpyAsync(c.mu_s.p, ms.data(), sizeof(float) * d,
                            hipMemcpyHostToDevice, c.stream));
@@ -286,6 +287,8 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
   c.xs16.release();
   c.xa32.release();
   c.xs_valid = false;
+  c.xb16.release();
+  c.xb_valid = false;
   c.pre_ok = false;
   c.n = n;
   c.d = d;
@@ -411,7 +414,7 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.gb_p1, &c.gb_p2, &c.gb_hist2, &c.gb_list, &c.gb_slots, &c.sim_cnt, &c.sim_off,
                     &c.sim_tmp, &c.sim_ms, &c.sim_mbase, &c.x_small, &c.x_buf, &c.x_prim, &c.f64x_A, &c.f64x_cnt, &c.f64x_E,
                     &c.f64x_T, &c.f64x_walk, &c.med_hist,
-                    &c.fb_accum, &c.xs16, &c.xa32, &c.mv_list, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
+                    &c.fb_accum, &c.xs16, &c.xa32, &c.xb16, &c.mv_list, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
                     &c.ll_state};
   for (DevBuf* b : bufs) b->release();
   c.h_small.release();

@@ -1040,6 +1040,17 @@ void prof_mark(Ctx& c, int i) {
   if (c.prof_cur >= 0) HIP_CHECK(hipEventRecord(c.prof_pool[(size_t)c.prof_cur + i], c.stream));
 }
 
+// End of a profiled screened step whose fallback total sits in fb_count
+// (screen_big levels): fold it into the profile, then the closing mark.
+void prof_end_screened(Ctx& c) {
+  if (c.prof_cur < 0) return;
+  c.fb_accum.ensure(sizeof(long long));
+  hipLaunchKernelGGL(fb_accumulate, dim3(1), dim3(64), 0, c.stream,
+                     c.fb_count.as<int32_t>() + c.fb_total_slot, c.fb_accum.as<long long>());
+  HIP_CHECK(hipGetLastError());
+  prof_mark(c, 2);
+}
+
 // Fold every recorded step's events into the profile accumulators (waits
 // for the last one).
 void prof_collect(Ctx& c) {

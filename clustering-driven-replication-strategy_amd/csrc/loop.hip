@@ -266,6 +266,17 @@ static double points_sqdev(Ctx& c, const double* ref_host) {
 }
 
 void plan32_launch(Ctx& c, int k, int QH, int MT);  // screen32.hip
+bool big_supported(const Ctx& c, int k);              // screen_big.hip
+void big_plan_device(Ctx& c, int k, const double* dC, const double* dmu, const long long* gate);
+bool big_step_dev(Ctx& c, int k, long long* dout, bool prof, const long long* gate);
+void prof_end_screened(Ctx& c);                       // lloyd.hip
+
+// Large-k plan of the loop's current centroids (begin, resume, and after
+// each finalize that moved them); ll_ref + d holds mu as fp64.
+static void ll_plan_big(Ctx& c) {
+  big_plan_device(c, c.ll_k, c.ll_C.as<double>(), c.ll_ref.as<double>() + c.d,
+                  c.ll_state.as<long long>());
+}
 
 static void ll_plan_shape(const Ctx& c, int& QH, int& MT) {
   QH = d4_of(c.d) / 4 <= 2 ? 1 : 2;
@@ -321,6 +332,7 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   c.ll_tol = tol;
   c.ll_x2 = std::isnan(x2_total) ? points_sqdev(c, ref) : x2_total;
   c.ll_devplan = screen32_supported(c, k) && !std::getenv("CDR_NO_DEVPLAN");
+  c.ll_devbig = !c.ll_devplan && big_supported(c, k) && !std::getenv("CDR_NO_DEVPLAN");
   plan32_point_side(c, c.ll_xxmax, c.ll_l1x);
   c.ll_C.ensure(sizeof(double) * (size_t)k * d);
   c.ll_new.ensure(sizeof(double) * (size_t)k * (d + 1));
@@ -345,6 +357,7 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   // the first step recomputes the running sums from scratch (see resume)
   c.run_valid = false;
   if (c.ll_devplan) ll_plan(c);
+  if (c.ll_devbig) ll_plan_big(c);
   CDR_CATCH
 }
 
@@ -364,6 +377,20 @@ int cdr_lloyd_enqueue_assign(cdr_ctx* h, int64_t* dsums) {
     c.ll_fin_sums = dsums ? dout : c.run_sums.as<long long>();
     c.ll_fin_slices = dsums ? 1 : kRunSlices;
     c.ll_fin_devstep = true;
+    c.last_k = c.ll_k;
+    c.have_labels = true;
+    c.last_screened = true;
+    c.last_fallback = -1;
+  } else if (c.ll_devbig && !c.ll_hostplan_once) {
+    // large k: screen_big on the plan big_plan_kernel built after the last
+    // finalize; the sums go to dout, the loop state gates every kernel
+    const bool prof = prof_step_begin(c);
+    if (!big_step_dev(c, c.ll_k, dout, prof, state))
+      CDR_FAIL(CDR_ERR_STATE, "lloyd loop: large-k step not supported");
+    if (prof) prof_end_screened(c);
+    c.ll_fin_sums = dout;
+    c.ll_fin_slices = 1;
+    c.ll_fin_devstep = false;
     c.last_k = c.ll_k;
     c.have_labels = true;
     c.last_screened = true;
@@ -427,6 +454,7 @@ int cdr_lloyd_enqueue_finalize(cdr_ctx* h, const int64_t* dsums) {
 #endif
   hipLaunchKernelGGL(ll_finalize, dim3(1), dim3(kFinThreads), 0, c.stream, a);
   HIP_CHECK(hipGetLastError());
+  if (c.ll_devbig) ll_plan_big(c);  // the next step's plan (skipped once the loop stopped)
   if (c.ll_fin_devstep && c.prof_cur >= 0) prof_mark(c, 2);
   CDR_CATCH
 }
@@ -483,6 +511,7 @@ int cdr_lloyd_resume(cdr_ctx* h, const double* C, int32_t add_steps, int32_t hos
   HIP_CHECK(hipGetLastError());
   c.ll_hostplan_once = host_plan_once != 0;
   if (c.ll_devplan && !c.ll_hostplan_once) ll_plan(c);
+  if (c.ll_devbig && !c.ll_hostplan_once) ll_plan_big(c);
   HIP_CHECK(hipStreamSynchronize(c.stream));  // C belongs to the caller
   // Steps enqueued after the stop did nothing, but the host marked the
   // running sums valid after each of them; a full (non-DELTA) step that was

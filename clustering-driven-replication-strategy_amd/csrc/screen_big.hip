@@ -52,11 +52,15 @@ typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
 struct BigArgs {
   const float* XT;      // pre-centred points [Q][n_pad][4]
+  const h8* XB;         // screen_big_sp: fp16 B fragments per 64-point group (big_frag_copy)
   int64_t n, n_pad;
   int d, k, Q, KB;      // Q = stored feature quads, KB = ceil(k / 32)
   const h8* frag;       // NPROD 1: [KB][DQ][64]; NPROD 3: [KB][2][DQ][64]
   const float* cinit;   // [KB * 32] C operand per centroid row (1e30 past k)
   float thr0, thr_rel;
+  const float* thr_dev;   // device plan: {thr0, thr_rel} in device memory (else the values above)
+  const long long* gate;  // device loop state: nothing runs once gate[0] == 0
+  unsigned jkeep;       // screen_big_sp: bits of a keyed value kept when its block is merged
   int32_t* labels;
   // GATHER input: per-region point lists of the previous level
   const int32_t* in_list;
@@ -83,6 +87,12 @@ __device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
 
 }  // namespace
 
+// Centroid order inside a 32-row block: MFMA row r (the A-operand row of lane
+// r and r + 32) holds centroid 32 b + big_row(r), chosen so that output value
+// i of lane half h (row 8 (i >> 2) + 4 h + (i & 3)) is centroid 32 b + 16 h + i:
+// a lane's keyed top-2 then carries the centroid's low bits directly.
+__host__ __device__ inline int big_row(int r) { return 16 * ((r >> 2) & 1) + 4 * (r >> 3) + (r & 3); }
+
 // DQ: 16-feature K chunks (d <= 16 DQ).  NPROD: 1 (A = -2 chi, B = xhi) or 3
 // (A1 = -2 chi, A3 = -2 clo; A1 xhi + A1 xlo + A3 xhi).  GATHER: points come
 // from the previous level's regions (a.in_*) instead of a dense sweep.
@@ -91,7 +101,10 @@ constexpr int kBigThreads = 1024;  // L1: one workgroup per CU, 4 waves per SIMD
 
 template <int DQ, int NPROD, bool GATHER, bool ALDS>
 __global__ __launch_bounds__(kBigThreads) void screen_big(BigArgs a) {
+  if (a.gate && a.gate[0] == 0) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0;
+  const float thr_rel = a.thr_dev ? a.thr_dev[1] : a.thr_rel;
   constexpr int NA = NPROD == 1 ? 1 : 2;
   float* scin = reinterpret_cast<float*>(smem);                       // [KB * 32]
   h8* sfrag = reinterpret_cast<h8*>(smem + (size_t)a.KB * 32 * 4);    // [KB][NA][DQ][64]
@@ -189,7 +202,7 @@ __global__ __launch_bounds__(kBigThreads) void screen_big(BigArgs a) {
         const int ib = (int)(kb & 15u);
         const float vb = __uint_as_float(kb & ~15u);
         const float vs = __uint_as_float(ks & ~15u);
-        const int jb = 32 * b + 8 * (ib >> 2) + 4 * h + (ib & 3);
+        const int jb = 32 * b + 16 * h + ib;
         const bool tk = vb < bv[t];
         sv[t] = fminf(fminf(sv[t], vs), tk ? bv[t] : vb);
         bi[t] = tk ? jb : bi[t];
@@ -213,7 +226,7 @@ __global__ __launch_bounds__(kBigThreads) void screen_big(BigArgs a) {
     const int64_t mypt = h == 0 ? pt[0] : pt[1];
     const bool myreal = h == 0 ? real[0] : real[1];
     // rows past k carry C = 1e30: never best, never a close runner-up
-    const bool cert = run > fmaf(best, a.thr_rel, a.thr0);  // NaN: never
+    const bool cert = run > fmaf(best, thr_rel, thr0);  // NaN: never
     if (myreal && cert) a.labels[mypt] = label;
     const unsigned long long need = __ballot(myreal && !cert);
     if (need) {
@@ -273,6 +286,188 @@ __global__ __launch_bounds__(kBigThreads) void screen_big(BigArgs a) {
   }
 }
 
+// The L1 B fragments of every 64-point group, built once per point set from
+// the pre-centred copy with the same fp16 conversion run_group applies
+// (pack_h2): [g][t][c][lane] h8, lane (h, p) = features 16 c + 8 h .. + 8 of
+// point 64 g + 32 t + p.  Half the bytes of the fp32 copy, and a wave's
+// fragment loads are 1 KiB contiguous.
+__global__ void big_frag_copy(const float* __restrict__ XT, int64_t n, int64_t n_pad, int Q,
+                              int DQ, uint4* __restrict__ xb) {
+  const f4* X4 = reinterpret_cast<const f4*>(XT);
+  const int64_t total = (n_pad >> 6) * 2 * DQ * 64;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(e & 63);
+    const int64_t r = e >> 6;
+    const int c = (int)(r % DQ);
+    const int64_t gt = r / DQ;
+    const int t = (int)(gt & 1);
+    const int64_t g = gt >> 1;
+    const int h = lane >> 5, p = lane & 31;
+    const int64_t pt = g * 64 + 32 * t + p;
+    const int q0 = 4 * c + 2 * h;
+    f4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+    if (pt < n && q0 < Q) v0 = X4[(int64_t)q0 * n_pad + pt];
+    if (pt < n && q0 + 1 < Q) v1 = X4[(int64_t)(q0 + 1) * n_pad + pt];
+    xb[e] = uint4{pack_h2(v0[0], v0[1]), pack_h2(v0[2], v0[3]), pack_h2(v1[0], v1[1]),
+                  pack_h2(v1[2], v1[3])};
+  }
+}
+
+// L1, software-pipelined (the product L1; screen_big<DQ, 1, false, true> is
+// kept for comparisons, CDR_BIG_L1=0).  Per 32-centroid block a wave issues
+// the block's MFMAs into one accumulator pair while it reduces the previous
+// block's values from the other pair, so its own VALU runs beside its
+// matrix work (PMC of the unpipelined kernel: MFMA busy 0.45 + VALU 0.38 of
+// the cycles, i.e. serialised).  Keys: the local top-2 keys value i as
+// (bits & ~15) | i (inline constants); with the row order of big_row, i is
+// centroid 32 b + 16 h + i, so the block merge is one v_and_or that writes
+// (b, h) above i, and the running (best, runner-up) keys carry the centroid
+// index in their low JB bits (no separate index or float compare).
+// NT threads per workgroup (one workgroup per CU): 768 = 3 waves per SIMD
+// (<= 168 VGPRs), 512 = 2 waves per SIMD (<= 256 VGPRs, no spills at DQ = 4)
+template <int DQ, int NT>
+__global__ __launch_bounds__(NT) void screen_big_sp(BigArgs a) {
+  if (a.gate && a.gate[0] == 0) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0;
+  const float thr_rel = a.thr_dev ? a.thr_dev[1] : a.thr_rel;
+  float* scin = reinterpret_cast<float*>(smem);                     // [KB * 32]
+  h8* sfrag = reinterpret_cast<h8*>(smem + (size_t)a.KB * 32 * 4);  // [KB][DQ][64]
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int p = lane & 31;
+  for (int i = threadIdx.x; i < a.KB * 32; i += blockDim.x) scin[i] = a.cinit[i];
+  {
+    const int nf = a.KB * DQ * 64;
+    for (int i = threadIdx.x; i < nf; i += blockDim.x) sfrag[i] = a.frag[i];
+  }
+  __syncthreads();
+  const int wpb = blockDim.x >> 6;
+  const int wave_id = blockIdx.x * wpb + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * wpb;
+  int32_t* region = a.out_list + (size_t)wave_id * a.out_cap;
+  float* region_best = a.out_best + (size_t)wave_id * a.out_cap;
+  int used = 0;
+  const h8* XB = a.XB;
+  const unsigned jkeep = a.jkeep;
+  const int KB = a.KB;
+  const int64_t items = (a.n + 63) >> 6;
+  // the group's B fragments: 2 DQ coalesced 16-byte loads per lane, the next
+  // group's issued before this group's blocks (one group of prefetch)
+  h8 BN[2][DQ];
+  auto fetch = [&](int64_t gg) {
+    if (gg < items) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < DQ; ++c) BN[t][c] = XB[((gg * 2 + t) * DQ + c) * 64 + lane];
+    }
+  };
+  fetch(wave_id);
+  for (int64_t g = wave_id; g < items; g += nwaves) {
+    const int64_t base = g << 6;
+    const int64_t pt[2] = {base + p, base + 32 + p};
+    const bool real[2] = {pt[0] < a.n, pt[1] < a.n};
+    h8 BH[2][DQ];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int c = 0; c < DQ; ++c) BH[t][c] = BN[t][c];
+    fetch(g + nwaves);
+    unsigned RB[2] = {~0u, ~0u}, RS[2] = {~0u, ~0u};
+    // the block's MFMAs: C operand rows from LDS, A fragments from LDS
+    auto mm = [&](int b, f16v (&acc)[2]) {
+      const f4* cr = reinterpret_cast<const f4*>(scin + 32 * b + 4 * h);
+      f16v ci;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f4 v = cr[2 * q];  // rows 8q + 4h .. + 4
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ci[4 * q + i] = v[i];
+      }
+      h8 A[DQ];
+#pragma unroll
+      for (int c = 0; c < DQ; ++c) A[c] = sfrag[((size_t)b * DQ + c) * 64 + lane];
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], BH[0][0], ci, 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], BH[1][0], ci, 0, 0, 0);
+#pragma unroll
+      for (int c = 1; c < DQ; ++c) {
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], BH[0][c], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], BH[1][c], acc[1], 0, 0, 0);
+      }
+    };
+    // keyed top-2 of each tile's 16 values (all >= 0: bits order), merged
+    // into the running keys with the block and lane half written above i
+    auto red = [&](int b, const f16v (&acc)[2]) {
+      const unsigned bo = ((unsigned)b << 5) | ((unsigned)h << 4);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        auto key = [&](int i) { return (__float_as_uint(acc[t][i]) & ~15u) | (unsigned)i; };
+        unsigned kb = min(key(0), key(1)), ks = max(key(0), key(1));
+#pragma unroll
+        for (int i = 2; i < 16; i += 2) {
+          const unsigned x = key(i), y = key(i + 1);
+          unsigned m;
+          asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m) : "v"(kb), "v"(x), "v"(y));
+          asm("v_min3_u32 %0, %1, %2, %3" : "=v"(kb) : "v"(kb), "v"(x), "v"(y));
+          ks = min(ks, m);
+        }
+        const unsigned kj = (kb & jkeep) | bo;
+        unsigned ms;
+        asm("v_min3_u32 %0, %1, %2, %3" : "=v"(ms) : "v"(max(RB[t], kj)), "v"(RS[t]), "v"(ks));
+        RS[t] = ms;
+        RB[t] = min(RB[t], kj);
+      }
+    };
+    f16v accA[2], accB[2];
+    mm(0, accA);
+    int b = 1;
+    for (; b + 1 < KB; b += 2) {
+      mm(b, accB);
+      red(b - 1, accA);
+      mm(b + 1, accA);
+      red(b, accB);
+    }
+    if (b < KB) {
+      mm(b, accB);
+      red(b - 1, accA);
+      red(b, accB);
+    } else {
+      red(b - 1, accA);
+    }
+    // lanes < 32 end with tile 0's point p (both halves), lanes >= 32 with
+    // tile 1's
+    unsigned b0 = RB[0], b1 = RB[1], s0 = RS[0], s1 = RS[1];
+    swap32(b0, b1);
+    swap32(s0, s1);
+    const unsigned kbest = min(b0, b1);
+    unsigned krun;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(krun) : "v"(max(b0, b1)), "v"(s0), "v"(s1));
+    const float best = __uint_as_float(kbest);
+    const int label = (int)(kbest & ~jkeep) | (int)(kbest & 15u);
+    const int64_t mypt = h == 0 ? pt[0] : pt[1];
+    const bool myreal = h == 0 ? real[0] : real[1];
+    // rows past k carry C = 1e30: never best, never a close runner-up
+    const bool cert = __uint_as_float(krun) > fmaf(best, thr_rel, thr0);
+    if (myreal && cert) a.labels[mypt] = label;
+    const unsigned long long need = __ballot(myreal && !cert);
+    if (need) {
+      const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+      if (myreal && !cert) {
+        region[used + rank] = (int32_t)mypt;
+        region_best[used + rank] = best;
+      }
+      used += __popcll(need);
+    }
+  }
+  if (lane == 0) {
+    a.out_count[wave_id] = used;
+    if (used) atomicAdd(a.out_count + nwaves, used);
+  }
+}
+
 // dst[i] = src[i] for 16-byte words; src is mapped pinned host memory.
 __global__ __launch_bounds__(256) void pull_host_big(const uint4* __restrict__ src,
                                                      uint4* __restrict__ dst, int64_t n16) {
@@ -289,6 +484,39 @@ __global__ __launch_bounds__(256) void pull_host_big(const uint4* __restrict__ s
 // order (np_sqdist, correctly rounded sqrt, first minimum by (root, index)).
 // A point with more than kMaxCand candidates goes to the flat overflow list
 // for exact_big (all k centroids).
+// np_sqdist (exact_math.h) for d >= 8 with the point's features in
+// registers (DMAX >= d, a compile-time bound so every index is static)
+template <int DMAX>
+__device__ __forceinline__ double np_sqdist_reg(const float (&x)[DMAX],
+                                                const double* __restrict__ cj, int d) {
+  double r[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const double t = (double)x[i] - cj[i];
+    r[i] = t * t;
+  }
+  const int dd = d - (d & 7);
+#pragma unroll
+  for (int f = 8; f < DMAX; f += 8) {
+    if (f < dd) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const double t = (double)x[f + i] - cj[f + i];
+        r[i] = r[i] + t * t;
+      }
+    }
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+  for (int f = 8; f < DMAX; ++f) {
+    if (f >= dd && f < d) {
+      const double t = (double)x[f] - cj[f];
+      res = res + t * t;
+    }
+  }
+  return res;
+}
+
 constexpr int kMaxCand = 16;
 constexpr int kMaxRegions = 8192;  // L1 waves (regions) the candidate level can index
 
@@ -297,6 +525,9 @@ __global__ __launch_bounds__(256) void cand_big(BigArgs a, const float* __restri
                                                 const double* __restrict__ C64,
                                                 int32_t* __restrict__ ovf,
                                                 int32_t* __restrict__ ovf_count, int abl) {
+  if (a.gate && a.gate[0] == 0) return;
+  const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0;
+  const float thr_rel = a.thr_dev ? a.thr_dev[1] : a.thr_rel;
   __shared__ int scnt[4][64];
   __shared__ int scand[4][64 * kMaxCand];
   __shared__ int schunk[kMaxRegions + 1];  // exclusive prefix of 64-point chunks per region
@@ -350,7 +581,7 @@ __global__ __launch_bounds__(256) void cand_big(BigArgs a, const float* __restri
         const int e = e0 + 32 * t + p;
         real[t] = e < cnt;
         pt[t] = real[t] ? (int64_t)src[e] : 0;
-        lim[t] = real[t] ? fmaf(srcb[e], a.thr_rel, a.thr0) : -1.0f;
+        lim[t] = real[t] ? fmaf(srcb[e], thr_rel, thr0) : -1.0f;
       }
       scnt[w][lane] = 0;
       h8 BH[2][DQ];
@@ -394,7 +625,7 @@ __global__ __launch_bounds__(256) void cand_big(BigArgs a, const float* __restri
 #pragma unroll
           for (int i = 0; i < 16; ++i)
             if (acc[t][i] <= lim[t]) {
-              const int j = 32 * b + 8 * (i >> 2) + 4 * h + (i & 3);
+              const int j = 32 * b + 16 * h + i;
               const int slot = atomicAdd(&scnt[w][32 * t + p], 1);
               if (slot < kMaxCand) scand[w][(32 * t + p) * kMaxCand + slot] = j;
             }
@@ -411,13 +642,21 @@ __global__ __launch_bounds__(256) void cand_big(BigArgs a, const float* __restri
         } else if (nc > kMaxCand || nc == 0) {
           ovf[atomicAdd(ovf_count, 1)] = (int32_t)mypt;
         } else {
+          // the point's features once (one batch of quad loads), then each
+          // candidate's fp64 row (L2-resident) in NumPy's pairwise order
+          float xv[16 * DQ];
+          const f4* X04 = reinterpret_cast<const f4*>(X0);
+#pragma unroll
+          for (int q = 0; q < 4 * DQ; ++q) {
+            const f4 v = q < a.Q ? X04[(int64_t)q * a.n_pad + mypt] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xv[4 * q + i] = v[i];
+          }
           double rb = INFINITY;
           int jb = 0x7fffffff;
           for (int s2 = 0; s2 < nc; ++s2) {
             const int j = scand[w][lane * kMaxCand + s2];
-            const double* cj = C64 + (size_t)j * a.d;
-            const double R = np_sqdist([&](int f) { return (double)X0[xidx(f, mypt, a.n_pad)]; },
-                                       [&](int f) { return cj[f]; }, a.d);
+            const double R = np_sqdist_reg<16 * DQ>(xv, C64 + (size_t)j * a.d, a.d);
             const double root = sqrt(R);
             if (root < rb || (root == rb && j < jb)) {
               rb = root;
@@ -442,7 +681,9 @@ __global__ __launch_bounds__(64) void exact_big(const float* __restrict__ X, int
                                                 int d, const double* __restrict__ C, int k,
                                                 const int32_t* __restrict__ list,
                                                 const int32_t* __restrict__ count,
-                                                int32_t* __restrict__ labels) {
+                                                int32_t* __restrict__ labels,
+                                                const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
   __shared__ double sx[128];
   const int lane = threadIdx.x;
   const int c8 = lane >> 3, r = lane & 7;
@@ -500,7 +741,9 @@ template <int FG>
 __global__ __launch_bounds__(1024) void update_big(const float* __restrict__ X, int64_t n,
                                                    int64_t n_pad, int d, int k,
                                                    const int32_t* __restrict__ labels,
-                                                   double fx, unsigned long long* __restrict__ out) {
+                                                   double fx, unsigned long long* __restrict__ out,
+                                                   const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* tsum = reinterpret_cast<double*>(smem);        // [FG][k]
   int* tcnt = reinterpret_cast<int*>(tsum + (size_t)FG * k);  // [k]
@@ -550,6 +793,13 @@ extern int lloyd_num_cus(int device);
 void ensure_precentered(Ctx& c);
 
 static int big_dq(int d) { return (d + 15) / 16; }
+// L1 workgroup size: 3 waves per SIMD while the pipelined kernel fits 168
+// VGPRs (DQ <= 2), else 2 (CDR_BIG_SP_NT=512|768 overrides, for comparisons)
+static int big_sp_threads(int DQ) {
+  static const int env = std::getenv("CDR_BIG_SP_NT") ? std::atoi(std::getenv("CDR_BIG_SP_NT")) : 0;
+  if (env == 512 || env == 768) return env;
+  return DQ <= 2 ? 768 : 512;
+}
 static size_t big_l1_lds(int k, int d) {
   const int KB = (k + 31) / 32;
   return (size_t)KB * 32 * 4 + (size_t)KB * big_dq(d) * 64 * 16;
@@ -571,38 +821,25 @@ struct PlanBig {
   std::vector<h8> frag1, frag3;
   std::vector<float> cinit;
   float thr1, thr3, thr_rel;
+  int jbits;
 };
 
 // Rigorous screen error bounds (see the file header); mirrors build_plan32's
-// terms with N = fp32 additions in the MFMA chain.
-static void build_plan_big(const Ctx& c, const double* C, int k, PlanBig& pl) {
-  const int d = c.d, DQ = big_dq(d), KB = (k + 31) / 32;
-  const double sc = std::ldexp(1.0, c.sigma);
-  std::vector<double> ch((size_t)k * d), cc(k, 0.0);
-  double ccmax = 0.0, l1c = 0.0;
-  for (int j = 0; j < k; ++j) {
-    double s = 0.0, l1 = 0.0;
-    for (int f = 0; f < d; ++f) {
-      const double v = (C[(size_t)j * d + f] - (double)c.mu[f]) * sc;
-      ch[(size_t)j * d + f] = v;
-      s += v * v;
-      l1 += std::fabs(v);
-    }
-    cc[j] = s;
-    ccmax = std::fmax(ccmax, s);
-    l1c = std::fmax(l1c, l1);
-  }
-  double xxmax = 0.0, l1x = 0.0;
-  for (int f = 0; f < d; ++f) {
-    const double dev =
-        std::fmax(c.fmax[f] - (double)c.mu[f], (double)c.mu[f] - c.fmin[f]) * sc;
-    xxmax += dev * dev;
-    l1x += dev;
-  }
-  xxmax *= 1.0 + 1e-6;
-  const double u = std::ldexp(1.0, -24);
-  const double eps = std::ldexp(1.0, -11), eta = std::ldexp(1.0, -25);
-  const double cx = std::sqrt(ccmax * xxmax);
+// terms with N = fp32 additions in the MFMA chain.  Shared by the host plan
+// (build_plan_big) and the device plan (big_plan_kernel): the same fp64
+// operations in the same order, so both give the same bits.
+struct BigBounds {
+  double D;
+  float thr1, thr3, thr_rel;
+  int jbits;
+};
+
+__host__ __device__ inline BigBounds big_bounds(double ccmax, double l1c, double xxmax,
+                                                double l1x, int DQ, int KB) {
+  BigBounds r;
+  const double u = ldexp(1.0, -24);
+  const double eps = ldexp(1.0, -11), eta = ldexp(1.0, -25);
+  const double cx = sqrt(ccmax * xxmax);
   // one product: |c.x - chi.xhi| <= 2 eps (1 + eps) ||c|| ||x|| + eta (l1x + (1 + eps) l1c)
   const double P1 = 2.0 * eps * (1.0 + eps) * cx + eta * (l1x + (1.0 + eps) * l1c);
   const double N1 = 16.0 * DQ + 1.0, N3 = 3.0 * 16.0 * DQ + 1.0;
@@ -610,56 +847,187 @@ static void build_plan_big(const Ctx& c, const double* C, int k, PlanBig& pl) {
   const double g3 = 2.0 * u * N3 / (1.0 - 2.0 * u * N3);
   const double E1a = 2.0 * P1 + g1 * (ccmax + 2.0 * xxmax + 4.0 * cx + 4.0) + u * (ccmax + 2.0 * xxmax + 4.0);
   // D >= max ||xhat||^2 + margin keeps every screen value >= 0
-  const double D = xxmax + 4.0 * E1a + std::ldexp(1.0, -20);
+  const double D = xxmax + 4.0 * E1a + ldexp(1.0, -20);
   const double sum1 = (ccmax + D) * (1.0 + u) + 2.0 * (1.0 + eps) * (1.0 + eps) * cx;
-  const double E1 = 2.0 * P1 + g1 * sum1 + u * (ccmax + D) + std::ldexp(1.0, -46) * (ccmax + D);
+  const double E1 = 2.0 * P1 + g1 * sum1 + u * (ccmax + D) + ldexp(1.0, -46) * (ccmax + D);
   // three products: the split leaves |c.x - (chi xhi + chi xlo + clo xhi)| <=
   // 2.4 2^-22 ||c|| ||x|| + 2^-24 (l1c + l1x)
-  const double P3 = 2.4 * std::ldexp(1.0, -22) * cx + std::ldexp(1.0, -24) * (l1c + l1x);
-  const double sum3 = (ccmax + D) * (1.0 + u) + 2.0 * (1.0 + std::ldexp(1.0, -9)) * cx;
-  const double E3 = 2.0 * P3 + g3 * sum3 + u * (ccmax + D) + std::ldexp(1.0, -46) * (ccmax + D);
+  const double P3 = 2.4 * ldexp(1.0, -22) * cx + ldexp(1.0, -24) * (l1c + l1x);
+  const double sum3 = (ccmax + D) * (1.0 + u) + 2.0 * (1.0 + ldexp(1.0, -9)) * cx;
+  const double E3 = 2.0 * P3 + g3 * sum3 + u * (ccmax + D) + ldexp(1.0, -46) * (ccmax + D);
   // reference slack: the fp64 distances and roots must not tie or flip
-  const double Wmax = (std::sqrt(ccmax) + std::sqrt(xxmax)) * (std::sqrt(ccmax) + std::sqrt(xxmax));
-  const double slack = std::ldexp(Wmax + 1.0, -38);
-  pl.thr1 = (float)((2.0 * E1 + slack) * 1.001);
-  pl.thr3 = (float)((2.0 * E3 + slack) * 1.001);
-  pl.thr_rel = 1.0f + std::ldexp(1.0f, -18);  // the 16-ulp key truncation
+  const double Wmax = (sqrt(ccmax) + sqrt(xxmax)) * (sqrt(ccmax) + sqrt(xxmax));
+  const double slack = ldexp(Wmax + 1.0, -38);
+  r.D = D;
+  r.thr1 = (float)((2.0 * E1 + slack) * 1.001);
+  r.thr3 = (float)((2.0 * E3 + slack) * 1.001);
+  // keys keep the centroid index in their low JB bits (screen_big_sp): best
+  // and runner-up are each within 2^JB ulps (2^(JB-23) relative) of their
+  // screen values, covered by 1 + 4 * 2^(JB-23); >= the old kernel's 16-ulp need
+  int JB = 5;
+  while ((1 << (JB - 5)) < KB) ++JB;
+  r.jbits = JB;
+  r.thr_rel = 1.0f + ldexpf(1.0f, JB - 21);
+  return r;
+}
+
+// The point side of the bounds: max ||xhat||^2 (with a 1e-6 margin) and max
+// ||xhat||_1 over the data's bounding box.
+static void big_point_side(const Ctx& c, double& xxmax, double& l1x) {
+  const double sc = std::ldexp(1.0, c.sigma);
+  xxmax = 0.0;
+  l1x = 0.0;
+  for (int f = 0; f < c.d; ++f) {
+    const double dev =
+        std::fmax(c.fmax[f] - (double)c.mu[f], (double)c.mu[f] - c.fmin[f]) * sc;
+    xxmax += dev * dev;
+    l1x += dev;
+  }
+  xxmax *= 1.0 + 1e-6;
+}
+
+// A1 fragment of one lane of centroid block b, feature chunk cq (the L1 / L2
+// A operand: -2 chi, rows in big_row order).
+__host__ __device__ inline h8 big_frag_lane(const double* C, const double* mu, double sc, int k,
+                                            int d, int b, int cq, int lane) {
+  const int j = 32 * b + big_row(lane & 31);
+  const int hh = lane >> 5;
+  h8 A1 = {};
+  for (int i = 0; i < 8; ++i) {
+    const int f = 16 * cq + 8 * hh + i;
+    if (j >= k || f >= d) continue;
+    const double v = (C[(size_t)j * d + f] - mu[f]) * sc;
+    const _Float16 hi = f64_to_f16(v);
+    A1[i] = f64_to_f16(-2.0 * (double)hi);
+  }
+  return A1;
+}
+
+static void build_plan_big(const Ctx& c, const double* C, int k, PlanBig& pl) {
+  const int d = c.d, DQ = big_dq(d), KB = (k + 31) / 32;
+  const double sc = std::ldexp(1.0, c.sigma);
+  std::vector<double> mu(d), cc(k, 0.0);
+  for (int f = 0; f < d; ++f) mu[f] = (double)c.mu[f];
+  double ccmax = 0.0, l1c = 0.0;
+  for (int j = 0; j < k; ++j) {
+    double s = 0.0, l1 = 0.0;
+    for (int f = 0; f < d; ++f) {
+      const double v = (C[(size_t)j * d + f] - mu[f]) * sc;
+      s += v * v;
+      l1 += std::fabs(v);
+    }
+    cc[j] = s;
+    ccmax = std::fmax(ccmax, s);
+    l1c = std::fmax(l1c, l1);
+  }
+  double xxmax, l1x;
+  big_point_side(c, xxmax, l1x);
+  const BigBounds bb = big_bounds(ccmax, l1c, xxmax, l1x, DQ, KB);
+  pl.thr1 = bb.thr1;
+  pl.thr3 = bb.thr3;
+  pl.thr_rel = bb.thr_rel;
+  pl.jbits = bb.jbits;
   pl.cinit.assign((size_t)KB * 32, 1.0e30f);
-  for (int j = 0; j < k; ++j) pl.cinit[j] = (float)(cc[j] + D);
+  for (int r = 0; r < KB * 32; ++r) {
+    const int j = 32 * (r / 32) + big_row(r % 32);
+    if (j < k) pl.cinit[r] = (float)(cc[j] + bb.D);
+  }
   pl.frag1.assign((size_t)KB * DQ * 64, h8{});
-  pl.frag3.assign((size_t)KB * 2 * DQ * 64, h8{});
   for (int b = 0; b < KB; ++b)
     for (int cq = 0; cq < DQ; ++cq)
-      for (int lane = 0; lane < 64; ++lane) {
-        const int j = 32 * b + (lane & 31);
-        const int hh = lane >> 5;
-        h8 A1 = {}, A3 = {};
-        for (int i = 0; i < 8; ++i) {
-          const int f = 16 * cq + 8 * hh + i;
-          if (j >= k || f >= d) continue;
-          const double v = ch[(size_t)j * d + f];
-          const _Float16 hi = (_Float16)v;
-          const _Float16 lo = (_Float16)(v - (double)hi);
-          A1[i] = (_Float16)(-2.0 * (double)hi);
-          A3[i] = (_Float16)(-2.0 * (double)lo);
-        }
-        pl.frag1[((size_t)b * DQ + cq) * 64 + lane] = A1;
-        pl.frag3[((size_t)(b * 2 + 0) * DQ + cq) * 64 + lane] = A1;
-        pl.frag3[((size_t)(b * 2 + 1) * DQ + cq) * 64 + lane] = A3;
-      }
+      for (int lane = 0; lane < 64; ++lane)
+        pl.frag1[((size_t)b * DQ + cq) * 64 + lane] =
+            big_frag_lane(C, mu.data(), sc, k, d, b, cq, lane);
+}
+
+// Device-resident loop (loop.hip): the same plan built on the device from the
+// loop's centroids, into the layout big_step uploads (frag1 | cinit | C |
+// {thr1, thr_rel}).  One 1024-thread workgroup; gated on the loop state.
+struct BigPlanArgs {
+  const double* C;
+  const double* mu;  // double[d]
+  double sc, xxmax, l1x;
+  int k, d, DQ, KB;
+  h8* frag1;
+  float* cinit;
+  double* C64;
+  float* thr;
+  const long long* gate;
+};
+
+__global__ __launch_bounds__(1024) void big_plan_kernel(BigPlanArgs a) {
+  if (a.gate && a.gate[0] == 0) return;
+  extern __shared__ double scc[];  // [k]
+  __shared__ double rmax[2][16];
+  __shared__ double sD;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int k = a.k, d = a.d;
+  double m0 = 0.0, m1 = 0.0;
+  for (int j = t; j < k; j += blockDim.x) {
+    double s = 0.0, l1 = 0.0;
+    for (int f = 0; f < d; ++f) {
+      const double v = (a.C[(size_t)j * d + f] - a.mu[f]) * a.sc;
+      s += v * v;
+      l1 += fabs(v);
+    }
+    scc[j] = s;
+    m0 = fmax(m0, s);
+    m1 = fmax(m1, l1);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    m0 = fmax(m0, __shfl_xor(m0, o));
+    m1 = fmax(m1, __shfl_xor(m1, o));
+  }
+  if (lane == 0) {
+    rmax[0][w] = m0;
+    rmax[1][w] = m1;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double ccmax = 0.0, l1c = 0.0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      ccmax = fmax(ccmax, rmax[0][i]);
+      l1c = fmax(l1c, rmax[1][i]);
+    }
+    const BigBounds bb = big_bounds(ccmax, l1c, a.xxmax, a.l1x, a.DQ, a.KB);
+    sD = bb.D;
+    a.thr[0] = bb.thr1;
+    a.thr[1] = bb.thr_rel;
+  }
+  __syncthreads();
+  const double D = sD;
+  for (int r = t; r < a.KB * 32; r += blockDim.x) {
+    const int j = 32 * (r / 32) + big_row(r % 32);
+    a.cinit[r] = j < k ? (float)(scc[j] + D) : 1.0e30f;
+  }
+  for (int e = t; e < a.KB * a.DQ * 64; e += blockDim.x) {
+    const int l = e & 63, bc = e >> 6;
+    a.frag1[e] = big_frag_lane(a.C, a.mu, a.sc, k, d, bc / a.DQ, bc % a.DQ, l);
+  }
+  for (int e = t; e < k * d; e += blockDim.x) a.C64[e] = a.C[e];
 }
 
 template <int DQ>
 static void launch_big_levels(Ctx& c, const BigArgs& a1, const BigArgs& a2, dim3 g1, dim3 g2,
                               size_t lds1, const double* dC, int32_t* ovf, int32_t* ovf_count,
-                              bool prof) {
+                              bool prof, bool sp) {
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&screen_big<DQ, 1, false, true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&screen_big_sp<DQ, 512>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&screen_big_sp<DQ, 768>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL((screen_big<DQ, 1, false, true>), g1, dim3(kBigThreads), lds1, c.stream, a1);
+  if (sp && big_sp_threads(DQ) == 768)
+    hipLaunchKernelGGL((screen_big_sp<DQ, 768>), g1, dim3(768), lds1, c.stream, a1);
+  else if (sp)
+    hipLaunchKernelGGL((screen_big_sp<DQ, 512>), g1, dim3(512), lds1, c.stream, a1);
+  else
+    hipLaunchKernelGGL((screen_big<DQ, 1, false, true>), g1, dim3(kBigThreads), lds1, c.stream,
+                       a1);
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);  // the L1 screen alone
 #ifdef CDR_EXPERIMENTS
@@ -675,28 +1043,43 @@ static void launch_big_levels(Ctx& c, const BigArgs& a1, const BigArgs& a2, dim3
 // One F32X Lloyd step in the large regime: labels for every point and the
 // exact int64 (k, d+1) sums/counts in dout (device).  Returns false when the
 // shape is not covered (nothing launched).
+// Plan buffer layout (c.frag): frag1 | cinit | C (fp64) | {thr1, thr_rel}.
+struct BigLayout {
+  size_t b1, bc, bC, bt, all;
+};
+static BigLayout big_layout(int k, int d) {
+  const int DQ = big_dq(d), KB = (k + 31) / 32;
+  BigLayout l;
+  l.b1 = (size_t)KB * DQ * 64 * sizeof(h8);
+  l.bc = (size_t)KB * 32 * sizeof(float);
+  l.bC = sizeof(double) * (size_t)k * d;
+  l.bt = 16;
+  l.all = (l.b1 + l.bc + l.bC + l.bt + 15) / 16 * 16;
+  return l;
+}
+
+static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* thr_dev,
+                       const long long* gate, long long* dout, bool prof);
+
 bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof) {
   if (!big_supported(c, k)) return false;
   ensure_precentered(c);
   PlanBig pl;
   build_plan_big(c, C, k, pl);
-  const int d = c.d, DQ = big_dq(d), KB = (k + 31) / 32, Q = d4_of(d) / 4;
-  const int cus = lloyd_num_cus(c.device);
+  const int d = c.d;
+  const BigLayout L = big_layout(k, d);
   // one upload: frag1 | cinit | C (fp64)
-  const size_t b1 = pl.frag1.size() * sizeof(h8), b3 = 0;
-  const size_t bc = pl.cinit.size() * sizeof(float), bC = sizeof(double) * (size_t)k * d;
-  const size_t ball = b1 + b3 + bc + bC;
   if (c.up_pending) HIP_CHECK(hipEventSynchronize(c.up_event));
-  c.h_up.ensure((ball + 15) / 16 * 16);
+  c.h_up.ensure(L.all);
   char* hp = static_cast<char*>(c.h_up.p);
-  memcpy(hp, pl.frag1.data(), b1);
-  memcpy(hp + b1 + b3, pl.cinit.data(), bc);
-  memcpy(hp + b1 + b3 + bc, C, bC);
-  c.frag.ensure((ball + 15) / 16 * 16);
+  memcpy(hp, pl.frag1.data(), L.b1);
+  memcpy(hp + L.b1, pl.cinit.data(), L.bc);
+  memcpy(hp + L.b1 + L.bc, C, L.bC);
+  c.frag.ensure(L.all);
   {
     void* hdev = nullptr;
     HIP_CHECK(hipHostGetDevicePointer(&hdev, c.h_up.p, 0));
-    const int64_t n16 = (int64_t)((ball + 15) / 16);
+    const int64_t n16 = (int64_t)((L.b1 + L.bc + L.bC + 15) / 16);
     hipLaunchKernelGGL(pull_host_big, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0,
                        c.stream, static_cast<const uint4*>(hdev), static_cast<uint4*>(c.frag.p),
                        n16);
@@ -705,15 +1088,62 @@ bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof) {
   if (!c.up_event) HIP_CHECK(hipEventCreateWithFlags(&c.up_event, hipEventDisableTiming));
   HIP_CHECK(hipEventRecord(c.up_event, c.stream));
   c.up_pending = true;
+  return big_launch(c, k, pl.thr1, pl.thr_rel, nullptr, nullptr, dout, prof);
+}
+
+// The device-resident loop's plan (loop.hip): built on the device from the
+// loop's centroids dC (fp64, k x d) into c.frag; gate = the loop state.
+void big_plan_device(Ctx& c, int k, const double* dC, const double* dmu, const long long* gate) {
+  const int d = c.d, DQ = big_dq(d), KB = (k + 31) / 32;
+  const BigLayout L = big_layout(k, d);
+  c.frag.ensure(L.all);
+  char* dp = static_cast<char*>(c.frag.p);
+  BigPlanArgs a;
+  a.C = dC;
+  a.mu = dmu;
+  a.sc = std::ldexp(1.0, c.sigma);
+  big_point_side(c, a.xxmax, a.l1x);
+  a.k = k;
+  a.d = d;
+  a.DQ = DQ;
+  a.KB = KB;
+  a.frag1 = reinterpret_cast<h8*>(dp);
+  a.cinit = reinterpret_cast<float*>(dp + L.b1);
+  a.C64 = reinterpret_cast<double*>(dp + L.b1 + L.bc);
+  a.thr = reinterpret_cast<float*>(dp + L.b1 + L.bc + L.bC);
+  a.gate = gate;
+  hipLaunchKernelGGL(big_plan_kernel, dim3(1), dim3(1024), sizeof(double) * (size_t)k, c.stream,
+                     a);
+  HIP_CHECK(hipGetLastError());
+}
+
+// One step on the device plan in c.frag (no host round trip); gate as above.
+bool big_step_dev(Ctx& c, int k, long long* dout, bool prof, const long long* gate) {
+  if (!big_supported(c, k)) return false;
+  ensure_precentered(c);
+  const BigLayout L = big_layout(k, c.d);
+  const float* thr = reinterpret_cast<const float*>(static_cast<char*>(c.frag.p) + L.b1 + L.bc +
+                                                    L.bC);
+  return big_launch(c, k, 0.0f, 0.0f, thr, gate, dout, prof);
+}
+
+static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* thr_dev,
+                       const long long* gate, long long* dout, bool prof) {
+  const int d = c.d, DQ = big_dq(d), KB = (k + 31) / 32, Q = d4_of(d) / 4;
+  const int cus = lloyd_num_cus(c.device);
+  const BigLayout L = big_layout(k, d);
   char* dp = static_cast<char*>(c.frag.p);
   const h8* dfrag1 = reinterpret_cast<const h8*>(dp);
-  const float* dcin = reinterpret_cast<const float*>(dp + b1 + b3);
-  const double* dC = reinterpret_cast<const double*>(dp + b1 + b3 + bc);
+  const float* dcin = reinterpret_cast<const float*>(dp + L.b1);
+  const double* dC = reinterpret_cast<const double*>(dp + L.b1 + L.bc);
+  int JB = 5;
+  while ((1 << (JB - 5)) < KB) ++JB;
 
   // level 1: persistent, one kBigThreads workgroup per CU (LDS-bound)
   const size_t lds1 = big_l1_lds(k, d);
   const int64_t groups = (c.n + 63) / 64;
-  const int wpb1 = kBigThreads / 64;
+  static const bool sp = !(std::getenv("CDR_BIG_L1") && std::atoi(std::getenv("CDR_BIG_L1")) == 0);
+  const int wpb1 = (sp ? big_sp_threads(DQ) : kBigThreads) / 64;
   const int nwg1 = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (groups + wpb1 - 1) / wpb1));
   const int nw1 = nwg1 * wpb1;
   if (nw1 > kMaxRegions) return false;
@@ -734,6 +1164,17 @@ bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof) {
   c.fb_layout = -1;       // screen32 must re-zero its counter layout
   BigArgs a;
   a.XT = c.xt32.as<float>();
+  a.XB = nullptr;
+  if (sp) {
+    if (!c.xb_valid) {
+      c.xb16.ensure((size_t)(c.n_pad >> 6) * 2 * DQ * 64 * 16);
+      hipLaunchKernelGGL(big_frag_copy, dim3(4096), dim3(256), 0, c.stream, c.xt32.as<float>(),
+                         c.n, c.n_pad, Q, DQ, c.xb16.as<uint4>());
+      HIP_CHECK(hipGetLastError());
+      c.xb_valid = true;
+    }
+    a.XB = c.xb16.as<h8>();
+  }
   a.n = c.n;
   a.n_pad = c.n_pad;
   a.d = d;
@@ -742,8 +1183,11 @@ bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof) {
   a.KB = KB;
   a.frag = dfrag1;
   a.cinit = dcin;
-  a.thr0 = pl.thr1;
-  a.thr_rel = pl.thr_rel;
+  a.thr0 = thr1;
+  a.thr_rel = thr_rel;
+  a.thr_dev = thr_dev;
+  a.gate = gate;
+  a.jkeep = ~((1u << JB) - 1u) | 15u;
   a.labels = c.labels.as<int32_t>();
   a.in_list = nullptr;
   a.in_count = nullptr;
@@ -758,16 +1202,23 @@ bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof) {
   a2.in_count = cnt1;
   a2.in_cap = cap1;
   a2.in_regions = nw1;
-  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_big<%d,1,false,true>", DQ);
+  if (sp)
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_big_sp<%d,%d>", DQ, big_sp_threads(DQ));
+  else
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen_big<%d,1,false,true>", DQ);
   if (prof) prof_mark(c, 0);
   switch (DQ) {
-    case 1: launch_big_levels<1>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
-    case 2: launch_big_levels<2>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
-    case 3: launch_big_levels<3>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
-    default: launch_big_levels<4>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof); break;
+    case 1: launch_big_levels<1>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof,
+                                  sp); break;
+    case 2: launch_big_levels<2>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof,
+                                  sp); break;
+    case 3: launch_big_levels<3>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof,
+                                  sp); break;
+    default: launch_big_levels<4>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof,
+                                  sp); break;
   }
   hipLaunchKernelGGL(exact_big, dim3(cus * 4), dim3(64), 0, c.stream, c.x32.as<float>(), c.n_pad,
-                     d, dC, k, ovf, ovf_count, c.labels.as<int32_t>());
+                     d, dC, k, ovf, ovf_count, c.labels.as<int32_t>(), gate);
   HIP_CHECK(hipGetLastError());
   // update from the labels
   const int len = k * (d + 1);
@@ -790,13 +1241,13 @@ bool big_step(Ctx& c, const double* C, int k, long long* dout, bool prof) {
   unsigned long long* uo = reinterpret_cast<unsigned long long*>(dout);
   if (FG == 16)
     hipLaunchKernelGGL(update_big<16>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
-                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo);
+                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo, gate);
   else if (FG == 8)
     hipLaunchKernelGGL(update_big<8>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
-                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo);
+                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo, gate);
   else
     hipLaunchKernelGGL(update_big<4>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
-                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo);
+                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo, gate);
   HIP_CHECK(hipGetLastError());
   c.run_valid = false;
   return true;

@@ -26,10 +26,12 @@ def _loop(ctx, C0, max_iter, tol, X=None, n=None):
 
 
 @pytest.mark.parametrize("n,d,k", [(200000, 16, 64), (90000, 8, 16), (50000, 5, 7),
-                                   (40000, 24, 33), (20000, 64, 300)])
+                                   (40000, 24, 33), (20000, 64, 300), (30000, 40, 700),
+                                   (12000, 9, 1100)])
 def test_loop_matches_oracle_fixed_steps(ctx, n, d, k):
-    """tol disabled: max_iter steps; screen32 shapes use the device plan,
-    the others (d > 16 or k > 64) the host-plan path through the same loop."""
+    """tol disabled: max_iter steps; screen32 shapes and the large-k shapes
+    (screen_big) use device-built plans, the others (e.g. d = 24, k = 33) the
+    host-plan path through the same loop."""
     X = synth.generate(n, 0, n, d, k, 31 * n + d)
     ctx.load_points(X)
     rng = np.random.default_rng(k)
