@@ -121,6 +121,12 @@ struct Ctx {
   // MFMA B fragments are loaded, [n_pad/64][2 tiles][DQ chunks][64 lanes] x 16 B
   DevBuf xb16;
   bool xb_valid = false;
+  bool xa_valid = false;  // xa32 built (ensure_rowmajor)
+  // large-k running sums (screen_big DELTA steps): int64 (k, d+1) of the
+  // current labels, valid while only large-k steps of k = big_k wrote them
+  DevBuf big_sums;
+  bool big_valid = false;
+  int big_k = 0;
   bool xs_valid = false;
   int xs_qh = 0;
   DevBuf mv_list;   // screen32d: per-wave regions of moved points {pt, old | new << 16}

@@ -261,6 +261,8 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   c.xt_valid = false;
   c.xs_valid = false;
   c.xb_valid = false;
+  c.xa_valid = false;
+  c.big_valid = false;
   c.mu_s.ensure(sizeof(float) * (d > 0 ? d : 1));
   HIP_CHECK(hipMemcpyAsync(c.mu_s.p, ms.data(), sizeof(float) * d,
                            hipMemcpyHostToDevice, c.stream));
@@ -275,6 +277,7 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   }
   c.have_labels = false;
   c.run_valid = false;
+  c.big_valid = false;
   c.seed_scanned = false;
 }
 
@@ -289,6 +292,8 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
   c.xs_valid = false;
   c.xb16.release();
   c.xb_valid = false;
+  c.xa_valid = false;
+  c.big_valid = false;
   c.pre_ok = false;
   c.n = n;
   c.d = d;
@@ -414,7 +419,7 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.gb_p1, &c.gb_p2, &c.gb_hist2, &c.gb_list, &c.gb_slots, &c.sim_cnt, &c.sim_off,
                     &c.sim_tmp, &c.sim_ms, &c.sim_mbase, &c.x_small, &c.x_buf, &c.x_prim, &c.f64x_A, &c.f64x_cnt, &c.f64x_E,
                     &c.f64x_T, &c.f64x_walk, &c.med_hist,
-                    &c.fb_accum, &c.xs16, &c.xa32, &c.xb16, &c.mv_list, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
+                    &c.fb_accum, &c.xs16, &c.xa32, &c.xb16, &c.big_sums, &c.mv_list, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
                     &c.ll_state};
   for (DevBuf* b : bufs) b->release();
   c.h_small.release();

@@ -1200,13 +1200,20 @@ __global__ void aos_copy_kernel(const float4* __restrict__ x, int64_t n_pad, int
 
 // Split screen copy and row-major copy (screen32d / fixup32), built once per
 // point set.
-static void ensure_split(Ctx& c, int QH) {
-  if (c.xs_valid && c.xs_qh == QH) return;
+// The row-major copy alone (also the large-k path's gathers, screen_big.hip).
+void ensure_rowmajor(Ctx& c) {
+  if (c.xa_valid) return;
   const int Q = d4_of(c.d) / 4;
   c.xa32.ensure(sizeof(float) * (size_t)c.n_pad * 4 * Q);
   hipLaunchKernelGGL(aos_copy_kernel, dim3(4096), dim3(256), 0, c.stream, c.x32.as<float4>(),
                      c.n_pad, Q, c.xa32.as<float4>());
   HIP_CHECK(hipGetLastError());
+  c.xa_valid = true;
+}
+
+static void ensure_split(Ctx& c, int QH) {
+  if (c.xs_valid && c.xs_qh == QH) return;
+  ensure_rowmajor(c);
   c.xs16.ensure((size_t)c.n_pad * 32 * QH);
   const float sig = (float)std::ldexp(1.0, c.sigma);
   if (QH == 1)
@@ -1372,6 +1379,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
     }
   }
   c.run_valid = false;
+  c.big_valid = false;  // screen32 writes the labels the large-k running sums follow
   c.last_delta = delta;
   if (thr_out) {
     thr_out[0] = pl.thr0;

@@ -61,6 +61,17 @@ struct BigArgs {
   const float* thr_dev;   // device plan: {thr0, thr_rel} in device memory (else the values above)
   const long long* gate;  // device loop state: nothing runs once gate[0] == 0
   unsigned jkeep;       // screen_big_sp: bits of a keyed value kept when its block is merged
+  // DELTA steps (labels of the previous large-k step in place): a label is
+  // written only when it changes, and the change {pt, old << 16 | new} goes
+  // to L1's per-wave regions (mv1, same capacity as out_list) or, from L2 /
+  // L3, to the flat list mv2 (count at mv2_count)
+  int delta;
+  int2* mv1;
+  int32_t* mv1_count;
+  int2* mv2;
+  int32_t* mv2_count;
+  const float* XA;      // the points row-major [n_pad][d4] (ensure_rowmajor)
+  int d4;
   int32_t* labels;
   // GATHER input: per-region point lists of the previous level
   const int32_t* in_list;
@@ -365,10 +376,16 @@ __global__ __launch_bounds__(NT) void screen_big_sp(BigArgs a) {
     }
   };
   fetch(wave_id);
+  int2* mv_region = a.delta ? a.mv1 + (size_t)wave_id * a.out_cap : nullptr;
+  int mv_used = 0;
   for (int64_t g = wave_id; g < items; g += nwaves) {
     const int64_t base = g << 6;
     const int64_t pt[2] = {base + p, base + 32 + p};
     const bool real[2] = {pt[0] < a.n, pt[1] < a.n};
+    // DELTA: the previous label of this lane's point (after the swap below:
+    // lanes < 32 tile 0's point, lanes >= 32 tile 1's), loaded now
+    const int64_t lpt = base + lane;
+    const int oldl = a.delta && lpt < a.n ? a.labels[lpt] : -1;
     h8 BH[2][DQ];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -450,7 +467,19 @@ __global__ __launch_bounds__(NT) void screen_big_sp(BigArgs a) {
     const bool myreal = h == 0 ? real[0] : real[1];
     // rows past k carry C = 1e30: never best, never a close runner-up
     const bool cert = __uint_as_float(krun) > fmaf(best, thr_rel, thr0);
-    if (myreal && cert) a.labels[mypt] = label;
+    if (!a.delta) {
+      if (myreal && cert) a.labels[mypt] = label;
+    } else {
+      const bool moved = myreal && cert && label != oldl;
+      if (moved) a.labels[mypt] = label;
+      const unsigned long long mvb = __ballot(moved);
+      if (mvb) {
+        const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(mvb >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((unsigned)mvb, 0u));
+        if (moved) mv_region[mv_used + r] = int2{(int)mypt, (oldl << 16) | label};
+        mv_used += __popcll(mvb);
+      }
+    }
     const unsigned long long need = __ballot(myreal && !cert);
     if (need) {
       const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
@@ -465,6 +494,7 @@ __global__ __launch_bounds__(NT) void screen_big_sp(BigArgs a) {
   if (lane == 0) {
     a.out_count[wave_id] = used;
     if (used) atomicAdd(a.out_count + nwaves, used);
+    if (a.delta) a.mv1_count[wave_id] = mv_used;
   }
 }
 
@@ -589,13 +619,21 @@ __global__ __launch_bounds__(256) void cand_big(BigArgs a, const float* __restri
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int c = 0; c < DQ; ++c) {
-          const int q0 = 4 * c + 2 * h;
-          f4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
-          if (real[t] && q0 < a.Q) v0 = X4[(int64_t)q0 * a.n_pad + pt[t]];
-          if (real[t] && q0 + 1 < a.Q) v1 = X4[(int64_t)(q0 + 1) * a.n_pad + pt[t]];
-          u4v H = {pack_h2(v0[0], v0[1]), pack_h2(v0[2], v0[3]), pack_h2(v1[0], v1[1]),
-                   pack_h2(v1[2], v1[3])};
-          BH[t][c] = __builtin_bit_cast(h8, H);
+          if (a.XB) {
+            // the point's fragment in its group's block of the fp16 copy (one
+            // 8 KB block per point, not DQ pages of the fp32 copy)
+            const int64_t q = pt[t];
+            const int64_t idx = (((q >> 6) * 2 + ((q >> 5) & 1)) * DQ + c) * 64 + h * 32 + (q & 31);
+            BH[t][c] = real[t] ? a.XB[idx] : h8{};
+          } else {
+            const int q0 = 4 * c + 2 * h;
+            f4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+            if (real[t] && q0 < a.Q) v0 = X4[(int64_t)q0 * a.n_pad + pt[t]];
+            if (real[t] && q0 + 1 < a.Q) v1 = X4[(int64_t)(q0 + 1) * a.n_pad + pt[t]];
+            u4v H = {pack_h2(v0[0], v0[1]), pack_h2(v0[2], v0[3]), pack_h2(v1[0], v1[1]),
+                     pack_h2(v1[2], v1[3])};
+            BH[t][c] = __builtin_bit_cast(h8, H);
+          }
         }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -646,9 +684,11 @@ __global__ __launch_bounds__(256) void cand_big(BigArgs a, const float* __restri
           // candidate's fp64 row (L2-resident) in NumPy's pairwise order
           float xv[16 * DQ];
           const f4* X04 = reinterpret_cast<const f4*>(X0);
+          const f4* XA4 = reinterpret_cast<const f4*>(a.XA);
 #pragma unroll
           for (int q = 0; q < 4 * DQ; ++q) {
-            const f4 v = q < a.Q ? X04[(int64_t)q * a.n_pad + mypt] : f4{0.f, 0.f, 0.f, 0.f};
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            if (q < a.Q) v = XA4 ? XA4[mypt * a.Q + q] : X04[(int64_t)q * a.n_pad + mypt];
 #pragma unroll
             for (int i = 0; i < 4; ++i) xv[4 * q + i] = v[i];
           }
@@ -663,7 +703,15 @@ __global__ __launch_bounds__(256) void cand_big(BigArgs a, const float* __restri
               jb = j;
             }
           }
-          a.labels[mypt] = jb;
+          if (!a.delta) {
+            a.labels[mypt] = jb;
+          } else {
+            const int oldl = a.labels[mypt];
+            if (jb != oldl) {
+              a.labels[mypt] = jb;
+              a.mv2[atomicAdd(a.mv2_count, 1)] = int2{(int)mypt, (oldl << 16) | jb};
+            }
+          }
         }
       }
     }
@@ -682,7 +730,9 @@ __global__ __launch_bounds__(64) void exact_big(const float* __restrict__ X, int
                                                 const int32_t* __restrict__ list,
                                                 const int32_t* __restrict__ count,
                                                 int32_t* __restrict__ labels,
-                                                const long long* __restrict__ gate) {
+                                                const long long* __restrict__ gate,
+                                                int2* __restrict__ mv2,
+                                                int32_t* __restrict__ mv2_count) {
   if (gate && gate[0] == 0) return;
   __shared__ double sx[128];
   const int lane = threadIdx.x;
@@ -729,7 +779,18 @@ __global__ __launch_bounds__(64) void exact_big(const float* __restrict__ X, int
         jmin = jo;
       }
     }
-    if (lane == 0) labels[pt] = jmin < k ? jmin : 0;
+    if (lane == 0) {
+      const int jl = jmin < k ? jmin : 0;
+      if (!mv2) {
+        labels[pt] = jl;
+      } else {  // DELTA step: record a change
+        const int oldl = labels[pt];
+        if (jl != oldl) {
+          labels[pt] = jl;
+          mv2[atomicAdd(mv2_count, 1)] = int2{(int)pt, (oldl << 16) | jl};
+        }
+      }
+    }
   }
 }
 
@@ -786,11 +847,83 @@ __global__ __launch_bounds__(1024) void update_big(const float* __restrict__ X, 
       if (tcnt[j]) atomicAdd(&out[(size_t)j * d1 + d], (unsigned long long)(long long)tcnt[j]);
 }
 
+__global__ void zero_big_gated(long long* __restrict__ p, int64_t n,
+                               const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0;
+}
+
+// DELTA update: the moves {pt, old << 16 | new} of L1's per-wave regions
+// (mv1, counts cnt1) and of L2 / L3 (flat mv2, count *cnt2) applied to the
+// running (k, d+1) int64 sums: +x into the new cluster, -x out of the old,
+// x gathered from the row-major copy.  blockIdx.y = feature group (FG
+// features), blockIdx.x = slice of the moves; an LDS table [FG][k] of fp64
+// (exact: grid values) per workgroup, then its nonzero cells as exact int64
+// fixed point with atomics.  Integer sums: equal to a full recompute.
+constexpr int kFixSlices = 32;
+
+template <int FG>
+__global__ __launch_bounds__(1024) void fixup_big(const float* __restrict__ XA, int d4, int d,
+                                                  int k, const int2* __restrict__ mv1,
+                                                  const int32_t* __restrict__ cnt1, int nw1,
+                                                  int cap1, const int2* __restrict__ mv2,
+                                                  const int32_t* __restrict__ cnt2, double fx,
+                                                  unsigned long long* __restrict__ out,
+                                                  const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* tsum = reinterpret_cast<double*>(smem);              // [FG][k]
+  int* tcnt = reinterpret_cast<int*>(tsum + (size_t)FG * k);   // [k]
+  const int g = blockIdx.y, f0 = FG * g;
+  const int G = gridDim.x, sl = blockIdx.x;
+  for (int i = threadIdx.x; i < FG * k; i += blockDim.x) tsum[i] = 0.0;
+  for (int i = threadIdx.x; i < k; i += blockDim.x) tcnt[i] = 0;
+  __syncthreads();
+  auto apply = [&](const int2* list, int64_t cnt) {
+    for (int64_t idx = threadIdx.x; idx < cnt * FG; idx += blockDim.x) {
+      const int64_t e = idx / FG;
+      const int ff = (int)(idx - e * FG);
+      const int f = f0 + ff;
+      const int2 m = list[e];
+      const int oldl = (int)((unsigned)m.y >> 16), newl = m.y & 0xFFFF;
+      if (f < d) {
+        const double x = (double)XA[(int64_t)m.x * d4 + f];
+        atomicAdd(&tsum[ff * k + newl], x);
+        atomicAdd(&tsum[ff * k + oldl], -x);
+      }
+      if (ff == 0 && g == 0) {
+        atomicAdd(&tcnt[newl], 1);
+        atomicAdd(&tcnt[oldl], -1);
+      }
+    }
+  };
+  for (int r = sl; r < nw1; r += G) apply(mv1 + (size_t)r * cap1, cnt1[r]);
+  {
+    const int64_t n2 = *cnt2, per = (n2 + G - 1) / G;
+    const int64_t e0 = (int64_t)sl * per, e1 = min(n2, e0 + per);
+    if (e1 > e0) apply(mv2 + e0, e1 - e0);
+  }
+  __syncthreads();
+  const int d1 = d + 1;
+  for (int i = threadIdx.x; i < FG * k; i += blockDim.x) {
+    const int f = f0 + i / k, j = i % k;
+    const double s = tsum[i];
+    if (f < d && s != 0.0)
+      atomicAdd(&out[(size_t)j * d1 + f], (unsigned long long)__double2ll_rn(s * fx));
+  }
+  if (g == 0)
+    for (int j = threadIdx.x; j < k; j += blockDim.x)
+      if (tcnt[j]) atomicAdd(&out[(size_t)j * d1 + d], (unsigned long long)(long long)tcnt[j]);
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 extern int lloyd_num_cus(int device);
 void ensure_precentered(Ctx& c);
+void ensure_rowmajor(Ctx& c);
 
 static int big_dq(int d) { return (d + 15) / 16; }
 // L1 workgroup size: 3 waves per SIMD while the pipelined kernel fits 168
@@ -1188,6 +1321,28 @@ static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* th
   a.thr_dev = thr_dev;
   a.gate = gate;
   a.jkeep = ~((1u << JB) - 1u) | 15u;
+  // DELTA: the running sums follow the labels of the previous large-k step
+  // of this k (pipelined L1 only); moves go to c.mv_list, the sums are
+  // updated by fixup_big instead of a pass over every point
+  static const bool nodelta = std::getenv("CDR_BIG_NODELTA") != nullptr;
+  const bool delta = sp && !nodelta && c.big_valid && c.big_k == k;
+  a.delta = delta ? 1 : 0;
+  a.mv1 = nullptr;
+  a.mv1_count = nullptr;
+  a.mv2 = nullptr;
+  a.mv2_count = nullptr;
+  if (sp) ensure_rowmajor(c);
+  a.XA = sp ? c.xa32.as<float>() : nullptr;
+  a.d4 = d4_of(d);
+  if (delta) {
+    c.mv_list.ensure(sizeof(int2) * 2 * slots);
+    c.mv_count.ensure(sizeof(int32_t) * (size_t)(nw1 + 2));
+    HIP_CHECK(hipMemsetAsync(c.mv_count.p, 0, sizeof(int32_t) * (size_t)(nw1 + 2), c.stream));
+    a.mv1 = c.mv_list.as<int2>();
+    a.mv1_count = c.mv_count.as<int32_t>();
+    a.mv2 = a.mv1 + slots;
+    a.mv2_count = a.mv1_count + nw1;
+  }
   a.labels = c.labels.as<int32_t>();
   a.in_list = nullptr;
   a.in_count = nullptr;
@@ -1218,37 +1373,59 @@ static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* th
                                   sp); break;
   }
   hipLaunchKernelGGL(exact_big, dim3(cus * 4), dim3(64), 0, c.stream, c.x32.as<float>(), c.n_pad,
-                     d, dC, k, ovf, ovf_count, c.labels.as<int32_t>(), gate);
+                     d, dC, k, ovf, ovf_count, c.labels.as<int32_t>(), gate, a.mv2, a.mv2_count);
   HIP_CHECK(hipGetLastError());
-  // update from the labels
+  // the sums: a full pass over the points (first step) or the moves only
   const int len = k * (d + 1);
-  HIP_CHECK(hipMemsetAsync(dout, 0, sizeof(long long) * len, c.stream));
+  c.big_sums.ensure(sizeof(long long) * len);
+  unsigned long long* bs = c.big_sums.as<unsigned long long>();
   const int FG = big_fg(k);
   const int ngrp = (d + FG - 1) / FG;
   const size_t ldsu = (size_t)FG * k * 8 + (size_t)k * 4;
-  const dim3 gu(cus, ngrp);
   static bool uattr = false;
   if (!uattr) {
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&update_big<16>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&update_big<8>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&update_big<4>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const void* fns[] = {reinterpret_cast<const void*>(&update_big<16>),
+                         reinterpret_cast<const void*>(&update_big<8>),
+                         reinterpret_cast<const void*>(&update_big<4>),
+                         reinterpret_cast<const void*>(&fixup_big<16>),
+                         reinterpret_cast<const void*>(&fixup_big<8>),
+                         reinterpret_cast<const void*>(&fixup_big<4>)};
+    for (const void* f : fns)
+      HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     uattr = true;
   }
   const double fx = std::ldexp(1.0, c.scale_bits);
-  unsigned long long* uo = reinterpret_cast<unsigned long long*>(dout);
-  if (FG == 16)
-    hipLaunchKernelGGL(update_big<16>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
-                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo, gate);
-  else if (FG == 8)
-    hipLaunchKernelGGL(update_big<8>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
-                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo, gate);
-  else
-    hipLaunchKernelGGL(update_big<4>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
-                       c.n_pad, d, k, c.labels.as<int32_t>(), fx, uo, gate);
+  if (!delta) {
+    hipLaunchKernelGGL(zero_big_gated, dim3(64), dim3(256), 0, c.stream,
+                       reinterpret_cast<long long*>(bs), (int64_t)len, gate);
+    const dim3 gu(cus, ngrp);
+    if (FG == 16)
+      hipLaunchKernelGGL(update_big<16>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
+                         c.n_pad, d, k, c.labels.as<int32_t>(), fx, bs, gate);
+    else if (FG == 8)
+      hipLaunchKernelGGL(update_big<8>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
+                         c.n_pad, d, k, c.labels.as<int32_t>(), fx, bs, gate);
+    else
+      hipLaunchKernelGGL(update_big<4>, gu, dim3(1024), ldsu, c.stream, c.x32.as<float>(), c.n,
+                         c.n_pad, d, k, c.labels.as<int32_t>(), fx, bs, gate);
+  } else {
+    const dim3 gf(kFixSlices, ngrp);
+    const float* XA = c.xa32.as<float>();
+    const int d4 = d4_of(d);
+    if (FG == 16)
+      hipLaunchKernelGGL(fixup_big<16>, gf, dim3(1024), ldsu, c.stream, XA, d4, d, k, a.mv1,
+                         a.mv1_count, nw1, cap1, a.mv2, a.mv2_count, fx, bs, gate);
+    else if (FG == 8)
+      hipLaunchKernelGGL(fixup_big<8>, gf, dim3(1024), ldsu, c.stream, XA, d4, d, k, a.mv1,
+                         a.mv1_count, nw1, cap1, a.mv2, a.mv2_count, fx, bs, gate);
+    else
+      hipLaunchKernelGGL(fixup_big<4>, gf, dim3(1024), ldsu, c.stream, XA, d4, d, k, a.mv1,
+                         a.mv1_count, nw1, cap1, a.mv2, a.mv2_count, fx, bs, gate);
+  }
   HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpyAsync(dout, bs, sizeof(long long) * len, hipMemcpyDeviceToDevice, c.stream));
+  c.big_valid = true;
+  c.big_k = k;
   c.run_valid = false;
   return true;
 }
