@@ -68,6 +68,9 @@ def cpu_baseline(d: int, k: int, seed: int, rows: int = 1_000_000, iters: int = 
 
     from oracle import kmeans_oracle, synth
 
+    # a bounded sample (~10-20 s of NumPy): the oracle's assignment is O(rows k d)
+    rows = max(8192, min(rows, int(rows * (16 * 64) / (d * k))))
+
     X = synth.generate(rows, 0, rows, d, k, seed)
     C = X[:k].copy()
     t0 = time.perf_counter()

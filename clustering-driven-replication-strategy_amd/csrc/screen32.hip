@@ -666,7 +666,9 @@ struct S32DArgs {
   int cap;
 };
 
-template <int QH, int MT>
+// PD: groups of 64 points per wave in flight (the loads of PD - 1 groups are
+// issued ahead of the one being screened)
+template <int QH, int MT, int PD>
 __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
   if (a.gate && a.gate[0] == 0) return;
   const int lane = threadIdx.x & 63;
@@ -775,15 +777,17 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
     }
   };
   const int64_t gs = nwaves;
-  int64_t G = wave;
-  Buf b0, b1;
-  load(b0, G);
-  for (; G < ngroups; G += 2 * gs) {
-    load(b1, G + gs);
-    process(b0, G);
-    if (G + gs >= ngroups) break;
-    load(b0, G + 2 * gs);
-    process(b1, G + gs);
+  Buf buf[PD];
+#pragma unroll
+  for (int i = 0; i < PD - 1; ++i) load(buf[i], wave + i * gs);
+  for (int64_t G = wave; G < ngroups; G += PD * gs) {
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+      const int64_t Gi = G + i * gs;
+      if (Gi >= ngroups) break;
+      load(buf[(i + PD - 1) % PD], Gi + (PD - 1) * gs);
+      process(buf[i], Gi);
+    }
   }
   if (lane == 0) {
     a.fb_count[wave] = fb_used;
@@ -1227,16 +1231,24 @@ static void ensure_split(Ctx& c, int QH) {
   c.xs_qh = QH;
 }
 
-template <int QH, int MT>
+template <int QH, int MT, int PD>
 static int s32d_blocks_per_cu() {
   static int nb = 0;
   if (!nb) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32d<QH, MT>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32d<QH, MT, PD>, 256, 0) != hipSuccess ||
         nb < 1)
       nb = 2;
     if (nb > 8) nb = 8;
   }
   return nb;
+}
+
+// Prefetch depth of screen32d: CDR_S32D_PD=2|3|4 (comparisons), else the
+// measured default per shape.
+static int s32d_depth(int QH) {
+  static const int env = std::getenv("CDR_S32D_PD") ? std::atoi(std::getenv("CDR_S32D_PD")) : 0;
+  if (env >= 2 && env <= 4) return env;
+  return QH == 1 ? 3 : 2;  // A/B at configs 2 and 3: 3 helps the d <= 8 screen (0.108 -> 0.102 ms), not d = 16
 }
 
 // A DELTA step on screen32d + fixup32 (labels and running sums as screen32's).
@@ -1247,10 +1259,23 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
   int bpc;
-  if (QH == 1 && MT == 1) bpc = s32d_blocks_per_cu<1, 1>();
-  else if (QH == 1) bpc = s32d_blocks_per_cu<1, 2>();
-  else if (MT == 1) bpc = s32d_blocks_per_cu<2, 1>();
-  else bpc = s32d_blocks_per_cu<2, 2>();
+  const int PD = s32d_depth(QH);
+  if (PD == 4) {
+    if (QH == 1 && MT == 1) bpc = s32d_blocks_per_cu<1, 1, 4>();
+    else if (QH == 1) bpc = s32d_blocks_per_cu<1, 2, 4>();
+    else if (MT == 1) bpc = s32d_blocks_per_cu<2, 1, 4>();
+    else bpc = s32d_blocks_per_cu<2, 2, 4>();
+  } else if (PD == 3) {
+    if (QH == 1 && MT == 1) bpc = s32d_blocks_per_cu<1, 1, 3>();
+    else if (QH == 1) bpc = s32d_blocks_per_cu<1, 2, 3>();
+    else if (MT == 1) bpc = s32d_blocks_per_cu<2, 1, 3>();
+    else bpc = s32d_blocks_per_cu<2, 2, 3>();
+  } else {
+    if (QH == 1 && MT == 1) bpc = s32d_blocks_per_cu<1, 1, 2>();
+    else if (QH == 1) bpc = s32d_blocks_per_cu<1, 2, 2>();
+    else if (MT == 1) bpc = s32d_blocks_per_cu<2, 1, 2>();
+    else bpc = s32d_blocks_per_cu<2, 2, 2>();
+  }
   int nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * bpc);
   if (nwg < 1) nwg = 1;
   const int nwaves = nwg * 4;
@@ -1281,13 +1306,22 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   a.mv_list = c.mv_list.as<int2>();
   a.mv_count = c.mv_count.as<int32_t>();
   a.cap = cap;
-  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32d<%d,%d>", QH, MT);
+  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32d<%d,%d,%d>", QH, MT, s32d_depth(QH));
   if (prof) prof_mark(c, 0);
   const dim3 grid(nwg), blk(256);
-  if (QH == 1 && MT == 1) hipLaunchKernelGGL((screen32d<1, 1>), grid, blk, 0, c.stream, a);
-  else if (QH == 1) hipLaunchKernelGGL((screen32d<1, 2>), grid, blk, 0, c.stream, a);
-  else if (MT == 1) hipLaunchKernelGGL((screen32d<2, 1>), grid, blk, 0, c.stream, a);
-  else hipLaunchKernelGGL((screen32d<2, 2>), grid, blk, 0, c.stream, a);
+#define CDR_S32D_LAUNCH(P)                                                                  \
+  if (QH == 1 && MT == 1) hipLaunchKernelGGL((screen32d<1, 1, P>), grid, blk, 0, c.stream, a); \
+  else if (QH == 1) hipLaunchKernelGGL((screen32d<1, 2, P>), grid, blk, 0, c.stream, a);       \
+  else if (MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P>), grid, blk, 0, c.stream, a);       \
+  else hipLaunchKernelGGL((screen32d<2, 2, P>), grid, blk, 0, c.stream, a);
+  if (PD == 4) {
+    CDR_S32D_LAUNCH(4)
+  } else if (PD == 3) {
+    CDR_S32D_LAUNCH(3)
+  } else {
+    CDR_S32D_LAUNCH(2)
+  }
+#undef CDR_S32D_LAUNCH
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
   FixArgs f;
