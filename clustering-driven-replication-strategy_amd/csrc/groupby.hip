@@ -1012,6 +1012,120 @@ __global__ __launch_bounds__(64 * kGwWaves) void gb_bucket_wave(
   }
 }
 
+// The same for buckets of at most 4 files (L <= 2, config 4's shape): the
+// per-file count / writes / reads / local and the concurrency maximum are
+// kept in each lane's registers (select by the event's file, no ballots and
+// no per-file LDS atomics), the payload is decoded with 32-bit field
+// extracts, and the bucket's rows come from one wave reduction per value at
+// the end.  The (file, second) counts stay in the wave's LDS grid.  The
+// ballot kernel above spent ~165 instructions per 64 events here.
+template <typename T>
+__global__ __launch_bounds__(64 * kGwWaves) void gb_bucket_wave4(
+    const T* __restrict__ pb, const unsigned* __restrict__ bbase, int64_t nbuckets, int64_t nf,
+    GbPay p, const int32_t* __restrict__ primary, long long* __restrict__ out,
+    int* __restrict__ big_list, int* __restrict__ big_count) {
+  extern __shared__ unsigned long long lds[];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int KW = gw_grid_words(p.L, p.sbits);
+  unsigned* grid = reinterpret_cast<unsigned*>(reinterpret_cast<unsigned char*>(lds) +
+                                               (size_t)wv * gw_wave_bytes(p.L, p.sbits));
+  const int F = 1 << p.L;
+  const int sb = p.sbits;
+  const int nw = gridDim.x * kGwWaves;
+  for (int b = blockIdx.x * kGwWaves + wv; b < nbuckets; b += nw) {
+    const int s0 = (int)bbase[b];
+    const int n = (int)bbase[b + 1] - s0;
+    if (n > kGbDenseCap) {
+      if (lane == 0) big_list[atomicAdd(big_count, 1)] = b;
+      continue;
+    }
+    const int64_t f0 = (int64_t)b << p.L;
+    const int nfl = (int)min((int64_t)F, nf - f0);
+    T v[kGwUnroll];
+#pragma unroll
+    for (int u = 0; u < kGwUnroll; ++u) {
+      const int i = u * 64 + lane;
+      v[u] = i < n ? pb[s0 + i] : (T)0;
+    }
+    const int pl = lane < nfl ? primary[f0 + lane] : -2;
+    const uint4 z = {0u, 0u, 0u, 0u};
+    for (int i = lane * 4; i < KW; i += 256) *reinterpret_cast<uint4*>(grid + i) = z;
+    // the bucket's primaries (client code = client + 1; -1: none)
+    int pc[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) pc[f] = __builtin_amdgcn_readlane(pl, f) + 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    unsigned A[4] = {0u, 0u, 0u, 0u}, B[4] = {0u, 0u, 0u, 0u}, M[4] = {0u, 0u, 0u, 0u};
+    for (int i0 = 0; i0 < n; i0 += 64 * kGwUnroll) {
+      if (i0 > 0) {
+#pragma unroll
+        for (int u = 0; u < kGwUnroll; ++u) {
+          const int i = i0 + u * 64 + lane;
+          v[u] = i < n ? pb[s0 + i] : (T)0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kGwUnroll; ++u) {
+        if (i0 + u * 64 >= n) break;  // wave-uniform
+        if (i0 + u * 64 + lane < n) {
+          const unsigned long long x = (unsigned long long)v[u];
+          const unsigned lo = (unsigned)x;  // op, client and (4-byte payloads) all fields
+          const unsigned fl = (unsigned)(x >> p.fshift) & (unsigned)(F - 1);
+          const unsigned sc = (unsigned)(x >> p.sshift) & ((1u << sb) - 1u);
+          const unsigned oc = __builtin_amdgcn_ubfe(lo, p.cbits, 2);
+          const int cc = (int)__builtin_amdgcn_ubfe(lo, 0, p.cbits);
+          const unsigned key = (fl << sb) | sc;
+          const unsigned sh = (key & 1u) << 4;
+          const unsigned old = atomicAdd(&grid[key >> 1], 1u << sh);
+          const unsigned cnt = __builtin_amdgcn_ubfe(old, sh, 16) + 1u;
+          const int pf = fl == 0 ? pc[0] : fl == 1 ? pc[1] : fl == 2 ? pc[2] : pc[3];
+          const unsigned loc = (cc != 0 && pf > 0 && cc == pf) ? 1u : 0u;
+          const unsigned va = 1u | ((oc == 1u) ? 0x10000u : 0u);
+          const unsigned vb = ((oc == 2u) ? 1u : 0u) | (loc << 16);
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            const bool m = fl == (unsigned)f;
+            A[f] += m ? va : 0u;
+            B[f] += m ? vb : 0u;
+            M[f] = max(M[f], m ? cnt : 0u);
+          }
+        }
+      }
+    }
+    // wave sums / maxima of the lanes' per-file values
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      for (int o = 32; o > 0; o >>= 1) {
+        A[f] += (unsigned)__shfl_xor((int)A[f], o);
+        B[f] += (unsigned)__shfl_xor((int)B[f], o);
+        M[f] = max(M[f], (unsigned)__shfl_xor((int)M[f], o));
+      }
+    }
+    // rows f0 .. f0 + nfl, six fields each: one contiguous run of the output
+    long long* o = out + f0 * 6;
+    if (lane < 6 * nfl) {
+      const int f = lane / 6, fld = lane - 6 * f;
+      const unsigned a = f == 0 ? A[0] : f == 1 ? A[1] : f == 2 ? A[2] : A[3];
+      const unsigned bb = f == 0 ? B[0] : f == 1 ? B[1] : f == 2 ? B[2] : B[3];
+      const unsigned mm = f == 0 ? M[0] : f == 1 ? M[1] : f == 2 ? M[2] : M[3];
+      long long val;
+      switch (fld) {
+        case 0: val = a & 0xFFFFu; break;
+        case 1: val = a >> 16; break;
+        case 2: val = bb & 0xFFFFu; break;
+        case 3: val = bb >> 16; break;
+        case 4: val = a & 0xFFFFu; break;
+        default: val = mm; break;
+      }
+      o[lane] = val;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // Buckets over the LDS capacity: the hash lives in global memory (2 n slots
 // from gslots + 2 * s0, so buckets never overlap).
 template <typename T>
@@ -1126,9 +1240,14 @@ void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, bo
     const int64_t wgrid = std::min<int64_t>(ceil_div(nb, (int64_t)kGwWaves),
                                             (int64_t)lloyd_num_cus(c.device) * per_cu);
     c.gb_last_grid = wgrid;
-    hipLaunchKernelGGL(gb_bucket_wave<T>, dim3(wgrid), dim3(64 * kGwWaves), lds_w, c.stream, pb,
-                       bbase, nb, nf, p, c.ev_primary.as<int32_t>(), c.ev_out.as<long long>(),
-                       c.gb_list.as<int>(), big);
+    if (L <= 2 && !getenv("CDR_GB_BALLOT"))
+      hipLaunchKernelGGL(gb_bucket_wave4<T>, dim3(wgrid), dim3(64 * kGwWaves), lds_w, c.stream,
+                         pb, bbase, nb, nf, p, c.ev_primary.as<int32_t>(),
+                         c.ev_out.as<long long>(), c.gb_list.as<int>(), big);
+    else
+      hipLaunchKernelGGL(gb_bucket_wave<T>, dim3(wgrid), dim3(64 * kGwWaves), lds_w, c.stream,
+                         pb, bbase, nb, nf, p, c.ev_primary.as<int32_t>(),
+                         c.ev_out.as<long long>(), c.gb_list.as<int>(), big);
   } else {
     if (dense)
       HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(

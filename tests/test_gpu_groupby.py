@@ -151,3 +151,16 @@ def test_block_dense_kernel_agrees_with_wave_kernel(ctx, monkeypatch, nf, span):
     b, _ = _check(ctx, f, op, cl, ts, prim, dense=1)
     np.testing.assert_array_equal(a, b)
     assert a[nf - 1, 5] >= 3000
+
+
+@pytest.mark.parametrize("nf,span", [(744_000, 600), (2_000, 30), (700, 3)])
+def test_register_bucket_kernel_agrees_with_ballot_kernel(ctx, monkeypatch, nf, span):
+    """Buckets of <= 4 files: the register-accumulating wave kernel (default)
+    and the ballot wave kernel (CDR_GB_BALLOT=1) give the oracle's counts."""
+    rng = np.random.default_rng(31 + nf)
+    f, op, cl, ts, prim = _events(rng, 3_000_000, nf, span_s=span, nclients=3)
+    a, info = _check(ctx, f, op, cl, ts, prim, dense=1)
+    assert info["L"] <= 2, info
+    monkeypatch.setenv("CDR_GB_BALLOT", "1")
+    b, _ = _check(ctx, f, op, cl, ts, prim, dense=1)
+    np.testing.assert_array_equal(a, b)
