@@ -125,6 +125,7 @@ struct Ctx {
   // large-k running sums (screen_big DELTA steps): int64 (k, d+1) of the
   // current labels, valid while only large-k steps of k = big_k wrote them
   DevBuf big_sums;
+  DevBuf big_chunks;  // L2 chunk numbering of L1's regions (big_chunk_prefix)
   bool big_valid = false;
   int big_k = 0;
   bool xs_valid = false;

@@ -718,6 +718,195 @@ __global__ __launch_bounds__(256) void cand_big(BigArgs a, const float* __restri
   }
 }
 
+// L2 with the A fragments and C rows in LDS (the product L2 after
+// screen_big_sp; cand_big reads them from global memory per chunk, 7x L1's
+// cost per point).  One NT-thread workgroup per CU; the chunk numbering of
+// L1's regions comes from big_chunk_prefix (global memory: the LDS holds the
+// fragments).  Per chunk of 64 points: the same one-product screen as L1
+// (bit-identical: same fragments, same B operands from xb16), candidates
+// S_j <= best thr_rel + T1 into per-point LDS lists (u16), then the exact
+// fp64 evaluation of each point's candidates as cand_big.
+__global__ __launch_bounds__(1024) void big_chunk_prefix(const int32_t* __restrict__ cnt, int R,
+                                                         int32_t* __restrict__ pre) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int r0 = 0; r0 < R; r0 += 1024) {
+    const int r = r0 + threadIdx.x;
+    const int v = r < R ? (cnt[r] + 63) >> 6 : 0;
+    int inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    int base = carry;
+    for (int q = 0; q < w; ++q) base += wsum[q];
+    if (r < R) pre[r] = base + inc - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = base + inc;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) pre[R] = carry;
+}
+
+template <int DQ, int NT>
+__global__ __launch_bounds__(NT) void cand_big_lds(BigArgs a, const double* __restrict__ C64,
+                                                   const int32_t* __restrict__ chunk_pre,
+                                                   int32_t* __restrict__ ovf,
+                                                   int32_t* __restrict__ ovf_count) {
+  if (a.gate && a.gate[0] == 0) return;
+  constexpr int NW = NT / 64;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* scin = reinterpret_cast<float*>(smem);                     // [KB * 32]
+  h8* sfrag = reinterpret_cast<h8*>(smem + (size_t)a.KB * 32 * 4);  // [KB][DQ][64]
+  int* scnt = reinterpret_cast<int*>(sfrag + (size_t)a.KB * DQ * 64);  // [NW][64]
+  unsigned short* scand = reinterpret_cast<unsigned short*>(scnt + NW * 64);  // [NW][64][kMaxCand]
+  const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0;
+  const float thr_rel = a.thr_dev ? a.thr_dev[1] : a.thr_rel;
+  const int R = a.in_regions;
+  const int nchunks = chunk_pre[R];
+  if (nchunks == 0) return;  // uniform over the grid
+  for (int i = threadIdx.x; i < a.KB * 32; i += blockDim.x) scin[i] = a.cinit[i];
+  for (int i = threadIdx.x; i < a.KB * DQ * 64; i += blockDim.x) sfrag[i] = a.frag[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int h = lane >> 5;
+  const int p = lane & 31;
+  const int wave_id = blockIdx.x * NW + w;
+  const int nwaves = gridDim.x * NW;
+  int* mycnt = scnt + w * 64;
+  unsigned short* mycand = scand + (size_t)w * 64 * kMaxCand;
+  const f4* XA4 = reinterpret_cast<const f4*>(a.XA);
+  for (int ch = wave_id; ch < nchunks; ch += nwaves) {
+    int lo = 0, hi = R;  // last r with chunk_pre[r] <= ch
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (chunk_pre[mid] <= ch) lo = mid; else hi = mid;
+    }
+    const int r = lo;
+    const int cnt = a.in_count[r];
+    const int e0 = (ch - chunk_pre[r]) * 64;
+    const int32_t* src = a.in_list + (size_t)r * a.in_cap;
+    const float* srcb = a.out_best + (size_t)r * a.in_cap;
+    int64_t pt[2];
+    bool real[2];
+    float lim[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int e = e0 + 32 * t + p;
+      real[t] = e < cnt;
+      pt[t] = real[t] ? (int64_t)src[e] : 0;
+      lim[t] = real[t] ? fmaf(srcb[e], thr_rel, thr0) : -1.0f;
+    }
+    mycnt[lane] = 0;
+    h8 BH[2][DQ];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int c = 0; c < DQ; ++c) {
+        const int64_t q = pt[t];
+        const int64_t idx = (((q >> 6) * 2 + ((q >> 5) & 1)) * DQ + c) * 64 + h * 32 + (q & 31);
+        BH[t][c] = real[t] ? a.XB[idx] : h8{};
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    auto mm = [&](int b, f16v (&acc)[2]) {
+      const f4* cr = reinterpret_cast<const f4*>(scin + 32 * b + 4 * h);
+      f16v ci;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f4 v = cr[2 * q];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ci[4 * q + i] = v[i];
+      }
+      h8 A[DQ];
+#pragma unroll
+      for (int c = 0; c < DQ; ++c) A[c] = sfrag[((size_t)b * DQ + c) * 64 + lane];
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], BH[0][0], ci, 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[0], BH[1][0], ci, 0, 0, 0);
+#pragma unroll
+      for (int c = 1; c < DQ; ++c) {
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], BH[0][c], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[c], BH[1][c], acc[1], 0, 0, 0);
+      }
+    };
+    auto take = [&](int b, const f16v (&acc)[2]) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (acc[t][i] <= lim[t]) {
+            const int slot = atomicAdd(&mycnt[32 * t + p], 1);
+            if (slot < kMaxCand)
+              mycand[(32 * t + p) * kMaxCand + slot] = (unsigned short)(32 * b + 16 * h + i);
+          }
+    };
+    f16v accA[2], accB[2];
+    mm(0, accA);
+    int b = 1;
+    for (; b + 1 < a.KB; b += 2) {
+      mm(b, accB);
+      take(b - 1, accA);
+      mm(b + 1, accA);
+      take(b, accB);
+    }
+    if (b < a.KB) {
+      mm(b, accB);
+      take(b - 1, accA);
+      take(b, accB);
+    } else {
+      take(b - 1, accA);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // lane l: point l of the chunk (tile l / 32, column l % 32)
+    const int e = e0 + lane;
+    if (e < cnt) {
+      const int64_t mypt = (int64_t)src[e];
+      const int nc = mycnt[lane];
+      if (nc > kMaxCand || nc == 0) {
+        ovf[atomicAdd(ovf_count, 1)] = (int32_t)mypt;
+      } else {
+        float xv[16 * DQ];
+#pragma unroll
+        for (int q = 0; q < 4 * DQ; ++q) {
+          const f4 v = q < a.Q ? XA4[mypt * a.Q + q] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xv[4 * q + i] = v[i];
+        }
+        double rb = INFINITY;
+        int jb = 0x7fffffff;
+        for (int s2 = 0; s2 < nc; ++s2) {
+          const int j = mycand[lane * kMaxCand + s2];
+          const double Rd = np_sqdist_reg<16 * DQ>(xv, C64 + (size_t)j * a.d, a.d);
+          const double root = sqrt(Rd);
+          if (root < rb || (root == rb && j < jb)) {
+            rb = root;
+            jb = j;
+          }
+        }
+        if (!a.delta) {
+          a.labels[mypt] = jb;
+        } else {
+          const int oldl = a.labels[mypt];
+          if (jb != oldl) {
+            a.labels[mypt] = jb;
+            a.mv2[atomicAdd(a.mv2_count, 1)] = int2{(int)mypt, (oldl << 16) | jb};
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // L3: exact fp64 assignment of the overflow list (flat, count at *count):
 // one wave per point.  Lane (c, r) = (lane >> 3, lane & 7) takes centroids
 // c, c + 8, ... and NumPy's pairwise accumulator r (features r, r + 8, ...,
@@ -1143,7 +1332,7 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(BigPlanArgs a) {
 template <int DQ>
 static void launch_big_levels(Ctx& c, const BigArgs& a1, const BigArgs& a2, dim3 g1, dim3 g2,
                               size_t lds1, const double* dC, int32_t* ovf, int32_t* ovf_count,
-                              bool prof, bool sp) {
+                              bool prof, bool sp, int32_t* chunk_pre) {
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&screen_big<DQ, 1, false, true>),
@@ -1168,8 +1357,25 @@ static void launch_big_levels(Ctx& c, const BigArgs& a1, const BigArgs& a2, dim3
 #else
   constexpr int abl = 0;
 #endif
-  hipLaunchKernelGGL((cand_big<DQ>), g2, dim3(256), 0, c.stream, a2, c.x32.as<float>(), dC, ovf,
-                     ovf_count, abl);
+  const size_t lds2 = big_l1_lds(a2.k, a2.d) + (size_t)8 * 64 * 4 + (size_t)8 * 64 * kMaxCand * 2;
+  if (sp && lds2 <= 160 * 1024) {
+    // L2 on LDS-resident fragments: chunk numbering first (global), then
+    // one workgroup per CU
+    int32_t* pre = chunk_pre;
+    hipLaunchKernelGGL(big_chunk_prefix, dim3(1), dim3(1024), 0, c.stream, a2.in_count,
+                       a2.in_regions, pre);
+    static bool lattr = false;
+    if (!lattr) {
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&cand_big_lds<DQ, 512>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      lattr = true;
+    }
+    hipLaunchKernelGGL((cand_big_lds<DQ, 512>), dim3(lloyd_num_cus(c.device)), dim3(512), lds2,
+                       c.stream, a2, dC, pre, ovf, ovf_count);
+  } else {
+    hipLaunchKernelGGL((cand_big<DQ>), g2, dim3(256), 0, c.stream, a2, c.x32.as<float>(), dC, ovf,
+                       ovf_count, abl);
+  }
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1292,6 +1498,8 @@ static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* th
   int32_t* ovf = list1 + 2 * slots;
   int32_t* cnt1 = c.fb_count.as<int32_t>();
   int32_t* ovf_count = cnt1 + nw1 + 1;
+  c.big_chunks.ensure(sizeof(int32_t) * (size_t)(nw1 + 1));
+  int32_t* chunk_pre = c.big_chunks.as<int32_t>();
   c.fb_regions = nw1;
   c.fb_total_slot = nw1;  // L1 leftovers: the "fallback" statistic
   c.fb_layout = -1;       // screen32 must re-zero its counter layout
@@ -1364,13 +1572,13 @@ static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* th
   if (prof) prof_mark(c, 0);
   switch (DQ) {
     case 1: launch_big_levels<1>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof,
-                                  sp); break;
+                                  sp, chunk_pre); break;
     case 2: launch_big_levels<2>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof,
-                                  sp); break;
+                                  sp, chunk_pre); break;
     case 3: launch_big_levels<3>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof,
-                                  sp); break;
+                                  sp, chunk_pre); break;
     default: launch_big_levels<4>(c, a, a2, dim3(nwg1), dim3(nwg2), lds1, dC, ovf, ovf_count, prof,
-                                  sp); break;
+                                  sp, chunk_pre); break;
   }
   hipLaunchKernelGGL(exact_big, dim3(cus * 4), dim3(64), 0, c.stream, c.x32.as<float>(), c.n_pad,
                      d, dC, k, ovf, ovf_count, c.labels.as<int32_t>(), gate, a.mv2, a.mv2_count);
