@@ -177,3 +177,65 @@ def test_config5_full_size_and_scoring(ctx):
     want = {f"C{j}": clf.classify_cluster({nm: np.float64(med[j, i]) for i, nm in enumerate(names)})
             for j in range(k)}
     assert got == want
+
+
+@pytest.mark.parametrize("n,d,k", [(300_000, 16, 64), (60_000, 64, 300), (40_000, 24, 33)])
+def test_sharded_device_loop_two_contexts(n, d, k):
+    """The multi-GPU step of bench.py / cdr_dist.DeviceLloyd (csrc/loop.hip with
+    a device all-reduce buffer: enqueue_assign -> SUM -> enqueue_finalize)
+    emulated with two contexts on one GPU and a device-tensor sum in place of
+    RCCL: centroids and labels equal the single-context loop's (screen32,
+    large-k DELTA and host-plan shapes)."""
+    import torch
+
+    import _cdr
+    from cdr_dist import Comm, device_lloyd, seed_sharded
+
+    X = synth.generate(n, 0, n, d, k, 7 * n + d)
+    steps = 5
+    full = _cdr.Context(0)
+    try:
+        full.load_points(X)
+        # k-means++ centres (as bench.py): no cluster empties in these steps,
+        # so no host reseed is involved
+        C0 = np.asarray(seed_sharded(full, Comm(), 0, n, k, random_state=42), dtype=np.float64)
+        np.random.seed(1)
+        C_ref, st_ref = device_lloyd(full, C0, steps, -1.0, lambda g: X[g], n)
+        lab_ref = full.labels()
+    finally:
+        full.close()
+    assert st_ref["steps"] == steps and st_ref["running"], st_ref
+    cut = (n // 2) // 8192 * 8192
+    ctxs = [_cdr.Context(0), _cdr.Context(0)]
+    try:
+        ctxs[0].load_points(X[:cut])
+        ctxs[1].load_points(X[cut:])
+        ref = C0[0].copy()
+        x2 = ctxs[0].points_sqdev(ref) + ctxs[1].points_sqdev(ref)
+        bufs = [torch.zeros(k * (d + 1), dtype=torch.int64, device="cuda") for _ in ctxs]
+        for c in ctxs:
+            c.lloyd_begin(C0, -1.0, ref, x2)
+        for _ in range(steps):
+            for c, b in zip(ctxs, bufs):
+                c.lloyd_enqueue_assign(b.data_ptr())
+            for c in ctxs:
+                c.synchronize()
+            tot = bufs[0] + bufs[1]
+            for b in bufs:
+                b.copy_(tot)
+            torch.cuda.synchronize()
+            for c, b in zip(ctxs, bufs):
+                c.lloyd_enqueue_finalize(b.data_ptr())
+        sts = [c.lloyd_status() for c in ctxs]
+        Cs = [c.lloyd_read()[0] for c in ctxs]
+        labs = np.concatenate([c.labels() for c in ctxs])
+        for c in ctxs:
+            c.lloyd_end()
+    finally:
+        for c in ctxs:
+            c.close()
+    assert all(s["steps"] == steps and s["running"] for s in sts), sts
+    np.testing.assert_array_equal(Cs[0], C_ref)
+    np.testing.assert_array_equal(Cs[1], C_ref)
+    np.testing.assert_array_equal(labs, lab_ref)
+    assert abs(sts[0]["inertia"] - st_ref["inertia"]) <= 1e-9 * st_ref["inertia"]
