@@ -199,6 +199,13 @@ struct Ctx {
 
   // ---- seeding ----
   DevBuf dmin;        // double[n_pad]
+  // exact pruning of the seeding update (seed.hip seed_prunable): the index
+  // of each point's nearest centre so far, the centres, their distances to
+  // the newest one
+  DevBuf seed_near;   // int32[n_pad]
+  DevBuf seed_cents;  // double[count][d]
+  DevBuf seed_ccd;    // double[count]
+  int seed_count = 0;
   DevBuf blocksums;   // double[nblocks]
   DevBuf xfer;        // per-block transfer records
   DevBuf cend;        // double[nblocks] running value after each block

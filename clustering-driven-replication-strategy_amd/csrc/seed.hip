@@ -107,10 +107,37 @@ __device__ double pw_tree(int64_t n, LF leaf) {
 // D > 0 (float points, d == D <= 16): each thread takes 4 points per
 // iteration with all their 16-byte feature-quad loads and dmin loads issued
 // before any arithmetic, and the NumPy-order distance unrolled for that d.
+// Exact pruning of the running minimum (the k-means++ D^2 step,
+// src/kmeans_plusplus.py:14-17): the point's nearest centre so far, c_a =
+// near[i], is at distance r with dmin = fl(r^2); if the new centre is at
+// least 2 r (1 + 2^-30) from c_a, the triangle inequality puts it at least
+// r (1 + 2^-30) from the point, so its computed squared distance (NumPy
+// order, relative error < 2^-45 at d <= 128) is >= dmin and min(dmin, .)
+// leaves dmin unchanged bit for bit: the point is not read at all.
+// ccd[j] = ||c_j - c_new|| (fp64, relative error < 2^-48).  dmin = +inf (no
+// centre yet) never prunes.
+__device__ __forceinline__ bool seed_prunable(double ccd_a, double dmin_old) {
+  return ccd_a >= 2.0 * sqrt(dmin_old) * (1.0 + 0x1p-30);
+}
+
+// ccd[j] = ||cents[j] - cen|| for the j < count centres so far.
+__global__ void seed_ccd_kernel(const double* __restrict__ cents, int count, int d,
+                                const double* __restrict__ cen, double* __restrict__ ccd) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int f = 0; f < d; ++f) {
+      const double t = cents[(size_t)j * d + f] - cen[f];
+      s += t * t;
+    }
+    ccd[j] = sqrt(s);
+  }
+}
+
 template <typename T, int D, bool TAIL>
 __global__ __launch_bounds__(256) void seed_update_kernel(
     const T* __restrict__ X, int64_t n, int64_t n_pad, int d, const double* __restrict__ cen,
-    double* __restrict__ dmin, double* __restrict__ blocksums, int64_t b_off) {
+    double* __restrict__ dmin, double* __restrict__ blocksums, int64_t b_off,
+    int32_t* __restrict__ near, const double* __restrict__ ccd, int cidx) {
   constexpr int kHalf = 4096;
   __shared__ double sdm[kHalf + kHalf / 16];
   __shared__ double swave[4];
@@ -130,14 +157,23 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
       for (int q0 = threadIdx.x; q0 < kHalf; q0 += 4 * 256) {
         f4v xv[4][Q];
         double old[4];
+        bool go[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int qi = h * kHalf + q0 + 256 * u;
           const int64_t i = base + qi;
+          go[u] = false;
           if (!TAIL || qi < m) {
+            old[u] = dmin[i];
+            go[u] = cidx == 0 || !seed_prunable(ccd[near[i]], old[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t i = base + h * kHalf + q0 + 256 * u;
+          if (go[u]) {
 #pragma unroll
             for (int qq = 0; qq < Q; ++qq) xv[u][qq] = X4[(int64_t)qq * n_pad + i];
-            old[u] = dmin[i];
           }
         }
 #pragma unroll
@@ -146,13 +182,19 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
           const int qi = h * kHalf + q;
           double v = 0.0;
           if (!TAIL || qi < m) {
-            auto xf = [&](int f) { return (double)xv[u][f >> 2][f & 3]; };
-            auto cf = [&](int f) { return cr[f]; };
-            const double R = np_sqdist(xf, cf, D);
-            const double r = sqrt(R);
-            const double t = r * r;
-            v = t < old[u] ? t : old[u];
-            dmin[base + qi] = v;
+            v = old[u];
+            if (go[u]) {
+              auto xf = [&](int f) { return (double)xv[u][f >> 2][f & 3]; };
+              auto cf = [&](int f) { return cr[f]; };
+              const double R = np_sqdist(xf, cf, D);
+              const double r = sqrt(R);
+              const double t = r * r;
+              if (t < old[u]) {
+                v = t;
+                dmin[base + qi] = t;
+                near[base + qi] = cidx;
+              }
+            }
           }
           sdm[spos(q)] = v;
         }
@@ -163,14 +205,20 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
         const int64_t i = base + qi;
         double v = 0.0;
         if (!TAIL || qi < m) {
-          auto xv = [&](int f) { return (double)X[xidx(f, i, n_pad)]; };
-          auto cv = [&](int f) { return cen[f]; };
-          const double R = np_sqdist(xv, cv, d);
-          const double r = sqrt(R);
-          const double t = r * r;
           const double old = dmin[i];
-          v = t < old ? t : old;
-          dmin[i] = v;
+          v = old;
+          if (cidx == 0 || !seed_prunable(ccd[near[i]], old)) {
+            auto xv = [&](int f) { return (double)X[xidx(f, i, n_pad)]; };
+            auto cv = [&](int f) { return cen[f]; };
+            const double R = np_sqdist(xv, cv, d);
+            const double r = sqrt(R);
+            const double t = r * r;
+            if (t < old) {
+              v = t;
+              dmin[i] = t;
+              near[i] = cidx;
+            }
+          }
         }
         sdm[spos(q)] = v;
       }
@@ -675,7 +723,37 @@ void seed_reset(Ctx& c) {
   c.dmin.ensure(sizeof(double) * c.n_pad);
   hipLaunchKernelGGL(fill_inf, dim3(1024), dim3(256), 0, c.stream, c.dmin.as<double>(), c.n_pad);
   HIP_CHECK(hipGetLastError());
+  c.seed_near.ensure(sizeof(int32_t) * c.n_pad);
+  HIP_CHECK(hipMemsetAsync(c.seed_near.p, 0, sizeof(int32_t) * c.n_pad, c.stream));
+  c.seed_count = 0;
   c.seed_scanned = false;
+}
+
+// Append the new centre (device copy in seed_scalar) to the centre list and
+// compute its distances to the earlier ones (the pruning table).
+static void seed_track(Ctx& c) {
+  const int d = c.d;
+  const size_t need = sizeof(double) * (size_t)(c.seed_count + 1) * d;
+  if (c.seed_cents.bytes < need) {
+    DevBuf grown;
+    grown.ensure(std::max(need, 2 * c.seed_cents.bytes));
+    if (c.seed_count > 0)
+      HIP_CHECK(hipMemcpyAsync(grown.p, c.seed_cents.p, sizeof(double) * (size_t)c.seed_count * d,
+                               hipMemcpyDeviceToDevice, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    c.seed_cents.release();
+    c.seed_cents = grown;
+    grown.p = nullptr;
+    grown.bytes = 0;
+  }
+  c.seed_ccd.ensure(sizeof(double) * (size_t)(c.seed_count + 1));
+  if (c.seed_count > 0)
+    hipLaunchKernelGGL(seed_ccd_kernel, dim3((c.seed_count + 255) / 256), dim3(256), 0, c.stream,
+                       c.seed_cents.as<double>(), c.seed_count, d, c.seed_scalar.as<double>(),
+                       c.seed_ccd.as<double>());
+  HIP_CHECK(hipMemcpyAsync(c.seed_cents.as<double>() + (size_t)c.seed_count * d,
+                           c.seed_scalar.p, sizeof(double) * d, hipMemcpyDeviceToDevice,
+                           c.stream));
 }
 
 void seed_update(Ctx& c, const double* cen) {
@@ -686,9 +764,17 @@ void seed_update(Ctx& c, const double* cen) {
   c.seed_scalar.ensure(sizeof(double) * (c.d + 8));
   HIP_CHECK(hipMemcpyAsync(c.seed_scalar.p, cen, sizeof(double) * c.d, hipMemcpyHostToDevice,
                            c.stream));
+  if (!c.seed_near.p) {  // dmin from an earlier session without the tracking buffers
+    c.seed_near.ensure(sizeof(int32_t) * c.n_pad);
+    HIP_CHECK(hipMemsetAsync(c.seed_near.p, 0, sizeof(int32_t) * c.n_pad, c.stream));
+  }
+  seed_track(c);
+  int32_t* near = c.seed_near.as<int32_t>();
+  const double* ccd = c.seed_ccd.as<double>();
+  const int cidx = c.seed_count;
   if (nb > 0) {
     typedef void (*SeedFn)(const float*, int64_t, int64_t, int, const double*, double*, double*,
-                           int64_t);
+                           int64_t, int32_t*, const double*, int);
 #define CDR_SU(D_) seed_update_kernel<float, D_, false>
     static const SeedFn fns[17] = {CDR_SU(0),  CDR_SU(1),  CDR_SU(2),  CDR_SU(3),  CDR_SU(4),
                                    CDR_SU(5),  CDR_SU(6),  CDR_SU(7),  CDR_SU(8),  CDR_SU(9),
@@ -701,12 +787,13 @@ void seed_update(Ctx& c, const double* cen) {
       if (f32)
         hipLaunchKernelGGL(fns[c.d <= 16 ? c.d : 0], dim3(nfull), dim3(256), 0, c.stream,
                            c.x32.as<float>(), c.n, c.n_pad, c.d, c.seed_scalar.as<double>(),
-                           c.dmin.as<double>(), c.blocksums.as<double>(), (int64_t)0);
+                           c.dmin.as<double>(), c.blocksums.as<double>(), (int64_t)0, near, ccd,
+                           cidx);
       else
         hipLaunchKernelGGL((seed_update_kernel<double, 0, false>), dim3(nfull), dim3(256), 0,
                            c.stream, c.x64.as<double>(), c.n, c.n_pad, c.d,
                            c.seed_scalar.as<double>(), c.dmin.as<double>(),
-                           c.blocksums.as<double>(), (int64_t)0);
+                           c.blocksums.as<double>(), (int64_t)0, near, ccd, cidx);
       HIP_CHECK(hipGetLastError());
     }
     if (nb > nfull) {
@@ -714,15 +801,16 @@ void seed_update(Ctx& c, const double* cen) {
         hipLaunchKernelGGL((seed_update_kernel<float, 0, true>), dim3(1), dim3(256), 0,
                            c.stream, c.x32.as<float>(), c.n, c.n_pad, c.d,
                            c.seed_scalar.as<double>(), c.dmin.as<double>(),
-                           c.blocksums.as<double>(), nfull);
+                           c.blocksums.as<double>(), nfull, near, ccd, cidx);
       else
         hipLaunchKernelGGL((seed_update_kernel<double, 0, true>), dim3(1), dim3(256), 0,
                            c.stream, c.x64.as<double>(), c.n, c.n_pad, c.d,
                            c.seed_scalar.as<double>(), c.dmin.as<double>(),
-                           c.blocksums.as<double>(), nfull);
+                           c.blocksums.as<double>(), nfull, near, ccd, cidx);
     }
     HIP_CHECK(hipGetLastError());
   }
+  c.seed_count += 1;
   c.seed_scanned = false;
 }
 
