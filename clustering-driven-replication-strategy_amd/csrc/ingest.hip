@@ -277,13 +277,15 @@ __device__ __forceinline__ int ts_finish(int y, int mo, int d, int hh, int mi, i
   const int mdays = mo == 2 ? 28 + leap : 30 + ((mo + (mo >> 3)) & 1);
   if (d < 1 || d > mdays) return 1;
   if (hh > 23 || mi > 59 || ss > 59) return 1;
-  const long long y2 = y - (mo <= 2);
-  const long long era = (y2 >= 0 ? y2 : y2 - 399) / 400;
-  const long long yoe = y2 - era * 400;
-  const long long doy = (153 * (mo + (mo > 2 ? -3 : 9)) + 2) / 5 + d - 1;
-  const long long doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
-  const long long days = era * 146097 + doe - 719468;
-  *out = ((days * 86400 + hh * 3600ll + mi * 60ll + ss) - off) * 1000000ll + us;
+  // 32-bit day arithmetic (|y| <= 9999: every term fits; constant divisions
+  // become multiply-high sequences, not 64-bit division loops)
+  const int y2 = y - (mo <= 2);
+  const int era = (y2 >= 0 ? y2 : y2 - 399) / 400;
+  const int yoe = y2 - era * 400;
+  const int doy = (153 * (mo + (mo > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const int doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  const int days = era * 146097 + doe - 719468;
+  *out = (((long long)days * 86400 + hh * 3600ll + mi * 60ll + ss) - off) * 1000000ll + us;
   return 0;
 }
 
@@ -392,23 +394,30 @@ __device__ __forceinline__ void parse_record(const uint8_t* buf, int64_t st, int
   // last comma (the commas after the fourth one are irrelevant)
   int64_t c0 = e, c1 = e, c2 = e, c3 = e;
   int fi = 0;
-  bool unsup = false;
+  unsigned bad = 0;
+  // four bytes at a time: exact per-byte flags (no borrow between bytes) of
+  // ',' and of the bytes the host tokeniser must take ('"', NUL, '\r')
+  auto zb = [](unsigned x) {
+    const unsigned t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    return ~(t | x | 0x7F7F7F7Fu);  // 0x80 in each zero byte of x
+  };
   for (int64_t k = s; k < e; k += 4) {
     const unsigned w = ld4(buf + k);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (k + j >= e) break;
-      const unsigned c = (w >> (8 * j)) & 0xFFu;
-      unsup |= (c == '"') | (c == 0) | (c == '\r');
-      if (c == ',') {
-        if (fi == 0) c0 = k + j;
-        else if (fi == 1) c1 = k + j;
-        else if (fi == 2) c2 = k + j;
-        else if (fi == 3) c3 = k + j;
-        ++fi;
-      }
+    const int64_t rem = e - k;
+    const unsigned live = rem >= 4 ? 0x80808080u : (0x80808080u & ((1u << (8 * rem)) - 1u));
+    bad |= (zb(w ^ 0x22222222u) | zb(w) | zb(w ^ 0x0D0D0D0Du)) & live;
+    unsigned cm = zb(w ^ 0x2C2C2C2Cu) & live;
+    while (cm && fi < 4) {
+      const int64_t at = k + (__builtin_ctz(cm) >> 3);
+      if (fi == 0) c0 = at;
+      else if (fi == 1) c1 = at;
+      else if (fi == 2) c2 = at;
+      else c3 = at;
+      ++fi;
+      cm &= cm - 1u;
     }
   }
+  bool unsup = bad != 0;
   const int64_t f1 = min(c0 + 1, e), f2 = min(c1 + 1, e), f3 = min(c2 + 1, e);
   // both dictionary probes go out first; the timestamp parse overlaps them
   const bool has_path = c1 > f1, has_client = c3 > f3 && nodes.mask;
