@@ -175,6 +175,11 @@ struct Ctx {
   // belong to the labels in `labels` (valid after a screen32 step with run_k)
   DevBuf run_sums;
   bool run_valid = false;
+  // screen32d's one-byte copy of `labels` (k <= 64): the DELTA screen reads a
+  // point's previous label from it (1 B instead of 4 B per point and step);
+  // valid while only screen32d / fixup32 wrote the labels since it was built
+  DevBuf lab8;
+  bool lab8_valid = false;
   int32_t run_k = 0;
   bool last_delta = false;
 #ifdef CDR_EXPERIMENTS

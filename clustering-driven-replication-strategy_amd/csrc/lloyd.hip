@@ -1102,6 +1102,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     screened = true;
   } else if (screen_supported(c, k)) {
     c.run_valid = false;  // the screen_fast / screen_kernel path keeps no running sums
+    c.lab8_valid = false;
     c.big_valid = false;
     screened = true;
     ScreenPlan pl;
@@ -1196,6 +1197,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     screened = true;  // large k / d: screen_big levels + update_big
   } else {
     c.run_valid = false;
+    c.lab8_valid = false;
     c.big_valid = false;
     // exact assignment for every point, then fixed-point sums from labels
     hipLaunchKernelGGL(assign_exact_all<float>, dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 8))),
@@ -1257,6 +1259,7 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
   check_k(c, k);
   if (c.mode != CDR_MODE_F64) CDR_FAIL(CDR_ERR_STATE, "lloyd_step_f64: points are not F64");
   c.run_valid = false;
+  c.lab8_valid = false;
   c.big_valid = false;
   const int d = c.d;
   const int cus = lloyd_num_cus(c.device);

@@ -356,6 +356,7 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   c.ll_hostplan_once = false;
   // the first step recomputes the running sums from scratch (see resume)
   c.run_valid = false;
+  c.lab8_valid = false;
   c.big_valid = false;
   if (c.ll_devplan) ll_plan(c);
   if (c.ll_devbig) ll_plan_big(c);
@@ -518,6 +519,7 @@ int cdr_lloyd_resume(cdr_ctx* h, const double* C, int32_t add_steps, int32_t hos
   // running sums valid after each of them; a full (non-DELTA) step that was
   // among them never zeroed and rebuilt them.  The next step starts afresh.
   c.run_valid = false;
+  c.lab8_valid = false;
   c.big_valid = false;
   CDR_CATCH
 }

@@ -650,6 +650,18 @@ __global__ void split_copy_kernel(const float* __restrict__ x, int64_t n, int64_
   }
 }
 
+// labels -> their one-byte copy (k <= 64), once per run of DELTA steps
+__global__ void lab8_kernel(const int32_t* __restrict__ labels, uint8_t* __restrict__ lab8,
+                            int64_t n_pad) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n_pad; i += stride) {
+    const int4 v = *reinterpret_cast<const int4*>(labels + i);  // n_pad: a multiple of 64
+    const unsigned w = (unsigned)(v.x & 255) | (unsigned)(v.y & 255) << 8 |
+                       (unsigned)(v.z & 255) << 16 | (unsigned)(v.w & 255) << 24;
+    *reinterpret_cast<unsigned*>(lab8 + i) = w;
+  }
+}
+
 struct S32DArgs {
   const unsigned char* XS;  // split copy (tiles of 32 points, 1024 QH bytes each)
   int64_t n, n_pad;
@@ -659,6 +671,7 @@ struct S32DArgs {
   const float* thr_dev;
   const long long* gate;
   int32_t* labels;
+  uint8_t* lab8;      // one-byte copy of labels (Ctx::lab8): read for the old label
   int2* fb_list;      // per-wave regions of uncertified points {pt, old label}
   int32_t* fb_count;  // per-wave counts, then the step total at [nwaves]
   int2* mv_list;      // per-wave regions of moved points
@@ -708,7 +721,7 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
 #pragma unroll
         for (int u = 0; u < QH; ++u)
           b.v[t][u] = *reinterpret_cast<const u4v*>(base + loff + t * kTile + 16 * u);
-      b.ob = a.labels[G * 64 + lane];
+      b.ob = a.lab8[G * 64 + lane];
     }
   };
   // (best, runner-up) keys of one 32-point tile, as screen32's tile()
@@ -760,7 +773,10 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
     const bool cert = vs > fmaf(vb, thr_rel, thr0);  // NaN: never certified
     const bool real = pt < a.n;
     const bool moved = cert && real && label != b.ob;
-    if (moved) a.labels[pt] = label;
+    if (moved) {
+      a.labels[pt] = label;
+      a.lab8[pt] = (uint8_t)label;
+    }
     const unsigned long long mv = __ballot(moved);
     if (mv) {
       const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(mv >> 32),
@@ -802,6 +818,7 @@ struct FixArgs {
   const double* cent;  // k x d fp64 centroids of the step
   int k, d;
   int32_t* labels;
+  uint8_t* lab8;  // kept equal to labels (screen32d reads it)
   const int2* fb_list;  // {pt, old label}
   const int32_t* fb_count;
   const int2* mv_list;
@@ -1030,6 +1047,7 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
         if (jmin >= k) jmin = 0;  // every root NaN: np.argmin of all-NaN is 0
         if (jmin != old && !(a.abl & 32)) {
           a.labels[own] = jmin;
+          a.lab8[own] = (uint8_t)jmin;
 #pragma unroll
           for (int f = 0; f < D; ++f) {
             atomicAdd(&tsum[f * TS + jmin], x[f]);
@@ -1290,6 +1308,13 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   }
   c.fb_regions = nwaves;
   c.fb_total_slot = nwaves + 1;
+  if (!c.lab8_valid) {  // first DELTA step since another path wrote the labels
+    c.lab8.ensure((size_t)c.n_pad);
+    hipLaunchKernelGGL(lab8_kernel, dim3(2048), dim3(256), 0, c.stream, c.labels.as<int32_t>(),
+                       c.lab8.as<uint8_t>(), c.n_pad);
+    HIP_CHECK(hipGetLastError());
+    c.lab8_valid = true;
+  }
   S32DArgs a;
   a.XS = c.xs16.as<unsigned char>();
   a.n = c.n;
@@ -1301,6 +1326,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   a.thr_dev = dthr;
   a.gate = gate;
   a.labels = c.labels.as<int32_t>();
+  a.lab8 = c.lab8.as<uint8_t>();
   a.fb_list = c.fb_list.as<int2>();
   a.fb_count = c.fb_count.as<int32_t>();
   a.mv_list = c.mv_list.as<int2>();
@@ -1331,6 +1357,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   f.k = k;
   f.d = c.d;
   f.labels = c.labels.as<int32_t>();
+  f.lab8 = c.lab8.as<uint8_t>();
   f.fb_list = c.fb_list.as<int2>();
   f.fb_count = c.fb_count.as<int32_t>();
   f.mv_list = c.mv_list.as<int2>();
@@ -1464,6 +1491,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
     c.run_k = k;
     return true;
   }
+  c.lab8_valid = false;  // the full screen writes the labels alone
   const size_t lds = (size_t)NF * KP * 8 + (size_t)KP * 4 + (size_t)k * 17 * 8;
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);

@@ -1635,6 +1635,7 @@ static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* th
   c.big_valid = true;
   c.big_k = k;
   c.run_valid = false;
+  c.lab8_valid = false;
   return true;
 }
 
