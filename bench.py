@@ -22,8 +22,11 @@ banners (RCCL) are pointed at stderr.
 
 roofline: the dominant kernel is the screen kernel (assign + fused update);
 algorithmic bytes per launch = n_local * (4*d + 4) (read the fp32 point, write
-its int32 label), divided by its mean duration from HIP events recorded on
-the context stream around every launch of the timed region.  `traffic` is
+its int32 label: SURVEY.md 8(d)), divided by its mean duration from HIP events
+recorded on the context stream around every launch of the timed region.  The
+DELTA screen streams a smaller fp16 copy of the points instead (32 bytes per
+point at d = 16 for screen32h, + a one-byte label): `kernel_bytes_per_launch`
+and `kernel_frac` state that kernel's own traffic against the same peak.  `traffic` is
 the PMC-measured HBM bytes per launch from profiles/ when a matching rocprof
 summary is committed there, else null.
 
@@ -487,6 +490,16 @@ def main() -> None:
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                     "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_ms": screen_ms}
+        # the bytes this kernel itself must stream: its fp16 screen copy (hi-only
+        # screen32h: 2 B per padded feature; screen32d: hi + lo) and the one-byte
+        # label it compares against
+        copy_b = {"screen32h": 2 * 16, "screen32d<1": 32, "screen32d<2": 64}
+        for pre, b in copy_b.items():
+            if kname.startswith(pre):
+                kb = n_local * (b + 1)
+                roofline["kernel_bytes_per_launch"] = kb
+                roofline["kernel_frac"] = kb / (screen_ms / 1e3) / 1e9 / HBM_PEAK_GBPS
+                break
     # (the fallback counter accumulates over every profiled-session step)
     fb_frac = prof["fallback_points"] / max(args.steps, 1) / max(n_local, 1)
 

@@ -131,6 +131,7 @@ __device__ inline void plan32_build(const double* __restrict__ C, int k, int d, 
         const size_t b_all = (size_t)MT * 2 * 64 * sizeof(plan_h8) +
                              (size_t)MT * 16 * 64 * sizeof(float) + sizeof(double) * (size_t)k * d;
         *reinterpret_cast<float*>(plan + b_all) = thr0;
+        reinterpret_cast<float*>(plan + b_all)[1] = (float)D;  // (the hi-only screen's bound)
       }
     }
   }

@@ -618,8 +618,9 @@ __global__ void precenter_kernel(const float* __restrict__ x, int64_t n, int64_t
 // xs16 tile of 32 points: [h = 0, 1][p = 0..31][hi(QH quads) | lo(QH quads)]
 // as fp16, where lane half h owns quads QH h .. QH h + QH - 1 (screen32's
 // layout; QH = 1: [hi(q), lo(q)] is the B operand itself).  Missing features
-// and padding rows are 0.
-template <int QH>
+// and padding rows are 0.  HO (QH = 2 only): the hi halves alone, 16 bytes per
+// (point, half) — the hi-only screen copy of screen32d<2, MT, PD, true>.
+template <int QH, bool HO = false>
 __global__ void split_copy_kernel(const float* __restrict__ x, int64_t n, int64_t n_pad, int d,
                                   const float* __restrict__ ms, float sig,
                                   uint4* __restrict__ xs) {
@@ -640,8 +641,10 @@ __global__ void split_copy_kernel(const float* __restrict__ x, int64_t n, int64_
       }
       split4(xt, hw[2 * u], hw[2 * u + 1], lw[2 * u], lw[2 * u + 1]);
     }
-    uint4* dst = xs + (size_t)t * QH;  // 16 QH bytes per (point, half)
-    if (QH == 1) {
+    uint4* dst = xs + (size_t)t * (HO ? 1 : QH);  // 16 QH bytes per (point, half)
+    if (HO) {
+      dst[0] = uint4{hw[0], hw[1], hw[2], hw[3]};
+    } else if (QH == 1) {
       dst[0] = uint4{hw[0], hw[1], lw[0], lw[1]};
     } else {
       dst[0] = uint4{hw[0], hw[1], hw[2], hw[3]};
@@ -668,6 +671,7 @@ struct S32DArgs {
   const h8* frag;
   const float* cinit;
   float thr0, thr_rel;
+  float Dv;                 // the plan's offset D (hi-only screen; device plan: thr_dev[1])
   const float* thr_dev;
   const long long* gate;
   int32_t* labels;
@@ -680,9 +684,24 @@ struct S32DArgs {
 };
 
 // PD: groups of 64 points per wave in flight (the loads of PD - 1 groups are
-// issued ahead of the one being screened)
-template <int QH, int MT, int PD>
+// issued ahead of the one being screened).
+//
+// HO (hi-only, QH = 2): the screen copy holds h = fp16(xhat) alone (32 bytes
+// per point at d = 16 instead of 64) and each tile takes two MFMAs, A1 x H and
+// A3 x H: the screen values are those of the point h, S_j = Shat_j +- E with
+// Shat_j = D + ||chat_j||^2 - 2 chat_j.h (E: the plan's bound, thr0 >= 2E + the
+// reference slack).  The true decision values T_j = ||chat_j||^2 - 2 chat_j.xhat
+// differ by 2 (chat_j - chat_b).delta, delta = h - xhat, |delta| <= dn =
+// 2^-11 (1 + 2^-9) ||h|| + 2^-23 (fp16 round to nearest, subnormals), and
+// |chat_j - chat_b| <= sqrt(G_j) + sqrt(G_b) with G_j = ||h - chat_j||^2 <=
+// S_j + E - D + ||h||^2.  A point is certified when
+//     v_s > v_b (1 + 2^-16) + thr0 + 2 dn (sqrt(G_s) + sqrt(G_b))
+// (v: the truncated keys, S_b <= v_b (1 + 2^-17), S_j >= v_s for every j != b).
+// Then sqrt(G_s) > 2 dn, so S - 2 dn sqrt(S + E - D + ||h||^2) grows with S
+// above v_s and the bound holds for every j != b: T_j - T_b > slack.
+template <int QH, int MT, int PD, bool HO = false>
 __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
+  static_assert(!HO || QH == 2, "hi-only screen: d > 8");
   if (a.gate && a.gate[0] == 0) return;
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
@@ -697,6 +716,7 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
     for (int i = 0; i < 16; ++i) Ci[m][i] = a.cinit[(m * 16 + i) * 64 + lane];
   }
   const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
+  const float Dlo = (a.thr_dev ? a.thr_dev[1] : a.Dv) * (1.0f - 0x1p-19f);  // < D
   const int wpb = blockDim.x >> 6;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
   const int nwaves = gridDim.x * wpb;
@@ -706,11 +726,12 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
   int fb_used = 0, mv_used = 0;
   // per group: two tiles of 1024 QH bytes; lane (h, p) reads 16 QH bytes at
   // (h * 32 + p) * 16 QH of each tile
-  constexpr int kTile = 1024 * QH;
-  const unsigned loff = (unsigned)((h * 32 + p) * 16 * QH);
+  constexpr int NL = HO ? 1 : QH;  // 16-byte loads per tile and lane
+  constexpr int kTile = 1024 * NL;
+  const unsigned loff = (unsigned)((h * 32 + p) * 16 * NL);
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
   struct Buf {
-    u4v v[2][QH];  // [tile][0] = H (QH = 2: hi of both quads; QH = 1: hi | lo), [tile][1] = L
+    u4v v[2][NL];  // [tile][0] = H (QH = 2: hi of both quads; QH = 1: hi | lo), [tile][1] = L
     int ob;
   };
   auto load = [&](Buf& b, int64_t G) {
@@ -719,19 +740,25 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int u = 0; u < QH; ++u)
+        for (int u = 0; u < NL; ++u)
           b.v[t][u] = *reinterpret_cast<const u4v*>(base + loff + t * kTile + 16 * u);
       b.ob = a.lab8[G * 64 + lane];
     }
   };
   // (best, runner-up) keys of one 32-point tile, as screen32's tile()
-  auto tile = [&](const u4v (&v)[QH], unsigned& bk, unsigned& sk) {
+  auto tile = [&](const u4v (&v)[NL], unsigned& bk, unsigned& sk, float& hp) {
     const h8 BH = __builtin_bit_cast(h8, v[0]);
     f16v acc[MT];
+    if constexpr (HO) {  // this lane's part of ||h||^2 (fp16 products are exact in fp32)
+      hp = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; i += 2)
+        hp = __builtin_amdgcn_fdot2(h2{BH[i], BH[i + 1]}, h2{BH[i], BH[i + 1]}, hp, false);
+    }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BH, Ci[m], 0, 0, 0);
-      if constexpr (QH == 2) {
+      if constexpr (QH == 2 && !HO) {
         const h8 BL = __builtin_bit_cast(h8, v[1]);
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BL, acc[m], 0, 0, 0);
       }
@@ -761,8 +788,9 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
     const int64_t base = G << 6;
     if (base >= a.n) return;  // wave-uniform: padding groups have no real points
     unsigned bA, sA, bB, sB;
-    tile(b.v[0], bA, sA);
-    tile(b.v[1], bB, sB);
+    float hA, hB;
+    tile(b.v[0], bA, sA, hA);
+    tile(b.v[1], bB, sB, hB);
     swap32(bA, bB);
     swap32(sA, sB);
     merge_top2(bA, sA, bB, sB);
@@ -770,7 +798,20 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
     const int label = (int)(bA & 63u);
     const float vb = __uint_as_float(bA & ~63u);
     const float vs = __uint_as_float(sA & ~63u);
-    const bool cert = vs > fmaf(vb, thr_rel, thr0);  // NaN: never certified
+    float thr = fmaf(vb, thr_rel, thr0);
+    if constexpr (HO) {  // the hi-only certificate (above the kernel)
+      unsigned ua = __float_as_uint(hA), ub = __float_as_uint(hB);
+      swap32(ua, ub);
+      // ||h||^2 from below by at most 9 roundings (and flushed fp16 subnormals)
+      const float hh = fmaf(__uint_as_float(ua) + __uint_as_float(ub), 1.0f + 0x1p-18f, 0x1p-20f);
+      // v_sqrt_f32 (1 ulp; its arguments kept normal)
+      const float dn = fmaf(0x1p-11f * (1.0f + 0x1p-9f), __builtin_amdgcn_sqrtf(hh), 0x1p-23f);
+      const float K = thr0 + hh - Dlo;  // G = S + E - D + ||h||^2 from above (16 ulp(D) spare)
+      const float Gs = fmaxf(vs + K, 0x1p-100f), Gb = fmaxf(fmaf(vb, thr_rel, K), 0x1p-100f);
+      thr += 2.0f * (1.0f + 0x1p-19f) * dn *
+             (__builtin_amdgcn_sqrtf(Gs) + __builtin_amdgcn_sqrtf(Gb));
+    }
+    const bool cert = vs > thr;  // NaN: never certified
     const bool real = pt < a.n;
     const bool moved = cert && real && label != b.ob;
     if (moved) {
@@ -836,6 +877,11 @@ struct FixArgs {
   const float* cinit;
   float thr0, thr_rel;
   const float* thr_dev;
+  // hi-only screen copy (screen32h): the re-screen splits the points itself
+  // from XA, as split_copy_kernel<2> does (the same hi / lo bits)
+  int ho;
+  const float* ms;  // -mu_f 2^sigma
+  float sig;
 };
 
 // Workgroup b applies the lists of screen32d waves 4b .. 4b+3 (a region
@@ -950,9 +996,28 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
         ptt[t] = rec.x;
         oldt[t] = rec.y;
         const int32_t q = ptt[t] < 0 ? 0 : ptt[t];
-        const unsigned char* src = a.XS + (size_t)(q >> 5) * kTile + (h * 32 + (q & 31)) * 16 * QH;
+        if (QH == 2 && a.ho) {
+          unsigned hw[4], lw[4];
 #pragma unroll
-        for (int u = 0; u < QH; ++u) v[t][u] = *reinterpret_cast<const u4v*>(src + 16 * u);
+          for (int u = 0; u < 2; ++u) {
+            const int qq = 2 * h + u;
+            const f4 xr = qq < Q ? XA4[(int64_t)q * Q + qq] : f4{0.f, 0.f, 0.f, 0.f};
+            f4 xt;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const int f = 4 * qq + c;
+              xt[c] = f < D ? fmaf(xr[c], a.sig, a.ms[f]) : 0.0f;
+            }
+            split4(xt, hw[2 * u], hw[2 * u + 1], lw[2 * u], lw[2 * u + 1]);
+          }
+          v[t][0] = u4v{hw[0], hw[1], hw[2], hw[3]};
+          v[t][QH - 1] = u4v{lw[0], lw[1], lw[2], lw[3]};
+        } else {
+          const unsigned char* src =
+              a.XS + (size_t)(q >> 5) * kTile + (h * 32 + (q & 31)) * 16 * QH;
+#pragma unroll
+          for (int u = 0; u < QH; ++u) v[t][u] = *reinterpret_cast<const u4v*>(src + 16 * u);
+        }
       }
       // this lane's point after the half swap: entry e0 + lane (tile lane >> 5)
       const int own = ptt[h];  // lane (h, p) owns entry e0 + 32 h + p
@@ -1076,6 +1141,7 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
 struct Plan32 {
   int QH, MT;
   float thr0, thr_rel;
+  float Dv = 0.0f;  // the offset D (device plan: in the plan buffer)
   std::vector<h8> frag;      // [MT][2][64]
   std::vector<float> cinit;  // [MT][16][64]
 };
@@ -1107,8 +1173,10 @@ void plan32_point_side(const Ctx& c, double& xxmax, double& l1x) {
   xxmax = 0.0;
   l1x = 0.0;
   for (int f = 0; f < c.d; ++f) {
+    // (also bounds |fp16(xhat_f)|: the hi-only screen treats h as the point)
     const double dev =
-        std::fmax(c.fmax[f] - (double)c.mu[f], (double)c.mu[f] - c.fmin[f]) * sc;
+        std::fmax(c.fmax[f] - (double)c.mu[f], (double)c.mu[f] - c.fmin[f]) * sc *
+            (1.0 + std::ldexp(1.0, -11)) + std::ldexp(1.0, -25);
     xxmax += dev * dev;
     l1x += dev;
   }
@@ -1141,6 +1209,7 @@ static bool build_plan32(const Ctx& c, const double* C, int k, Plan32& pl) {
   double xxmax, l1x, D;
   plan32_point_side(c, xxmax, l1x);
   plan32_bounds(ccmax, l1c, xxmax, l1x, pl.QH, D, pl.thr0);
+  pl.Dv = (float)D;
   pl.thr_rel = 1.0f + std::ldexp(1.0f, -16);  // the 64-ulp key truncation (2^-18 rel.)
   const int MT = pl.MT;
   pl.frag.assign((size_t)MT * 2 * 64, h8{});
@@ -1233,12 +1302,17 @@ void ensure_rowmajor(Ctx& c) {
   c.xa_valid = true;
 }
 
+// QH = 1, 2: the hi / lo split copy; 3: the hi-only copy of d > 8 (HO)
 static void ensure_split(Ctx& c, int QH) {
   if (c.xs_valid && c.xs_qh == QH) return;
   ensure_rowmajor(c);
-  c.xs16.ensure((size_t)c.n_pad * 32 * QH);
+  c.xs16.ensure((size_t)c.n_pad * 32 * (QH == 3 ? 1 : QH));
   const float sig = (float)std::ldexp(1.0, c.sigma);
-  if (QH == 1)
+  if (QH == 3)
+    hipLaunchKernelGGL((split_copy_kernel<2, true>), dim3(4096), dim3(256), 0, c.stream,
+                       c.x32.as<float>(), c.n, c.n_pad, c.d, c.mu_s.as<float>(), sig,
+                       c.xs16.as<uint4>());
+  else if (QH == 1)
     hipLaunchKernelGGL(split_copy_kernel<1>, dim3(4096), dim3(256), 0, c.stream, c.x32.as<float>(),
                        c.n, c.n_pad, c.d, c.mu_s.as<float>(), sig, c.xs16.as<uint4>());
   else
@@ -1249,11 +1323,11 @@ static void ensure_split(Ctx& c, int QH) {
   c.xs_qh = QH;
 }
 
-template <int QH, int MT, int PD>
+template <int QH, int MT, int PD, bool HO = false>
 static int s32d_blocks_per_cu() {
   static int nb = 0;
   if (!nb) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32d<QH, MT, PD>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32d<QH, MT, PD, HO>, 256, 0) != hipSuccess ||
         nb < 1)
       nb = 2;
     if (nb > 8) nb = 8;
@@ -1271,14 +1345,22 @@ static int s32d_depth(int QH) {
 
 // A DELTA step on screen32d + fixup32 (labels and running sums as screen32's).
 static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const float* dcinit,
-                           const double* dcent, float thr0, float thr_rel, const float* dthr,
-                           long long* dout, long long* hout, bool prof, long long* gate) {
-  ensure_split(c, QH);
+                           const double* dcent, float thr0, float thr_rel, float Dv,
+                           const float* dthr, long long* dout, long long* hout, bool prof,
+                           long long* gate) {
+  // d > 8: the hi-only screen (half the bytes; CDR_S32D_HO=0: the split copy)
+  static const bool ho_env = !std::getenv("CDR_S32D_HO") || std::atoi(std::getenv("CDR_S32D_HO"));
+  const bool HO = QH == 2 && ho_env;
+  ensure_split(c, HO ? 3 : QH);
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
   int bpc;
   const int PD = s32d_depth(QH);
-  if (PD == 4) {
+  if (HO) {
+    if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 2, true>() : s32d_blocks_per_cu<2, 2, 2, true>();
+    else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 3, true>() : s32d_blocks_per_cu<2, 2, 3, true>();
+    else bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 4, true>() : s32d_blocks_per_cu<2, 2, 4, true>();
+  } else if (PD == 4) {
     if (QH == 1 && MT == 1) bpc = s32d_blocks_per_cu<1, 1, 4>();
     else if (QH == 1) bpc = s32d_blocks_per_cu<1, 2, 4>();
     else if (MT == 1) bpc = s32d_blocks_per_cu<2, 1, 4>();
@@ -1323,6 +1405,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   a.cinit = dcinit;
   a.thr0 = thr0;
   a.thr_rel = thr_rel;
+  a.Dv = Dv;
   a.thr_dev = dthr;
   a.gate = gate;
   a.labels = c.labels.as<int32_t>();
@@ -1332,11 +1415,16 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   a.mv_list = c.mv_list.as<int2>();
   a.mv_count = c.mv_count.as<int32_t>();
   a.cap = cap;
-  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32d<%d,%d,%d>", QH, MT, s32d_depth(QH));
+  if (HO)
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>", MT, PD);
+  else
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32d<%d,%d,%d>", QH, MT, PD);
   if (prof) prof_mark(c, 0);
   const dim3 grid(nwg), blk(256);
 #define CDR_S32D_LAUNCH(P)                                                                  \
-  if (QH == 1 && MT == 1) hipLaunchKernelGGL((screen32d<1, 1, P>), grid, blk, 0, c.stream, a); \
+  if (HO && MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P, true>), grid, blk, 0, c.stream, a); \
+  else if (HO) hipLaunchKernelGGL((screen32d<2, 2, P, true>), grid, blk, 0, c.stream, a);      \
+  else if (QH == 1 && MT == 1) hipLaunchKernelGGL((screen32d<1, 1, P>), grid, blk, 0, c.stream, a); \
   else if (QH == 1) hipLaunchKernelGGL((screen32d<1, 2, P>), grid, blk, 0, c.stream, a);       \
   else if (MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P>), grid, blk, 0, c.stream, a);       \
   else hipLaunchKernelGGL((screen32d<2, 2, P>), grid, blk, 0, c.stream, a);
@@ -1374,6 +1462,9 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   f.thr0 = thr0;
   f.thr_rel = thr_rel;
   f.thr_dev = dthr;
+  f.ho = HO;
+  f.ms = c.mu_s.as<float>();
+  f.sig = (float)std::ldexp(1.0, c.sigma);
 #ifdef CDR_EXPERIMENTS
   if (const char* e = std::getenv("CDR_FIX_ABL")) f.abl = std::atoi(e);
 #endif
@@ -1485,8 +1576,8 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
       devplan ? reinterpret_cast<const float*>(static_cast<char*>(c.frag.p) + b_all) : nullptr;
   const bool lean = delta && !dbg && !std::getenv("CDR_NO_LEAN");
   if (lean) {
-    screen32d_step(c, pl.QH, pl.MT, k, dfrag, dcinit, dcent, pl.thr0, pl.thr_rel, dthr, dout,
-                   hout, prof, gate);
+    screen32d_step(c, pl.QH, pl.MT, k, dfrag, dcinit, dcent, pl.thr0, pl.thr_rel, pl.Dv, dthr,
+                   dout, hout, prof, gate);
     c.run_valid = true;
     c.run_k = k;
     return true;
