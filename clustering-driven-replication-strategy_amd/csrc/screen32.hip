@@ -699,9 +699,16 @@ struct S32DArgs {
 // (v: the truncated keys, S_b <= v_b (1 + 2^-17), S_j >= v_s for every j != b).
 // Then sqrt(G_s) > 2 dn, so S - 2 dn sqrt(S + E - D + ||h||^2) grows with S
 // above v_s and the bound holds for every j != b: T_j - T_b > slack.
-template <int QH, int MT, int PD, bool HO = false>
+//
+// LR (with HO): the screen copy streams through a per-wave LDS ring of PD
+// slots with global_load_lds_dwordx4 (no VGPRs hold loads in flight, so PD - 1
+// groups ahead cost no occupancy); the wave waits for its own slot with an
+// explicit vmcnt (loads complete in issue order) and reads it back with
+// ds_read_b128 at the same lane offset.
+template <int QH, int MT, int PD, bool HO = false, bool LR = false>
 __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
   static_assert(!HO || QH == 2, "hi-only screen: d > 8");
+  static_assert(!LR || (HO && PD <= 4), "LDS ring: hi-only screen, at most 4 slots");
   if (a.gate && a.gate[0] == 0) return;
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
@@ -834,6 +841,53 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
     }
   };
   const int64_t gs = nwaves;
+  if constexpr (LR) {
+    constexpr int kSlot = 2048 + 64;  // two hi tiles of 1024 bytes, 64 one-byte labels
+    __shared__ __attribute__((aligned(16))) unsigned char ring[4 * PD * kSlot];
+    unsigned char* wring = ring + (threadIdx.x >> 6) * PD * kSlot;  // this wave's slots
+    // 3 vector-memory operations per group, all LDS DMA (nothing lands in
+    // VGPRs, so the compiler adds no vmcnt wait of its own): two tile loads
+    // and the labels (16 lanes x 4 bytes)
+    auto issue = [&](int slot, int64_t G) {
+      if (G < ngroups) {
+        const unsigned char* src = a.XS + (size_t)G * 2048 + lane * 16;
+        unsigned char* dst = wring + slot * kSlot;  // wave-uniform (M0)
+        __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(src + 1024, dst + 1024, 16, 0, 0);
+        if (lane < 16) __builtin_amdgcn_global_load_lds(a.lab8 + G * 64 + lane * 4, dst + 2048, 4, 0, 0);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < PD - 1; ++i) issue(i, wave + i * gs);
+    for (int64_t G = wave; G < ngroups; G += PD * gs) {
+#pragma unroll
+      for (int i = 0; i < PD; ++i) {
+        const int64_t Gi = G + i * gs;
+        if (Gi >= ngroups) break;
+        issue((i + PD - 1) % PD, Gi + (PD - 1) * gs);
+        // groups issued after Gi (wave-uniform): wait until 3 x that many remain
+        const int64_t later64 = (ngroups - 1 - Gi) / gs;
+        const int later = later64 < PD - 1 ? (int)later64 : PD - 1;
+        if (later >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else if (later == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        Buf b;
+        const unsigned char* src = wring + i * kSlot + lane * 16;
+        b.v[0][0] = *reinterpret_cast<const u4v*>(src);
+        b.v[1][0] = *reinterpret_cast<const u4v*>(src + 1024);
+        b.ob = wring[i * kSlot + 2048 + lane];
+        process(b, Gi);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      a.fb_count[wave] = fb_used;
+      a.mv_count[wave] = mv_used;
+      if (fb_used) atomicAdd(a.fb_count + nwaves, fb_used);
+    }
+    return;
+  }
   Buf buf[PD];
 #pragma unroll
   for (int i = 0; i < PD - 1; ++i) load(buf[i], wave + i * gs);
@@ -1323,11 +1377,11 @@ static void ensure_split(Ctx& c, int QH) {
   c.xs_qh = QH;
 }
 
-template <int QH, int MT, int PD, bool HO = false>
+template <int QH, int MT, int PD, bool HO = false, bool LR = false>
 static int s32d_blocks_per_cu() {
   static int nb = 0;
   if (!nb) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32d<QH, MT, PD, HO>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32d<QH, MT, PD, HO, LR>, 256, 0) != hipSuccess ||
         nb < 1)
       nb = 2;
     if (nb > 8) nb = 8;
@@ -1351,12 +1405,20 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   // d > 8: the hi-only screen (half the bytes; CDR_S32D_HO=0: the split copy)
   static const bool ho_env = !std::getenv("CDR_S32D_HO") || std::atoi(std::getenv("CDR_S32D_HO"));
   const bool HO = QH == 2 && ho_env;
+  // hi-only: LDS ring of CDR_S32H_LR slots per wave (2..4; 0: register prefetch);
+  // A/B at config 3: 2 slots 0.90-0.91 ms, 3-4 slots 0.92-0.95, registers 0.93
+  static const int lr_env = std::getenv("CDR_S32H_LR") ? std::atoi(std::getenv("CDR_S32H_LR")) : 2;
+  const int LRn = HO && lr_env >= 2 && lr_env <= 4 ? lr_env : 0;
   ensure_split(c, HO ? 3 : QH);
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
   int bpc;
-  const int PD = s32d_depth(QH);
-  if (HO) {
+  const int PD = LRn ? LRn : s32d_depth(QH);
+  if (LRn) {
+    if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 2, true, true>() : s32d_blocks_per_cu<2, 2, 2, true, true>();
+    else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 3, true, true>() : s32d_blocks_per_cu<2, 2, 3, true, true>();
+    else bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 4, true, true>() : s32d_blocks_per_cu<2, 2, 4, true, true>();
+  } else if (HO) {
     if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 2, true>() : s32d_blocks_per_cu<2, 2, 2, true>();
     else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 3, true>() : s32d_blocks_per_cu<2, 2, 3, true>();
     else bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 4, true>() : s32d_blocks_per_cu<2, 2, 4, true>();
@@ -1415,14 +1477,18 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   a.mv_list = c.mv_list.as<int2>();
   a.mv_count = c.mv_count.as<int32_t>();
   a.cap = cap;
-  if (HO)
+  if (LRn)
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>lds", MT, PD);
+  else if (HO)
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>", MT, PD);
   else
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32d<%d,%d,%d>", QH, MT, PD);
   if (prof) prof_mark(c, 0);
   const dim3 grid(nwg), blk(256);
 #define CDR_S32D_LAUNCH(P)                                                                  \
-  if (HO && MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P, true>), grid, blk, 0, c.stream, a); \
+  if (LRn && MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P, true, true>), grid, blk, 0, c.stream, a); \
+  else if (LRn) hipLaunchKernelGGL((screen32d<2, 2, P, true, true>), grid, blk, 0, c.stream, a);       \
+  else if (HO && MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P, true>), grid, blk, 0, c.stream, a); \
   else if (HO) hipLaunchKernelGGL((screen32d<2, 2, P, true>), grid, blk, 0, c.stream, a);      \
   else if (QH == 1 && MT == 1) hipLaunchKernelGGL((screen32d<1, 1, P>), grid, blk, 0, c.stream, a); \
   else if (QH == 1) hipLaunchKernelGGL((screen32d<1, 2, P>), grid, blk, 0, c.stream, a);       \

@@ -228,6 +228,36 @@ def test_incremental_update_equals_full_recompute(ctx, n, d, k, monkeypatch):
             C[-1] = X[12345 % n]
 
 
+@pytest.mark.parametrize("d", [16, 11])
+def test_hi_only_screen_near_ties(ctx, d):
+    """The DELTA steps of d > 8 screen fp16(xhat) alone (screen32h): points put
+    on the bisectors of centroid pairs and a few fp16 ulps off them must still
+    get the reference's label (the per-point certificate sends them to the
+    exact fallback)."""
+    n, k = 200000, 64
+    X = synth.generate(n, 0, n, d, k, 4242 + d).copy()
+    rng = np.random.default_rng(d)
+    C2 = X[rng.choice(n, k, replace=False)].astype(np.float64)
+    m = n // 4  # a quarter of the points: near-ties of the second step's centroids
+    a = rng.integers(0, k, m)
+    b = (a + 1 + rng.integers(0, k - 1, m)) % k
+    eps = rng.choice([0.0, 2.0 ** -11, -2.0 ** -11, 2.0 ** -13, -2.0 ** -13, 2.0 ** -20], m)
+    P = 0.5 * (C2[a] + C2[b]) + eps[:, None] * (C2[b] - C2[a])
+    P = np.clip(np.round(P * 2.0 ** 24) * 2.0 ** -24, 0.0, 1.0 - 2.0 ** -24)
+    X[:m] = P.astype(np.float32)
+    ctx.load_points(X)
+    assert ctx.info()["mode"] == 1
+    S = ctx.info()["scale_bits"]
+    C1 = C2 + rng.normal(0, 1e-3, C2.shape)
+    for step, C in enumerate((C1, C2, C2)):
+        out = ctx.lloyd_step(C)
+        exp_lab, exp = ko.lloyd_partials(X, C, S)
+        np.testing.assert_array_equal(ctx.labels(), exp_lab, err_msg=f"step {step}")
+        np.testing.assert_array_equal(out, exp, err_msg=f"step {step}")
+        if step == 1:  # the near-ties went to the exact fallback
+            assert ctx.fallback_count() > m // 10, ctx.fallback_count()
+
+
 @pytest.mark.parametrize("n,outlier", [(3_000_001, False), (1_200_000, True)])
 def test_seeding_many_blocks_vs_oracle(ctx, n, outlier):
     """Seeding over hundreds of 8192-blocks: the block-transfer walk crosses
