@@ -844,17 +844,19 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
   if constexpr (LR) {
     constexpr int kSlot = 2048 + 64;  // two hi tiles of 1024 bytes, 64 one-byte labels
     __shared__ __attribute__((aligned(16))) unsigned char ring[4 * PD * kSlot];
-    unsigned char* wring = ring + (threadIdx.x >> 6) * PD * kSlot;  // this wave's slots
+    // this wave's slots (a scalar base: M0 without per-load readfirstlane)
+    unsigned char* wring = ring + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * PD * kSlot;
     // 3 vector-memory operations per group, all LDS DMA (nothing lands in
     // VGPRs, so the compiler adds no vmcnt wait of its own): two tile loads
     // and the labels (16 lanes x 4 bytes)
     auto issue = [&](int slot, int64_t G) {
       if (G < ngroups) {
-        const unsigned char* src = a.XS + (size_t)G * 2048 + lane * 16;
+        const unsigned char* gx = a.XS + (size_t)G * 2048;  // scalar base + lane offset
+        const unsigned char* gl = a.lab8 + G * 64;
         unsigned char* dst = wring + slot * kSlot;  // wave-uniform (M0)
-        __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(src + 1024, dst + 1024, 16, 0, 0);
-        if (lane < 16) __builtin_amdgcn_global_load_lds(a.lab8 + G * 64 + lane * 4, dst + 2048, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(gx + (unsigned)(lane * 16), dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(gx + (unsigned)(1024 + lane * 16), dst + 1024, 16, 0, 0);
+        if (lane < 16) __builtin_amdgcn_global_load_lds(gl + (unsigned)(lane * 4), dst + 2048, 4, 0, 0);
       }
     };
 #pragma unroll
@@ -866,8 +868,9 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
         if (Gi >= ngroups) break;
         issue((i + PD - 1) % PD, Gi + (PD - 1) * gs);
         // groups issued after Gi (wave-uniform): wait until 3 x that many remain
-        const int64_t later64 = (ngroups - 1 - Gi) / gs;
-        const int later = later64 < PD - 1 ? (int)later64 : PD - 1;
+        int later = 0;
+#pragma unroll
+        for (int j = 1; j < PD; ++j) later += Gi + j * gs < ngroups ? 1 : 0;
         if (later >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
         else if (later == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
