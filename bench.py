@@ -491,9 +491,9 @@ def main() -> None:
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                     "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_ms": screen_ms}
         # the bytes this kernel itself must stream: its fp16 screen copy (hi-only
-        # screen32h: 2 B per padded feature; screen32d: hi + lo) and the one-byte
+        # screen32h / screen32h1: 2 B per padded feature; screen32d: hi + lo) and the one-byte
         # label it compares against
-        copy_b = {"screen32h": 2 * 16, "screen32d<1": 32, "screen32d<2": 64}
+        copy_b = {"screen32h1": 2 * 8, "screen32h": 2 * 16, "screen32d<1": 32, "screen32d<2": 64}
         for pre, b in copy_b.items():
             if kname.startswith(pre):
                 kb = n_local * (b + 1)

@@ -619,7 +619,8 @@ __global__ void precenter_kernel(const float* __restrict__ x, int64_t n, int64_t
 // as fp16, where lane half h owns quads QH h .. QH h + QH - 1 (screen32's
 // layout; QH = 1: [hi(q), lo(q)] is the B operand itself).  Missing features
 // and padding rows are 0.  HO (QH = 2 only): the hi halves alone, 16 bytes per
-// (point, half) — the hi-only screen copy of screen32d<2, MT, PD, true>.
+// (point, half) — the hi-only screen copy of screen32d<2, MT, PD, true>; with
+// QH = 1 the hi quad alone, 8 bytes per (point, half).
 template <int QH, bool HO = false>
 __global__ void split_copy_kernel(const float* __restrict__ x, int64_t n, int64_t n_pad, int d,
                                   const float* __restrict__ ms, float sig,
@@ -642,7 +643,9 @@ __global__ void split_copy_kernel(const float* __restrict__ x, int64_t n, int64_
       split4(xt, hw[2 * u], hw[2 * u + 1], lw[2 * u], lw[2 * u + 1]);
     }
     uint4* dst = xs + (size_t)t * (HO ? 1 : QH);  // 16 QH bytes per (point, half)
-    if (HO) {
+    if (HO && QH == 1) {  // 8 bytes per (point, half)
+      reinterpret_cast<uint2*>(xs)[t] = uint2{hw[0], hw[1]};
+    } else if (HO) {
       dst[0] = uint4{hw[0], hw[1], hw[2], hw[3]};
     } else if (QH == 1) {
       dst[0] = uint4{hw[0], hw[1], lw[0], lw[1]};
@@ -707,8 +710,10 @@ struct S32DArgs {
 // ds_read_b128 at the same lane offset.
 template <int QH, int MT, int PD, bool HO = false, bool LR = false>
 __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
-  static_assert(!HO || QH == 2, "hi-only screen: d > 8");
-  static_assert(!LR || (HO && PD <= 4), "LDS ring: hi-only screen, at most 4 slots");
+  static_assert(!LR || (HO && QH == 2 && PD <= 4), "LDS ring: hi-only d > 8, at most 4 slots");
+  // H1: hi-only with d <= 8.  Lane half h holds hi(q_h) (8 bytes); the B
+  // operand is [hi, hi] against A = [-2 chi, -2 clo]: one MFMA per tile
+  constexpr bool H1 = HO && QH == 1;
   if (a.gate && a.gate[0] == 0) return;
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
@@ -721,6 +726,9 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
     for (int u = 0; u < 2; ++u) A[m][u] = a.frag[(m * 2 + u) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 16; ++i) Ci[m][i] = a.cinit[(m * 16 + i) * 64 + lane];
+    if constexpr (H1)  // plan (QH = 1): A1 = [-2chi, -2chi], A3 = [-2clo, 0]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) A[m][0][4 + i] = A[m][1][i];
   }
   const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
   const float Dlo = (a.thr_dev ? a.thr_dev[1] : a.Dv) * (1.0f - 0x1p-19f);  // < D
@@ -733,9 +741,9 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
   int fb_used = 0, mv_used = 0;
   // per group: two tiles of 1024 QH bytes; lane (h, p) reads 16 QH bytes at
   // (h * 32 + p) * 16 QH of each tile
-  constexpr int NL = HO ? 1 : QH;  // 16-byte loads per tile and lane
-  constexpr int kTile = 1024 * NL;
-  const unsigned loff = (unsigned)((h * 32 + p) * 16 * NL);
+  constexpr int NL = HO ? 1 : QH;  // 16-byte loads per tile and lane (H1: one 8-byte load)
+  constexpr int kTile = H1 ? 512 : 1024 * NL;
+  const unsigned loff = (unsigned)((h * 32 + p) * (H1 ? 8 : 16 * NL));
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
   struct Buf {
     u4v v[2][NL];  // [tile][0] = H (QH = 2: hi of both quads; QH = 1: hi | lo), [tile][1] = L
@@ -747,8 +755,14 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int u = 0; u < NL; ++u)
-          b.v[t][u] = *reinterpret_cast<const u4v*>(base + loff + t * kTile + 16 * u);
+        for (int u = 0; u < NL; ++u) {
+          if constexpr (H1) {
+            const uint2 w = *reinterpret_cast<const uint2*>(base + loff + t * kTile);
+            b.v[t][u] = u4v{w.x, w.y, w.x, w.y};
+          } else {
+            b.v[t][u] = *reinterpret_cast<const u4v*>(base + loff + t * kTile + 16 * u);
+          }
+        }
       b.ob = a.lab8[G * 64 + lane];
     }
   };
@@ -759,7 +773,7 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
     if constexpr (HO) {  // this lane's part of ||h||^2 (fp16 products are exact in fp32)
       hp = 0.0f;
 #pragma unroll
-      for (int i = 0; i < 8; i += 2)
+      for (int i = 0; i < (H1 ? 4 : 8); i += 2)
         hp = __builtin_amdgcn_fdot2(h2{BH[i], BH[i + 1]}, h2{BH[i], BH[i + 1]}, hp, false);
     }
 #pragma unroll
@@ -769,7 +783,7 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
         const h8 BL = __builtin_bit_cast(h8, v[1]);
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BL, acc[m], 0, 0, 0);
       }
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][1], BH, acc[m], 0, 0, 0);
+      if constexpr (!H1) acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][1], BH, acc[m], 0, 0, 0);
     }
     auto key = [&](int m, int i) {
       return (__float_as_uint(acc[m][i]) & ~63u) | (unsigned)(32 * m + 8 * (i >> 2) + (i & 3));
@@ -1053,11 +1067,11 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
         ptt[t] = rec.x;
         oldt[t] = rec.y;
         const int32_t q = ptt[t] < 0 ? 0 : ptt[t];
-        if (QH == 2 && a.ho) {
+        if (a.ho) {  // QH quads of half h, split as split_copy_kernel<QH> does
           unsigned hw[4], lw[4];
 #pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int qq = 2 * h + u;
+          for (int u = 0; u < QH; ++u) {
+            const int qq = QH * h + u;
             const f4 xr = qq < Q ? XA4[(int64_t)q * Q + qq] : f4{0.f, 0.f, 0.f, 0.f};
             f4 xt;
 #pragma unroll
@@ -1067,8 +1081,12 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
             }
             split4(xt, hw[2 * u], hw[2 * u + 1], lw[2 * u], lw[2 * u + 1]);
           }
-          v[t][0] = u4v{hw[0], hw[1], hw[2], hw[3]};
-          v[t][QH - 1] = u4v{lw[0], lw[1], lw[2], lw[3]};
+          if constexpr (QH == 1) {
+            v[t][0] = u4v{hw[0], hw[1], lw[0], lw[1]};
+          } else {
+            v[t][0] = u4v{hw[0], hw[1], hw[2], hw[3]};
+            v[t][QH - 1] = u4v{lw[0], lw[1], lw[2], lw[3]};
+          }
         } else {
           const unsigned char* src =
               a.XS + (size_t)(q >> 5) * kTile + (h * 32 + (q & 31)) * 16 * QH;
@@ -1359,13 +1377,17 @@ void ensure_rowmajor(Ctx& c) {
   c.xa_valid = true;
 }
 
-// QH = 1, 2: the hi / lo split copy; 3: the hi-only copy of d > 8 (HO)
+// QH = 1, 2: the hi / lo split copy; 3: the hi-only copy of d > 8, 4: of d <= 8 (HO)
 static void ensure_split(Ctx& c, int QH) {
   if (c.xs_valid && c.xs_qh == QH) return;
   ensure_rowmajor(c);
-  c.xs16.ensure((size_t)c.n_pad * 32 * (QH == 3 ? 1 : QH));
+  c.xs16.ensure((size_t)c.n_pad * (QH == 4 ? 16 : QH == 3 ? 32 : 32 * QH));
   const float sig = (float)std::ldexp(1.0, c.sigma);
-  if (QH == 3)
+  if (QH == 4)
+    hipLaunchKernelGGL((split_copy_kernel<1, true>), dim3(4096), dim3(256), 0, c.stream,
+                       c.x32.as<float>(), c.n, c.n_pad, c.d, c.mu_s.as<float>(), sig,
+                       c.xs16.as<uint4>());
+  else if (QH == 3)
     hipLaunchKernelGGL((split_copy_kernel<2, true>), dim3(4096), dim3(256), 0, c.stream,
                        c.x32.as<float>(), c.n, c.n_pad, c.d, c.mu_s.as<float>(), sig,
                        c.xs16.as<uint4>());
@@ -1407,12 +1429,12 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
                            long long* gate) {
   // d > 8: the hi-only screen (half the bytes; CDR_S32D_HO=0: the split copy)
   static const bool ho_env = !std::getenv("CDR_S32D_HO") || std::atoi(std::getenv("CDR_S32D_HO"));
-  const bool HO = QH == 2 && ho_env;
+  const bool HO = ho_env;
   // hi-only: LDS ring of CDR_S32H_LR slots per wave (2..4; 0: register prefetch);
   // A/B at config 3: 2 slots 0.90-0.91 ms, 3-4 slots 0.92-0.95, registers 0.93
   static const int lr_env = std::getenv("CDR_S32H_LR") ? std::atoi(std::getenv("CDR_S32H_LR")) : 2;
-  const int LRn = HO && lr_env >= 2 && lr_env <= 4 ? lr_env : 0;
-  ensure_split(c, HO ? 3 : QH);
+  const int LRn = HO && QH == 2 && lr_env >= 2 && lr_env <= 4 ? lr_env : 0;
+  ensure_split(c, HO ? (QH == 2 ? 3 : 4) : QH);
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
   int bpc;
@@ -1421,6 +1443,10 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 2, true, true>() : s32d_blocks_per_cu<2, 2, 2, true, true>();
     else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 3, true, true>() : s32d_blocks_per_cu<2, 2, 3, true, true>();
     else bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 4, true, true>() : s32d_blocks_per_cu<2, 2, 4, true, true>();
+  } else if (HO && QH == 1) {
+    if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<1, 1, 2, true>() : s32d_blocks_per_cu<1, 2, 2, true>();
+    else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<1, 1, 3, true>() : s32d_blocks_per_cu<1, 2, 3, true>();
+    else bpc = MT == 1 ? s32d_blocks_per_cu<1, 1, 4, true>() : s32d_blocks_per_cu<1, 2, 4, true>();
   } else if (HO) {
     if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 2, true>() : s32d_blocks_per_cu<2, 2, 2, true>();
     else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 3, true>() : s32d_blocks_per_cu<2, 2, 3, true>();
@@ -1483,7 +1509,8 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   if (LRn)
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>lds", MT, PD);
   else if (HO)
-    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>", MT, PD);
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), QH == 1 ? "screen32h1<%d,%d>" : "screen32h<%d,%d>",
+             MT, PD);
   else
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32d<%d,%d,%d>", QH, MT, PD);
   if (prof) prof_mark(c, 0);
@@ -1491,6 +1518,8 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
 #define CDR_S32D_LAUNCH(P)                                                                  \
   if (LRn && MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P, true, true>), grid, blk, 0, c.stream, a); \
   else if (LRn) hipLaunchKernelGGL((screen32d<2, 2, P, true, true>), grid, blk, 0, c.stream, a);       \
+  else if (HO && QH == 1 && MT == 1) hipLaunchKernelGGL((screen32d<1, 1, P, true>), grid, blk, 0, c.stream, a); \
+  else if (HO && QH == 1) hipLaunchKernelGGL((screen32d<1, 2, P, true>), grid, blk, 0, c.stream, a); \
   else if (HO && MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P, true>), grid, blk, 0, c.stream, a); \
   else if (HO) hipLaunchKernelGGL((screen32d<2, 2, P, true>), grid, blk, 0, c.stream, a);      \
   else if (QH == 1 && MT == 1) hipLaunchKernelGGL((screen32d<1, 1, P>), grid, blk, 0, c.stream, a); \

@@ -228,9 +228,9 @@ def test_incremental_update_equals_full_recompute(ctx, n, d, k, monkeypatch):
             C[-1] = X[12345 % n]
 
 
-@pytest.mark.parametrize("d", [16, 11])
+@pytest.mark.parametrize("d", [16, 11, 8, 5])
 def test_hi_only_screen_near_ties(ctx, d):
-    """The DELTA steps of d > 8 screen fp16(xhat) alone (screen32h): points put
+    """The DELTA steps screen fp16(xhat) alone (screen32h, screen32h1): points put
     on the bisectors of centroid pairs and a few fp16 ulps off them must still
     get the reference's label (the per-point certificate sends them to the
     exact fallback)."""
