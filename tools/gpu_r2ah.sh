@@ -14,6 +14,6 @@ timeout -k 10 400 python -u bench.py --config 5 --steps 10 --warmup 2 > gpurun_o
 for f in bench2 bench4 bench5; do python3 -c "import json;d=json.load(open('gpurun_out/$f.json'));print('$f',d['value'],d['ms_per_step'],d['roofline']['frac'],d.get('cpu_baseline',{}).get('value'))"; done
 
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run -- python3 bench.py --config 3 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof3.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof3.log; exit 7; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof3 -o run -- python3 bench.py --config 3 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof3.log 2>&1 || { echo PROF_FAIL; tail -20 gpurun_out/prof3.log; exit 7; }
 find gpurun_out/prof3 -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/prof3_kernel_stats.csv
 echo ALL_OK
