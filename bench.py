@@ -499,6 +499,9 @@ def main() -> None:
                 kb = n_local * (b + 1)
                 roofline["kernel_bytes_per_launch"] = kb
                 roofline["kernel_frac"] = kb / (screen_ms / 1e3) / 1e9 / HBM_PEAK_GBPS
+                roofline["note"] = ("achieved/frac: SURVEY 8(d) bytes (fp32 point + int32 label); "
+                                    "the kernel streams its fp16 copy + 1-byte label instead "
+                                    "(kernel_bytes_per_launch, kernel_frac), DESIGN.md 4.3c")
                 break
     # (the fallback counter accumulates over every profiled-session step)
     fb_frac = prof["fallback_points"] / max(args.steps, 1) / max(n_local, 1)
