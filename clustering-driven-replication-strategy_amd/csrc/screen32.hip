@@ -924,6 +924,8 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
   }
 }
 
+constexpr int kFixMaxR = 16;  // screen waves per fixup32 workgroup at most
+
 struct FixArgs {
   const float* XA;     // the points row-major, d4 floats per point (one line each)
   int64_t n_pad;
@@ -937,6 +939,7 @@ struct FixArgs {
   const int32_t* mv_count;
   int cap;
   int regions;  // screen32d waves
+  int fr;       // screen waves (list regions) per workgroup, <= kFixMaxR
   double fx;    // 2^S
   unsigned long long* run_sums;  // kRunSlices x (k, d+1)
   const long long* gate;
@@ -955,7 +958,7 @@ struct FixArgs {
   float sig;
 };
 
-// Workgroup b applies the lists of screen32d waves 4b .. 4b+3 (a region
+// Workgroup b applies the lists of screen32d waves FR b .. FR b + FR - 1 (a region
 // spread over the whole workgroup) to an LDS table (rows padded to 65: the
 // lanes of one point hit different banks).
 // * Moves, 4 lanes per point (lane q: feature quad q): +x into the new
@@ -977,10 +980,11 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
   __shared__ double tsum[D * TS];
   __shared__ int tcnt[64];
   __shared__ double cs[64 * CS];
-  __shared__ int s_mv[5], s_fb[5];
+  __shared__ int s_mv[kFixMaxR + 1], s_fb[kFixMaxR + 1];
+  const int FR = a.fr;
   const int k = a.k;
-  const int r0 = blockIdx.x * 4;
-  if (threadIdx.x < 4) {
+  const int r0 = blockIdx.x * FR;
+  if (threadIdx.x < FR) {
     const int r = r0 + threadIdx.x;
     s_mv[threadIdx.x + 1] = r < a.regions ? a.mv_count[r] : 0;
     s_fb[threadIdx.x + 1] = r < a.regions ? a.fb_count[r] : 0;
@@ -996,18 +1000,18 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     s_mv[0] = s_fb[0] = 0;
-    for (int r = 1; r <= 4; ++r) {
+    for (int r = 1; r <= FR; ++r) {
       s_mv[r] += s_mv[r - 1];
       s_fb[r] += s_fb[r - 1];
     }
   }
   __syncthreads();
-  const int nmv = s_mv[4], nfb = s_fb[4];
+  const int nmv = s_mv[FR], nfb = s_fb[FR];
   if (nmv == 0 && nfb == 0) return;  // uniform: nothing changes here
   const f4* XA4 = reinterpret_cast<const f4*>(a.XA);  // point i: XA4[i * Q + q]
   auto region_of = [&](const int* pre, int e, int& r, int& i) {
     r = 0;
-    while (r < 3 && e >= pre[r + 1]) ++r;
+    while (r < FR - 1 && e >= pre[r + 1]) ++r;
     i = e - pre[r];
   };
   const int g = threadIdx.x >> 2, q4 = threadIdx.x & 3;
@@ -1566,7 +1570,11 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
 #ifdef CDR_EXPERIMENTS
   if (const char* e = std::getenv("CDR_FIX_ABL")) f.abl = std::atoi(e);
 #endif
-  const dim3 fgrid((nwaves + 3) / 4);
+  // list regions per fixup workgroup: CDR_FIX_FR (1..16); A/B at config 3 (100M and
+  // the 12.5M shard): 8 leaves 79-82 / 34 us beside the screen, 4 91-93 / 42, 16 106 / 39
+  static const int fr_env = std::getenv("CDR_FIX_FR") ? std::atoi(std::getenv("CDR_FIX_FR")) : 8;
+  f.fr = fr_env >= 1 && fr_env <= kFixMaxR ? fr_env : 8;
+  const dim3 fgrid((nwaves + f.fr - 1) / f.fr);
   switch (c.d) {
 #define CDR_FIX(D_)                                                                  \
   case D_:                                                                           \
