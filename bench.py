@@ -390,7 +390,7 @@ def main() -> None:
     import numpy as np
 
     import _cdr
-    from cdr_dist import Comm, DeviceLloyd, row_fetcher, seed_sharded, shard_rows
+    from cdr_dist import Comm, DeviceLloyd, row_fetcher, seed_sharded, shard_rows, unify_points
 
     if args.config == "4":
         features_bench(args, world, rank, dist, device, json_fd)
@@ -413,6 +413,8 @@ def main() -> None:
 
         ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     ctx.generate_points(n_total, begin, n_local, d, k, args.seed)
+    unify_points(ctx, comm, n_total)  # one scale / screen transform on every rank
+    native = comm.attach_native(ctx)  # each step's all-reduce issued from C (csrc/comm.hip)
     ctx.synchronize()
 
     t0 = time.perf_counter()
@@ -521,7 +523,9 @@ def main() -> None:
         "data": "synthetic (device generator, oracle/synth.py formula; 2^-24-grid blobs)",
         "config": {"workload": desc, "n_files": n_total, "d": d, "k": k,
                    "parallelism": f"rows sharded over {world} GPU(s), RCCL all-reduce of "
-                                  f"k x (d+1) int64 per step",
+                                  f"k x (d+1) int64 per step" + (
+                                      " (ncclAllReduce enqueued from libcdr between the "
+                                      "step's kernels)" if native else " (none at 1 GPU)"),
                    "screen": "fp16 hi/lo split MFMA (certified) + exact fp64 fallback; "
                              "int64 fixed-point sums (results bit-identical to fp64 NumPy)",
                    "loop": "device-resident (means, shift, convergence test on the device; "

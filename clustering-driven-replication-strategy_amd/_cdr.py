@@ -57,6 +57,8 @@ SIGNATURES = {
     "cdr_points_generate": ([_P, _I64, _I64, _I64, _I32, _I32, _U64], None),
     "cdr_points_info": ([_P, _PI64, _PI32, _PI32, _PI32], None),
     "cdr_points_get_rows": ([_P, _P, _I64, _P], None),
+    "cdr_points_stats": ([_P, _P], None),
+    "cdr_points_restat": ([_P, _P, _I64], None),
     "cdr_seed_reset": ([_P], None),
     "cdr_seed_update": ([_P, _P], None),
     "cdr_seed_num_blocks": ([_P, _PI64], None),
@@ -79,6 +81,10 @@ SIGNATURES = {
     "cdr_lloyd_read": ([_P, _P, _P, _P], None),
     "cdr_lloyd_resume": ([_P, _P, _I32, _I32], None),
     "cdr_lloyd_end": ([_P], None),
+    "cdr_lloyd_enqueue_steps": ([_P, _I32], None),
+    "cdr_comm_unique_id": ([_P], None),
+    "cdr_comm_init": ([_P, _P, _I32, _I32], None),
+    "cdr_comm_destroy": ([_P], None),
     "cdr_build_id": ([], ctypes.c_char_p),
     "cdr_medians_segmented": ([_P, _P, _P, _I64, _P], None),
     "cdr_medians_by_label": ([_P, _I32, _P], None),
@@ -187,6 +193,13 @@ def device_count() -> int:
     return int(n.value)
 
 
+def comm_unique_id() -> bytes:
+    """A fresh 128-byte RCCL unique id (one rank creates it and broadcasts)."""
+    out = np.zeros(128, dtype=np.uint8)
+    _check(load_library().cdr_comm_unique_id(_ptr(out)))
+    return out.tobytes()
+
+
 def host_seq_sum(v: np.ndarray, init: float = 0.0) -> float:
     """((init + v[0]) + v[1]) + ... in fp64 (plain C on the host)."""
     v = np.ascontiguousarray(v, dtype=np.float64)
@@ -239,6 +252,18 @@ class Context:
         _check(self._lib.cdr_points_info(self._h, ctypes.byref(n), ctypes.byref(d),
                                          ctypes.byref(mode), ctypes.byref(s)))
         return {"n": n.value, "d": d.value, "mode": mode.value, "scale_bits": s.value}
+
+    def points_stats(self) -> np.ndarray:
+        """This shard's point statistics (include/cdr.h cdr_points_stats)."""
+        st = np.zeros(2 * self.info()["d"] + 3, dtype=np.uint64)
+        _check(self._lib.cdr_points_stats(self._h, _ptr(st)))
+        return st
+
+    def points_restat(self, st: np.ndarray, n_sum: int) -> None:
+        """Mode / scale / screen transform from statistics combined over
+        every shard (cdr_points_restat)."""
+        st = np.ascontiguousarray(st, dtype=np.uint64)
+        _check(self._lib.cdr_points_restat(self._h, _ptr(st), int(n_sum)))
 
     def get_rows(self, idx) -> np.ndarray:
         idx = np.ascontiguousarray(np.atleast_1d(idx), dtype=np.int64)
@@ -375,6 +400,21 @@ class Context:
 
     def lloyd_end(self) -> None:
         _check(self._lib.cdr_lloyd_end(self._h))
+
+    def lloyd_enqueue_steps(self, m: int) -> None:
+        """m loop steps (assign, all-reduce over the context's communicator,
+        finalize) enqueued from C (cdr_lloyd_enqueue_steps)."""
+        _check(self._lib.cdr_lloyd_enqueue_steps(self._h, int(m)))
+
+    # -- native collective (csrc/comm.hip) ----------------------------------
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
+        uid = np.frombuffer(bytes(unique_id), dtype=np.uint8).copy()
+        if uid.size != 128:
+            raise ValueError("unique_id must be 128 bytes")
+        _check(self._lib.cdr_comm_init(self._h, _ptr(uid), int(nranks), int(rank)))
+
+    def comm_destroy(self) -> None:
+        _check(self._lib.cdr_comm_destroy(self._h))
 
     def debug_screen(self, C: np.ndarray):
         C = np.ascontiguousarray(C, dtype=np.float64)
@@ -624,6 +664,7 @@ def loaded_library_path() -> str | None:
 
 
 __all__ = ["Context", "default_context", "load_library", "device_count", "host_seq_sum",
+           "comm_unique_id",
            "MODE_F32X", "MODE_F64", "SEED_BLOCK", "SIGNATURES", "LIB_PATH"]
 
 if __name__ == "__main__":  # pragma: no cover

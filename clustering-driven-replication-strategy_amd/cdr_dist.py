@@ -17,11 +17,14 @@ the single-process run:
   fixed-point sums/counts; one SUM all-reduce (integer, hence exact and
   order-free) over RCCL; every rank then forms the identical means.  With
   the device-resident loop (``device_lloyd``, csrc/loop.hip) the means, the
-  shift and the convergence test run on the device after the all-reduce, so
-  a step is three enqueues and no host round trip; the host only polls every
-  few steps and takes over exactly when the reference's host logic is needed
-  (empty cluster: np.random.randint on every rank in j order, the row
-  broadcast by its owner; a shift too close to tol: np.linalg.norm).
+  shift and the convergence test run on the device after the all-reduce, and
+  with a libcdr communicator (``Comm.attach_native``, csrc/comm.hip) a chunk
+  of steps — assign, ncclAllReduce, finalize each — is enqueued by one C
+  call; the host only polls every few steps and takes over exactly when the
+  reference's host logic is needed (empty cluster: np.random.randint on every
+  rank in j order, the row broadcast by its owner; a shift too close to tol:
+  np.linalg.norm).  ``unify_points`` gives every shard the same storage mode,
+  scale and screen transform, so these decisions agree on every rank.
 
 ``Comm`` hides the backend: NCCL (=RCCL on ROCm) keeps the all-reduced
 tensor on the GPU; gloo (the CPU test backend) uses host tensors.
@@ -52,6 +55,26 @@ class Comm:
         self.rank = dist.get_rank() if dist else 0
         self.world = dist.get_world_size() if dist else 1
         self.device = device  # torch.device for NCCL, None for gloo / single
+        self.native = set()  # ids of contexts with a libcdr RCCL communicator
+
+    def attach_native(self, ctx) -> bool:
+        """Give ``ctx`` its own RCCL communicator over the same ranks
+        (csrc/comm.hip), so that the device loop issues each step's
+        all-reduce from C (cdr_lloyd_enqueue_steps).  Only under NCCL (RCCL)
+        with device tensors; collective: every rank calls it."""
+        if self.device is None or not self.dist or not hasattr(ctx, "comm_init"):
+            return False
+        import torch
+
+        import _cdr
+
+        uid = np.frombuffer(_cdr.comm_unique_id(), dtype=np.uint8) if self.rank == 0 \
+            else np.zeros(128, dtype=np.uint8)
+        t = torch.from_numpy(uid.copy()).to(self.device)
+        self.dist.broadcast(t, 0)
+        ctx.comm_init(t.cpu().numpy().tobytes(), self.world, self.rank)
+        self.native.add(id(ctx))
+        return True
 
     def _t(self, arr):
         import torch
@@ -182,6 +205,26 @@ class Comm:
         return t.cpu().numpy()
 
 
+_SIGN = np.uint64(1 << 63)
+
+
+def unify_points(ctx, comm: Comm | None, n_total: int) -> None:
+    """One storage mode, fixed-point scale and screen transform for every
+    shard (include/cdr.h cdr_points_restat): the int64 sums of the all-reduce
+    must share one scale, and the device loop's stop decisions (the fp16
+    screen-range guard) must be the same on every rank.  Statistics are
+    combined with MIN (per-feature minima) and MAX (everything else) over the
+    ranks; collective: every rank calls it after loading its shard."""
+    st = ctx.points_stats()
+    if comm is not None and comm.world > 1:
+        d = (st.size - 3) // 2
+        s = (st ^ _SIGN).view(np.int64)  # unsigned order -> signed order
+        lo = comm.allreduce_i64(s[:d], "min")
+        hi = comm.allreduce_i64(s[d:], "max")
+        st = np.concatenate([lo, hi]).view(np.uint64) ^ _SIGN
+    ctx.points_restat(st, n_total)
+
+
 def _fetch_row(ctx, comm: Comm, owner: int, local_idx: int, d: int) -> np.ndarray:
     row = ctx.get_rows([local_idx])[0] if comm.rank == owner else np.zeros(d)
     return comm.bcast(np.asarray(row, dtype=np.float64), owner)
@@ -255,13 +298,20 @@ class DeviceLloyd:
             x2 = comm.allreduce_sum_f64(x2)
         ctx.lloyd_begin(C, tol, ref, x2, round32=self.dtype == np.float32)
         self.buf, self.ptr = None, None
-        if comm is not None and comm.world > 1:
+        # steps enqueued from C (one call per chunk): a single shard, or a
+        # context with its own RCCL communicator (Comm.attach_native)
+        self.native = hasattr(ctx, "lloyd_enqueue_steps") and (
+            comm is None or id(ctx) in comm.native or comm.world == 1)
+        if not self.native and comm is not None and comm.world > 1:
             self.buf, self.ptr = comm.lloyd_buffer(self.k * (self.d + 1))
         self.steps = 0
         self.converged = False
         self.status = None
 
     def enqueue(self, m: int) -> None:
+        if self.native:
+            self.ctx.lloyd_enqueue_steps(m)
+            return
         for _ in range(m):
             self.ctx.lloyd_enqueue_assign(self.ptr)
             if self.buf is not None:

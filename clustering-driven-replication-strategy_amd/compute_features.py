@@ -124,7 +124,7 @@ def java_double(x: float) -> str:
     t = Decimal(repr(abs(x))).as_tuple()
     digits = "".join(map(str, t.digits)).rstrip("0") or "0"
     exp10 = len(t.digits) + t.exponent - 1  # position of the leading digit
-    if len(digits) == 1:
+    if len(digits) == 1 and abs(x) < 2.2250738585072014e-308:
         # JDK 19+ Double.toString: when the shortest decimal has one digit,
         # two-digit decimals that round to x compete and the closest to x
         # wins (only subnormals near 4.9E-324 have one): Double.MIN_VALUE

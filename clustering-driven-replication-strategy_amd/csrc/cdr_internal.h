@@ -102,6 +102,9 @@ struct Ctx {
   DevBuf x32;              // F32X: float  [d4/4][n_pad][4]   (xidx)
   DevBuf x64;              // F64 : double [d4/4][n_pad][4]   (xidx)
   std::vector<double> fmin, fmax;  // per-feature min / max (host)
+  // this shard's statistics (run_stats layout, 2d + 3 words): kept so that a
+  // sharded caller can combine them over the ranks (cdr_points_restat)
+  std::vector<unsigned long long> st_local;
   double absmax = 0.0;
   // screen transform  xhat = (x - mu_f) * 2^sigma
   std::vector<float> mu;
@@ -202,6 +205,11 @@ struct Ctx {
   int ll_fin_slices = 1;
   bool ll_fin_devstep = false;  // the last assign was a device-plan screen32 step
 
+  // ---- native collective (comm.hip): RCCL communicator of the loop ----
+  void* comm = nullptr;  // ncclComm_t
+  int comm_ranks = 1, comm_rank = 0;
+  DevBuf comm_buf;  // the step's (k, d+1) int64 sums, all-reduced in place
+
   // ---- seeding ----
   DevBuf dmin;        // double[n_pad]
   // exact pruning of the seeding update (seed.hip seed_prunable): the index
@@ -288,6 +296,11 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums);
 void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
                        const double* creation_s, double observation_end,
                        double* out);
+
+// comm.hip: SUM all-reduce of n int64 in place on the context stream over the
+// context's communicator; release of that communicator
+void comm_allreduce_i64(Ctx& c, long long* buf, size_t n);
+void comm_release(Ctx& c);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

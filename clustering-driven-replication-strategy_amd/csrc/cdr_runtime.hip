@@ -117,6 +117,13 @@ __global__ void rowmajor_to_soa64(const double* __restrict__ src, int64_t rows,
   }
 }
 
+__global__ void soa32_to_soa64(const float* __restrict__ src, int64_t count,
+                               double* __restrict__ dst) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count;
+       t += (int64_t)gridDim.x * blockDim.x)
+    dst[t] = (double)src[t];
+}
+
 __global__ void soa64_to_soa32(const double* __restrict__ src, int64_t count,
                                float* __restrict__ dst) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count;
@@ -194,6 +201,7 @@ static void run_stats(Ctx& c, bool f32, std::vector<unsigned long long>& st) {
                            hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
   dst.release();
+  c.st_local = st;
 }
 
 // Decide the storage mode and the screen transform from the statistics.
@@ -208,7 +216,7 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   c.fmax.assign(d, 0.0);
   c.absmax = 0.0;
   for (int f = 0; f < d; ++f) {
-    if (c.n > 0) {
+    if (st[f] <= st[d + f]) {  // (an empty shard before cdr_points_restat: no range)
       c.fmin[f] = key_to_double(st[f]);
       c.fmax[f] = key_to_double(st[d + f]);
     }
@@ -251,6 +259,8 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   // fp32 when every |x - mu| is < 2^24 grid steps, mu is itself on the grid and
   // the smallest step 2^(sigma - S) is a normal float.
   c.pre_ok = c.mode == CDR_MODE_F32X && c.n > 0 && (c.sigma - S) >= -126;
+  for (int f = 0; f < d; ++f)
+    if (!(st[f] <= st[d + f])) c.pre_ok = false;
   for (int f = 0; f < d && c.pre_ok; ++f) {
     const double mu = (double)c.mu[f];
     if (std::ldexp(std::rint(std::ldexp(mu, S)), -S) != mu) c.pre_ok = false;
@@ -410,7 +420,8 @@ int cdr_destroy(cdr_ctx* h) {
   Ctx& c = h->c;
   (void)hipSetDevice(c.device);
   (void)hipStreamSynchronize(c.stream);
-  DevBuf* bufs[] = {&c.x32, &c.x64, &c.xt32, &c.muf, &c.mu_s, &c.labels, &c.cent64, &c.frag,
+  comm_release(c);
+  DevBuf* bufs[] = {&c.comm_buf, &c.x32, &c.x64, &c.xt32, &c.muf, &c.mu_s, &c.labels, &c.cent64, &c.frag,
                     &c.partials, &c.out_sums, &c.fb_list, &c.fb_count, &c.f64_sums,
                     &c.f64_counts, &c.dmin, &c.blocksums, &c.xfer, &c.cend,
                     &c.seed_scalar, &c.med_vals, &c.med_off, &c.med_out, &c.med_tmp,
@@ -479,6 +490,49 @@ int cdr_points_generate(cdr_ctx* h, int64_t n_total, int64_t row_begin,
   HIP_CHECK(hipSetDevice(c.device));
   reset_points(c, n_local, d);
   points_generate(c, n_total, row_begin, n_blobs, seed);
+  CDR_CATCH
+}
+
+int cdr_points_stats(cdr_ctx* h, uint64_t* st) {
+  CDR_TRY
+  if (!h || !st) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  if (c.mode == 0 || c.st_local.size() != (size_t)(2 * c.d + 3))
+    CDR_FAIL(CDR_ERR_STATE, "no points loaded");
+  for (size_t i = 0; i < c.st_local.size(); ++i) st[i] = c.st_local[i];
+  CDR_CATCH
+}
+
+int cdr_points_restat(cdr_ctx* h, const uint64_t* st, int64_t n_sum) {
+  CDR_TRY
+  if (!h || !st) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  if (c.mode == 0) CDR_FAIL(CDR_ERR_STATE, "no points loaded");
+  const int d = c.d;
+  std::vector<unsigned long long> g(st, st + 2 * d + 3);
+  // the combined statistics must cover this shard's
+  for (int f = 0; f < d && c.n > 0; ++f)
+    if (g[f] > c.st_local[f] || g[d + f] < c.st_local[d + f])
+      CDR_FAIL(CDR_ERR_ARG, "restat: statistics do not cover this shard");
+  const int old_mode = c.mode;
+  const std::vector<unsigned long long> keep = c.st_local;
+  decide_mode(c, g, false, n_sum);
+  c.st_local = keep;
+  if (old_mode == CDR_MODE_F32X && c.mode == CDR_MODE_F64) {
+    // another shard is not on an fp32 grid: this one's exact fp32 values
+    // become its fp64 copy
+    const int64_t cnt = (int64_t)d4_of(d) * c.n_pad;
+    c.x64.ensure(sizeof(double) * (size_t)cnt);
+    hipLaunchKernelGGL(soa32_to_soa64, dim3(grid_for(cnt, 256)), dim3(256), 0, c.stream,
+                       c.x32.as<float>(), cnt, c.x64.as<double>());
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    c.x32.release();
+  } else if (old_mode == CDR_MODE_F64 && c.mode == CDR_MODE_F32X) {
+    CDR_FAIL(CDR_ERR_ARG, "restat: a shard stored as F64 cannot become F32X");
+  }
+  HIP_CHECK(hipStreamSynchronize(c.stream));
   CDR_CATCH
 }
 

@@ -112,17 +112,27 @@ __global__ __launch_bounds__(256) void x_pack(const int32_t* __restrict__ file,
   }
 }
 
-__global__ void x_unpack(const XRec* __restrict__ in, int64_t n, long long file_begin,
-                         int32_t* __restrict__ file, uint8_t* __restrict__ op,
-                         int32_t* __restrict__ client, long long* __restrict__ ts) {
+// Also the largest client id received (*cmax, zeroed by the caller): the
+// group-by sizes its packed client field from it, and records from a rank
+// whose slice went through the host tokeniser may carry ids no local ingest saw.
+__global__ __launch_bounds__(256) void x_unpack(const XRec* __restrict__ in, int64_t n,
+                                                long long file_begin, int32_t* __restrict__ file,
+                                                uint8_t* __restrict__ op,
+                                                int32_t* __restrict__ client,
+                                                long long* __restrict__ ts, int* __restrict__ cmax) {
+  int hi = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const XRec x = in[i];
     ts[i] = x.ts;
     file[i] = (int32_t)(x.file - file_begin);
     op[i] = (uint8_t)(x.cop & 0xFF);
-    client[i] = x.cop >> 8;  // arithmetic shift: the signed 24-bit client
+    const int cl = x.cop >> 8;  // arithmetic shift: the signed 24-bit client
+    client[i] = cl;
+    hi = max(hi, cl);
   }
+  for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_xor(hi, o));
+  if ((threadIdx.x & 63) == 0 && hi > 0) atomicMax(cmax, hi);
 }
 
 int xgrid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256), 4096)); }
@@ -203,11 +213,16 @@ int cdr_features_exchange_unpack(cdr_ctx* h, const void* recv, int64_t n, int64_
   c.ev_op.ensure(n1);
   c.ev_client.ensure(4 * n1);
   c.ev_ts.ensure(8 * n1);
+  c.x_small.ensure(64);
+  int* dcmax = c.x_small.as<int>();
+  HIP_CHECK(hipMemsetAsync(dcmax, 0, sizeof(int), c.stream));
   if (n > 0)
     hipLaunchKernelGGL(x_unpack, dim3(xgrid(n)), dim3(256), 0, c.stream, c.x_buf.as<XRec>(), n,
                        (long long)file_begin, c.ev_file.as<int32_t>(), c.ev_op.as<uint8_t>(),
-                       c.ev_client.as<int32_t>(), c.ev_ts.as<long long>());
+                       c.ev_client.as<int32_t>(), c.ev_ts.as<long long>(), dcmax);
   HIP_CHECK(hipGetLastError());
+  int cmax = 0;
+  HIP_CHECK(hipMemcpyAsync(&cmax, dcmax, sizeof(int), hipMemcpyDeviceToHost, c.stream));
   // the owned rows' primaries move to the front
   const int64_t nfl = file_end - file_begin;
   if (nfl > 0 && file_begin > 0) {
@@ -220,6 +235,9 @@ int cdr_features_exchange_unpack(cdr_ctx* h, const void* recv, int64_t n, int64_
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.ev_n = n;
   c.ev_nf = nfl;
+  // the packed client field must hold every received id (and the owned
+  // primaries the local manifest gave: keep the wider of the two)
+  c.ev_cmax = std::max(c.ev_cmax, cmax);
   CDR_CATCH
 }
 

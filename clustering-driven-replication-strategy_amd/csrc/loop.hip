@@ -363,12 +363,11 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   CDR_CATCH
 }
 
-int cdr_lloyd_enqueue_assign(cdr_ctx* h, int64_t* dsums) {
-  CDR_TRY
-  if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
-  Ctx& c = h->c;
-  HIP_CHECK(hipSetDevice(c.device));
-  ll_require(c);
+}  // extern "C"
+
+namespace cdr {
+
+static void ll_enqueue_assign(Ctx& c, int64_t* dsums) {
   long long* dout = dsums ? reinterpret_cast<long long*>(dsums) : c.ll_sums.as<long long>();
   long long* state = c.ll_state.as<long long>();
   if (c.ll_devplan && !c.ll_hostplan_once) {
@@ -413,15 +412,9 @@ int cdr_lloyd_enqueue_assign(cdr_ctx* h, int64_t* dsums) {
     }
   }
   c.ll_enqueued += 1;
-  CDR_CATCH
 }
 
-int cdr_lloyd_enqueue_finalize(cdr_ctx* h, const int64_t* dsums) {
-  CDR_TRY
-  if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
-  Ctx& c = h->c;
-  HIP_CHECK(hipSetDevice(c.device));
-  ll_require(c);
+static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
   if (dsums && reinterpret_cast<const long long*>(dsums) != c.ll_fin_sums)
     CDR_FAIL(CDR_ERR_ARG, "lloyd finalize: pass the buffer given to the assign");
   const int kd = c.ll_k * c.d;
@@ -458,6 +451,52 @@ int cdr_lloyd_enqueue_finalize(cdr_ctx* h, const int64_t* dsums) {
   HIP_CHECK(hipGetLastError());
   if (c.ll_devbig) ll_plan_big(c);  // the next step's plan (skipped once the loop stopped)
   if (c.ll_fin_devstep && c.prof_cur >= 0) prof_mark(c, 2);
+}
+
+}  // namespace cdr
+
+extern "C" {
+
+int cdr_lloyd_enqueue_assign(cdr_ctx* h, int64_t* dsums) {
+  CDR_TRY
+  if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  ll_require(c);
+  ll_enqueue_assign(c, dsums);
+  CDR_CATCH
+}
+
+int cdr_lloyd_enqueue_finalize(cdr_ctx* h, const int64_t* dsums) {
+  CDR_TRY
+  if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  ll_require(c);
+  ll_enqueue_finalize(c, dsums);
+  CDR_CATCH
+}
+
+int cdr_lloyd_enqueue_steps(cdr_ctx* h, int32_t m) {
+  CDR_TRY
+  if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
+  if (m < 0) CDR_FAIL(CDR_ERR_ARG, "m must be >= 0");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  ll_require(c);
+  // with a communicator: the step's sums go to comm_buf, which RCCL sums in
+  // place over the ranks on this stream before the finalize reads it
+  const size_t cells = (size_t)c.ll_k * (c.d + 1);
+  int64_t* buf = nullptr;
+  if (c.comm) {
+    c.comm_buf.ensure(sizeof(long long) * cells);
+    buf = c.comm_buf.as<int64_t>();
+  }
+  for (int32_t i = 0; i < m; ++i) {
+    ll_enqueue_assign(c, buf);
+    if (c.comm) comm_allreduce_i64(c, reinterpret_cast<long long*>(buf), cells);
+    ll_enqueue_finalize(c, buf);
+  }
   CDR_CATCH
 }
 

@@ -557,7 +557,11 @@ __global__ __launch_bounds__(256) void publish32(const long long* __restrict__ o
                                                  int* __restrict__ fbc, int nwaves,
                                                  long long* __restrict__ fb_acc,
                                                  const long long* __restrict__ gate) {
-  if (gate && gate[0] == 0) return;
+  if (gate && gate[0] == 0) {  // a stopped loop contributes nothing to the all-reduce
+    if (dout)
+      for (int i = threadIdx.x; i < cells; i += blockDim.x) dout[i] = 0;
+    return;
+  }
   for (int i = threadIdx.x; i < cells; i += blockDim.x) {
     long long v = 0;
     for (int sl = 0; sl < kRunSlices; ++sl) v += out[(size_t)sl * cells + i];

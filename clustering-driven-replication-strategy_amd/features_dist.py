@@ -8,7 +8,8 @@ Partition (DESIGN.md §features sharding):
 * log — rank r ingests the newline-aligned byte range [r L / W, (r+1) L / W)
   of the access log (``log_slice``; a line belongs to the rank whose range
   holds its first byte), on the device (csrc/ingest.hip) or, for CSV quoting,
-  with the host tokeniser;
+  with the host tokeniser; when any slice holds a quote every rank cuts at
+  CSV record starts instead, so a quoted newline never splits a record;
 * exchange — one all-to-all (RCCL on the GPU path) of 16-byte event records
   sends every event to the owner of its file row (csrc/exchange.hip), so the
   owner's group-by (csrc/groupby.hip) sees all events of its files: the
@@ -65,13 +66,61 @@ def _line_start(fh, x: int, size: int) -> int:
         pos += len(chunk)
 
 
-def log_slice(path: str, rank: int, world: int) -> bytes:
-    """Rank `rank`'s newline-aligned byte range of the log."""
+_Q, _C, _NL = ord('"'), ord(","), ord("\n")
+
+
+def _record_start(fh, x: int, size: int) -> int:
+    """First CSV record start at or after byte x, reading the log from byte 0
+    the way csv.reader does (excel dialect, the host path of
+    compute_features.load_access_log): a newline inside a quoted field does
+    not end the record.  Linear in x; only used for logs that hold quotes."""
+    if x <= 0:
+        return 0
+    if x >= size:
+        return size
+    fh.seek(0)
+    inq = qpend = False  # inside a quoted field / a quote seen inside one
+    fstart = True        # at the first byte of a field
+    pos = 0
+    while True:
+        chunk = fh.read(1 << 16)
+        if not chunk:
+            return size
+        for i, c in enumerate(chunk):
+            if inq:
+                if qpend:
+                    qpend = False
+                    if c == _Q:  # "" inside quotes: a literal quote
+                        continue
+                    inq = False  # the quoted part ended; c continues the field
+                elif c == _Q:
+                    qpend = True
+                    continue
+                else:
+                    continue
+            if c == _Q and fstart:
+                inq, fstart = True, False
+            elif c == _C:
+                fstart = True
+            elif c == _NL:
+                fstart = True
+                if pos + i + 1 >= x:
+                    return pos + i + 1
+            else:
+                fstart = c == 13  # after a CR a new record (and field) begins
+        pos += len(chunk)
+
+
+def log_slice(path: str, rank: int, world: int, quoted: bool = False) -> bytes:
+    """Rank `rank`'s byte range of the log: cut at newlines, or (quoted: the
+    log holds CSV quoting) at record starts, so that a quoted field with a
+    newline stays on one rank as csv.reader keeps it in one record."""
     path = cf._strip_scheme(path)
     size = os.path.getsize(path)
+    start = _record_start if quoted else _line_start
     with open(path, "rb") as fh:
-        a = _line_start(fh, (size * rank) // world, size)
-        b = _line_start(fh, (size * (rank + 1)) // world, size)
+        a = start(fh, (size * rank) // world, size)
+        b = start(fh, (size * (rank + 1)) // world, size)
         fh.seek(a)
         return fh.read(b - a)
 
@@ -108,6 +157,8 @@ def sharded_compute_features(manifest: str, access_log: str, ctx, comm: Comm):
     prim, nodes = cf.encode_primary(primary)
     # 1) this rank's slice of the log -> resident events (global rows)
     data = log_slice(access_log, rank, world)
+    if int(comm.allreduce_i64(np.array([b'"' in data], dtype=np.int64), "max")[0]):
+        data = log_slice(access_log, rank, world, quoted=True)
     ctx.ingest_manifest(paths, prim, nodes)
     st = ctx.ingest_log(data)
     if st[2] >= 0:  # CSV syntax the device tokeniser leaves to the host

@@ -70,6 +70,16 @@ int cdr_points_generate(cdr_ctx* ctx, int64_t n_total, int64_t row_begin,
                         uint64_t seed);
 int cdr_points_info(cdr_ctx* ctx, int64_t* n, int32_t* d, int32_t* mode,
                     int32_t* scale_bits);
+/* Points sharded over ranks: every rank must use the same
+ * storage mode, fixed-point scale S and screen transform, or the int64 sums
+ * of the all-reduce and the device loop's stop decisions would differ per
+ * rank.  cdr_points_stats: this shard's statistics st[2d + 3] (uint64 order
+ * keys of the per-feature minima, then maxima; max(-lsb) + 200000; not-fp32
+ * flag; non-finite flag).  cdr_points_restat: re-decide mode / S / transform
+ * from statistics combined over every shard (MIN of the minimum keys, MAX of
+ * every other word) and the global row count n_sum.                         */
+int cdr_points_stats(cdr_ctx* ctx, uint64_t* st);
+int cdr_points_restat(cdr_ctx* ctx, const uint64_t* st, int64_t n_sum);
 /* Copy local rows idx[0..m) to host as float64 (m, d). */
 int cdr_points_get_rows(cdr_ctx* ctx, const int64_t* idx, int64_t m,
                         double* out);
@@ -164,6 +174,21 @@ int cdr_lloyd_status(cdr_ctx* ctx, int64_t* status, double* values);
 int cdr_lloyd_read(cdr_ctx* ctx, double* C, double* means, int64_t* counts);
 int cdr_lloyd_resume(cdr_ctx* ctx, const double* C, int32_t add_steps, int32_t host_plan_once);
 int cdr_lloyd_end(cdr_ctx* ctx);
+/* m loop steps enqueued by one call: assign, the SUM all-reduce of the
+ * (k, d+1) int64 sums over the context's communicator (cdr_comm_init; none:
+ * a single shard), finalize — no host synchronisation and no host code
+ * between a step's kernels and its collective.                              */
+int cdr_lloyd_enqueue_steps(cdr_ctx* ctx, int32_t m);
+
+/* ---- native collective for the loop: RCCL over xGMI ------------------- */
+/* One communicator per context (one process per GPU).  cdr_comm_unique_id
+ * writes the 128-byte ncclUniqueId (one rank creates it, the caller
+ * broadcasts it); cdr_comm_init joins the nranks-rank communicator as `rank`
+ * on the context's device; cdr_comm_destroy leaves it.  librccl is bound at
+ * run time; CDR_ERR_UNSUPPORTED when it cannot be loaded.                   */
+int cdr_comm_unique_id(void* id128);
+int cdr_comm_init(cdr_ctx* ctx, const void* id128, int32_t nranks, int32_t rank);
+int cdr_comm_destroy(cdr_ctx* ctx);
 /* Name of the last screen kernel launched (for the bench's roofline line);
  * NUL-terminated, truncated to len.                                          */
 int cdr_profile_kernel(cdr_ctx* ctx, char* buf, int32_t len);

@@ -176,3 +176,52 @@ def test_two_ranks_match_single_process(tmp_path, empty):
     np.random.seed(0)
     C_ref = _reference_lloyd(X, C0, 6, 1e-4 if empty else -1.0)
     np.testing.assert_array_equal(np.load(tmp_path / "C.npy"), C_ref)
+
+
+class StatsShard:
+    """points_stats / points_restat double for cdr_dist.unify_points."""
+
+    def __init__(self, st):
+        self.st, self.got = st, None
+
+    def points_stats(self):
+        return self.st.copy()
+
+    def points_restat(self, st, n_sum):
+        self.got = (st.copy(), n_sum)
+
+
+def _unify_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    from cdr_dist import Comm, unify_points
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = StatsShard(_unify_stats()[rank])
+    unify_points(sh, Comm(dist, None), 12345)
+    np.save(os.path.join(out_dir, f"st{rank}.npy"), sh.got[0])
+    assert sh.got[1] == 12345
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _unify_stats():
+    """Three shards' statistics (d = 2): order keys on both sides of 2^63."""
+    big = 1 << 63
+    return [np.array([big + 5, big - 7, big + 9, big - 1, 200024, 0, 0], dtype=np.uint64),
+            np.array([big + 3, big - 9, big + 2, big + 4, 200030, 1, 0], dtype=np.uint64),
+            np.array([~np.uint64(0), big + 1, 0, big - 3, 200010, 0, 1], dtype=np.uint64)]
+
+
+def test_unify_points_combines_stats(tmp_path):
+    """cdr_dist.unify_points: unsigned MIN of the minimum keys and MAX of every
+    other word over the ranks (through the signed int64 all-reduce)."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    world = 3
+    mp.spawn(_unify_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    sts = _unify_stats()
+    want = np.concatenate([np.minimum.reduce([s[:2] for s in sts]),
+                           np.maximum.reduce([s[2:] for s in sts])])
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"st{r}.npy"), want)

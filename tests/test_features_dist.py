@@ -177,9 +177,46 @@ def test_file_bounds_and_log_slices(tmp_path):
             assert x == b"" or x[-1:] == b"\n" or end == len(data)
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_sharded_features_equal_single_process(tmp_path, world):
+def test_quoted_log_slices_keep_records(tmp_path):
+    """A quoted field with newlines (and doubled quotes) never straddles two
+    ranks' slices: the slices' records are csv.reader's records of the whole
+    log, for every world size and wherever the byte cut lands."""
+    import csv
+    import io
+
+    from features_dist import log_slice
+
+    lines = ["2025-11-01T12:00:00.000Z,/a.bin,READ,dn1,1"]
+    lines += ['2025-11-01T12:00:01.000Z,"/b\n\n""q""\n.bin",WRITE,dn2,2'] * 3
+    lines += ['2025-11-01T12:00:02.000Z,/c"d.bin,READ,dn3,3', "", "x,\"y\nz\",READ,dn1,4\r"]
+    data = ("\n".join(lines) + "\n").encode()
+    p = tmp_path / "q.log"
+    p.write_bytes(data)
+    want = list(csv.reader(io.StringIO(data.decode(), newline="")))
+    for w in range(1, 12):
+        parts = [log_slice(str(p), r, w, quoted=True) for r in range(w)]
+        assert b"".join(parts) == data
+        got = [rec for x in parts for rec in csv.reader(io.StringIO(x.decode(), newline=""))]
+        assert got == want, w
+
+
+def _quoted_case(tmp_path):
+    """_case with records whose quoted path holds newlines, placed across
+    the byte cuts of 2 and 3 ranks."""
     man, log = _case(tmp_path)
+    with open(log) as fh:
+        lines = fh.read().rstrip("\n").split("\n")
+    q = ('2025-11-01T12:05:00.000Z,"/user/root/synth/' + "\n" * 300 + 'synth_7.bin",READ,dn1,9')
+    lines = [x for i, line in enumerate(lines) for x in ([line, q] if i % 3 == 2 else [line])]
+    with open(log, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    return man, log
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("quoted", [False, True], ids=["plain", "quoted-newlines"])
+def test_sharded_features_equal_single_process(tmp_path, world, quoted):
+    man, log = (_quoted_case if quoted else _case)(tmp_path)
     if world == 1:
         from cdr_dist import Comm
         from features_dist import sharded_compute_features

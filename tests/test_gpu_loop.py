@@ -239,3 +239,111 @@ def test_sharded_device_loop_two_contexts(n, d, k):
     np.testing.assert_array_equal(Cs[1], C_ref)
     np.testing.assert_array_equal(labs, lab_ref)
     assert abs(sts[0]["inertia"] - st_ref["inertia"]) <= 1e-9 * st_ref["inertia"]
+
+
+def _two_context_loop(parts, C0, steps, unify, n_total):
+    """enqueue_assign -> device-tensor SUM -> enqueue_finalize on one context
+    per shard (the multi-GPU step emulated on one GPU); returns the contexts'
+    statuses, centroids and labels."""
+    import torch
+
+    import _cdr
+    from cdr_dist import unify_points
+
+    k, d = C0.shape
+    ctxs = [_cdr.Context(0) for _ in parts]
+    try:
+        for c, X in zip(ctxs, parts):
+            c.load_points(X)
+        if unify:  # cdr_dist.unify_points with the MIN / MAX all-reduce done here
+            sts = [c.points_stats() for c in ctxs]
+            dd = (sts[0].size - 3) // 2
+            g = np.concatenate([np.minimum(*[s[:dd] for s in sts]),
+                                np.maximum(*[s[dd:] for s in sts])])
+            for c in ctxs:
+                c.points_restat(g, n_total)
+        ref = C0[0].copy()
+        x2 = sum(c.points_sqdev(ref) for c in ctxs)
+        bufs = [torch.zeros(k * (d + 1), dtype=torch.int64, device="cuda") for _ in ctxs]
+        for c in ctxs:
+            c.lloyd_begin(C0, -1.0, ref, x2)
+        for _ in range(steps):
+            for c, b in zip(ctxs, bufs):
+                c.lloyd_enqueue_assign(b.data_ptr())
+            for c in ctxs:
+                c.synchronize()
+            tot = sum(bufs[1:], bufs[0].clone())
+            for b in bufs:
+                b.copy_(tot)
+            torch.cuda.synchronize()
+            for c, b in zip(ctxs, bufs):
+                c.lloyd_enqueue_finalize(b.data_ptr())
+        sts = [c.lloyd_status() for c in ctxs]
+        Cs = [c.lloyd_read()[0] for c in ctxs]
+        labs = np.concatenate([c.labels() for c in ctxs])
+        for c in ctxs:
+            c.lloyd_end()
+    finally:
+        for c in ctxs:
+            c.close()
+    return sts, Cs, labs
+
+
+def test_unified_transform_two_shards_of_different_ranges(ctx):
+    """each shard used to take its screen transform
+    (mu, sigma) from its own ranges, so the fp16 range guard of the device
+    plan could stop one rank's loop and not the other's.  Shard 0 holds
+    points in [0, 2^-10), shard 1 in [0, 1): with per-shard transforms the
+    centroids from shard 1 are out of shard 0's fp16 range (its loop stops
+    for the host plan at once); with cdr_dist.unify_points both use the
+    global transform, run every step, and equal the single-context loop."""
+    from cdr_dist import device_lloyd, seed_sharded, Comm
+
+    n, d, k = 2 * 65536, 16, 32
+    X = synth.generate(n, 0, n, d, k, 99)
+    X[: n // 2] = np.ldexp(np.floor(np.ldexp(X[: n // 2], 14)), -24)  # same 2^-24 grid
+    ctx.load_points(X)
+    C0 = np.asarray(seed_sharded(ctx, Comm(), 0, n, k, random_state=42), dtype=np.float64)
+    np.random.seed(1)
+    C_ref, st_ref = device_lloyd(ctx, C0, 5, -1.0, lambda g: X[g], n)
+    lab_ref = ctx.labels()
+    assert st_ref["steps"] == 5 and st_ref["running"], st_ref
+    parts = [X[: n // 2], X[n // 2:]]
+    sts, _, _ = _two_context_loop(parts, C0, 1, False, n)
+    assert [s["running"] for s in sts] == [False, True], sts  # the divergence being fixed
+    assert sts[0]["reason"] == ctx.LL_HOST_PLAN
+    sts, Cs, labs = _two_context_loop(parts, C0, 5, True, n)
+    assert all(s["steps"] == 5 and s["running"] for s in sts), sts
+    np.testing.assert_array_equal(Cs[0], C_ref)
+    np.testing.assert_array_equal(Cs[1], C_ref)
+    np.testing.assert_array_equal(labs, lab_ref)
+
+
+def test_native_rccl_step_world1(ctx):
+    """The loop's all-reduce issued from C (csrc/comm.hip): a one-rank RCCL
+    communicator on the context, cdr_lloyd_enqueue_steps runs assign ->
+    ncclAllReduce -> finalize per step; results equal the loop without it."""
+    import _cdr
+    from cdr_dist import device_lloyd
+
+    n, d, k = 300_000, 16, 64
+    X = synth.generate(n, 0, n, d, k, 1234)
+    rng = np.random.default_rng(3)
+    C0 = X[np.sort(rng.choice(n, k, replace=False))]
+    ctx.load_points(X)
+    np.random.seed(2)
+    C_ref, st_ref = device_lloyd(ctx, C0, 6, -1.0, lambda g: X[g], n)
+    lab_ref = ctx.labels()
+    b = _cdr.Context(ctx.device)
+    try:
+        b.load_points(X)
+        b.comm_init(_cdr.comm_unique_id(), 1, 0)
+        np.random.seed(2)
+        C, st = device_lloyd(b, C0, 6, -1.0, lambda g: X[g], n)
+        np.testing.assert_array_equal(C, C_ref)
+        np.testing.assert_array_equal(b.labels(), lab_ref)
+        assert st["steps"] == st_ref["steps"] == 6
+        assert st["inertia"] == st_ref["inertia"]
+        b.comm_destroy()
+    finally:
+        b.close()
