@@ -507,6 +507,8 @@ def main() -> None:
                 break
     # (the fallback counter accumulates over every profiled-session step)
     fb_frac = prof["fallback_points"] / max(args.steps, 1) / max(n_local, 1)
+    # points the pruned screen (screen32p) handed to its k-way MFMA screen
+    q_frac = prof["queued_points"] / max(args.steps, 1) / max(n_local, 1)
 
     out = {
         "metric": METRIC,
@@ -533,6 +535,7 @@ def main() -> None:
         "roofline": roofline,
         "step_kernels_ms": step_kernel_ms,
         "fallback_frac": fb_frac,
+        "queued_frac": q_frac,
         "seed_s": seed_s,
         "final_shift": st["shift"],
         "final_inertia": st["inertia"],

@@ -344,10 +344,10 @@ class Context:
         _check(self._lib.cdr_profile_reset(self._h, max(int(every), 1) if enable else 0))
 
     def profile_read(self) -> dict:
-        out = np.zeros(4, dtype=np.float64)
+        out = np.zeros(5, dtype=np.float64)
         _check(self._lib.cdr_profile_read(self._h, _ptr(out)))
         return {"screen_ms": out[0], "steps": int(out[1]), "step_ms": out[2],
-                "fallback_points": int(out[3])}
+                "fallback_points": int(out[3]), "queued_points": int(out[4])}
 
     def profile_kernel(self) -> str:
         buf = ctypes.create_string_buffer(96)

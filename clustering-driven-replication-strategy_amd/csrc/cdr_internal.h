@@ -183,6 +183,10 @@ struct Ctx {
   // valid while only screen32d / fixup32 wrote the labels since it was built
   DevBuf lab8;
   bool lab8_valid = false;
+  // DELTA steps on the pruned screen (screen32p, triangle-inequality
+  // certificates) instead of the k-way MFMA screen; switched off when too
+  // many points of a step stay uncertified (clusters not separated)
+  bool prune_on = true;
   int32_t run_k = 0;
   bool last_delta = false;
 #ifdef CDR_EXPERIMENTS

@@ -1044,7 +1044,7 @@ void prof_mark(Ctx& c, int i) {
 // (screen_big levels): fold it into the profile, then the closing mark.
 void prof_end_screened(Ctx& c) {
   if (c.prof_cur < 0) return;
-  c.fb_accum.ensure(sizeof(long long));
+  c.fb_accum.ensure(2 * sizeof(long long));
   hipLaunchKernelGGL(fb_accumulate, dim3(1), dim3(64), 0, c.stream,
                      c.fb_count.as<int32_t>() + c.fb_total_slot, c.fb_accum.as<long long>());
   HIP_CHECK(hipGetLastError());
@@ -1223,7 +1223,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
       prof_mark(c, 0);
       prof_mark(c, 1);
     } else if (!s32) {  // screen32's publish32 sums its fallback total itself
-      c.fb_accum.ensure(sizeof(long long));
+      c.fb_accum.ensure(2 * sizeof(long long));
       hipLaunchKernelGGL(fb_accumulate, dim3(1), dim3(64), 0, c.stream,
                          c.fb_count.as<int32_t>() + c.fb_total_slot, c.fb_accum.as<long long>());
       HIP_CHECK(hipGetLastError());
@@ -1401,8 +1401,8 @@ int cdr_profile_reset(cdr_ctx* h, int32_t enable) {
   c.prof_seen = 0;
   c.prof_screen_ms = c.prof_step_ms = c.prof_fb_points = 0.0;
   c.prof_launches = 0;
-  c.fb_accum.ensure(sizeof(long long));
-  HIP_CHECK(hipMemsetAsync(c.fb_accum.p, 0, sizeof(long long), c.stream));
+  c.fb_accum.ensure(2 * sizeof(long long));
+  HIP_CHECK(hipMemsetAsync(c.fb_accum.p, 0, 2 * sizeof(long long), c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
   CDR_CATCH
 }
@@ -1413,16 +1413,17 @@ int cdr_profile_read(cdr_ctx* h, double* out) {
   Ctx& c = h->c;
   HIP_CHECK(hipSetDevice(c.device));
   prof_collect(c);
-  long long fb = 0;
+  long long fb[2] = {0, 0};
   if (c.fb_accum.p) {
-    HIP_CHECK(hipMemcpyAsync(&fb, c.fb_accum.p, sizeof(long long), hipMemcpyDeviceToHost,
-                             c.stream));
+    HIP_CHECK(hipMemcpyAsync(fb, c.fb_accum.p, std::min(c.fb_accum.bytes, sizeof(fb)),
+                             hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
   }
   out[0] = c.prof_screen_ms;
   out[1] = (double)c.prof_launches;
   out[2] = c.prof_step_ms;
-  out[3] = c.prof_fb_points + (double)fb;
+  out[3] = c.prof_fb_points + (double)fb[0];
+  out[4] = (double)fb[1];
   CDR_CATCH
 }
 

@@ -288,8 +288,7 @@ static void ll_plan_shape(const Ctx& c, int& QH, int& MT) {
 static void ll_plan(Ctx& c) {
   int QH, MT;
   ll_plan_shape(c, QH, MT);
-  c.frag.ensure(((size_t)MT * 2 * 64 * 16 + (size_t)MT * 16 * 64 * 4 +
-                 sizeof(double) * (size_t)c.ll_k * c.d + 16 + 15) / 16 * 16);
+  c.frag.ensure(plan32_layout(MT, c.ll_k, c.d).all);
   plan32_launch(c, c.ll_k, QH, MT);
 }
 
@@ -437,7 +436,7 @@ static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
   a.state = c.ll_state.as<long long>();
   a.fbc = c.ll_fin_devstep ? c.fb_count.as<int>() : nullptr;
   a.nwaves = c.fb_regions;
-  c.fb_accum.ensure(sizeof(long long));
+  c.fb_accum.ensure(2 * sizeof(long long));
   a.fb_acc = c.prof_on ? c.fb_accum.as<long long>() : nullptr;
   a.plan = c.ll_devplan ? static_cast<unsigned char*>(c.frag.p) : nullptr;
   ll_plan_shape(c, a.QH, a.MT);

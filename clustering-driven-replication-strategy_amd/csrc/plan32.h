@@ -11,6 +11,53 @@ namespace cdr {
 
 typedef _Float16 plan_h8 __attribute__((ext_vector_type(8)));
 
+// Plan buffer layout (host upload and device plan alike):
+//   frag [MT][2][64] h8 | cinit [MT][16][64] f32 | C copy k x d f64 |
+//   thr0, D (f32; device plan) | prune block (16-byte aligned):
+//   c32 [64][kPrStr] f32 | E [64] f32 | h [64] f32  (screen32p, plan32_prune)
+constexpr int kPrStr = 20;  // c32 row stride in floats (16-byte aligned rows)
+constexpr size_t kPrBytes = sizeof(float) * (64 * kPrStr + 64 + 64);
+struct Plan32Layout {
+  size_t cinit, cent, thr, prune, all;
+};
+__host__ __device__ inline Plan32Layout plan32_layout(int MT, int k, int d) {
+  Plan32Layout L;
+  L.cinit = (size_t)MT * 2 * 64 * sizeof(plan_h8);
+  L.cent = L.cinit + (size_t)MT * 16 * 64 * sizeof(float);
+  L.thr = L.cent + sizeof(double) * (size_t)k * d;
+  L.prune = (L.thr + 16 + 15) / 16 * 16;
+  L.all = L.prune + kPrBytes;
+  return L;
+}
+
+// Bound on ||fp16(xhat32) - xhat|| over the point set (screen32p): xhat32 =
+// fma(x, 2^sigma, -mu 2^sigma) errs by <= 2^-24 |xhat| (0 when exact) and the
+// fp16 rounding by <= 2^-11 |xhat32| + 2^-25 per feature; with dev_f >=
+// |xhat_f| (plan32_point_side: xxmax = sum dev_f^2)
+// ||h - xhat|| <= (2^-11 + 2^-23) sqrt(xxmax) + 2^-25 sqrt(16).
+__host__ __device__ inline double plan32_prune_dn(double xxmax) {
+  return ((ldexp(1.0, -11) + ldexp(1.0, -23)) * sqrt(xxmax) + ldexp(1.0, -23)) *
+         (1.0 + ldexp(1.0, -20));
+}
+
+// From the rounding error e2 = ||c32 - v||^2 and n2 = ||v||^2 of one centroid
+// (v = (C - mu) 2^sigma in fp64, within 2^-52 ||v|| of the exact chat):
+// ec >= ||c32 - chat||; E >= (dn + ec)(1 + 2^-20) as fp32.
+__host__ __device__ inline double plan32_prune_ec(double e2, double n2) {
+  return (sqrt(e2) + ldexp(sqrt(n2), -52)) * (1.0 + ldexp(1.0, -40)) + ldexp(1.0, -80);
+}
+__host__ __device__ inline float plan32_prune_E(double dn, double ec) {
+  return (float)((dn + ec) * (1.0 + ldexp(1.0, -20)));
+}
+// h_r from the smallest squared fp64 distance smin of c32_r to another c32_j
+// (exact differences of floats, <= 18 roundings): a lower bound of
+// min_j ||chat_r - chat_j|| rounded down into fp32; +inf when k = 1.
+__host__ __device__ inline float plan32_prune_h(double smin, double ec_r, double ecmax) {
+  if (!(smin < INFINITY)) return INFINITY;
+  const double lo = sqrt(smin) * (1.0 - ldexp(1.0, -44)) - ec_r - ecmax;
+  return lo > 0.0 ? (float)(lo * (1.0 - ldexp(1.0, -22))) : 0.0f;
+}
+
 // Certification constants from the centroid side (ccmax =
 // max ||chat||^2, l1c = max ||chat||_1) and the point side.  Shared by the
 // host plan (build_plan32) and the device plan (plan32_kernel): the same
@@ -173,6 +220,59 @@ __device__ inline void plan32_build(const double* __restrict__ C, int k, int d, 
     cinit[idx] = row < k ? (float)(cc[row] + sD) : 1.0e30f;
   }
   for (int i = t; i < k * d; i += blockDim.x) cent[i] = C[i];
+  // prune block (screen32p): fp32 centroids, their bounds, nearest-centroid
+  // distances (the host's build_plan32 computes the same quantities)
+  const Plan32Layout L = plan32_layout(MT, k, d);
+  float* pc = reinterpret_cast<float*>(plan + L.prune);
+  float* pE = pc + 64 * kPrStr;
+  float* ph = pE + 64;
+  __shared__ float c32[64 * 16];
+  __shared__ double pec[64];
+  __shared__ unsigned long long smin_b[64], ecmax_b;
+  if (t == 0) ecmax_b = 0ull;
+  for (int e = t; e < 64 * kPrStr; e += blockDim.x) {
+    const int j = e / kPrStr, f = e - j * kPrStr;
+    float cf = 0.0f;
+    if (j < k && f < d) cf = (float)((C[(size_t)j * d + f] - mu[f]) * sc);
+    pc[e] = cf;
+    if (f < 16) c32[j * 16 + f] = cf;
+  }
+  if (t < 64) smin_b[t] = __double_as_longlong(INFINITY);
+  __syncthreads();
+  if (t < 64) {
+    double e2 = 0.0, n2 = 0.0;
+    if (t < k)
+      for (int f = 0; f < d; ++f) {
+        const double v = (C[(size_t)t * d + f] - mu[f]) * sc;
+        const double r = (double)c32[t * 16 + f] - v;  // exact
+        e2 += r * r;
+        n2 += v * v;
+      }
+    const double ec = plan32_prune_ec(e2, n2);
+    pec[t] = ec;
+    pE[t] = plan32_prune_E(plan32_prune_dn(xxmax), ec);
+    if (t < k) atomicMax(&ecmax_b, (unsigned long long)__double_as_longlong(ec));
+  }
+  {  // row r = t % 64, columns j = t / 64 + G i: the smallest squared distance
+    const int r = t & 63, G = blockDim.x >> 6;
+    double sm = INFINITY;
+    if (r < k)
+      for (int j = t >> 6; j < k; j += G) {
+        if (j == r) continue;
+        double s2 = 0.0;
+        for (int f = 0; f < 16; ++f) {
+          const double df = (double)c32[r * 16 + f] - (double)c32[j * 16 + f];
+          s2 += df * df;
+        }
+        sm = fmin(sm, s2);
+      }
+    atomicMin(&smin_b[r], (unsigned long long)__double_as_longlong(sm));  // >= 0: bits order
+  }
+  __syncthreads();
+  if (t < 64)
+    ph[t] = t < k ? plan32_prune_h(__longlong_as_double(smin_b[t]), pec[t],
+                                   __longlong_as_double(ecmax_b))
+                  : INFINITY;
 }
 
 }  // namespace cdr

@@ -1219,6 +1219,346 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Pruned DELTA screen: screen32p (d <= 16, k <= 64; configs 2 and 3).
+//
+// screen32h spends ~213 VALU per 64 points on the k-way screen (64 MFMA values
+// and a keyed top-2 per point) and is VALU-issue bound.  After the first step
+// almost every point stays with its label a deep inside its cluster, where one
+// distance decides it.  screen32p gives each lane ONE point and first tries
+// the triangle inequality in distance space (t_j = ||xhat - chat_j|| =
+// 2^sigma ||x - C_j||, the reference's distance up to a power of two):
+//   t_j >= ||chat_a - chat_j|| - t_a >= h_a - t_a   for every j != a,
+// h_a = min_j ||chat_a - chat_j||, so a is the argmin when 2 t_a < h_a (with
+// margins).  t_a comes from the hi-only screen copy h = fp16(xhat) in fp32
+// (16 v_fma_mix differences and packed fp32 squares against c32_a) and is
+// bounded rigorously:
+//   | ||h - c32_a|| - sqrt(q_a) | <= 2^-19 sqrt(q_a)   (q_a: 2 roundings + 9
+//       along any summation path, every term >= 0; v_sqrt_f32 1 ulp),
+//   ||h - xhat|| <= dn  (the fp16 rounding of the point, screen32_prune_dn),
+//   ||c32_a - chat_a|| <= ec_a  (the fp32 rounding of the centroid),
+// so ub_a = sqrt(q_a)(1 + 2^-18) + E_a with E_a >= (dn + ec_a)(1 + 2^-20)
+// bounds t_a from above, and the point keeps a when
+//   h_a (1 - 2^-22) - ub_a > ub_a (1 + 2^-20):
+// every other exact distance then exceeds t_a by more than 2^-21 relative,
+// far above the reference's own fp64 rounding (< 2^-45), so np.argmin of the
+// reference's norms is a (src/kmeans_plusplus.py:33-34).
+//
+// The points this test cannot decide (near a second centroid, or of a
+// centroid far from its points) are appended — their 32 (d <= 8: 16) bytes
+// and {pt, a} — to a per-wave LDS queue laid out as the MFMA B operands.
+// Whenever 64 are queued the wave runs screen32h's k-way screen and hi-only
+// certificate on them (the same plan, keys and bounds), so the MFMA work
+// shrinks to the queued fraction; its moved points go to the move region,
+// its uncertified ones to the fallback region, exactly as in screen32d, and
+// fixup32 finishes the step.  Every point is still read and decided every
+// step.
+//
+// c32, E and h come with the step's plan (the prune block, plan32.h: built by
+// plan32_build on the device right after the centroids move, or by the host's
+// build_plan32), so a workgroup only stages 5.6 KB of it into LDS.
+// ---------------------------------------------------------------------------
+struct S32PArgs {
+  const unsigned char* XS;  // hi-only screen copy (screen32h / screen32h1 layout)
+  int64_t n, n_pad;
+  int k, d;
+  const float* prune;  // the plan's prune block (plan32.h: c32 | E | h)
+  // the k-way screen of the queued points: screen32h's plan
+  const h8* frag;
+  const float* cinit;
+  float thr0, thr_rel, Dv;
+  const float* thr_dev;
+  const long long* gate;
+  int32_t* labels;
+  uint8_t* lab8;
+  int2* fb_list;  // per-wave regions {pt, old label}
+  int32_t* fb_count;
+  int2* mv_list;  // per-wave regions {pt, old | new << 16}
+  int32_t* mv_count;
+  int cap;
+  long long* q_acc;  // profiling: points queued for the k-way screen (null: off)
+};
+
+// fp32 (lo / hi fp16 half of w) - c, one rounding (v_fma_mix_f32)
+__device__ __forceinline__ float mix_sub_lo(unsigned w, float c) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(w), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float mix_sub_hi(unsigned w, float c) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r)
+      : "v"(w), "v"(c));
+  return r;
+}
+
+// QH: 2 for d = 9..16 (16 bytes per point half), 1 for d <= 8 (8 bytes);
+// MT: 32-centroid tiles of the k-way screen; PD: groups in flight per wave.
+template <int QH, int MT, int PD>
+__global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
+  if (a.gate && a.gate[0] == 0) return;
+  constexpr bool H1 = QH == 1;
+  constexpr int kTile = H1 ? 512 : 1024;  // bytes per 32-point tile
+  constexpr int kHalf = kTile / 2;
+  constexpr int kPB = H1 ? 8 : 16;        // bytes per (point, half)
+  constexpr int NWH = kPB / 4;            // dwords per point half
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float c32s[64 * kPrStr];
+  __shared__ float eb[64], hc[64];
+  // per wave: a ring of 2 blocks x 64 queued points (2 tiles each, B layout)
+  __shared__ __attribute__((aligned(16))) unsigned char qd[4][2][2 * kTile];
+  __shared__ int2 qm[4][128];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = t >> 6;
+  const int h = lane >> 5;
+  const int p = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
+  const int nwaves = gridDim.x * 4;
+  const int64_t ngroups = a.n_pad >> 6;
+  struct Buf {
+    unsigned w[2 * NWH];  // the lane's point: half 0 then half 1 (packed fp16 pairs)
+    int ob;
+  };
+  // lane l: point 64 G + l = tile 2 G + (l >> 5), column l & 31
+  const unsigned loff = (unsigned)(h * kTile + p * kPB);
+  auto load = [&](Buf& b, int64_t G) {
+    if (G < ngroups) {
+      const unsigned char* base = a.XS + (size_t)G * (2 * kTile);  // wave-uniform
+      if constexpr (H1) {
+        const uint2 u0 = *reinterpret_cast<const uint2*>(base + loff);
+        const uint2 u1 = *reinterpret_cast<const uint2*>(base + loff + kHalf);
+        b.w[0] = u0.x; b.w[1] = u0.y; b.w[2] = u1.x; b.w[3] = u1.y;
+      } else {
+        const uint4 u0 = *reinterpret_cast<const uint4*>(base + loff);
+        const uint4 u1 = *reinterpret_cast<const uint4*>(base + loff + kHalf);
+        b.w[0] = u0.x; b.w[1] = u0.y; b.w[2] = u0.z; b.w[3] = u0.w;
+        b.w[4] = u1.x; b.w[5] = u1.y; b.w[6] = u1.z; b.w[7] = u1.w;
+      }
+      b.ob = a.lab8[G * 64 + lane];
+    }
+  };
+  const int64_t gs = nwaves;
+  Buf buf[PD];
+  // the first groups' loads overlap the prologue
+#pragma unroll
+  for (int i = 0; i < PD - 1; ++i) load(buf[i], wave + i * gs);
+
+  // ---- k-way screen plan (screen32d<QH, MT, PD, HO = true>), staged in LDS
+  // and read by a wave only when it drains its queue (no VGPRs held):
+  // fragments [MT][2][64] h8, C operand as [MT][4][2 halves][4] per 16 values
+  __shared__ h8 sA[MT * 2 * 64];
+  __shared__ __attribute__((aligned(16))) float sC[MT * 4 * 2 * 4];
+  for (int i = t; i < MT * 2 * 64; i += blockDim.x) sA[i] = a.frag[i];
+  for (int i = t; i < MT * 16 * 64; i += blockDim.x) {
+    // cinit[(m * 16 + ii) * 64 + ln]: row 32 m + 8 (ii >> 2) + 4 (ln >> 5) + (ii & 3)
+    // depends on (m, ii, ln >> 5) only; column ln & 31 repeats it
+    const int ln = i & 63, mi = i >> 6, m = mi >> 4, ii = mi & 15;
+    if ((ln & 31) == 0)
+      sC[((m * 4 + (ii >> 2)) * 2 + (ln >> 5)) * 4 + (ii & 3)] = a.cinit[i];
+  }
+  const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
+  const float Dlo = (a.thr_dev ? a.thr_dev[1] : a.Dv) * (1.0f - 0x1p-19f);  // < D
+
+  // the plan's fp32 centroids, their bounds E and nearest-centroid distances h
+  for (int i = t; i < 64 * kPrStr + 128; i += blockDim.x) {
+    const float v = a.prune[i];
+    if (i < 64 * kPrStr) c32s[i] = v;
+    else if (i < 64 * kPrStr + 64) eb[i - 64 * kPrStr] = v;
+    else hc[i - 64 * kPrStr - 64] = v;
+  }
+  __syncthreads();
+
+  int2* fb_region = a.fb_list + (size_t)wave * a.cap;
+  int2* mv_region = a.mv_list + (size_t)wave * a.cap;
+  int fb_used = 0, mv_used = 0;
+  // q = ||h - c32_j||^2: one fma_mix difference per feature, packed fp32 squares
+  auto dist2 = [&](const Buf& b, int j) -> float {
+    const float* c = c32s + j * kPrStr;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 acc = {0.0f, 0.0f};
+    // dword i of the lane's point holds features 2i, 2i + 1 (half 0 then half 1)
+#pragma unroll
+    for (int i = 0; i < 2 * NWH; ++i) {
+      const f2 df = {mix_sub_lo(b.w[i], c[2 * i]), mix_sub_hi(b.w[i], c[2 * i + 1])};
+      acc = __builtin_elementwise_fma(df, df, acc);
+    }
+    return acc.x + acc.y;
+  };
+  // (best, runner-up) keys of one 32-point tile of queued points, screen32d's tile()
+  // The centroid tiles m are screened one after another (a loop that is not
+  // unrolled, fragments and C operand read from LDS inside it), so only one
+  // tile's accumulators are ever live: 4 waves per SIMD instead of 3.
+  auto tile = [&](const u4v& v, unsigned& bk, unsigned& sk, float& hp) {
+    const h8 BH = __builtin_bit_cast(h8, v);
+    hp = 0.0f;  // this lane's part of ||h||^2 (fp16 products are exact in fp32)
+#pragma unroll
+    for (int i = 0; i < (H1 ? 4 : 8); i += 2)
+      hp = __builtin_amdgcn_fdot2(h2{BH[i], BH[i + 1]}, h2{BH[i], BH[i + 1]}, hp, false);
+    unsigned b = 0xFFFFFFFFu, s = 0xFFFFFFFFu;
+#pragma nounroll
+    for (int m = 0; m < MT; ++m) {
+      h8 A0 = sA[(m * 2 + 0) * 64 + lane];
+      const h8 A1 = sA[(m * 2 + 1) * 64 + lane];
+      if constexpr (H1)  // plan (QH = 1): A1 = [-2chi, -2chi], A3 = [-2clo, 0]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A0[4 + i] = A1[i];
+      f16v acc;
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const f4 c4v = *reinterpret_cast<const f4*>(sC + ((m * 4 + i4) * 2 + h) * 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * i4 + i] = c4v[i];
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, BH, acc, 0, 0, 0);
+      if constexpr (!H1) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, BH, acc, 0, 0, 0);
+      const unsigned rb = 32u * (unsigned)m;
+      auto key = [&](int i) {
+        return (__float_as_uint(acc[i]) & ~63u) | (rb + (unsigned)(8 * (i >> 2) + (i & 3)));
+      };
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        const unsigned x = key(q), y = key(q + 1);
+        unsigned tq;
+        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(tq) : "v"(b), "v"(x), "v"(y));
+        asm("v_min3_u32 %0, %1, %2, %3" : "=v"(b) : "v"(b), "v"(x), "v"(y));
+        s = min(s, tq);
+      }
+    }
+    bk = b | ((unsigned)h << 2);
+    sk = s | ((unsigned)h << 2);
+  };
+  // the k-way screen of queue block qb (nvalid entries), then its lists
+  auto drain = [&](int qb, int nvalid) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's queue writes
+    const unsigned char* src = qd[wv][qb];
+    u4v v[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      if constexpr (H1) {
+        const uint2 x = *reinterpret_cast<const uint2*>(src + tt * kTile + lane * kPB);
+        v[tt] = u4v{x.x, x.y, x.x, x.y};
+      } else {
+        v[tt] = *reinterpret_cast<const u4v*>(src + tt * kTile + lane * kPB);
+      }
+    }
+    const int2 meta = qm[wv][qb * 64 + lane];  // lane l owns entry l after the swap
+    unsigned bA = 0, sA = 0, bB = 0, sB = 0;
+    float hA = 0.0f, hB = 0.0f;
+    // one point tile at a time (a loop that is not unrolled)
+#pragma nounroll
+    for (int tt = 0; tt < 2; ++tt) {
+      unsigned bk, sk;
+      float hp;
+      tile(tt == 0 ? v[0] : v[1], bk, sk, hp);
+      if (tt == 0) {
+        bA = bk;
+        sA = sk;
+        hA = hp;
+      } else {
+        bB = bk;
+        sB = sk;
+        hB = hp;
+      }
+    }
+    swap32(bA, bB);
+    swap32(sA, sB);
+    merge_top2(bA, sA, bB, sB);
+    const int label = (int)(bA & 63u);
+    const float vb = __uint_as_float(bA & ~63u);
+    const float vs = __uint_as_float(sA & ~63u);
+    float thr = fmaf(vb, thr_rel, thr0);
+    {  // the hi-only certificate (screen32d)
+      unsigned ua = __float_as_uint(hA), ub = __float_as_uint(hB);
+      swap32(ua, ub);
+      const float hh = fmaf(__uint_as_float(ua) + __uint_as_float(ub), 1.0f + 0x1p-18f, 0x1p-20f);
+      const float dn = fmaf(0x1p-11f * (1.0f + 0x1p-9f), __builtin_amdgcn_sqrtf(hh), 0x1p-23f);
+      const float K = thr0 + hh - Dlo;
+      const float Gs = fmaxf(vs + K, 0x1p-100f), Gb = fmaxf(fmaf(vb, thr_rel, K), 0x1p-100f);
+      thr += 2.0f * (1.0f + 0x1p-19f) * dn * (__builtin_amdgcn_sqrtf(Gs) + __builtin_amdgcn_sqrtf(Gb));
+    }
+    const bool valid = lane < nvalid;
+    const bool cert = vs > thr;  // NaN: never certified
+    const int pt = meta.x, ob = meta.y;
+    const bool moved = valid && cert && label != ob;
+    if (moved) {
+      a.labels[pt] = label;
+      a.lab8[pt] = (uint8_t)label;
+    }
+    const unsigned long long mv = __ballot(moved);
+    if (mv) {
+      const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(mv >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((unsigned)mv, 0u));
+      if (moved) mv_region[mv_used + r] = int2{pt, ob | (label << 16)};
+      mv_used += __popcll(mv);
+    }
+    const unsigned long long need = __ballot(valid && !cert);
+    if (need) {
+      const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+      if (valid && !cert) fb_region[fb_used + r] = int2{pt, ob};
+      fb_used += __popcll(need);
+    }
+  };
+  int qh = 0, qn = 0;  // queue head (next slot, mod 128) and length: wave-uniform
+  int qtot = 0;        // points this wave queued (profiling)
+  auto process = [&](const Buf& b, int64_t G) {
+    const int64_t base = G << 6;
+    if (base >= a.n) return;  // wave-uniform: padding groups have no real points
+    const int64_t pt = base + lane;
+    const bool real = pt < a.n;
+    const int ao = b.ob;
+    const float qa = dist2(b, ao);
+    const float uba = fmaf(__builtin_amdgcn_sqrtf(qa), 1.0f + 0x1p-18f, eb[ao]);
+    const bool keep = fmaf(hc[ao], 1.0f - 0x1p-22f, -uba) > uba * (1.0f + 0x1p-20f);
+    const bool q = real && !keep;
+    const unsigned long long m = __ballot(q);
+    if (m) {
+      if (q) {
+        const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        const int slot = (qh + r) & 127;
+        const int e = slot & 63;
+        unsigned char* dst = qd[wv][slot >> 6] + (e >> 5) * kTile + (e & 31) * kPB;
+        if constexpr (H1) {
+          *reinterpret_cast<uint2*>(dst) = uint2{b.w[0], b.w[1]};
+          *reinterpret_cast<uint2*>(dst + kHalf) = uint2{b.w[2], b.w[3]};
+        } else {
+          *reinterpret_cast<uint4*>(dst) = uint4{b.w[0], b.w[1], b.w[2], b.w[3]};
+          *reinterpret_cast<uint4*>(dst + kHalf) = uint4{b.w[4], b.w[5], b.w[6], b.w[7]};
+        }
+        qm[wv][slot] = int2{(int)pt, ao};
+      }
+      const int c = __popcll(m);
+      qh = (qh + c) & 127;
+      qn += c;
+      qtot += c;
+      if (qn >= 64) {
+        drain(((qh - qn) & 127) >> 6, 64);
+        qn -= 64;
+      }
+    }
+  };
+  for (int64_t G = wave; G < ngroups; G += PD * gs) {
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+      const int64_t Gi = G + i * gs;
+      if (Gi >= ngroups) break;
+      load(buf[(i + PD - 1) % PD], Gi + (PD - 1) * gs);
+      process(buf[i], Gi);
+    }
+  }
+  if (qn > 0) {  // the partial block (queue tail at a block start: 64 | qh - qn)
+    drain(((qh - qn) & 127) >> 6, qn);
+  }
+  if (lane == 0) {
+    a.fb_count[wave] = fb_used;
+    a.mv_count[wave] = mv_used;
+    if (fb_used) atomicAdd(a.fb_count + nwaves, fb_used);
+    if (a.q_acc && qtot) atomicAdd(reinterpret_cast<unsigned long long*>(a.q_acc),
+                                   (unsigned long long)qtot);
+  }
+}
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 struct Plan32 {
@@ -1227,6 +1567,7 @@ struct Plan32 {
   float Dv = 0.0f;  // the offset D (device plan: in the plan buffer)
   std::vector<h8> frag;      // [MT][2][64]
   std::vector<float> cinit;  // [MT][16][64]
+  std::vector<float> prune;  // the prune block (plan32.h: c32 | E | h)
 };
 
 extern int lloyd_num_cus(int device);
@@ -1304,6 +1645,41 @@ static bool build_plan32(const Ctx& c, const double* C, int k, Plan32& pl) {
                   pl.frag[(m * 2 + 1) * 64 + lane], cin);
       for (int i = 0; i < 16; ++i) pl.cinit[(m * 16 + i) * 64 + lane] = cin[i];
     }
+  // prune block (screen32p), the quantities plan32_build computes on the device
+  pl.prune.assign(kPrBytes / sizeof(float), 0.0f);
+  float* pc = pl.prune.data();
+  float* pE = pc + 64 * kPrStr;
+  float* ph = pE + 64;
+  std::vector<double> ec(64, 0.0);
+  double ecmax = 0.0;
+  const double dn = plan32_prune_dn(xxmax);
+  for (int j = 0; j < 64; ++j) {
+    double e2 = 0.0, n2 = 0.0;
+    for (int f = 0; f < d && j < k; ++f) {
+      const double v = (C[(size_t)j * d + f] - (double)c.mu[f]) * sc;
+      const float cf = (float)v;
+      pc[j * kPrStr + f] = cf;
+      const double r = (double)cf - v;
+      e2 += r * r;
+      n2 += v * v;
+    }
+    ec[j] = plan32_prune_ec(e2, n2);
+    pE[j] = plan32_prune_E(dn, ec[j]);
+    if (j < k) ecmax = std::fmax(ecmax, ec[j]);
+  }
+  for (int r = 0; r < 64; ++r) {
+    double sm = INFINITY;
+    for (int j = 0; j < k && r < k; ++j) {
+      if (j == r) continue;
+      double s2 = 0.0;
+      for (int f = 0; f < 16; ++f) {
+        const double df = (double)pc[r * kPrStr + f] - (double)pc[j * kPrStr + f];
+        s2 += df * df;
+      }
+      sm = std::fmin(sm, s2);
+    }
+    ph[r] = r < k ? plan32_prune_h(sm, ec[r], ecmax) : INFINITY;
+  }
   return true;
 }
 
@@ -1422,6 +1798,34 @@ static int s32d_blocks_per_cu() {
   return nb;
 }
 
+#define CDR_S32P_ALL(X) X(1, 1, 2) X(1, 1, 3) X(1, 2, 2) X(1, 2, 3) \
+                        X(2, 1, 2) X(2, 1, 3) X(2, 2, 2) X(2, 2, 3)
+
+static int screen32p_blocks_per_cu(int QH, int MT, int PD) {
+  static int cache[2][2][2] = {};
+  int& nb = cache[QH - 1][MT - 1][PD - 2];
+  if (!nb) {
+    hipError_t e = hipErrorInvalidValue;
+#define CDR_S32P_OCC(Q_, M_, P_) \
+    if (QH == Q_ && MT == M_ && PD == P_) \
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32p<Q_, M_, P_>, 256, 0);
+    CDR_S32P_ALL(CDR_S32P_OCC)
+#undef CDR_S32P_OCC
+    if (e != hipSuccess || nb < 1) nb = 2;
+    if (nb > 8) nb = 8;
+  }
+  return nb;
+}
+
+static void screen32p_launch(int QH, int MT, int PD, dim3 grid, hipStream_t s,
+                             const S32PArgs& p) {
+#define CDR_S32P_GO(Q_, M_, P_) \
+  if (QH == Q_ && MT == M_ && PD == P_) \
+    hipLaunchKernelGGL((screen32p<Q_, M_, P_>), grid, dim3(256), 0, s, p);
+  CDR_S32P_ALL(CDR_S32P_GO)
+#undef CDR_S32P_GO
+}
+
 // Prefetch depth of screen32d: CDR_S32D_PD=2|3|4 (comparisons), else the
 // measured default per shape.
 static int s32d_depth(int QH) {
@@ -1445,9 +1849,17 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   ensure_split(c, HO ? (QH == 2 ? 3 : 4) : QH);
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
+  // pruned screen (screen32p) on the hi-only copy: CDR_PRUNE=0 turns it off,
+  // CDR_PRUNE_PD (2..3) groups in flight
+  static const bool pr_env = !std::getenv("CDR_PRUNE") || std::atoi(std::getenv("CDR_PRUNE"));
+  static const int pr_pd = std::getenv("CDR_PRUNE_PD") ? std::atoi(std::getenv("CDR_PRUNE_PD")) : 3;
+  const bool PR = pr_env && HO && c.prune_on;
+  const int PPD = pr_pd == 2 ? 2 : 3;
   int bpc;
-  const int PD = LRn ? LRn : s32d_depth(QH);
-  if (LRn) {
+  const int PD = PR ? PPD : LRn ? LRn : s32d_depth(QH);
+  if (PR) {
+    bpc = screen32p_blocks_per_cu(QH, MT, PPD);
+  } else if (LRn) {
     if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 2, true, true>() : s32d_blocks_per_cu<2, 2, 2, true, true>();
     else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 3, true, true>() : s32d_blocks_per_cu<2, 2, 3, true, true>();
     else bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 4, true, true>() : s32d_blocks_per_cu<2, 2, 4, true, true>();
@@ -1514,6 +1926,36 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   a.mv_list = c.mv_list.as<int2>();
   a.mv_count = c.mv_count.as<int32_t>();
   a.cap = cap;
+  const dim3 grid(nwg), blk(256);
+  if (PR) {
+    S32PArgs p;
+    p.XS = a.XS;
+    p.n = c.n;
+    p.n_pad = c.n_pad;
+    p.k = k;
+    p.d = c.d;
+    p.prune = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(dfrag) +
+                                             plan32_layout(MT, k, c.d).prune);
+    p.gate = gate;
+    p.labels = a.labels;
+    p.lab8 = a.lab8;
+    p.fb_list = a.fb_list;
+    p.fb_count = a.fb_count;
+    p.mv_list = a.mv_list;
+    p.mv_count = a.mv_count;
+    p.cap = cap;
+    p.frag = dfrag;
+    p.cinit = dcinit;
+    p.thr0 = thr0;
+    p.thr_rel = thr_rel;
+    p.Dv = Dv;
+    p.thr_dev = dthr;
+    c.fb_accum.ensure(2 * sizeof(long long));
+    p.q_acc = c.prof_on ? c.fb_accum.as<long long>() + 1 : nullptr;
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32p<%d,%d,%d>", QH, MT, PPD);
+    if (prof) prof_mark(c, 0);
+    screen32p_launch(QH, MT, PPD, grid, c.stream, p);
+  } else {
   if (LRn)
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>lds", MT, PD);
   else if (HO)
@@ -1522,7 +1964,6 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   else
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32d<%d,%d,%d>", QH, MT, PD);
   if (prof) prof_mark(c, 0);
-  const dim3 grid(nwg), blk(256);
 #define CDR_S32D_LAUNCH(P)                                                                  \
   if (LRn && MT == 1) hipLaunchKernelGGL((screen32d<2, 1, P, true, true>), grid, blk, 0, c.stream, a); \
   else if (LRn) hipLaunchKernelGGL((screen32d<2, 2, P, true, true>), grid, blk, 0, c.stream, a);       \
@@ -1542,6 +1983,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     CDR_S32D_LAUNCH(2)
   }
 #undef CDR_S32D_LAUNCH
+  }
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
   FixArgs f;
@@ -1599,7 +2041,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     HIP_CHECK(hipHostGetDevicePointer(&hp, hout, 0));
     hout_dev = static_cast<long long*>(hp);
   }
-  c.fb_accum.ensure(sizeof(long long));
+  c.fb_accum.ensure(2 * sizeof(long long));
   if (dout || hout_dev || !gate) {
     hipLaunchKernelGGL(publish32, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(),
                        len, dout, hout_dev, gate ? nullptr : c.fb_count.as<int32_t>(), nwaves,
@@ -1651,25 +2093,27 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   const int KP = 32 * pl.MT, NF = 8 * pl.QH;
   // plan buffer: fragments | C operand | centroids (fp64, for the fused
   // exact fallback) | thr0 (device plan only)
-  const size_t b_frag = (size_t)pl.MT * 2 * 64 * sizeof(h8);
-  const size_t b_cinit = (size_t)pl.MT * 16 * 64 * sizeof(float);
-  const size_t b_cent = sizeof(double) * (size_t)k * c.d;
-  const size_t b_all = b_frag + b_cinit + b_cent;
-  c.frag.ensure((b_all + 16 + 15) / 16 * 16);
+  const Plan32Layout PL = plan32_layout(pl.MT, k, c.d);
+  const size_t b_frag = PL.cinit;
+  const size_t b_cinit = PL.cent - PL.cinit;
+  const size_t b_cent = PL.thr - PL.cent;
+  const size_t b_all = PL.thr;
+  c.frag.ensure(PL.all);
   if (!devplan) {  // (device plan: built by plan32_kernel / ll_finalize)
     // one pinned upload per step; the previous step's copy must have left the
     // staging buffer
     if (c.up_pending) HIP_CHECK(hipEventSynchronize(c.up_event));
-    c.h_up.ensure((b_all + 15) / 16 * 16);
+    c.h_up.ensure(PL.all);
     memcpy(c.h_up.p, pl.frag.data(), b_frag);
     memcpy(static_cast<char*>(c.h_up.p) + b_frag, pl.cinit.data(), b_cinit);
     memcpy(static_cast<char*>(c.h_up.p) + b_frag + b_cinit, C, b_cent);
+    memcpy(static_cast<char*>(c.h_up.p) + PL.prune, pl.prune.data(), kPrBytes);
     // the device pulls the staging buffer itself (pinned, mapped host memory)
     // with one small kernel on the stream: no DMA-engine copy in the step (a
     // runtime H2D copy here stalled the host for 7-16 ms once per run)
     void* hdev = nullptr;
     HIP_CHECK(hipHostGetDevicePointer(&hdev, c.h_up.p, 0));
-    const int64_t n16 = (int64_t)((b_all + 15) / 16);
+    const int64_t n16 = (int64_t)(PL.all / 16);
     hipLaunchKernelGGL(pull_host_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0,
                        c.stream, static_cast<const uint4*>(hdev), static_cast<uint4*>(c.frag.p),
                        n16);
@@ -1783,7 +2227,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
     HIP_CHECK(hipHostGetDevicePointer(&hp, hout, 0));
     hout_dev = static_cast<long long*>(hp);
   }
-  c.fb_accum.ensure(sizeof(long long));
+  c.fb_accum.ensure(2 * sizeof(long long));
   if (dout || hout_dev || !gate) {
     // (device loop with no all-reduce buffer: ll_finalize reads the slices and
     // moves the fallback counter itself)

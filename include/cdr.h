@@ -131,8 +131,9 @@ int cdr_lloyd_stats(cdr_ctx* ctx, int64_t* n_fallback);
 /* Profiling: enable != 0 starts collecting HIP-event timings of every
  * enable-th following F32X step (1: every step; the event records cost the GPU
  * a few microseconds each) on the context stream; cdr_profile_read returns
- * out[4] = {screen kernel ms (sum), steps, whole step kernels ms (sum),
- * fallback points (sum)}.                                                    */
+ * out[5] = {screen kernel ms (sum), steps, whole step kernels ms (sum),
+ * fallback points (sum), points the pruned screen queued for its k-way MFMA
+ * screen (sum)}.                                                             */
 int cdr_profile_reset(cdr_ctx* ctx, int32_t enable);
 int cdr_profile_read(cdr_ctx* ctx, double* out);
 

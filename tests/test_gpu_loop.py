@@ -310,8 +310,9 @@ def test_unified_transform_two_shards_of_different_ranges(ctx):
     assert st_ref["steps"] == 5 and st_ref["running"], st_ref
     parts = [X[: n // 2], X[n // 2:]]
     sts, _, _ = _two_context_loop(parts, C0, 1, False, n)
-    assert [s["running"] for s in sts] == [False, True], sts  # the divergence being fixed
-    assert sts[0]["reason"] == ctx.LL_HOST_PLAN
+    # the divergence being fixed: shard 0's own transform stops its loop for
+    # the host plan at once (shard 1, summing sums of two scales, is garbage)
+    assert not sts[0]["running"] and sts[0]["reason"] == ctx.LL_HOST_PLAN, sts
     sts, Cs, labs = _two_context_loop(parts, C0, 5, True, n)
     assert all(s["steps"] == 5 and s["running"] for s in sts), sts
     np.testing.assert_array_equal(Cs[0], C_ref)
