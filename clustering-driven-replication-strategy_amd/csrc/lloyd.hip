@@ -1089,7 +1089,10 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   // host path: screen32 publishes the sums and the fallback total straight
   // into mapped pinned memory (h_small)
   if (!out_dev) c.h_small.ensure(sizeof(long long) * (len + 1) + 64);
-  bool s32 = screen32_supported(c, k) &&
+  // CDR_EXACT_ASSIGN=1 (read per step; tests): the exact fp64 NumPy-order
+  // assignment of every point (assign_exact_all), no screen
+  const bool exact_only = std::getenv("CDR_EXACT_ASSIGN") && std::atoi(std::getenv("CDR_EXACT_ASSIGN"));
+  bool s32 = !exact_only && screen32_supported(c, k) &&
              screen32_step(c, C, k, out_dev ? dout : nullptr,
                            out_dev ? nullptr : c.h_small.as<long long>(), prof, g_dbg_ptr,
                            g_dbg_ptr ? g_dbg_thr : nullptr, nullptr);
@@ -1100,7 +1103,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   }
   if (s32) {
     screened = true;
-  } else if (screen_supported(c, k)) {
+  } else if (!exact_only && screen_supported(c, k)) {
     c.run_valid = false;  // the screen_fast / screen_kernel path keeps no running sums
     c.lab8_valid = false;
     c.big_valid = false;
@@ -1193,7 +1196,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
                        c.stream, c.partials.as<long long>(), nwg, len, d,
                        KS, reinterpret_cast<unsigned long long*>(dout));
     HIP_CHECK(hipGetLastError());
-  } else if (big_step(c, C, k, dout, prof)) {
+  } else if (!exact_only && big_step(c, C, k, dout, prof)) {
     screened = true;  // large k / d: screen_big levels + update_big
   } else {
     c.run_valid = false;

@@ -59,6 +59,7 @@ struct FinArgs {
   unsigned char* plan;
   int QH, MT;
   double sc, xxmax, l1x;
+  int abl;  // timing experiments only (0 in the product build)
 };
 
 constexpr int kFinThreads = 512;
@@ -208,6 +209,286 @@ __global__ __launch_bounds__(kFinThreads) void ll_finalize(FinArgs a) {
     __syncthreads();
     plan32_build(staged ? lC : Cnew, k, d, a.QH, a.MT, ref + d, a.sc, a.xxmax, a.l1x, state,
                  a.plan);
+  }
+}
+
+// ll_finalize for the screen32 device plan (k <= 64, d <= 16), written for
+// latency: it is a single workgroup between two full-GPU launches, so its
+// time is its chain of dependent phases.  Thread t owns row j = t / 8 and the
+// feature pair 2 (t % 8), 2 (t % 8) + 1 of it, from the loads of the sums to
+// the plan entries of those two elements:
+//   loads (every slice of its cells, its centroid values: one round trip)
+//   -> means, shift / inertia terms -> wave sums -> [sync] -> the decision
+//   (every thread, from the 8 wave partials) -> fp16 halves, fp32 centroid,
+//   row values staged -> [sync] -> row sums (one thread per row, the host's
+//   order), nearest-centroid distances (8 lanes per row) -> maxima -> [sync]
+//   -> bounds (every thread) -> fragments, C operand, prune block.
+// Same results as ll_finalize + plan32_build (same fp64 operations per value;
+// the row sums in the same sequential order).
+__global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
+  long long* __restrict__ state = a.state;
+  if (a.abl & 8) {  // (the step still counts, so the host's polling goes on)
+    if (threadIdx.x == 0) state[1] += 1;
+    return;
+  }
+  const int k = a.k, d = a.d, d1 = d + 1, cells = k * d1;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int j = t >> 3, f0 = 2 * (t & 7);
+  const bool row = j < k;
+  const bool v0 = row && f0 < d, v1 = row && f0 + 1 < d;
+  // ---- loads ----
+  long long s0[kRunSlices], s1[kRunSlices], sn[kRunSlices];
+#pragma unroll
+  for (int sl = 0; sl < kRunSlices; ++sl) {
+    const bool on = sl < a.nslices;
+    const long long* base = a.sums + (size_t)sl * cells + (size_t)j * d1;
+    s0[sl] = on && v0 ? base[f0] : 0;
+    s1[sl] = on && v1 ? base[f0 + 1] : 0;
+    sn[sl] = on && row ? base[d] : 0;
+  }
+  const double c0 = v0 ? a.C[j * d + f0] : 0.0, c1 = v1 ? a.C[j * d + f0 + 1] : 0.0;
+  const double r0 = v0 ? a.ref[f0] : 0.0, r1 = v1 ? a.ref[f0 + 1] : 0.0;
+  const double mu0 = v0 ? a.ref[d + f0] : 0.0, mu1 = v1 ? a.ref[d + f0 + 1] : 0.0;
+  const long long st0 = state[0];
+  if (st0 == 0) return;  // uniform: the loop has stopped
+  if (a.abl & 1) {
+    long long z = 0;
+#pragma unroll
+    for (int sl = 0; sl < kRunSlices; ++sl) z += s0[sl] + s1[sl] + sn[sl];
+    if (z == 0x7fffffffffffffffll) state[7] = z + (long long)(c0 + c1 + r0 + r1 + mu0 + mu1);
+    if (threadIdx.x == 0) state[1] += 1;
+    return;
+  }
+  // ---- means, shift / inertia terms ----
+  long long S0 = 0, S1 = 0, cnt = 0;
+#pragma unroll
+  for (int sl = 0; sl < kRunSlices; ++sl) {
+    S0 += s0[sl];
+    S1 += s1[sl];
+    cnt += sn[sl];
+  }
+  double* __restrict__ Cnew = a.Cnew;
+  long long* cnt_out = reinterpret_cast<long long*>(Cnew + (size_t)k * d);
+  if (row && (t & 7) == 0) cnt_out[j] = cnt;
+  if (t == 0 && a.fbc) {
+    const int fb = a.fbc[a.nwaves];
+    a.fbc[a.nwaves] = 0;
+    a.fbc[a.nwaves + 1] = fb;
+    if (a.fb_acc) a.fb_acc[0] += fb;
+  }
+  // the host's np.ldexp(acc.astype(float64), -S) / counts (kmeans_plusplus.py)
+  const double sj0 = ldexp((double)S0, -a.sbits), sj1 = ldexp((double)S1, -a.sbits);
+  double m0 = sj0 / (double)cnt, m1 = sj1 / (double)cnt;
+  if (a.round32) {
+    m0 = (double)(float)m0;
+    m1 = (double)(float)m1;
+  }
+  if (v0) Cnew[j * d + f0] = m0;
+  if (v1) Cnew[j * d + f0 + 1] = m1;
+  double ss = 0.0, cross = 0.0, quad = 0.0;
+  int empty = row && cnt == 0;
+  if (row && cnt != 0) {
+    if (v0) {
+      const double df = m0 - c0, ct = c0 - r0;
+      ss += df * df;
+      cross += ct * (sj0 - (double)cnt * r0);
+      quad += (double)cnt * (ct * ct);
+    }
+    if (v1) {
+      const double df = m1 - c1, ct = c1 - r1;
+      ss += df * df;
+      cross += ct * (sj1 - (double)cnt * r1);
+      quad += (double)cnt * (ct * ct);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {  // fixed pattern: deterministic
+    ss += __shfl_xor(ss, o);
+    cross += __shfl_xor(cross, o);
+    quad += __shfl_xor(quad, o);
+    empty |= __shfl_xor(empty, o);
+  }
+  __shared__ double r_ss[8], r_cross[8], r_quad[8];
+  __shared__ int r_empty[8];
+  if (lane == 0) {
+    r_ss[wv] = ss;
+    r_cross[wv] = cross;
+    r_quad[wv] = quad;
+    r_empty[wv] = empty;
+  }
+  __syncthreads();
+  // ---- the decision (every thread, the same fixed order) ----
+  double sst = 0.0, crs = 0.0, qd = 0.0;
+  int emp = 0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    sst += r_ss[w];
+    crs += r_cross[w];
+    qd += r_quad[w];
+    emp |= r_empty[w];
+  }
+  long long reason = kLLRun;
+  int mv = 0;
+  if (emp) {
+    reason = kLLEmpty;
+  } else {
+    const double sh = sqrt(sst);
+    mv = 1;
+    if (a.tol > 0.0 && !(sh > a.tol * (1.0 + a.margin))) {
+      if (sh < a.tol * (1.0 - a.margin)) {
+        reason = kLLConverged;  // shift < tol: the reference breaks after moving
+      } else {
+        reason = kLLAmbiguous;  // too close to call in fp64: the host decides
+        mv = 0;
+      }
+    }
+  }
+  if (t == 0) {
+    if (mv) state[1] += 1;
+    if (reason != kLLRun) {
+      state[0] = 0;
+      state[2] = reason;
+    }
+    state[3] = __double_as_longlong(sst);
+    state[4] = __double_as_longlong(a.x2 - 2.0 * crs + qd);
+  }
+  if (!mv) return;
+  if (v0) a.C[j * d + f0] = m0;
+  if (v1) a.C[j * d + f0 + 1] = m1;
+  if (!a.plan || reason != kLLRun || (a.abl & 2)) return;
+  // ---- the next step's plan (plan32_build, per element) ----
+  unsigned char* __restrict__ plan = a.plan;
+  const int QH = a.QH, MT = a.MT;
+  const Plan32Layout L = plan32_layout(MT, k, d);
+  plan_h8* frag = reinterpret_cast<plan_h8*>(plan);
+  float* cinit = reinterpret_cast<float*>(plan + L.cinit);
+  double* cent = reinterpret_cast<double*>(plan + L.cent);
+  float* pc = reinterpret_cast<float*>(plan + L.prune);
+  float* pE = pc + 64 * kPrStr;
+  float* ph = pE + 64;
+  __shared__ _Float16 m2h[64 * 16], m2l[64 * 16];
+  __shared__ double vrow[64 * 16];
+  __shared__ float c32[64 * 16];
+  __shared__ double cc[64];
+  const double vv[2] = {v0 ? (m0 - mu0) * a.sc : 0.0, v1 ? (m1 - mu1) * a.sc : 0.0};
+  const double mm[2] = {m0, m1};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int f = f0 + u;
+    const double v = vv[u];
+    const _Float16 hi = f64_to_f16(v);
+    const _Float16 lo = f64_to_f16(v - (double)hi);
+    m2h[j * 16 + f] = f64_to_f16(-2.0 * (double)hi);
+    m2l[j * 16 + f] = f64_to_f16(-2.0 * (double)lo);
+    vrow[j * 16 + f] = v;
+    const float cf = (float)v;
+    c32[j * 16 + f] = cf;
+    pc[j * kPrStr + f] = cf;
+    if (row && f < d) cent[j * d + f] = mm[u];
+  }
+  if ((t & 7) < 2) pc[j * kPrStr + 16 + 2 * (t & 7)] = 0.0f, pc[j * kPrStr + 17 + 2 * (t & 7)] = 0.0f;
+  __syncthreads();
+  // ---- row sums (host order), nearest-centroid distances, maxima ----
+  double s = 0.0, l1 = 0.0, ca = 0.0, e2 = 0.0;
+  if ((t & 7) == 0 && row) {
+    for (int f = 0; f < d; ++f) {
+      const double v = vrow[j * 16 + f];
+      s += v * v;
+      l1 += fabs(v);
+      ca = fmax(ca, fabs(v));
+      const double r = (double)c32[j * 16 + f] - v;  // exact
+      e2 += r * r;
+    }
+    cc[j] = s;
+  }
+  const double ec = plan32_prune_ec(e2, s);
+  double sm = INFINITY;  // smallest squared distance of c32_j to another c32
+  if (row && !(a.abl & 4))
+    for (int jj = t & 7; jj < k; jj += 8) {
+      if (jj == j) continue;
+      double s2 = 0.0;
+#pragma unroll
+      for (int f = 0; f < 16; ++f) {
+        const double df = (double)c32[j * 16 + f] - (double)c32[jj * 16 + f];
+        s2 += df * df;
+      }
+      sm = fmin(sm, s2);
+    }
+  sm = fmin(sm, __shfl_xor(sm, 1));
+  sm = fmin(sm, __shfl_xor(sm, 2));
+  sm = fmin(sm, __shfl_xor(sm, 4));
+  const bool head = (t & 7) == 0 && row;
+  double ccmax = head ? s : 0.0, l1c = head ? l1 : 0.0, cabs = head ? ca : 0.0,
+         ecmax = head ? ec : 0.0;
+#pragma unroll
+  for (int o = 32; o >= 8; o >>= 1) {  // max is exact: any order
+    ccmax = fmax(ccmax, __shfl_xor(ccmax, o));
+    l1c = fmax(l1c, __shfl_xor(l1c, o));
+    cabs = fmax(cabs, __shfl_xor(cabs, o));
+    ecmax = fmax(ecmax, __shfl_xor(ecmax, o));
+  }
+  __shared__ double x_cc[8], x_l1[8], x_ca[8], x_ec[8];
+  if (lane == 0) {
+    x_cc[wv] = ccmax;
+    x_l1[wv] = l1c;
+    x_ca[wv] = cabs;
+    x_ec[wv] = ecmax;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    ccmax = fmax(ccmax, x_cc[w]);
+    l1c = fmax(l1c, x_l1[w]);
+    cabs = fmax(cabs, x_ca[w]);
+    ecmax = fmax(ecmax, x_ec[w]);
+  }
+  if (!(cabs <= 1024.0)) {  // fp16 split range (and NaN) guard: the host plans this step
+    if (t == 0) {
+      state[0] = 0;
+      state[2] = kLLHostPlan;
+    }
+    return;
+  }
+  double D;
+  float thr0;
+  plan32_bounds(ccmax, l1c, a.xxmax, a.l1x, QH, D, thr0);
+  if (t == 0) {
+    reinterpret_cast<float*>(plan + L.thr)[0] = thr0;
+    reinterpret_cast<float*>(plan + L.thr)[1] = (float)D;
+  }
+  if ((t & 7) == 0) {
+    pE[j] = plan32_prune_E(plan32_prune_dn(a.xxmax), row ? ec : 0.0);
+    ph[j] = row ? plan32_prune_h(sm, ec, ecmax) : INFINITY;
+  }
+  for (int idx = t; idx < MT * 64; idx += blockDim.x) {  // the layout of plan32_lane
+    const int m = idx >> 6, ln = idx & 63;
+    const int h = ln >> 5, jr = 32 * m + (ln & 31);
+    plan_h8 A1, A3;
+    for (int i = 0; i < 8; ++i) {
+      A1[i] = (_Float16)0.0f;
+      A3[i] = (_Float16)0.0f;
+    }
+    for (int uq = 0; uq < QH; ++uq)
+      for (int i = 0; i < 4; ++i) {
+        const int f = 4 * (QH * h + uq) + i;
+        if (jr >= k || f >= d) continue;
+        const _Float16 x = m2h[jr * 16 + f], y = m2l[jr * 16 + f];
+        if (QH == 1) {
+          A1[i] = x;
+          A1[4 + i] = x;
+          A3[i] = y;
+        } else {
+          A1[4 * uq + i] = x;
+          A3[4 * uq + i] = y;
+        }
+      }
+    frag[(m * 2 + 0) * 64 + ln] = A1;
+    frag[(m * 2 + 1) * 64 + ln] = A3;
+  }
+  for (int idx = t; idx < MT * 16 * 64; idx += blockDim.x) {
+    const int ln = idx & 63, mi = idx >> 6, m = mi >> 4, i = mi & 15;
+    const int rw = 32 * m + 8 * (i >> 2) + 4 * (ln >> 5) + (i & 3);
+    cinit[idx] = rw < k ? (float)(cc[rw] + D) : 1.0e30f;
   }
 }
 
@@ -443,10 +724,18 @@ static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
   a.sc = std::ldexp(1.0, c.sigma);
   a.xxmax = c.ll_xxmax;
   a.l1x = c.ll_l1x;
+  a.abl = 0;
 #ifdef CDR_EXPERIMENTS
+  if (const char* e = std::getenv("CDR_FIN_ABL")) a.abl = std::atoi(e);
   if (std::getenv("CDR_FIN_NOPLAN")) a.plan = nullptr;  // timing experiments only
 #endif
-  hipLaunchKernelGGL(ll_finalize, dim3(1), dim3(kFinThreads), 0, c.stream, a);
+  // screen32 device plan: the latency-oriented finalize (CDR_FIN_OLD=1: the
+  // generic one, for comparisons)
+  static const bool fin_old = std::getenv("CDR_FIN_OLD") && std::atoi(std::getenv("CDR_FIN_OLD"));
+  if (a.plan && c.ll_k <= 64 && c.d <= 16 && a.nslices <= kRunSlices && !fin_old)
+    hipLaunchKernelGGL(ll_finalize32, dim3(1), dim3(512), 0, c.stream, a);
+  else
+    hipLaunchKernelGGL(ll_finalize, dim3(1), dim3(kFinThreads), 0, c.stream, a);
   HIP_CHECK(hipGetLastError());
   if (c.ll_devbig) ll_plan_big(c);  // the next step's plan (skipped once the loop stopped)
   if (c.ll_fin_devstep && c.prof_cur >= 0) prof_mark(c, 2);

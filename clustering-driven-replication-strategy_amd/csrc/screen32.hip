@@ -1302,8 +1302,9 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   constexpr int kPB = H1 ? 8 : 16;        // bytes per (point, half)
   constexpr int NWH = kPB / 4;            // dwords per point half
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) float c32s[64 * kPrStr];
-  __shared__ float eb[64], hc[64];
+  __shared__ __attribute__((aligned(16))) float c32s[64 * kPrStr + 128];
+  float* const eb = c32s + 64 * kPrStr;  // E_j
+  float* const hc = eb + 64;             // h_j
   // per wave: a ring of 2 blocks x 64 queued points (2 tiles each, B layout)
   __shared__ __attribute__((aligned(16))) unsigned char qd[4][2][2 * kTile];
   __shared__ int2 qm[4][128];
@@ -1315,26 +1316,52 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
   const int nwaves = gridDim.x * 4;
   const int64_t ngroups = a.n_pad >> 6;
+  typedef unsigned u2v __attribute__((ext_vector_type(2)));
   struct Buf {
+    u4v q0, q1;           // the loaded halves (QH = 2)
+    u2v h0, h1;           // (QH = 1)
     unsigned w[2 * NWH];  // the lane's point: half 0 then half 1 (packed fp16 pairs)
     int ob;
   };
   // lane l: point 64 G + l = tile 2 G + (l >> 5), column l & 31
-  const unsigned loff = (unsigned)(h * kTile + p * kPB);
+  unsigned loff = (unsigned)(h * kTile + p * kPB);
+  unsigned lane4 = (unsigned)lane;
+  // The group loads are issued from inline asm (SGPR base + lane offset) and
+  // waited for with an explicit vmcnt: the compiler neither sees them nor
+  // inserts waits of its own (its waits for conditional loads were vmcnt(0),
+  // which drained the prefetch every few groups).  Vector-memory operations
+  // complete in issue order, so before group i the wave waits until at most
+  // 3 (PD - 1) of them are outstanding: the later groups' loads (and any
+  // stores issued after them) may stay in flight.  A group past the end
+  // reloads the last one (every iteration issues exactly 3 loads).
   auto load = [&](Buf& b, int64_t G) {
-    if (G < ngroups) {
-      const unsigned char* base = a.XS + (size_t)G * (2 * kTile);  // wave-uniform
-      if constexpr (H1) {
-        const uint2 u0 = *reinterpret_cast<const uint2*>(base + loff);
-        const uint2 u1 = *reinterpret_cast<const uint2*>(base + loff + kHalf);
-        b.w[0] = u0.x; b.w[1] = u0.y; b.w[2] = u1.x; b.w[3] = u1.y;
-      } else {
-        const uint4 u0 = *reinterpret_cast<const uint4*>(base + loff);
-        const uint4 u1 = *reinterpret_cast<const uint4*>(base + loff + kHalf);
-        b.w[0] = u0.x; b.w[1] = u0.y; b.w[2] = u0.z; b.w[3] = u0.w;
-        b.w[4] = u1.x; b.w[5] = u1.y; b.w[6] = u1.z; b.w[7] = u1.w;
-      }
-      b.ob = a.lab8[G * 64 + lane];
+    const int64_t Gc = G < ngroups ? G : ngroups - 1;
+    const unsigned char* base = a.XS + (size_t)Gc * (2 * kTile);  // wave-uniform
+    const uint8_t* lbase = a.lab8 + Gc * 64;
+    if constexpr (H1) {
+      asm volatile("global_load_dwordx2 %0, %1, %2\n\t"
+                   "global_load_dwordx2 %3, %1, %2 offset:256"
+                   : "=&v"(b.h0), "+v"(loff), "+s"(base), "=&v"(b.h1)::"memory");
+    } else {
+      asm volatile("global_load_dwordx4 %0, %1, %2\n\t"
+                   "global_load_dwordx4 %3, %1, %2 offset:512"
+                   : "=&v"(b.q0), "+v"(loff), "+s"(base), "=&v"(b.q1)::"memory");
+    }
+    asm volatile("global_load_ubyte %0, %1, %2" : "=&v"(b.ob), "+v"(lane4), "+s"(lbase)::"memory");
+  };
+  // wait for buffer b, `later` groups having been issued after it
+  auto wait = [&](Buf& b, int later) {
+    if constexpr (H1) {
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(6)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob)::"memory");
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob)::"memory");
+      else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob)::"memory");
+      b.w[0] = b.h0.x; b.w[1] = b.h0.y; b.w[2] = b.h1.x; b.w[3] = b.h1.y;
+    } else {
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(6)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob)::"memory");
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob)::"memory");
+      else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob)::"memory");
+      b.w[0] = b.q0.x; b.w[1] = b.q0.y; b.w[2] = b.q0.z; b.w[3] = b.q0.w;
+      b.w[4] = b.q1.x; b.w[5] = b.q1.y; b.w[6] = b.q1.z; b.w[7] = b.q1.w;
     }
   };
   const int64_t gs = nwaves;
@@ -1348,24 +1375,28 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   // fragments [MT][2][64] h8, C operand as [MT][4][2 halves][4] per 16 values
   __shared__ h8 sA[MT * 2 * 64];
   __shared__ __attribute__((aligned(16))) float sC[MT * 4 * 2 * 4];
-  for (int i = t; i < MT * 2 * 64; i += blockDim.x) sA[i] = a.frag[i];
-  for (int i = t; i < MT * 16 * 64; i += blockDim.x) {
-    // cinit[(m * 16 + ii) * 64 + ln]: row 32 m + 8 (ii >> 2) + 4 (ln >> 5) + (ii & 3)
-    // depends on (m, ii, ln >> 5) only; column ln & 31 repeats it
-    const int ln = i & 63, mi = i >> 6, m = mi >> 4, ii = mi & 15;
-    if ((ln & 31) == 0)
-      sC[((m * 4 + (ii >> 2)) * 2 + (ln >> 5)) * 4 + (ii & 3)] = a.cinit[i];
-  }
+  // Every global load of the staging is issued before the first LDS store
+  // (one round trip for the whole prologue, not one per loop iteration).
+  // cinit[(m * 16 + ii) * 64 + ln] belongs to row 32 m + 8 (ii >> 2) + 4 (ln >> 5)
+  // + (ii & 3): one value per (m, ii, ln >> 5), kept as sC[m][ii >> 2][ln >> 5][ii & 3].
+  constexpr int kPr4 = (64 * kPrStr + 128) / 4;  // prune block in float4
+  static_assert(kPr4 <= 512 && MT * 2 * 64 <= 256, "prologue: two float4 per thread");
+  const f4* prune4 = reinterpret_cast<const f4*>(a.prune);
+  const f4 pv0 = prune4[t];
+  const f4 pv1 = t + 256 < kPr4 ? prune4[t + 256] : f4{0.f, 0.f, 0.f, 0.f};
+  h8 av = {};
+  if (t < MT * 2 * 64) av = a.frag[t];
+  float cv = 0.0f;
+  const int cm = t >> 5, ci4 = (t >> 3) & 3, chh = (t >> 2) & 1, cc = t & 3;
+  if (t < MT * 32) cv = a.cinit[(cm * 16 + ci4 * 4 + cc) * 64 + chh * 32];
   const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
   const float Dlo = (a.thr_dev ? a.thr_dev[1] : a.Dv) * (1.0f - 0x1p-19f);  // < D
-
-  // the plan's fp32 centroids, their bounds E and nearest-centroid distances h
-  for (int i = t; i < 64 * kPrStr + 128; i += blockDim.x) {
-    const float v = a.prune[i];
-    if (i < 64 * kPrStr) c32s[i] = v;
-    else if (i < 64 * kPrStr + 64) eb[i - 64 * kPrStr] = v;
-    else hc[i - 64 * kPrStr - 64] = v;
-  }
+  // the plan's fp32 centroids c32, their bounds E and nearest-centroid distances h
+  // (contiguous in the plan and here: c32s | eb | hc)
+  reinterpret_cast<f4*>(c32s)[t] = pv0;
+  if (t + 256 < kPr4) reinterpret_cast<f4*>(c32s)[t + 256] = pv1;
+  if (t < MT * 2 * 64) sA[t] = av;
+  if (t < MT * 32) sC[t] = cv;
   __syncthreads();
 
   int2* fb_region = a.fb_list + (size_t)wave * a.cap;
@@ -1373,14 +1404,19 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   int fb_used = 0, mv_used = 0;
   // q = ||h - c32_j||^2: one fma_mix difference per feature, packed fp32 squares
   auto dist2 = [&](const Buf& b, int j) -> float {
-    const float* c = c32s + j * kPrStr;
+    const f4* c4 = reinterpret_cast<const f4*>(c32s + j * kPrStr);  // 16-byte rows
     typedef float f2 __attribute__((ext_vector_type(2)));
     f2 acc = {0.0f, 0.0f};
     // dword i of the lane's point holds features 2i, 2i + 1 (half 0 then half 1)
 #pragma unroll
-    for (int i = 0; i < 2 * NWH; ++i) {
-      const f2 df = {mix_sub_lo(b.w[i], c[2 * i]), mix_sub_hi(b.w[i], c[2 * i + 1])};
-      acc = __builtin_elementwise_fma(df, df, acc);
+    for (int q = 0; q < NWH; ++q) {
+      const f4 cq = c4[q];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = 2 * q + u;
+        const f2 df = {mix_sub_lo(b.w[i], cq[2 * u]), mix_sub_hi(b.w[i], cq[2 * u + 1])};
+        acc = __builtin_elementwise_fma(df, df, acc);
+      }
     }
     return acc.x + acc.y;
   };
@@ -1544,9 +1580,11 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
       const int64_t Gi = G + i * gs;
       if (Gi >= ngroups) break;
       load(buf[(i + PD - 1) % PD], Gi + (PD - 1) * gs);
+      wait(buf[i], PD - 1);
       process(buf[i], Gi);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the reloads past the end
   if (qn > 0) {  // the partial block (queue tail at a block start: 64 | qh - qn)
     drain(((qh - qn) & 127) >> 6, qn);
   }
@@ -1859,6 +1897,8 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   const int PD = PR ? PPD : LRn ? LRn : s32d_depth(QH);
   if (PR) {
     bpc = screen32p_blocks_per_cu(QH, MT, PPD);
+    static const int bpc_env = std::getenv("CDR_S32P_BPC") ? std::atoi(std::getenv("CDR_S32P_BPC")) : 0;
+    if (bpc_env >= 1 && bpc_env < bpc) bpc = bpc_env;
   } else if (LRn) {
     if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 2, true, true>() : s32d_blocks_per_cu<2, 2, 2, true, true>();
     else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 3, true, true>() : s32d_blocks_per_cu<2, 2, 3, true, true>();

@@ -143,6 +143,23 @@ def test_config3_full_size(ctx):
         b.close()
 
 
+def test_config3_every_label_exact(ctx, monkeypatch):
+    """all 100M labels of a DELTA step on the default screen
+    (pruned screen32p + queued k-way MFMA screen + fixup32) equal the exact
+    fp64 NumPy-order assignment of the same centroids (assign_exact_all on
+    every point, CDR_EXACT_ASSIGN), and so do the int64 sums."""
+    n, d, k = 100_000_000, 16, 64
+    C_prev, C, st, lab = _config_common(ctx, n, d, k, 3, 2_000)
+    acc = ctx.lloyd_step(C_prev)  # host-plan DELTA step on the same centroids
+    np.testing.assert_array_equal(ctx.labels(), lab)
+    monkeypatch.setenv("CDR_EXACT_ASSIGN", "1")
+    acc_x = ctx.lloyd_step(C_prev)
+    monkeypatch.delenv("CDR_EXACT_ASSIGN")
+    lab_x = ctx.labels()
+    assert (lab_x != lab).sum() == 0
+    np.testing.assert_array_equal(acc_x, acc)
+
+
 def test_config5_full_size_and_scoring(ctx):
     """BASELINE config 5: 50M x 64, k = 1024 (screen_big MFMA path) + replica
     scoring per cluster: labels of a 10k sample = the oracle, sums of two
