@@ -322,6 +322,101 @@ def ingest_bench(args, world: int, rank: int, dist, device, json_fd: int) -> Non
         dist.destroy_process_group()
 
 
+F64_CFG = (10_000_000, 5, "F64 leg: 10M files x d=5 min-max-normalised features (not on a "
+                          "2^-S grid: src/main.py:81 data), k={k}")
+
+
+def f64_data(n: int, d: int, k: int, seed: int):
+    """Blob data min-max normalised per column as src/main.py:81 does (values
+    off any 2^-S grid, so the points load in F64 mode)."""
+    import numpy as np
+
+    from oracle import synth
+
+    X = synth.generate(n, 0, n, d, k, seed)
+    mn, mx = X.min(axis=0), X.max(axis=0)
+    return (X - mn) / (mx - mn)
+
+
+def f64_bench(args, world: int, rank: int, json_fd: int) -> None:
+    """F64 mode (`main.py`'s real data path): exact fp64
+    NumPy-order assignment of every point (assign_exact_all) + exact
+    sequential-order cluster sums (csrc/f64sum.hip), one host round trip per
+    step (cdr_lloyd_step_f64), centroids = sums / counts on the host as
+    src/kmeans_plusplus.py:41 does.  Single GPU (replicas at N > 1)."""
+    import numpy as np
+
+    import _cdr
+
+    n, d, desc = F64_CFG
+    if args.n_total:
+        n = args.n_total
+    k = args.k or 16
+    X = f64_data(n, d, k, args.seed)
+    ctx = _cdr.Context(int(os.environ.get("LOCAL_RANK", "0")))
+    ctx.load_points(X)
+    if ctx.info()["mode"] != _cdr.MODE_F64:
+        raise RuntimeError("F64 leg: the points did not load in F64 mode")
+    C = X[np.sort(np.random.default_rng(42).choice(n, k, replace=False))].copy()
+
+    def step(C):
+        sums, counts = ctx.lloyd_step_f64(C)
+        nz = counts > 0
+        C = C.copy()
+        C[nz] = sums[nz] / counts[nz, None]
+        return C
+
+    for _ in range(args.warmup):
+        C = step(C)
+    ctx.synchronize()
+    ctx.profile_reset(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        C = step(C)
+    elapsed = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile_reset(False)
+    assign_ms = prof["screen_ms"] / max(prof["steps"], 1)
+    kern_ms = prof["step_ms"] / max(prof["steps"], 1)
+    alg = n * (8 * d + 4)  # read the fp64 point, write its int32 label
+    achieved = alg / (assign_ms / 1e3) / 1e9
+    out = {
+        "metric": "Lloyd point-iters/sec, F64 mode (exact fp64 assignment + exact sequential sums)",
+        "value": world * n * args.steps / elapsed, "unit": "point-iters/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic blobs, min-max normalised on the host (non-grid fp64)",
+        "config": {"workload": desc.format(k=k), "n_files": n, "d": d, "k": k,
+                   "parallelism": "one GPU (independent replicas at N > 1)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel": ctx.profile_kernel(), "alg_bytes_per_launch": alg,
+                     "kernel_ms": assign_ms},
+        "step_kernels_ms": kern_ms,
+        "f64_blocks_walked": ctx.f64_walked(),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import kmeans_oracle
+
+        rows, iters = 1_000_000, 2
+        Xs = X[:rows]
+        Cs = Xs[:k].copy()
+        c0 = time.perf_counter()
+        for _ in range(iters):
+            lab = kmeans_oracle.assign(Xs, Cs)
+            Cs = kmeans_oracle.update(Xs, lab, Cs, rows)
+        dt = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": rows * iters / dt, "unit": "point-iters/s", "cores": 1,
+                               "kind": "port",
+                               "sample": f"{rows} rows x {iters} Lloyd iterations of the same "
+                                         f"F64 data, d={d}, k={k}; NumPy oracle restatement of "
+                                         "src/kmeans_plusplus.py:33-43, 1 thread",
+                               "seconds": dt}
+    if rank == 0:
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    ctx.close()
+
+
 def pmc_traffic(config: str, n_local: int):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -357,7 +452,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="3", choices=sorted(CONFIGS) + ["4", "4-ingest"])
+    ap.add_argument("--config", default="3", choices=sorted(CONFIGS) + ["4", "4-ingest", "f64"])
+    ap.add_argument("--k", type=int, default=0, help="k of the f64 leg (default 16)")
     ap.add_argument("--n-total", type=int, default=0,
                     help="override the per-config point count (testing only)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
@@ -397,6 +493,11 @@ def main() -> None:
         return
     if args.config == "4-ingest":
         ingest_bench(args, world, rank, dist, device, json_fd)
+        return
+    if args.config == "f64":
+        f64_bench(args, world, rank, json_fd)
+        if dist is not None:
+            dist.destroy_process_group()
         return
     n_cfg, d, k, desc = CONFIGS[args.config]
     if args.n_total:

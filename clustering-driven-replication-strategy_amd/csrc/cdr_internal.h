@@ -168,6 +168,7 @@ struct Ctx {
   double prof_screen_ms = 0.0, prof_step_ms = 0.0, prof_fb_points = 0.0;
   int64_t prof_launches = 0;
   DevBuf fb_accum;  // int64: fallback points summed over the steps (publish32)
+  DevBuf q_acc;     // int64 per screen32p wave: points queued for the k-way screen (profiling)
   char prof_kernel[96] = {0};  // name of the last screen kernel launched
   int fb_layout = -1;     // screen32: nwaves the fb_count buffer was zeroed for
   int fb_total_slot = 0;  // fb_count index holding the last step's fallback total

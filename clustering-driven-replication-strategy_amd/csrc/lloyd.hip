@@ -812,11 +812,32 @@ __global__ void seq_sums_f64(const double* __restrict__ X, int64_t n, int64_t n_
   sums[j] = res;
 }
 
-__global__ void count_labels(const int32_t* __restrict__ labels, int64_t n, int k,
-                             unsigned long long* __restrict__ counts) {
+// Cluster sizes of the labels: one LDS histogram per wave (k <= kCountLds),
+// added into the global counts once per (workgroup, cluster).  (One global
+// atomic per point serialised on the k addresses: 28 ms at 10M points, k = 16.)
+constexpr int kCountLds = 4096;
+__global__ __launch_bounds__(256) void count_labels(const int32_t* __restrict__ labels, int64_t n,
+                                                    int k, unsigned long long* __restrict__ counts) {
+  extern __shared__ unsigned hist[];  // [4 waves][k] when k <= kCountLds
+  const bool lds = k <= kCountLds;
+  if (lds) {
+    for (int i = threadIdx.x; i < 4 * k; i += blockDim.x) hist[i] = 0u;
+    __syncthreads();
+  }
+  unsigned* wh = hist + (threadIdx.x >> 6) * k;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&counts[labels[i]], 1ull);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int l = labels[i];
+    if (lds) atomicAdd(&wh[l], 1u);
+    else atomicAdd(&counts[l], 1ull);
+  }
+  if (!lds) return;
+  __syncthreads();
+  for (int j = threadIdx.x; j < k; j += blockDim.x) {
+    const unsigned long long v = (unsigned long long)hist[j] + hist[k + j] + hist[2 * k + j] +
+                                 hist[3 * k + j];
+    if (v) atomicAdd(&counts[j], v);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1267,23 +1288,28 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
   const int d = c.d;
   const int cus = lloyd_num_cus(c.device);
   upload_centroids(c, C, k);
+  const bool prof = prof_step_begin(c);
+  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "assign_exact_all<double>");
+  if (prof) prof_mark(c, 0);
   hipLaunchKernelGGL(assign_exact_all<double>,
                      dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 8))),
                      dim3(256), 0, c.stream, c.x64.as<double>(), c.n, c.n_pad, d,
                      c.cent64.as<double>(), k, c.labels.as<int32_t>());
   HIP_CHECK(hipGetLastError());
+  if (prof) prof_mark(c, 1);
   c.f64_sums.ensure(sizeof(double) * (size_t)k * d);
   c.f64_counts.ensure(sizeof(long long) * k * 2);
   long long* cnt_pre = c.f64_counts.as<long long>() + k;
   HIP_CHECK(hipMemsetAsync(cnt_pre, 0, sizeof(long long) * k, c.stream));
-  hipLaunchKernelGGL(count_labels, dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), 1024))),
-                     dim3(256), 0, c.stream, c.labels.as<int32_t>(), c.n, k,
-                     reinterpret_cast<unsigned long long*>(cnt_pre));
+  hipLaunchKernelGGL(count_labels, dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 2))),
+                     dim3(256), k <= kCountLds ? sizeof(unsigned) * 4 * k : 0, c.stream,
+                     c.labels.as<int32_t>(), c.n, k, reinterpret_cast<unsigned long long*>(cnt_pre));
   HIP_CHECK(hipGetLastError());
   if (!getenv("CDR_F64_SERIAL") && f64_sums_parallel(c, k, c.f64_sums.as<double>())) {
     // f64sum.hip: exact row-order sums in parallel; counts from count_labels
     HIP_CHECK(hipMemcpyAsync(c.f64_counts.p, cnt_pre, sizeof(long long) * k,
                              hipMemcpyDeviceToDevice, c.stream));
+    if (prof) prof_mark(c, 2);
     std::vector<long long> w((size_t)k * d);
     HIP_CHECK(hipMemcpyAsync(w.data(), c.f64x_walk.p, sizeof(long long) * w.size(),
                              hipMemcpyDeviceToHost, c.stream));
@@ -1296,6 +1322,7 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
                        c.x64.as<double>(), c.n, c.n_pad, d, k, c.labels.as<int32_t>(), cnt_pre,
                        c.f64_sums.as<double>(), c.f64_counts.as<long long>());
     HIP_CHECK(hipGetLastError());
+    if (prof) prof_mark(c, 2);
     c.f64x_walked = -1;
   }
   HIP_CHECK(hipMemcpyAsync(sums, c.f64_sums.p, sizeof(double) * (size_t)k * d,
@@ -1406,6 +1433,7 @@ int cdr_profile_reset(cdr_ctx* h, int32_t enable) {
   c.prof_launches = 0;
   c.fb_accum.ensure(2 * sizeof(long long));
   HIP_CHECK(hipMemsetAsync(c.fb_accum.p, 0, 2 * sizeof(long long), c.stream));
+  if (c.q_acc.p) HIP_CHECK(hipMemsetAsync(c.q_acc.p, 0, c.q_acc.bytes, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
   CDR_CATCH
 }
@@ -1417,11 +1445,14 @@ int cdr_profile_read(cdr_ctx* h, double* out) {
   HIP_CHECK(hipSetDevice(c.device));
   prof_collect(c);
   long long fb[2] = {0, 0};
-  if (c.fb_accum.p) {
+  std::vector<long long> q(c.q_acc.bytes / sizeof(long long));
+  if (c.fb_accum.p)
     HIP_CHECK(hipMemcpyAsync(fb, c.fb_accum.p, std::min(c.fb_accum.bytes, sizeof(fb)),
                              hipMemcpyDeviceToHost, c.stream));
-    HIP_CHECK(hipStreamSynchronize(c.stream));
-  }
+  if (!q.empty())
+    HIP_CHECK(hipMemcpyAsync(q.data(), c.q_acc.p, c.q_acc.bytes, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  for (long long v : q) fb[1] += v;
   out[0] = c.prof_screen_ms;
   out[1] = (double)c.prof_launches;
   out[2] = c.prof_step_ms;

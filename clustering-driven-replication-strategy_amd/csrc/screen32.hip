@@ -902,10 +902,9 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
+    if (lane == 0) {  // (the step's total: fixup32)
       a.fb_count[wave] = fb_used;
       a.mv_count[wave] = mv_used;
-      if (fb_used) atomicAdd(a.fb_count + nwaves, fb_used);
     }
     return;
   }
@@ -921,10 +920,9 @@ __global__ __launch_bounds__(256) void screen32d(S32DArgs a) {
       process(buf[i], Gi);
     }
   }
-  if (lane == 0) {
+  if (lane == 0) {  // (the step's total: fixup32)
     a.fb_count[wave] = fb_used;
     a.mv_count[wave] = mv_used;
-    if (fb_used) atomicAdd(a.fb_count + nwaves, fb_used);
   }
 }
 
@@ -947,6 +945,7 @@ struct FixArgs {
   double fx;    // 2^S
   unsigned long long* run_sums;  // kRunSlices x (k, d+1)
   const long long* gate;
+  int32_t* fb_total;  // the step's fallback total (fb_count[regions])
   int abl;  // timing experiments only (0 in the product build): 1 no moves, 2 no fallback,
            // 4 no flush, 8 first candidate only, 16 no point gather, 32 no label / table change
   // the step's screen (the uncertified points are screened again)
@@ -1011,6 +1010,8 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
   }
   __syncthreads();
   const int nmv = s_mv[FR], nfb = s_fb[FR];
+  // the step's fallback total (screen32d / screen32p write per-wave counts only)
+  if (threadIdx.x == 0 && nfb) atomicAdd(a.fb_total, nfb);
   if (nmv == 0 && nfb == 0) return;  // uniform: nothing changes here
   const f4* XA4 = reinterpret_cast<const f4*>(a.XA);  // point i: XA4[i * Q + q]
   auto region_of = [&](const int* pre, int e, int& r, int& i) {
@@ -1275,7 +1276,9 @@ struct S32PArgs {
   int2* mv_list;  // per-wave regions {pt, old | new << 16}
   int32_t* mv_count;
   int cap;
-  long long* q_acc;  // profiling: points queued for the k-way screen (null: off)
+  long long* q_acc;  // profiling: points queued for the k-way screen, per wave (null: off)
+  int abl;  // timing experiments only (0 in the product build): 1 no drains,
+            // 2 no per-point work (loads and the label byte only)
 };
 
 // fp32 (lo / hi fp16 half of w) - c, one rounding (v_fma_mix_f32)
@@ -1543,6 +1546,10 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
     const int64_t pt = base + lane;
     const bool real = pt < a.n;
     const int ao = b.ob;
+    if (a.abl & 2) {  // timing experiments: streaming only
+      if (b.w[0] == 0x7fffffffu && b.w[2 * NWH - 1] == 0x7fffffffu) fb_used += ao;
+      return;
+    }
     const float qa = dist2(b, ao);
     const float uba = fmaf(__builtin_amdgcn_sqrtf(qa), 1.0f + 0x1p-18f, eb[ao]);
     const bool keep = fmaf(hc[ao], 1.0f - 0x1p-22f, -uba) > uba * (1.0f + 0x1p-20f);
@@ -1569,7 +1576,7 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
       qn += c;
       qtot += c;
       if (qn >= 64) {
-        drain(((qh - qn) & 127) >> 6, 64);
+        if (!(a.abl & 1)) drain(((qh - qn) & 127) >> 6, 64);
         qn -= 64;
       }
     }
@@ -1588,12 +1595,13 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   if (qn > 0) {  // the partial block (queue tail at a block start: 64 | qh - qn)
     drain(((qh - qn) & 127) >> 6, qn);
   }
+  // per-wave counts only: fixup32 adds the step's fallback total (one atomic
+  // per fixup workgroup); thousands of same-address atomics at the end of
+  // this kernel serialised in L2 for tens of microseconds
   if (lane == 0) {
     a.fb_count[wave] = fb_used;
     a.mv_count[wave] = mv_used;
-    if (fb_used) atomicAdd(a.fb_count + nwaves, fb_used);
-    if (a.q_acc && qtot) atomicAdd(reinterpret_cast<unsigned long long*>(a.q_acc),
-                                   (unsigned long long)qtot);
+    if (a.q_acc) a.q_acc[wave] += qtot;  // (profiling) this wave's own slot
   }
 }
 // ---------------------------------------------------------------------------
@@ -1990,8 +1998,15 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     p.thr_rel = thr_rel;
     p.Dv = Dv;
     p.thr_dev = dthr;
-    c.fb_accum.ensure(2 * sizeof(long long));
-    p.q_acc = c.prof_on ? c.fb_accum.as<long long>() + 1 : nullptr;
+    if (c.prof_on && c.q_acc.bytes < sizeof(long long) * nwaves) {  // (zeroed when grown)
+      c.q_acc.ensure(sizeof(long long) * nwaves);
+      HIP_CHECK(hipMemsetAsync(c.q_acc.p, 0, c.q_acc.bytes, c.stream));
+    }
+    p.q_acc = c.prof_on ? c.q_acc.as<long long>() : nullptr;
+    p.abl = 0;
+#ifdef CDR_EXPERIMENTS
+    if (const char* e = std::getenv("CDR_S32P_ABL")) p.abl = std::atoi(e);
+#endif
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32p<%d,%d,%d>", QH, MT, PPD);
     if (prof) prof_mark(c, 0);
     screen32p_launch(QH, MT, PPD, grid, c.stream, p);
@@ -2043,6 +2058,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   f.fx = std::ldexp(1.0, c.scale_bits);
   f.run_sums = c.run_sums.as<unsigned long long>();
   f.gate = gate;
+  f.fb_total = c.fb_count.as<int32_t>() + nwaves;
   f.abl = 0;
   f.XS = c.xs16.as<unsigned char>();
   f.frag = dfrag;
