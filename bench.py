@@ -474,6 +474,14 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = None
+    if args.rccl and "RANK" not in os.environ:  # one process without a launcher
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
     if world > 1 or args.rccl:
         import torch  # first: libcdr then binds to torch's HIP runtime
         import torch.distributed as tdist

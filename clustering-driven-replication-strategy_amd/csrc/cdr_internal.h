@@ -315,6 +315,23 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 bool prof_step_begin(Ctx& c);
 void prof_mark(Ctx& c, int i);
 
+// The step's fallback total from the screens' per-wave counts fbc[0, nwaves)
+// (the DELTA screens write per-wave counts only: thousands of same-address
+// atomics at the end of a kernel serialise in L2).  One workgroup, every
+// thread calls it; the total is returned on every thread.
+__device__ inline int block_sum_counts(const int* __restrict__ fbc, int nwaves) {
+  __shared__ int s_total;
+  if (threadIdx.x == 0) s_total = 0;
+  __syncthreads();
+  int v = 0;
+  for (int i = threadIdx.x; i < nwaves; i += blockDim.x) v += fbc[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(&s_total, v);
+  __syncthreads();
+  return s_total;
+}
+
 // fp64 -> fp16 with one round-to-nearest-even, identical on host and device
 // (the screen fragments are built by both: build_plan32 and plan32_build).
 // Branch-free: round to odd into fp32 (truncate, then set the lowest bit when

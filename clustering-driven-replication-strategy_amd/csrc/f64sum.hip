@@ -80,9 +80,16 @@ __global__ __launch_bounds__(256) void f64_predict(const double* __restrict__ A,
   if (t >= k * d) return;
   const int j = t / d;
   double carry = 0.0;
+  // one round ahead (a single wave scans the sequence: latency-bound)
+  auto fetch = [&](int64_t b0) -> double {
+    const int64_t b = b0 + lane;
+    return (b < nb && cnt[b * k + j]) ? A[b * k * d + t] : 0.0;
+  };
+  double vn = fetch(0);
   for (int64_t b0 = 0; b0 < nb; b0 += 64) {
     const int64_t b = b0 + lane;
-    const double v = (b < nb && cnt[b * k + j]) ? A[b * k * d + t] : 0.0;
+    const double v = vn;
+    if (b0 + 64 < nb) vn = fetch(b0 + 64);
     double inc = v;
     for (int o = 1; o < 64; o <<= 1) {
       const double u = __shfl_up(inc, o);
@@ -241,16 +248,25 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
       }
     }
   };
-  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+  // the round's (count, prediction, transfer) per lane, loaded one round ahead
+  // (a single wave walks the sequence: the load latency would set its time)
+  auto fetch = [&](int64_t b0, unsigned& c, int& el, Xfer& xl) {
     const int64_t bl = b0 + lane;
     const bool in = bl < nb;
-    const unsigned c = in ? cnt[bl * k + j] : 0u;
-    const int el = in ? E[bl * k * d + t] : kENone;
-    Xfer xl;
-    xl.d0 = 0;
-    xl.dd = 0;
-    xl.flags = 4;
-    if (in && c) xl = T[bl * k * d + t];
+    c = in ? cnt[bl * k + j] : 0u;
+    el = in ? E[bl * k * d + t] : kENone;
+    xl = in ? T[bl * k * d + t] : Xfer{0, 0, 4};
+  };
+  unsigned cn;
+  int eln;
+  Xfer xn;
+  fetch(0, cn, eln, xn);
+  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+    const unsigned c = cn;
+    const int el = eln;
+    Xfer xl = xn;
+    if (!c) xl = Xfer{0, 0, 4};
+    if (b0 + 64 < nb) fetch(b0 + 64, cn, eln, xn);
     const unsigned long long live = __ballot(c != 0);
     int i = 0;  // next block of this round (wave-uniform)
     while (i < 64) {

@@ -128,11 +128,13 @@ __global__ __launch_bounds__(kFinThreads) void ll_finalize(FinArgs a) {
   int empty = 0;
   long long* cnt_out = reinterpret_cast<long long*>(Cnew + (size_t)k * d);
   for (int j = t; j < k; j += blockDim.x) cnt_out[j] = sum_at((size_t)j * d1 + d);
-  if (t == 0 && a.fbc) {
-    const int fb = a.fbc[a.nwaves];
-    a.fbc[a.nwaves] = 0;
-    a.fbc[a.nwaves + 1] = fb;
-    if (a.fb_acc) a.fb_acc[0] += fb;
+  if (a.fbc) {  // (uniform)
+    const int fb = block_sum_counts(a.fbc, a.nwaves);
+    if (t == 0) {
+      a.fbc[a.nwaves] = 0;
+      a.fbc[a.nwaves + 1] = fb;
+      if (a.fb_acc) a.fb_acc[0] += fb;
+    }
   }
 #pragma unroll 4
   for (int e = t; e < k * d; e += blockDim.x) {
@@ -270,12 +272,10 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
   double* __restrict__ Cnew = a.Cnew;
   long long* cnt_out = reinterpret_cast<long long*>(Cnew + (size_t)k * d);
   if (row && (t & 7) == 0) cnt_out[j] = cnt;
-  if (t == 0 && a.fbc) {
-    const int fb = a.fbc[a.nwaves];
-    a.fbc[a.nwaves] = 0;
-    a.fbc[a.nwaves + 1] = fb;
-    if (a.fb_acc) a.fb_acc[0] += fb;
-  }
+  // the per-wave fallback counts (the step's total: the decision sync below)
+  int fbv = 0;
+  if (a.fbc)
+    for (int i = t; i < a.nwaves; i += blockDim.x) fbv += a.fbc[i];
   // the host's np.ldexp(acc.astype(float64), -S) / counts (kmeans_plusplus.py)
   const double sj0 = ldexp((double)S0, -a.sbits), sj1 = ldexp((double)S1, -a.sbits);
   double m0 = sj0 / (double)cnt, m1 = sj1 / (double)cnt;
@@ -307,16 +307,25 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
     cross += __shfl_xor(cross, o);
     quad += __shfl_xor(quad, o);
     empty |= __shfl_xor(empty, o);
+    fbv += __shfl_xor(fbv, o);
   }
   __shared__ double r_ss[8], r_cross[8], r_quad[8];
-  __shared__ int r_empty[8];
+  __shared__ int r_empty[8], r_fb[8];
   if (lane == 0) {
     r_ss[wv] = ss;
     r_cross[wv] = cross;
     r_quad[wv] = quad;
     r_empty[wv] = empty;
+    r_fb[wv] = fbv;
   }
   __syncthreads();
+  if (t == 0 && a.fbc) {
+    int fb = 0;
+    for (int w = 0; w < 8; ++w) fb += r_fb[w];
+    a.fbc[a.nwaves] = 0;
+    a.fbc[a.nwaves + 1] = fb;
+    if (a.fb_acc) a.fb_acc[0] += fb;
+  }
   // ---- the decision (every thread, the same fixed order) ----
   double sst = 0.0, crs = 0.0, qd = 0.0;
   int emp = 0;

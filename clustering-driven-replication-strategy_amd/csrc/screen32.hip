@@ -568,12 +568,14 @@ __global__ __launch_bounds__(256) void publish32(const long long* __restrict__ o
     if (dout) dout[i] = v;
     if (hout) hout[i] = v;
   }
-  if (threadIdx.x == 0 && fbc) {
-    const int fb = fbc[nwaves];
-    fbc[nwaves] = 0;
-    fbc[nwaves + 1] = fb;
-    if (hout) hout[cells] = fb;
-    if (fb_acc) fb_acc[0] += fb;
+  if (fbc) {  // (uniform)
+    const int fb = block_sum_counts(fbc, nwaves);
+    if (threadIdx.x == 0) {
+      fbc[nwaves] = 0;
+      fbc[nwaves + 1] = fb;
+      if (hout) hout[cells] = fb;
+      if (fb_acc) fb_acc[0] += fb;
+    }
   }
 }
 
@@ -945,7 +947,6 @@ struct FixArgs {
   double fx;    // 2^S
   unsigned long long* run_sums;  // kRunSlices x (k, d+1)
   const long long* gate;
-  int32_t* fb_total;  // the step's fallback total (fb_count[regions])
   int abl;  // timing experiments only (0 in the product build): 1 no moves, 2 no fallback,
            // 4 no flush, 8 first candidate only, 16 no point gather, 32 no label / table change
   // the step's screen (the uncertified points are screened again)
@@ -974,31 +975,103 @@ struct FixArgs {
 //   point evaluates its candidates in index order in exact fp64 NumPy order
 //   with a correctly rounded sqrt: np.argmin of np.linalg.norm, first index on
 //   ties (src/kmeans_plusplus.py:33-34).
-template <int D, int MT>
-__global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
-  if (a.gate && a.gate[0] == 0) return;
-  constexpr int CS = D + 1;
-  constexpr int Q = (D + 3) / 4;
-  constexpr int TS = 65;  // table row stride
-  __shared__ double tsum[D * TS];
-  __shared__ int tcnt[64];
-  __shared__ double cs[64 * CS];
-  __shared__ int s_mv[kFixMaxR + 1], s_fb[kFixMaxR + 1];
-  const int FR = a.fr;
-  const int k = a.k;
-  const int r0 = blockIdx.x * FR;
-  if (threadIdx.x < FR) {
-    const int r = r0 + threadIdx.x;
-    s_mv[threadIdx.x + 1] = r < a.regions ? a.mv_count[r] : 0;
-    s_fb[threadIdx.x + 1] = r < a.regions ? a.fb_count[r] : 0;
+template <int Q>
+struct FixDims {
+  static constexpr int QH = Q <= 2 ? 1 : 2;  // quads per lane half of the split screen
+  static constexpr int DM = 4 * Q;           // features a point row holds (d <= DM)
+};
+constexpr int kFixTS = 65;  // table row stride
+// LDS of one fixup workgroup: tsum [16][kFixTS] | cs [64][17] (fp64) | tcnt [64] |
+// s_mv, s_fb [kFixMaxR + 1]
+constexpr size_t kFixLdsBytes =
+    sizeof(double) * (16 * kFixTS + 64 * 17) + sizeof(int) * (64 + 2 * (kFixMaxR + 1));
+struct FixLds {
+  double* tsum;
+  double* cs;
+  int* tcnt;
+  int* s_mv;
+  int* s_fb;
+  __device__ explicit FixLds(unsigned char* base) {
+    tsum = reinterpret_cast<double*>(base);
+    cs = tsum + 16 * kFixTS;
+    tcnt = reinterpret_cast<int*>(cs + 64 * 17);
+    s_mv = tcnt + 64;
+    s_fb = s_mv + kFixMaxR + 1;
   }
+};
+
+// The lists of screen waves r0 .. r0 + FR - 1 applied by one workgroup to an
+// LDS table (rows padded to 65: the lanes of one point hit different banks),
+// then to slice `slice` of the running sums.  The caller has put the regions'
+// counts in s_mv[1 .. FR] / s_fb[1 .. FR]; every thread calls it.  Q: feature
+// quads of a point row (d <= 4 Q; d itself is a runtime value).
+// * Moves, 4 lanes per point (lane q: feature quad q): +x into the new
+//   cluster, -x out of the old one.
+// * Uncertified points, 64 per wave: the split screen of screen32d is
+//   computed for them (the same plan, so the same values), and every centroid
+//   whose key is within the certification threshold of the best key is a
+//   candidate (|S_j - T_j| <= E for all j: the reference's argmin is among
+//   them; a point is certified exactly when the best is the only one).  The
+//   lane owning the point evaluates its candidates in index order in exact fp64
+//   NumPy order with a correctly rounded sqrt: np.argmin of np.linalg.norm,
+//   first index on ties (src/kmeans_plusplus.py:33-34).
+// np_sqdist (exact_math.h: NumPy's pairwise order of sum((x - c)^2)) for a
+// runtime d <= 16 with every index a constant, so that x stays in registers:
+// d < 8 sequential from 0.0; else 8 accumulators over the first 8 (d & ~7)
+// features, the fixed tree, then the tail in order.
+__device__ __forceinline__ double np_sqdist16(const float (&x)[16], const double* c, int d) {
+  auto sq = [&](int f) {
+    const double u = (double)x[f] - c[f];
+    return u * u;
+  };
+  if (d < 8) {
+    double res = 0.0;
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+      if (f < d) res = res + sq(f);
+    return res;
+  }
+  double r[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = sq(i);
+  if (d >= 16) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = r[i] + sq(8 + i);
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  const int dd = d - (d & 7);
+#pragma unroll
+  for (int f = 8; f < 16; ++f)
+    if (f >= dd && f < d) res = res + sq(f);
+  return res;
+}
+
+// Plan operands of the re-screen: from global memory (fixup32) or from the
+// screen's LDS copies (screen32p: sA [MT][2][64] h8, sC [MT][4][2][4] f32).
+struct FixPlan {
+  const h8* sA;
+  const float* sC;
+};
+template <int Q, int MT>
+__device__ __forceinline__ void fixup_regions(const FixArgs& a, int r0, int FR, int slice,
+                                              const FixLds& L, FixPlan P = FixPlan{nullptr, nullptr}) {
+  constexpr int CS = 17;
+  constexpr int TS = kFixTS;
+  constexpr int QH = FixDims<Q>::QH;
+  constexpr int DM = FixDims<Q>::DM;
+  double* tsum = L.tsum;
+  double* cs = L.cs;
+  int* tcnt = L.tcnt;
+  int* s_mv = L.s_mv;
+  int* s_fb = L.s_fb;
+  const int k = a.k, d = a.d;
   // the step's centroids (fp64), loaded by every thread at once
 #pragma unroll 4
-  for (int i = threadIdx.x; i < k * D; i += blockDim.x) {
+  for (int i = threadIdx.x; i < k * d; i += blockDim.x) {
     const double v = a.cent[i];
-    cs[(i / D) * CS + i % D] = v;
+    cs[(i / d) * CS + i % d] = v;
   }
-  for (int i = threadIdx.x; i < D * TS; i += blockDim.x) tsum[i] = 0.0;
+  for (int i = threadIdx.x; i < DM * TS; i += blockDim.x) tsum[i] = 0.0;
   for (int i = threadIdx.x; i < 64; i += blockDim.x) tcnt[i] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1010,8 +1083,6 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
   }
   __syncthreads();
   const int nmv = s_mv[FR], nfb = s_fb[FR];
-  // the step's fallback total (screen32d / screen32p write per-wave counts only)
-  if (threadIdx.x == 0 && nfb) atomicAdd(a.fb_total, nfb);
   if (nmv == 0 && nfb == 0) return;  // uniform: nothing changes here
   const f4* XA4 = reinterpret_cast<const f4*>(a.XA);  // point i: XA4[i * Q + q]
   auto region_of = [&](const int* pre, int e, int& r, int& i) {
@@ -1032,7 +1103,7 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int f = 4 * q4 + c;
-        if (f < D) {
+        if (f < d) {
           atomicAdd(&tsum[f * TS + to], (double)xq[c]);
           atomicAdd(&tsum[f * TS + from], -(double)xq[c]);
         }
@@ -1044,27 +1115,42 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
     }
   }
   if (nfb && !(a.abl & 2)) {
-    constexpr int QH = D <= 8 ? 1 : 2;
     constexpr int kTile = 1024 * QH;
     typedef unsigned u4v __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int h = lane >> 5, p = lane & 31;
-    h8 A[MT][2];
-    f16v Ci[MT];
+    // centroid tile m's screen values of B (one tile's accumulator live at a
+    // time: this body also runs in screen32p's tail, beside its registers)
+    auto screen_m = [&](int m, const u4v (&vt)[QH]) -> f16v {
+      const h8 A0 = P.sA ? P.sA[(m * 2 + 0) * 64 + lane] : a.frag[(m * 2 + 0) * 64 + lane];
+      const h8 A1 = P.sA ? P.sA[(m * 2 + 1) * 64 + lane] : a.frag[(m * 2 + 1) * 64 + lane];
+      f16v acc;
+      if (P.sC) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const f4 c4v = *reinterpret_cast<const f4*>(P.sC + ((m * 4 + i4) * 2 + h) * 4);
 #pragma unroll
-      for (int u = 0; u < 2; ++u) A[m][u] = a.frag[(m * 2 + u) * 64 + lane];
+          for (int i = 0; i < 4; ++i) acc[4 * i4 + i] = c4v[i];
+        }
+      } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) Ci[m][i] = a.cinit[(m * 16 + i) * 64 + lane];
-    }
+        for (int i = 0; i < 16; ++i) acc[i] = a.cinit[(m * 16 + i) * 64 + lane];
+      }
+      const h8 BH = __builtin_bit_cast(h8, vt[0]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, BH, acc, 0, 0, 0);
+      if constexpr (QH == 2) {
+        const h8 BL = __builtin_bit_cast(h8, vt[QH - 1]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, BL, acc, 0, 0, 0);
+      }
+      return __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, BH, acc, 0, 0, 0);
+    };
     const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
     auto rec_of = [&](int e) -> int2 {
       int r, i;
       region_of(s_fb, e, r, i);
       return a.fb_list[(size_t)(r0 + r) * a.cap + i];
     };
-    for (int e0 = wv * 64; e0 < nfb; e0 += 256) {
+    for (int e0 = wv * 64; e0 < nfb; e0 += blockDim.x) {
       // tile t holds list entries e0 + 32 t .. + 31; lane (h, p) the B
       // operand of entry e0 + 32 t + p (its half h), as screen32d loads it
       int32_t ptt[2], oldt[2];
@@ -1086,7 +1172,7 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const int f = 4 * qq + c;
-              xt[c] = f < D ? fmaf(xr[c], a.sig, a.ms[f]) : 0.0f;
+              xt[c] = f < d ? fmaf(xr[c], a.sig, a.ms[f]) : 0.0f;
             }
             split4(xt, hw[2 * u], hw[2 * u + 1], lw[2 * u], lw[2 * u + 1]);
           }
@@ -1104,8 +1190,8 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
         }
       }
       // this lane's point after the half swap: entry e0 + lane (tile lane >> 5)
-      const int own = ptt[h];  // lane (h, p) owns entry e0 + 32 h + p
-      const int old = oldt[h];
+      const int own = h ? ptt[1] : ptt[0];  // lane (h, p) owns entry e0 + 32 h + p
+      const int old = h ? oldt[1] : oldt[0];   // (selects: no indexed private arrays)
       const int e_own = e0 + lane;
       const bool live = e_own < nfb;
       f4 xq[Q];
@@ -1120,37 +1206,30 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
       unsigned mine[2], other[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const h8 BH = __builtin_bit_cast(h8, v[t][0]);
-        f16v acc[MT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BH, Ci[m], 0, 0, 0);
-          if constexpr (QH == 2) {
-            const h8 BL = __builtin_bit_cast(h8, v[t][1]);
-            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], BL, acc[m], 0, 0, 0);
-          }
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][1], BH, acc[m], 0, 0, 0);
-        }
         // best key of the point over both halves (as screen32d forms keys)
         unsigned bk = 0xFFFFFFFFu;
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
+#pragma nounroll
+        for (int m = 0; m < MT; ++m) {
+          const f16v acc = screen_m(m, v[t]);
+          const unsigned rb = 32u * (unsigned)m;
 #pragma unroll
           for (int i = 0; i < 16; ++i)
-            bk = min(bk, (__float_as_uint(acc[m][i]) & ~63u) |
-                             (unsigned)(32 * m + 8 * (i >> 2) + (i & 3)));
+            bk = min(bk, (__float_as_uint(acc[i]) & ~63u) | (rb + (unsigned)(8 * (i >> 2) + (i & 3))));
+        }
         bk |= (unsigned)h << 2;
         bk = min(bk, (unsigned)__shfl_xor((int)bk, 32));
         const float tau = fmaf(__uint_as_float(bk & ~63u), thr_rel, thr0);
         unsigned cm = 0;
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
+#pragma nounroll
+        for (int m = 0; m < MT; ++m) {  // the same values again (recomputed, bit-identical)
+          const f16v acc = screen_m(m, v[t]);
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             // not excluded: key value <= tau (NaN: a candidate)
-            const float kv = __uint_as_float(__float_as_uint(acc[m][i]) & ~63u);
+            const float kv = __uint_as_float(__float_as_uint(acc[i]) & ~63u);
             if (!(kv > tau)) cm |= 1u << (16 * m + i);
           }
+        }
         mine[t] = cm;
         other[t] = (unsigned)__shfl_xor((int)cm, 32);
       }
@@ -1158,10 +1237,10 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
       // those of half 1 - h in other[h]; as a 64-bit row mask
       unsigned long long cand = 0;
       {
-        const unsigned mh[2] = {h == 0 ? mine[0] : other[1], h == 0 ? other[0] : mine[1]};
+        const unsigned mh0 = h == 0 ? mine[0] : other[1], mh1 = h == 0 ? other[0] : mine[1];
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-          unsigned mm = mh[hh];  // rows of half hh of tile h
+          unsigned mm = hh ? mh1 : mh0;  // rows of half hh of tile h
           while (mm) {
             const int bb = __builtin_ctz(mm);
             mm &= mm - 1;
@@ -1172,18 +1251,16 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
         if (k < 64) cand &= (1ull << k) - 1;
       }
       if (live) {
-        double x[D];
+        float x[16];  // (fp32 data: converted exactly where used)
 #pragma unroll
-        for (int f = 0; f < D; ++f) x[f] = (double)xq[f >> 2][f & 3];
+        for (int f = 0; f < 16; ++f) x[f] = f < DM ? xq[f >> 2][f & 3] : 0.0f;
         double sb = INFINITY, rb = INFINITY;
         int jmin = 0x7fffffff;
         unsigned long long cmk = (a.abl & 8) ? (cand & (~cand + 1)) : cand;
         while (cmk) {  // increasing j
           const int j = __builtin_ctzll(cmk);
           cmk &= cmk - 1;
-          const double* cj = cs + j * CS;
-          const double sq =
-              np_sqdist([&](int f) { return x[f]; }, [&](int f) { return cj[f]; }, D);
+          const double sq = np_sqdist16(x, cs + j * CS, d);
           if (sq < sb) {  // sqrt is monotone: only a smaller square can give a smaller root
             const double rt = sqrt(sq);
             sb = sq;
@@ -1198,9 +1275,11 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
           a.labels[own] = jmin;
           a.lab8[own] = (uint8_t)jmin;
 #pragma unroll
-          for (int f = 0; f < D; ++f) {
-            atomicAdd(&tsum[f * TS + jmin], x[f]);
-            atomicAdd(&tsum[f * TS + old], -x[f]);
+          for (int f = 0; f < DM; ++f) {
+            if (f < d) {
+              atomicAdd(&tsum[f * TS + jmin], (double)x[f]);
+              atomicAdd(&tsum[f * TS + old], -(double)x[f]);
+            }
           }
           atomicAdd(&tcnt[jmin], 1);
           atomicAdd(&tcnt[old], -1);
@@ -1210,16 +1289,30 @@ __global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
   }
   __syncthreads();
   if (a.abl & 4) return;
-  const int d1 = a.d + 1, cells = k * d1;
-  unsigned long long* out = a.run_sums + (size_t)(blockIdx.x % kRunSlices) * cells;
+  const int d1 = d + 1, cells = k * d1;
+  unsigned long long* out = a.run_sums + (size_t)slice * cells;
   for (int e = threadIdx.x; e < cells; e += blockDim.x) {
     const int j = e / d1, r = e - j * d1;
-    const long long v = r < a.d ? __double2ll_rn(tsum[r * TS + j] * a.fx) : (long long)tcnt[j];
+    const long long v = r < d ? __double2ll_rn(tsum[r * TS + j] * a.fx) : (long long)tcnt[j];
     if (v) atomicAdd(&out[e], (unsigned long long)v);
   }
 }
 
-// ---------------------------------------------------------------------------
+// One workgroup per FR screen waves (a.fr), after the screen (screen32d).
+template <int Q, int MT>
+__global__ __launch_bounds__(256, 3) void fixup32(FixArgs a) {
+  if (a.gate && a.gate[0] == 0) return;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kFixLdsBytes];
+  const FixLds L(lds);
+  const int FR = a.fr;
+  const int r0 = blockIdx.x * FR;
+  if (threadIdx.x < FR) {
+    const int r = r0 + threadIdx.x;
+    L.s_mv[threadIdx.x + 1] = r < a.regions ? a.mv_count[r] : 0;
+    L.s_fb[threadIdx.x + 1] = r < a.regions ? a.fb_count[r] : 0;
+  }
+  fixup_regions<Q, MT>(a, r0, FR, blockIdx.x % kRunSlices, L);
+}
 // Pruned DELTA screen: screen32p (d <= 16, k <= 64; configs 2 and 3).
 //
 // screen32h spends ~213 VALU per 64 points on the k-way screen (64 MFMA values
@@ -1277,6 +1370,8 @@ struct S32PArgs {
   int32_t* mv_count;
   int cap;
   long long* q_acc;  // profiling: points queued for the k-way screen, per wave (null: off)
+  FixArgs fx;        // the fused fixup (fixup32's arguments, fr = 4)
+  int fuse;
   int abl;  // timing experiments only (0 in the product build): 1 no drains,
             // 2 no per-point work (loads and the label byte only)
 };
@@ -1296,8 +1391,9 @@ __device__ __forceinline__ float mix_sub_hi(unsigned w, float c) {
 
 // QH: 2 for d = 9..16 (16 bytes per point half), 1 for d <= 8 (8 bytes);
 // MT: 32-centroid tiles of the k-way screen; PD: groups in flight per wave.
-template <int QH, int MT, int PD>
-__global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
+template <int Q, int MT, int PD>
+__global__ __launch_bounds__(256, 5) void screen32p(S32PArgs a) {
+  constexpr int QH = FixDims<Q>::QH;
   if (a.gate && a.gate[0] == 0) return;
   constexpr bool H1 = QH == 1;
   constexpr int kTile = H1 ? 512 : 1024;  // bytes per 32-point tile
@@ -1309,8 +1405,14 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   float* const eb = c32s + 64 * kPrStr;  // E_j
   float* const hc = eb + 64;             // h_j
   // per wave: a ring of 2 blocks x 64 queued points (2 tiles each, B layout)
-  __shared__ __attribute__((aligned(16))) unsigned char qd[4][2][2 * kTile];
-  __shared__ int2 qm[4][128];
+  // per wave: a ring of 2 blocks x 64 queued points (2 tiles each, B layout)
+  // and their {pt, old label}; after the last drain the same LDS holds the
+  // fused fixup's table (FixLds)
+  constexpr size_t kQBytes = 4 * 2 * 2 * kTile + 4 * 128 * sizeof(int2);
+  __shared__ __attribute__((aligned(16))) unsigned char qlds[kQBytes > kFixLdsBytes ? kQBytes : kFixLdsBytes];
+  typedef unsigned char QRow[2][2 * kTile];
+  QRow* qd = reinterpret_cast<QRow*>(qlds);
+  int2 (*qm)[128] = reinterpret_cast<int2 (*)[128]>(qlds + 4 * 2 * 2 * kTile);
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wv = t >> 6;
@@ -1337,32 +1439,32 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   // 3 (PD - 1) of them are outstanding: the later groups' loads (and any
   // stores issued after them) may stay in flight.  A group past the end
   // reloads the last one (every iteration issues exactly 3 loads).
-  auto load = [&](Buf& b, int64_t G) {
+  auto load = [&](Buf& b, int64_t G) __attribute__((always_inline)) {
     const int64_t Gc = G < ngroups ? G : ngroups - 1;
     const unsigned char* base = a.XS + (size_t)Gc * (2 * kTile);  // wave-uniform
     const uint8_t* lbase = a.lab8 + Gc * 64;
     if constexpr (H1) {
       asm volatile("global_load_dwordx2 %0, %1, %2\n\t"
                    "global_load_dwordx2 %3, %1, %2 offset:256"
-                   : "=&v"(b.h0), "+v"(loff), "+s"(base), "=&v"(b.h1)::"memory");
+                   : "=&v"(b.h0), "+v"(loff), "+s"(base), "=&v"(b.h1));
     } else {
       asm volatile("global_load_dwordx4 %0, %1, %2\n\t"
                    "global_load_dwordx4 %3, %1, %2 offset:512"
-                   : "=&v"(b.q0), "+v"(loff), "+s"(base), "=&v"(b.q1)::"memory");
+                   : "=&v"(b.q0), "+v"(loff), "+s"(base), "=&v"(b.q1));
     }
-    asm volatile("global_load_ubyte %0, %1, %2" : "=&v"(b.ob), "+v"(lane4), "+s"(lbase)::"memory");
+    asm volatile("global_load_ubyte %0, %1, %2" : "=&v"(b.ob), "+v"(lane4), "+s"(lbase));
   };
   // wait for buffer b, `later` groups having been issued after it
-  auto wait = [&](Buf& b, int later) {
+  auto wait = [&](Buf& b, int later) __attribute__((always_inline)) {
     if constexpr (H1) {
-      if (later >= 2) asm volatile("s_waitcnt vmcnt(6)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob)::"memory");
-      else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob)::"memory");
-      else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob)::"memory");
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(6)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob));
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob));
+      else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b.h0), "+v"(b.h1), "+v"(b.ob));
       b.w[0] = b.h0.x; b.w[1] = b.h0.y; b.w[2] = b.h1.x; b.w[3] = b.h1.y;
     } else {
-      if (later >= 2) asm volatile("s_waitcnt vmcnt(6)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob)::"memory");
-      else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob)::"memory");
-      else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob)::"memory");
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(6)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob));
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob));
+      else asm volatile("s_waitcnt vmcnt(0)" : "+v"(b.q0), "+v"(b.q1), "+v"(b.ob));
       b.w[0] = b.q0.x; b.w[1] = b.q0.y; b.w[2] = b.q0.z; b.w[3] = b.q0.w;
       b.w[4] = b.q1.x; b.w[5] = b.q1.y; b.w[6] = b.q1.z; b.w[7] = b.q1.w;
     }
@@ -1406,7 +1508,7 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   int2* mv_region = a.mv_list + (size_t)wave * a.cap;
   int fb_used = 0, mv_used = 0;
   // q = ||h - c32_j||^2: one fma_mix difference per feature, packed fp32 squares
-  auto dist2 = [&](const Buf& b, int j) -> float {
+  auto dist2 = [&](const Buf& b, int j) __attribute__((always_inline)) -> float {
     const f4* c4 = reinterpret_cast<const f4*>(c32s + j * kPrStr);  // 16-byte rows
     typedef float f2 __attribute__((ext_vector_type(2)));
     f2 acc = {0.0f, 0.0f};
@@ -1427,7 +1529,7 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   // The centroid tiles m are screened one after another (a loop that is not
   // unrolled, fragments and C operand read from LDS inside it), so only one
   // tile's accumulators are ever live: 4 waves per SIMD instead of 3.
-  auto tile = [&](const u4v& v, unsigned& bk, unsigned& sk, float& hp) {
+  auto tile = [&](const u4v& v, unsigned& bk, unsigned& sk, float& hp) __attribute__((always_inline)) {
     const h8 BH = __builtin_bit_cast(h8, v);
     hp = 0.0f;  // this lane's part of ||h||^2 (fp16 products are exact in fp32)
 #pragma unroll
@@ -1467,7 +1569,7 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
     sk = s | ((unsigned)h << 2);
   };
   // the k-way screen of queue block qb (nvalid entries), then its lists
-  auto drain = [&](int qb, int nvalid) {
+  auto drain = [&](int qb, int nvalid) __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's queue writes
     const unsigned char* src = qd[wv][qb];
     u4v v[2];
@@ -1523,24 +1625,24 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
       a.labels[pt] = label;
       a.lab8[pt] = (uint8_t)label;
     }
+    // both lists in straight-line code (two identical guarded blocks were
+    // merged by the optimiser into one updating fb_used / mv_used through a
+    // pointer, which put both counters in scratch memory)
+    const bool unc = valid && !cert;
     const unsigned long long mv = __ballot(moved);
-    if (mv) {
-      const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(mv >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((unsigned)mv, 0u));
-      if (moved) mv_region[mv_used + r] = int2{pt, ob | (label << 16)};
-      mv_used += __popcll(mv);
-    }
-    const unsigned long long need = __ballot(valid && !cert);
-    if (need) {
-      const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
-      if (valid && !cert) fb_region[fb_used + r] = int2{pt, ob};
-      fb_used += __popcll(need);
-    }
+    const unsigned long long need = __ballot(unc);
+    const int rm = __builtin_amdgcn_mbcnt_hi((unsigned)(mv >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((unsigned)mv, 0u));
+    const int rn = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+    if (moved) mv_region[mv_used + rm] = int2{pt, ob | (label << 16)};
+    if (unc) fb_region[fb_used + rn] = int2{pt, ob};
+    mv_used += __popcll(mv);
+    fb_used += __popcll(need);
   };
   int qh = 0, qn = 0;  // queue head (next slot, mod 128) and length: wave-uniform
   int qtot = 0;        // points this wave queued (profiling)
-  auto process = [&](const Buf& b, int64_t G) {
+  auto process = [&](const Buf& b, int64_t G) __attribute__((always_inline)) {
     const int64_t base = G << 6;
     if (base >= a.n) return;  // wave-uniform: padding groups have no real points
     const int64_t pt = base + lane;
@@ -1595,14 +1697,24 @@ __global__ __launch_bounds__(256) void screen32p(S32PArgs a) {
   if (qn > 0) {  // the partial block (queue tail at a block start: 64 | qh - qn)
     drain(((qh - qn) & 127) >> 6, qn);
   }
-  // per-wave counts only: fixup32 adds the step's fallback total (one atomic
-  // per fixup workgroup); thousands of same-address atomics at the end of
-  // this kernel serialised in L2 for tens of microseconds
+  // per-wave counts only (their sum is the step's fallback total, formed by
+  // the finalize): thousands of same-address atomics at the end of this
+  // kernel serialised in L2 for tens of microseconds
   if (lane == 0) {
     a.fb_count[wave] = fb_used;
     a.mv_count[wave] = mv_used;
     if (a.q_acc) a.q_acc[wave] += qtot;  // (profiling) this wave's own slot
   }
+  if (!a.fuse) return;
+  // ---- fixup32's work for this workgroup's four waves, fused: no extra
+  // launch, and the tail of one workgroup overlaps the others' streaming ----
+  __syncthreads();  // every queue drained (its LDS becomes the table); lists written
+  const FixLds L(qlds);
+  if (lane == 0) {
+    L.s_mv[wv + 1] = mv_used;
+    L.s_fb[wv + 1] = fb_used;
+  }
+  fixup_regions<Q, MT>(a.fx, blockIdx.x * 4, 4, blockIdx.x % kRunSlices, L, FixPlan{sA, sC});
 }
 // ---------------------------------------------------------------------------
 // host side
@@ -1844,16 +1956,17 @@ static int s32d_blocks_per_cu() {
   return nb;
 }
 
-#define CDR_S32P_ALL(X) X(1, 1, 2) X(1, 1, 3) X(1, 2, 2) X(1, 2, 3) \
-                        X(2, 1, 2) X(2, 1, 3) X(2, 2, 2) X(2, 2, 3)
+#define CDR_S32P_ALL(X) X(1, 1, 3) X(1, 2, 3) X(2, 1, 3) X(2, 2, 3) \
+                        X(3, 1, 3) X(3, 2, 3) X(4, 1, 3) X(4, 2, 3)
 
-static int screen32p_blocks_per_cu(int QH, int MT, int PD) {
-  static int cache[2][2][2] = {};
-  int& nb = cache[QH - 1][MT - 1][PD - 2];
+// (Q: feature quads; PD: 3 groups in flight)
+static int screen32p_blocks_per_cu(int Q, int MT, int PD) {
+  static int cache[4][2] = {};
+  int& nb = cache[Q - 1][MT - 1];
   if (!nb) {
     hipError_t e = hipErrorInvalidValue;
 #define CDR_S32P_OCC(Q_, M_, P_) \
-    if (QH == Q_ && MT == M_ && PD == P_) \
+    if (Q == Q_ && MT == M_ && PD == P_) \
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32p<Q_, M_, P_>, 256, 0);
     CDR_S32P_ALL(CDR_S32P_OCC)
 #undef CDR_S32P_OCC
@@ -1863,10 +1976,10 @@ static int screen32p_blocks_per_cu(int QH, int MT, int PD) {
   return nb;
 }
 
-static void screen32p_launch(int QH, int MT, int PD, dim3 grid, hipStream_t s,
+static void screen32p_launch(int Q, int MT, int PD, dim3 grid, hipStream_t s,
                              const S32PArgs& p) {
 #define CDR_S32P_GO(Q_, M_, P_) \
-  if (QH == Q_ && MT == M_ && PD == P_) \
+  if (Q == Q_ && MT == M_ && PD == P_) \
     hipLaunchKernelGGL((screen32p<Q_, M_, P_>), grid, dim3(256), 0, s, p);
   CDR_S32P_ALL(CDR_S32P_GO)
 #undef CDR_S32P_GO
@@ -1895,16 +2008,18 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   ensure_split(c, HO ? (QH == 2 ? 3 : 4) : QH);
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
-  // pruned screen (screen32p) on the hi-only copy: CDR_PRUNE=0 turns it off,
-  // CDR_PRUNE_PD (2..3) groups in flight
+  // pruned screen (screen32p) on the hi-only copy: CDR_PRUNE=0 turns it off
   static const bool pr_env = !std::getenv("CDR_PRUNE") || std::atoi(std::getenv("CDR_PRUNE"));
-  static const int pr_pd = std::getenv("CDR_PRUNE_PD") ? std::atoi(std::getenv("CDR_PRUNE_PD")) : 3;
   const bool PR = pr_env && HO && c.prune_on;
-  const int PPD = pr_pd == 2 ? 2 : 3;
+  const int PPD = 3;
+  const int PQ = d4_of(c.d) / 4;
+  // the fixup fused into screen32p's tail (CDR_PRUNE_FUSE=0: a separate fixup32)
+  static const bool fuse_env =
+      !std::getenv("CDR_PRUNE_FUSE") || std::atoi(std::getenv("CDR_PRUNE_FUSE"));
   int bpc;
   const int PD = PR ? PPD : LRn ? LRn : s32d_depth(QH);
   if (PR) {
-    bpc = screen32p_blocks_per_cu(QH, MT, PPD);
+    bpc = screen32p_blocks_per_cu(PQ, MT, PPD);
     static const int bpc_env = std::getenv("CDR_S32P_BPC") ? std::atoi(std::getenv("CDR_S32P_BPC")) : 0;
     if (bpc_env >= 1 && bpc_env < bpc) bpc = bpc_env;
   } else if (LRn) {
@@ -1974,7 +2089,38 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   a.mv_list = c.mv_list.as<int2>();
   a.mv_count = c.mv_count.as<int32_t>();
   a.cap = cap;
+  FixArgs f;
+  f.XA = c.xa32.as<float>();
+  f.n_pad = c.n_pad;
+  f.cent = dcent;
+  f.k = k;
+  f.d = c.d;
+  f.labels = c.labels.as<int32_t>();
+  f.lab8 = c.lab8.as<uint8_t>();
+  f.fb_list = c.fb_list.as<int2>();
+  f.fb_count = c.fb_count.as<int32_t>();
+  f.mv_list = c.mv_list.as<int2>();
+  f.mv_count = c.mv_count.as<int32_t>();
+  f.cap = cap;
+  f.regions = nwaves;
+  f.fx = std::ldexp(1.0, c.scale_bits);
+  f.run_sums = c.run_sums.as<unsigned long long>();
+  f.gate = gate;
+  f.abl = 0;
+  f.XS = c.xs16.as<unsigned char>();
+  f.frag = dfrag;
+  f.cinit = dcinit;
+  f.thr0 = thr0;
+  f.thr_rel = thr_rel;
+  f.thr_dev = dthr;
+  f.ho = HO;
+  f.ms = c.mu_s.as<float>();
+  f.sig = (float)std::ldexp(1.0, c.sigma);
+#ifdef CDR_EXPERIMENTS
+  if (const char* e = std::getenv("CDR_FIX_ABL")) f.abl = std::atoi(e);
+#endif
   const dim3 grid(nwg), blk(256);
+  const bool fused = PR && fuse_env;
   if (PR) {
     S32PArgs p;
     p.XS = a.XS;
@@ -2007,9 +2153,13 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
 #ifdef CDR_EXPERIMENTS
     if (const char* e = std::getenv("CDR_S32P_ABL")) p.abl = std::atoi(e);
 #endif
-    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32p<%d,%d,%d>", QH, MT, PPD);
+    p.fx = f;
+    p.fx.fr = 4;
+    p.fuse = fused ? 1 : 0;
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32p<%d,%d,%d>%s", PQ, MT, PPD,
+             fused ? "+fixup" : "");
     if (prof) prof_mark(c, 0);
-    screen32p_launch(QH, MT, PPD, grid, c.stream, p);
+    screen32p_launch(PQ, MT, PPD, grid, c.stream, p);
   } else {
   if (LRn)
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>lds", MT, PD);
@@ -2041,51 +2191,18 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   }
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
-  FixArgs f;
-  f.XA = c.xa32.as<float>();
-  f.n_pad = c.n_pad;
-  f.cent = dcent;
-  f.k = k;
-  f.d = c.d;
-  f.labels = c.labels.as<int32_t>();
-  f.lab8 = c.lab8.as<uint8_t>();
-  f.fb_list = c.fb_list.as<int2>();
-  f.fb_count = c.fb_count.as<int32_t>();
-  f.mv_list = c.mv_list.as<int2>();
-  f.mv_count = c.mv_count.as<int32_t>();
-  f.cap = cap;
-  f.regions = nwaves;
-  f.fx = std::ldexp(1.0, c.scale_bits);
-  f.run_sums = c.run_sums.as<unsigned long long>();
-  f.gate = gate;
-  f.fb_total = c.fb_count.as<int32_t>() + nwaves;
-  f.abl = 0;
-  f.XS = c.xs16.as<unsigned char>();
-  f.frag = dfrag;
-  f.cinit = dcinit;
-  f.thr0 = thr0;
-  f.thr_rel = thr_rel;
-  f.thr_dev = dthr;
-  f.ho = HO;
-  f.ms = c.mu_s.as<float>();
-  f.sig = (float)std::ldexp(1.0, c.sigma);
-#ifdef CDR_EXPERIMENTS
-  if (const char* e = std::getenv("CDR_FIX_ABL")) f.abl = std::atoi(e);
-#endif
   // list regions per fixup workgroup: CDR_FIX_FR (1..16); A/B at config 3 (100M and
   // the 12.5M shard): 8 leaves 79-82 / 34 us beside the screen, 4 91-93 / 42, 16 106 / 39
   static const int fr_env = std::getenv("CDR_FIX_FR") ? std::atoi(std::getenv("CDR_FIX_FR")) : 8;
   f.fr = fr_env >= 1 && fr_env <= kFixMaxR ? fr_env : 8;
   const dim3 fgrid((nwaves + f.fr - 1) / f.fr);
-  switch (c.d) {
-#define CDR_FIX(D_)                                                                  \
-  case D_:                                                                           \
-    if (MT == 1) hipLaunchKernelGGL((fixup32<D_, 1>), fgrid, blk, 0, c.stream, f);    \
-    else hipLaunchKernelGGL((fixup32<D_, 2>), fgrid, blk, 0, c.stream, f);            \
+  if (!fused) switch (d4_of(c.d) / 4) {
+#define CDR_FIX(Q_)                                                                  \
+  case Q_:                                                                           \
+    if (MT == 1) hipLaunchKernelGGL((fixup32<Q_, 1>), fgrid, blk, 0, c.stream, f);    \
+    else hipLaunchKernelGGL((fixup32<Q_, 2>), fgrid, blk, 0, c.stream, f);            \
     break;
-    CDR_FIX(1) CDR_FIX(2) CDR_FIX(3) CDR_FIX(4) CDR_FIX(5) CDR_FIX(6) CDR_FIX(7) CDR_FIX(8)
-    CDR_FIX(9) CDR_FIX(10) CDR_FIX(11) CDR_FIX(12) CDR_FIX(13) CDR_FIX(14) CDR_FIX(15)
-    CDR_FIX(16)
+    CDR_FIX(1) CDR_FIX(2) CDR_FIX(3) CDR_FIX(4)
 #undef CDR_FIX
     default: CDR_FAIL(CDR_ERR_STATE, "screen32d: d > 16");
   }
