@@ -218,8 +218,37 @@ def pipeline_case():
     np.savez_compressed(os.path.join(pdir, "main_kmeans.npz"), centroids=C, labels=labels)
 
 
+def float32_cases():
+    """The reference on float32 X: its centroids have X's
+    dtype (kmeans_plusplus.py:6, :37), so seeding distances, probabilities and
+    means are computed in float32.  The same data as float64 for contrast.
+    tests/test_float32_input.py pins the drop-in's float32 semantics (fp64
+    distances, exact means rounded to float32) against these runs: seeds and
+    labels equal, centroids within the north_star's 1e-5 relative."""
+    ref = load_ref("kmeans_plusplus")
+    out = {}
+    for i, (n, d, k, seed, rs) in enumerate([(3000, 5, 4, 11, 42), (4000, 8, 16, 12, 7),
+                                              (2500, 16, 8, 13, 3)]):
+        X = synth.generate(n, 0, n, d, k, seed).astype(np.float32)
+        for tag, Xc in (("f32", X), ("f64", X.astype(np.float64))):
+            np.random.seed(i)
+            init = ref.kmeans_plusplus_init(Xc, k, random_state=rs)
+            np.random.seed(i)
+            C, labels = ref.kmeans(Xc, k, number_of_files=n, random_state=rs)
+            out[f"c{i}_{tag}_init"] = init
+            out[f"c{i}_{tag}_centroids"] = C
+            out[f"c{i}_{tag}_labels"] = labels
+        out[f"c{i}_X"] = X
+        out[f"c{i}_meta"] = np.array([n, d, k, seed, rs, i], dtype=np.int64)
+    np.savez_compressed(os.path.join(GOLD, "kmeans_f32_cases.npz"), **out)
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
+    if "--only-f32" in sys.argv:
+        float32_cases()
+        return
+    float32_cases()
     cases, terr = kmeans_cases()
     save_kmeans(cases, terr)
     scoring_cases()
