@@ -65,6 +65,10 @@ SIGNATURES = {
     "cdr_seed_block_sums": ([_P, _P], None),
     "cdr_seed_scan": ([_P, _F64, _F64, _PF64], None),
     "cdr_seed_search": ([_P, _F64, _F64, _PI64], None),
+    "cdr_seed_scan_begin": ([_P, _F64, _F64, _PI64, _PI64], None),
+    "cdr_seed_scan_items": ([_P, _P, _I64, _PI64], None),
+    "cdr_seed_scan_end": ([_P, _F64, _PF64], None),
+    "cdr_seed_program_eval": ([_P, _I64, _F64, _PF64, _PI32], None),
     "cdr_lloyd_step": ([_P, _P, _I32, _P, _I32], None),
     "cdr_lloyd_step_f64": ([_P, _P, _I32, _P, _P], None),
     "cdr_lloyd_labels": ([_P, _P], None),
@@ -200,6 +204,22 @@ def comm_unique_id() -> bytes:
     return out.tobytes()
 
 
+# cdr_seed_item (include/cdr.h): one item of a shard's cumsum program
+SEED_ITEM = np.dtype([("d0", "<i8"), ("d1", "<i8"), ("p", "<f8"), ("e", "<i4"),
+                      ("kind", "<i4")])
+SEED_RUN, SEED_CROSS, SEED_CONST, SEED_FINE, SEED_MARK, SEED_END, SEED_SKIP, SEED_BAD = range(8)
+
+
+def seed_program_eval(items: np.ndarray, c_in: float) -> tuple[float, bool]:
+    """Runs a cumsum program (cdr_seed_program_eval, host only): the running
+    value after the shard from c_in, and whether every item held."""
+    items = np.ascontiguousarray(items, dtype=SEED_ITEM)
+    c, ok = _F64(), _I32()
+    _check(load_library().cdr_seed_program_eval(_ptr(items), items.size, float(c_in),
+                                                ctypes.byref(c), ctypes.byref(ok)))
+    return float(c.value), bool(ok.value)
+
+
 def host_seq_sum(v: np.ndarray, init: float = 0.0) -> float:
     """((init + v[0]) + v[1]) + ... in fp64 (plain C on the host)."""
     v = np.ascontiguousarray(v, dtype=np.float64)
@@ -294,6 +314,28 @@ class Context:
     def seed_scan(self, total: float, c_in: float = 0.0) -> float:
         v = _F64()
         _check(self._lib.cdr_seed_scan(self._h, float(total), float(c_in), ctypes.byref(v)))
+        return float(v.value)
+
+    def seed_scan_begin(self, total: float, c_guess: float) -> tuple[int, int]:
+        """Builds this shard's cumsum program under a guess of its starting
+        running value; returns (items, FINE items), items -1 when it did
+        not fit (cdr_seed_scan_begin)."""
+        ni, nf = _I64(), _I64()
+        _check(self._lib.cdr_seed_scan_begin(self._h, float(total), float(c_guess),
+                                             ctypes.byref(ni), ctypes.byref(nf)))
+        return int(ni.value), int(nf.value)
+
+    def seed_scan_items(self, n_items: int) -> np.ndarray:
+        out = np.zeros(max(int(n_items), 0), dtype=SEED_ITEM)
+        got = _I64()
+        _check(self._lib.cdr_seed_scan_items(self._h, _ptr(out) if out.size else None, out.size,
+                                             ctypes.byref(got)))
+        return out[: got.value]
+
+    def seed_scan_end(self, c_in: float) -> float:
+        """The exact scan from c_in with the program of seed_scan_begin."""
+        v = _F64()
+        _check(self._lib.cdr_seed_scan_end(self._h, float(c_in), ctypes.byref(v)))
         return float(v.value)
 
     def seed_search(self, c_last: float, u: float) -> int:

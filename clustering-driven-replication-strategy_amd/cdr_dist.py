@@ -245,6 +245,78 @@ def _owner_of(offsets: np.ndarray, gidx: int) -> int:
     return int(np.searchsorted(offsets, gidx, side="right") - 1)
 
 
+SEED_PROGRAM_CAP = 4096  # items per rank in the all-gathered cumsum programs
+
+
+def _program_record(prog) -> np.ndarray:
+    """A rank's program padded to SEED_PROGRAM_CAP items, as int64 words for
+    the all-gather: item 0 holds the count in d0 (-1: no usable program)."""
+    from _cdr import SEED_ITEM
+
+    rec = np.zeros(SEED_PROGRAM_CAP + 1, dtype=SEED_ITEM)
+    if prog is None or prog.size > SEED_PROGRAM_CAP:
+        rec[0]["d0"] = -1
+    else:
+        rec[0]["d0"] = prog.size
+        rec[1:1 + prog.size] = prog
+    return rec.view(np.int64)
+
+
+def shard_scan(ctx, comm: Comm, parts, total: float):
+    """np.cumsum(dist_sq / total) over the sharded rows (kmeans_plusplus.py:19):
+    returns the running value after the last shard (c_last); afterwards every
+    rank's ctx can answer seed_search.
+
+    Every rank builds its shard's cumsum program in parallel from a guess of
+    the running value at its first row (the earlier shards' block sums /
+    total; include/cdr.h cdr_seed_scan_begin).  The first rank's start is
+    exactly 0, so it scans outright and publishes a constant.  The programs
+    are all-gathered and every rank composes them in rank order on the host
+    (cdr_seed_program_eval), which gives each rank its exact start; a guess
+    that does not hold for the exact start is detected there, and then the
+    rank-ordered chain of exact scans runs instead (same result)."""
+    world, rank = comm.world, comm.rank
+    if world == 1:
+        return ctx.seed_scan(total, 0.0)
+    if hasattr(ctx, "seed_scan_begin"):
+        from _cdr import SEED_CONST, SEED_ITEM, seed_program_eval
+
+        if rank == 0:
+            prog = np.zeros(1, dtype=SEED_ITEM)
+            prog[0]["kind"] = SEED_CONST
+            prog[0]["p"] = ctx.seed_scan(total, 0.0)
+        else:
+            before = sum(int(p.size) for p in parts[:rank])
+            guess = float(np.sum(np.concatenate(parts)[:before])) / total
+            ni, nf = ctx.seed_scan_begin(total, guess)
+            prog = ctx.seed_scan_items(ni) if 0 <= ni <= SEED_PROGRAM_CAP and nf == 0 else None
+        recs = comm.allgather(_program_record(prog))
+        c, c_mine, ok = 0.0, 0.0, True
+        for r, words in enumerate(recs):
+            rec = np.ascontiguousarray(words, dtype=np.int64).view(SEED_ITEM)
+            cnt = int(rec[0]["d0"])
+            if cnt < 0:
+                ok = False
+                break
+            if r == rank:
+                c_mine = c
+            c, good = seed_program_eval(rec[1:1 + cnt], c)
+            if not good:
+                ok = False
+                break
+        if ok:
+            if rank > 0:
+                mine = ctx.seed_scan_end(c_mine)
+                if mine != seed_program_eval(prog, c_mine)[0]:
+                    raise RuntimeError("seed program and shard scan disagree")
+            return c
+    c = 0.0
+    for r in range(world):  # rank-ordered chain of exact scans
+        mine = ctx.seed_scan(total, c) if rank == r else 0.0
+        c = float(comm.bcast(np.array([mine], dtype=np.float64), r)[0])
+    return c
+
+
 def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_state=None,
                  host_seq_sum=None) -> np.ndarray:
     """kmeans_plusplus_init over the sharded rows (float64 centroids)."""
@@ -262,14 +334,11 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
         ctx.seed_reset()
     for i in range(1, k):
         ctx.seed_update(C[i - 1])
-        blocks = np.concatenate(comm.allgather(ctx.seed_block_sums()))
-        total = host_seq_sum(blocks)
+        parts = comm.allgather(ctx.seed_block_sums())
+        total = host_seq_sum(np.concatenate(parts))
         if not (total > 0.0) or total == np.inf:
             raise ValueError("Probabilities contain NaN")
-        c = 0.0
-        for r in range(comm.world):  # rank-ordered chain of exact scans
-            mine = ctx.seed_scan(total, c) if comm.rank == r else 0.0
-            c = float(comm.bcast(np.array([mine], dtype=np.float64), r)[0])
+        c = shard_scan(ctx, comm, parts, total)
         u = rng.random()
         hits = np.concatenate(comm.allgather(np.array([ctx.seed_search(c, u)], dtype=np.int64)))
         owner = int(np.flatnonzero(hits >= 0)[0])

@@ -227,6 +227,13 @@ struct Ctx {
   DevBuf blocksums;   // double[nblocks]
   DevBuf xfer;        // per-block transfer records
   DevBuf cend;        // double[nblocks] running value after each block
+  DevBuf seg_tails, seg_ents, seg_scan, seg_items, seg_meta;  // cumsum program (seed.hip)
+  double seed_prog_total = 0.0;
+  bool seed_prog_ready = false;
+  long long seed_fallbacks = 0;  // programs whose guess failed (block walk instead)
+  DevBuf seed_tail_plan;  // pairwise layout of the partial last block (seed.hip)
+  int64_t seed_tail_m = -1;
+  int seed_tail_nleaves = 0, seed_tail_npost = 0;
   DevBuf seed_scalar; // small device scratch
   double seed_c_in = 0.0;
   bool seed_scanned = false;
@@ -281,6 +288,9 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums,
 void seed_reset(Ctx& c);
 void seed_update(Ctx& c, const double* cent);
 void seed_scan(Ctx& c, double total, double c_in, double* c_out);
+void seed_scan_begin(Ctx& c, double total, double c_guess, int64_t* n_items, int64_t* n_fine);
+void seed_scan_items(Ctx& c, cdr_seed_item* out, int64_t cap, int64_t* n_items);
+void seed_scan_end(Ctx& c, double c_in, double* c_out);
 void seed_search(Ctx& c, double c_last, double u, int64_t* idx);
 
 void medians_segmented(Ctx& c, const double* values, const int64_t* offsets,

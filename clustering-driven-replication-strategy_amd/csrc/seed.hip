@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "cdr_internal.h"
 #include "exact_math.h"
@@ -95,15 +96,16 @@ __device__ double pw_tree(int64_t n, LF leaf) {
 // two halves of 4096 (pw(8192) = pw(4096) + pw(4096)); each half's values sit
 // in LDS (one pad slot per 16).
 //
-// Full blocks (TAIL = false): the 32 pairwise leaves of 128 of a half are
+// Full blocks: the 32 pairwise leaves of 128 of a half are
 // summed by 8 threads each — thread (leaf L, j) adds NumPy's accumulator r_j
 // = a(j) + a(j + 8) + ... sequentially, shfl_xor 1, 2, 4 forms
 // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), shfl_xor 8, 16, 32 and
 // then a 4-wave LDS step combine the leaves in the balanced tree of
 // pw(4096).
-// TAIL = true: the one partial block (m < 8192) at b_off; its pairwise tree
-// is enumerated by one thread (a stack: scratch memory, kept out of the
-// full-block kernel).
+// The one partial block (m < 8192) is the grid's last workgroup: it updates
+// its dmin values with the others and leaves its pairwise sum to
+// seed_tail_sum_kernel (a stack walk of the tree: scratch memory, kept out
+// of this kernel).
 // D > 0 (float points, d == D <= 16): each thread takes 4 points per
 // iteration with all their 16-byte feature-quad loads and dmin loads issued
 // before any arithmetic, and the NumPy-order distance unrolled for that d.
@@ -133,33 +135,39 @@ __global__ void seed_ccd_kernel(const double* __restrict__ cents, int count, int
   }
 }
 
-template <typename T, int D, bool TAIL>
+template <typename T, int D>
 __global__ __launch_bounds__(256) void seed_update_kernel(
     const T* __restrict__ X, int64_t n, int64_t n_pad, int d, const double* __restrict__ cen,
-    double* __restrict__ dmin, double* __restrict__ blocksums, int64_t b_off,
-    int32_t* __restrict__ near, const double* __restrict__ ccd, int cidx) {
+    double* __restrict__ dmin, double* __restrict__ blocksums, int32_t* __restrict__ near,
+    const double* __restrict__ ccd, int cidx) {
   constexpr int kHalf = 4096;
   __shared__ double sdm[kHalf + kHalf / 16];
   __shared__ double swave[4];
-  const int64_t b = blockIdx.x + b_off;
+  const int64_t b = blockIdx.x;
   const int64_t base = b * kSeedBlock;
-  const int m = TAIL ? (int)(n - base) : kSeedBlock;
+  const int m = (n - base) < kSeedBlock ? (int)(n - base) : kSeedBlock;
+  const bool TAIL = m < kSeedBlock;  // workgroup-uniform: the partial last block
   auto spos = [](int q) { return q + (q >> 4); };
   double halves[2] = {0.0, 0.0};
   for (int h = 0; h < 2; ++h) {
     if constexpr (D > 0) {
       constexpr int Q = (D + 3) / 4;
+      // points per thread and iteration: all their loads issue before any
+      // arithmetic (fewer for wide rows: registers)
+      constexpr int U = D <= 16 ? 4 : (D <= 32 ? 2 : 1);
+      // the centre in registers for narrow rows, else uniform (scalar) loads
+      constexpr int CR = D <= 16 ? D : 1;
       typedef float f4v __attribute__((ext_vector_type(4)));
       const f4v* X4 = reinterpret_cast<const f4v*>(X);
-      double cr[D];
+      double cr[CR];
 #pragma unroll
-      for (int f = 0; f < D; ++f) cr[f] = cen[f];
-      for (int q0 = threadIdx.x; q0 < kHalf; q0 += 4 * 256) {
-        f4v xv[4][Q];
-        double old[4];
-        bool go[4];
+      for (int f = 0; f < CR; ++f) cr[f] = cen[f];
+      for (int q0 = threadIdx.x; q0 < kHalf; q0 += U * 256) {
+        f4v xv[U][Q];
+        double old[U];
+        bool go[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int qi = h * kHalf + q0 + 256 * u;
           const int64_t i = base + qi;
           go[u] = false;
@@ -169,7 +177,7 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int64_t i = base + h * kHalf + q0 + 256 * u;
           if (go[u]) {
 #pragma unroll
@@ -177,7 +185,7 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int q = q0 + 256 * u;
           const int qi = h * kHalf + q;
           double v = 0.0;
@@ -185,7 +193,7 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
             v = old[u];
             if (go[u]) {
               auto xf = [&](int f) { return (double)xv[u][f >> 2][f & 3]; };
-              auto cf = [&](int f) { return cr[f]; };
+              auto cf = [&](int f) { return D <= 16 ? cr[f < CR ? f : 0] : cen[f]; };
               const double R = np_sqdist(xf, cf, D);
               const double r = sqrt(R);
               const double t = r * r;
@@ -224,7 +232,7 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
       }
     }
     __syncthreads();
-    if constexpr (!TAIL) {
+    if (!TAIL) {
       const int t = threadIdx.x;
       const int L = t >> 3, j = t & 7;
       double r = sdm[spos(128 * L + j)];
@@ -238,37 +246,43 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
       __syncthreads();
     }
   }
-  if constexpr (!TAIL) {
-    if (threadIdx.x == 0) blocksums[b] = halves[0] + halves[1];
-  } else {
-    __shared__ double sleaf[160];
-    __shared__ int soff[160], slen[160];
-    __shared__ int sleaves;
-    // partial (last) block: enumerate the pairwise leaves, sum them in
-    // parallel from global memory, combine in tree order.
-    __threadfence_block();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int cnt = 0;
-      pw_tree((int64_t)m, [&](int64_t off, int len) {
-        soff[cnt] = (int)off;
-        slen[cnt] = len;
-        ++cnt;
-        return 0.0;
-      });
-      sleaves = cnt;  // <= 128 leaves of (64, 128] elements for m < 8192
+  if (!TAIL && threadIdx.x == 0) blocksums[b] = halves[0] + halves[1];
+}
+
+// The partial last block's pairwise sum (m < 8192 elements at base): its
+// pairwise tree depends on m alone, so the host lays it out once
+// (seed_tail_plan: the leaves' (offset, length) pairs, then the tree in
+// postfix, 1 = next leaf, 0 = add the top two); the leaves are summed in
+// parallel from global memory and one thread combines them from LDS.  Its
+// dmin values come from the seed_update_kernel launch before it (the block
+// is that grid's last workgroup, updated with the other blocks).
+constexpr int kTailLeaves = 160;
+__global__ __launch_bounds__(256) void seed_tail_sum_kernel(const double* __restrict__ dmin,
+                                                            int64_t b,
+                                                            const int* __restrict__ plan,
+                                                            int nleaves, int npost,
+                                                            double* __restrict__ blocksums) {
+  __shared__ double sleaf[kTailLeaves];
+  __shared__ double sst[32];
+  const int64_t base = b * kSeedBlock;
+  const int t = threadIdx.x;
+  if (t < nleaves) {
+    const int off = plan[2 * t], len = plan[2 * t + 1];
+    sleaf[t] = np_pw_leaf([&](int i) { return dmin[base + off + i]; }, len);
+  }
+  __syncthreads();
+  if (t == 0) {
+    const int* post = plan + 2 * nleaves;
+    int sp = 0, li = 0;
+    for (int i = 0; i < npost; ++i) {
+      if (post[i]) {
+        sst[sp++] = sleaf[li++];
+      } else {
+        --sp;
+        sst[sp - 1] = sst[sp - 1] + sst[sp];
+      }
     }
-    __syncthreads();
-    const int cnt = sleaves;
-    if (threadIdx.x < cnt) {
-      const int off = soff[threadIdx.x], len = slen[threadIdx.x];
-      sleaf[threadIdx.x] = np_pw_leaf([&](int i) { return dmin[base + off + i]; }, len);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int cur = 0;
-      blocksums[b] = pw_tree((int64_t)m, [&](int64_t, int) { return sleaf[cur++]; });
-    }
+    blocksums[b] = sst[0];
   }
 }
 
@@ -710,6 +724,506 @@ __global__ __launch_bounds__(64) void search_kernel(const double* __restrict__ d
   if (lane == 0) *result = found;
 }
 
+// ---- cumulative-sum programs ----------------------------------------------
+//
+// The exact running value through the shard in three parallel passes and one
+// short sequential one, instead of walk_kernel's block-by-block walk (which
+// also stays, as the fallback):
+//  seg_block_kernel  per block: the binade of every element's running value
+//                    is guessed from an approximate prefix (approx[b] plus
+//                    in-block sums).  An element whose guessed value stays in
+//                    one binade joins the current run (a transfer, as above);
+//                    one whose guessed value changes binade is a crossing,
+//                    added exactly at evaluation.  The block becomes
+//                    run x run x ... run (at most kKC crossings; more, or a
+//                    guess that breaks a run, make it opaque: walked element
+//                    by element at evaluation).
+//  seg_plan_kernel   a segmented scan of the block tails over the blocks
+//                    (segments start at blocks with crossings) and the
+//                    shard's program: RUN / CROSS / FINE / MARK items, a few
+//                    per crossing (~log2(c_last / c_first) of them).
+//  seg_eval_kernel   one wave runs the program from the exact c_in.  A RUN
+//                    applies when the running value is in its binade and
+//                    stays there (N + D < 2^53), the transfer test above; a
+//                    failed test is a wrong guess and the scan falls back to
+//                    walk_kernel.
+//  seg_fill_kernel   cend[b] from the value at the block's segment head and
+//                    the scanned transfer.
+// A program without FINE items is the shard's exact function c_in -> c_out:
+// sharded seeding all-gathers the programs and every rank composes them
+// (cdr_seed_program_eval) instead of a rank-ordered chain of scans.
+
+struct Part {
+  long long d0, d1;
+  int e;   // binade exponent (kNoE when empty)
+  int st;  // 0 empty (identity), 1 transfer, 2 broken (the guess cannot hold)
+};
+constexpr int kNoE = -100000;
+constexpr long long kD52 = 1ll << 52;
+
+// cdr_seed_item (include/cdr.h)
+struct SeedItem {
+  long long d0, d1;
+  double p;
+  int e;
+  int kind;
+};
+static_assert(sizeof(SeedItem) == sizeof(cdr_seed_item), "cdr_seed_item layout");
+enum : int {
+  kItRun = CDR_SEED_RUN,
+  kItCross = CDR_SEED_CROSS,
+  kItConst = CDR_SEED_CONST,
+  kItFine = CDR_SEED_FINE,
+  kItMark = CDR_SEED_MARK,
+  kItEnd = CDR_SEED_END,
+  kItSkip = CDR_SEED_SKIP,
+  kItBad = CDR_SEED_BAD
+};
+
+__host__ __device__ __forceinline__ Part part_empty() { return Part{0, 0, kNoE, 0}; }
+
+// L then R
+__host__ __device__ __forceinline__ Part part_compose(const Part& L, const Part& R) {
+  if (L.st == 0) return R;
+  if (R.st == 0) return L;
+  if (L.st != 1 || R.st != 1 || L.e != R.e) return Part{0, 0, L.e, 2};
+  Part o{L.d0 + ((L.d0 & 1) ? R.d1 : R.d0), L.d1 + ((L.d1 & 1) ? R.d0 : R.d1), L.e, 1};
+  if (o.d0 >= kD52 || o.d1 >= kD52) o.st = 2;
+  return o;
+}
+
+__host__ __device__ __forceinline__ bool sp_binade(double c, int& e, long long& N) {
+  const unsigned long long bits = __builtin_bit_cast(unsigned long long, c);
+  const int ef = (int)((bits >> 52) & 0x7FF);
+  if (ef == 0 || ef >= 2046 || (bits >> 63)) return false;
+  e = ef - 1023;
+  N = (long long)((bits & 0xFFFFFFFFFFFFFull) | (1ull << 52));
+  return true;
+}
+__host__ __device__ __forceinline__ double sp_value(int e, long long N) {
+  const unsigned long long bits =
+      ((unsigned long long)(e + 1023) << 52) | ((unsigned long long)N & 0xFFFFFFFFFFFFFull);
+  return __builtin_bit_cast(double, bits);
+}
+
+// One RUN / SKIP / BAD / CROSS / CONST item applied to the running value c
+// (MARK and END leave it; FINE cannot be applied here).  False: the item does
+// not hold for this c (the guessed binade was wrong).
+__host__ __device__ __forceinline__ bool item_apply(const SeedItem& it, double& c) {
+  switch (it.kind) {
+    case kItRun: {
+      int e;
+      long long N;
+      if (!sp_binade(c, e, N) || e != it.e) return false;
+      const long long N2 = N + ((N & 1) ? it.d1 : it.d0);
+      if (N2 >= (1ll << 53)) return false;
+      c = sp_value(e, N2);
+      return true;
+    }
+    case kItSkip:
+    case kItMark:
+    case kItEnd:
+      return true;
+    case kItCross:
+      c = c + it.p;
+      return true;
+    case kItConst:
+      c = it.p;
+      return true;
+    default:
+      return false;
+  }
+}
+
+__host__ __device__ __forceinline__ SeedItem run_item(const Part& P) {
+  return SeedItem{P.d0, P.d1, 0.0, P.e, P.st == 0 ? kItSkip : (P.st == 1 ? kItRun : kItBad)};
+}
+
+// Element p joins run P under binade e (range_transfer_v's step).
+__device__ __forceinline__ void part_add(Part& P, double p, int e) {
+  if (P.st == 0) P = Part{0, 0, e, 1};
+  if (P.st != 1) return;
+  if (P.e != e) {
+    P.st = 2;
+    return;
+  }
+  const double f = ldexp(p, 52 - e);
+  if (!(f < 4503599627370496.0)) {
+    P.st = 2;
+    return;
+  }
+  const double fl = floor(f);
+  const double frac = f - fl;
+  const long long k = (long long)fl;
+  const long long up = frac > 0.5 ? 1 : 0;
+  const bool tie = frac == 0.5;
+  P.d0 += k + up + ((tie && ((P.d0 ^ k) & 1)) ? 1 : 0);
+  P.d1 += k + up + ((tie && ((1 ^ P.d1 ^ k) & 1)) ? 1 : 0);
+  if (P.d0 >= kD52 || P.d1 >= kD52) P.st = 2;
+}
+
+__device__ __forceinline__ Part shfl_up_part(const Part& P, int o) {
+  return Part{__shfl_up(P.d0, o), __shfl_up(P.d1, o), __shfl_up(P.e, o), __shfl_up(P.st, o)};
+}
+__device__ __forceinline__ Part shfl_part(const Part& P, int l) {
+  return Part{__shfl(P.d0, l), __shfl(P.d1, l), __shfl(P.e, l), __shfl(P.st, l)};
+}
+
+__device__ __forceinline__ int gbin(double c) {
+  int e;
+  long long N;
+  return sp_binade(c, e, N) ? e : kNoE;
+}
+
+// A guessed running value within 2^-24 (relative) of its binade's edges: the
+// exact value may sit on either side (a sequential fp64 sum of n terms is
+// within n 2^-53 of the real sum, < 2^-24 for n < 2^29), so elements next to
+// it are crossings, added exactly whatever the binade turns out to be.
+__device__ __forceinline__ bool gnear(double c) {
+  const unsigned long long m = __builtin_bit_cast(unsigned long long, c) & 0xFFFFFFFFFFFFFull;
+  return m < (1ull << 28) || m > (1ull << 52) - (1ull << 28);
+}
+
+constexpr int kKC = 32;  // crossings recorded per block
+struct SegTail {
+  Part t;      // the run after the block's last crossing (the whole block: none)
+  int ncross;  // crossings in the block
+  int opaque;  // walked element by element at evaluation
+};
+struct SegEnt {
+  Part pre;  // the run before the crossing (from the block start or the previous crossing)
+  double p;  // the crossing element
+};
+struct SegScan {
+  Part s;        // transfer from the block's segment head (exclusive) through the block
+  long long lh;  // segment head block (-1: the shard start)
+};
+
+// One workgroup per block, one wave per 1024-element pass (8 waves); lane l
+// of wave w owns elements [1024 w + 16 l, +16).  The passes are linked
+// through LDS: their sums (the guessed running value at each pass start),
+// their crossing counts (where each pass's entries go) and their tail runs
+// (the run open at each pass start).
+constexpr int kSegWaves = kSeedBlock / kPass;  // 8
+__global__ __launch_bounds__(512) void seg_block_kernel(const double* __restrict__ dmin,
+                                                        int64_t n, double S,
+                                                        const double* __restrict__ approx,
+                                                        int64_t nblocks,
+                                                        SegTail* __restrict__ tails,
+                                                        SegEnt* __restrict__ ents) {
+  __shared__ double s_sum[kSegWaves];
+  __shared__ int s_m[kSegWaves], s_bad[kSegWaves], s_h[kSegWaves];
+  __shared__ Part s_t[kSegWaves];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x;
+  const int64_t base = b * kSeedBlock;
+  SegEnt* eb = ents + b * kKC;
+  const int64_t lo = base + (int64_t)w * kPass + (int64_t)lane * 16;
+  const int cnt = lo >= n ? 0 : (n - lo < 16 ? (int)(n - lo) : 16);
+  // dmin is allocated to n_pad (a multiple of the block): whole lanes load
+  double p[16];
+  {
+    const double2* src = reinterpret_cast<const double2*>(dmin + lo);
+    double2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = src[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      p[2 * j] = 2 * j < cnt ? v[j].x / S : 0.0;
+      p[2 * j + 1] = 2 * j + 1 < cnt ? v[j].y / S : 0.0;
+    }
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s += p[j];
+  double inc = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const double t = __shfl_up(inc, o);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) s_sum[w] = inc;
+  __syncthreads();
+  // guessed running value at each pass start: the same sequence in every wave
+  double A = approx[b], Anext = 0.0;
+  for (int v = 0; v <= w; ++v) {
+    Anext = A + s_sum[v];
+    if (v < w) A = Anext;
+  }
+  const double Aend = (b + 1 < nblocks) ? approx[b + 1] : -1.0;
+  const double ex = __shfl_up(inc, 1);
+  const double a0 = A + (lane ? ex : 0.0);
+  double a1 = __shfl_down(a0, 1);
+  if (lane == 63) a1 = (w == kSegWaves - 1 && Aend >= 0.0) ? Aend : Anext;
+  // crossings under the guess
+  unsigned xm = 0;
+  {
+    double cb = a0;
+    int gb = gbin(cb);
+    bool nb_ = gnear(cb);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < cnt) {
+        const double ca = (j == cnt - 1) ? a1 : cb + p[j];
+        const int ga = gbin(ca);
+        const bool na = gnear(ca);
+        if (gb == kNoE || ga != gb || nb_ || na) xm |= 1u << j;
+        cb = ca;
+        gb = ga;
+        nb_ = na;
+      }
+    }
+  }
+  const int m = __popc(xm);
+  int mi = m;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(mi, o);
+    if (lane >= o) mi += t;
+  }
+  if (lane == 63) s_m[w] = mi;
+  __syncthreads();
+  int basew = 0, mtot = 0;
+  for (int v = 0; v < kSegWaves; ++v) {
+    if (v < w) basew += s_m[v];
+    mtot += s_m[v];
+  }
+  const bool over = mtot > kKC;  // block-uniform
+  Part Sx = part_empty();
+  Part F = part_empty();
+  double p0 = 0.0;
+  bool bad = false;
+  const int bl = basew + mi - m;  // this lane's first entry
+  if (!over) {
+    Part cur = part_empty();
+    int jj = 0;
+    double cb = a0;
+    int gb = gbin(cb);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < cnt) {
+        const double ca = (j == cnt - 1) ? a1 : cb + p[j];
+        if ((xm >> j) & 1) {
+          if (jj == 0) {
+            F = cur;
+            p0 = p[j];
+          } else {
+            eb[bl + jj] = SegEnt{cur, p[j]};
+            bad |= cur.st == 2;
+          }
+          ++jj;
+          cur = part_empty();
+        } else {
+          part_add(cur, p[j], gb);
+        }
+        cb = ca;
+        gb = gbin(ca);
+      }
+    }
+    // segmented inclusive scan of the lane tails (heads: lanes with a crossing)
+    Sx = cur;
+    int hs = m > 0;
+    for (int o = 1; o < 64; o <<= 1) {
+      const Part L = shfl_up_part(Sx, o);
+      const int hl = __shfl_up(hs, o);
+      if (lane >= o) {
+        if (!hs) Sx = part_compose(L, Sx);
+        hs |= hl;
+      }
+    }
+  }
+  const unsigned long long hm = __ballot(m > 0);
+  const Part S63 = shfl_part(Sx, 63);
+  if (lane == 0) {
+    s_t[w] = S63;
+    s_h[w] = hm != 0ull;
+  }
+  Part Sp = shfl_up_part(Sx, 1);
+  if (lane == 0) Sp = part_empty();
+  const int anybad = __ballot(bad) != 0ull;
+  if (lane == 0) s_bad[w] = anybad;
+  __syncthreads();
+  // the run open at this pass's start: passes since the last one with a crossing
+  Part open = part_empty();
+  for (int v = 0; v < w; ++v) open = s_h[v] ? s_t[v] : part_compose(open, s_t[v]);
+  bool badw = false;
+  if (!over && m > 0) {
+    const bool prevh = (hm & ((1ull << lane) - 1)) != 0;
+    const Part pre = part_compose(prevh ? Sp : part_compose(open, Sp), F);
+    eb[bl] = SegEnt{pre, p0};
+    badw = pre.st == 2;
+  }
+  const int badf = __ballot(badw) != 0ull;
+  __syncthreads();
+  if (lane == 0 && badf) s_bad[w] = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Part t = part_empty();
+    int anyb = 0;
+    for (int v = 0; v < kSegWaves; ++v) {
+      t = s_h[v] ? s_t[v] : part_compose(t, s_t[v]);
+      anyb |= s_bad[v];
+    }
+    const bool opq = over || anyb || t.st == 2;
+    tails[b] = SegTail{t, opq ? 0 : mtot, opq ? 1 : 0};
+  }
+}
+
+constexpr int kPlanT = 1024;
+constexpr int64_t kItemCap = 1 << 16;  // program items per shard (more: fallback)
+
+// Single workgroup: segmented scan of the block tails and the program.
+__global__ __launch_bounds__(1024) void seg_plan_kernel(const SegTail* __restrict__ tails,
+                                                        const SegEnt* __restrict__ ents,
+                                                        int64_t nb, SegScan* __restrict__ scan,
+                                                        SeedItem* __restrict__ items, int64_t cap,
+                                                        long long* __restrict__ meta) {
+  __shared__ Part sP[kPlanT];
+  __shared__ int sH[kPlanT];
+  __shared__ long long sI[kPlanT], sL[kPlanT], sF[kPlanT];
+  const int t = threadIdx.x;
+  const int64_t per = (nb + kPlanT - 1) / kPlanT;
+  const int64_t lo = (int64_t)t * per;
+  const int64_t hi = (lo + per) < nb ? (lo + per) : nb;
+  {
+    Part agg = part_empty();
+    int hh = 0;
+    long long ni = 0, lh = -1, nf = 0;
+    for (int64_t b = lo; b < hi; ++b) {
+      const SegTail T = tails[b];
+      if (T.ncross > 0 || T.opaque) {
+        agg = T.opaque ? part_empty() : T.t;
+        hh = 1;
+        lh = b;
+        ni += T.opaque ? 3 : 2 + 2 * (long long)T.ncross;
+        nf += T.opaque;
+      } else {
+        agg = part_compose(agg, T.t);
+      }
+    }
+    sP[t] = agg;
+    sH[t] = hh;
+    sI[t] = ni;
+    sL[t] = lh;
+    sF[t] = nf;
+  }
+  __syncthreads();
+  for (int o = 1; o < kPlanT; o <<= 1) {
+    Part L = part_empty();
+    int hl = 0;
+    long long il = 0, ll = -1, fl = 0;
+    if (t >= o) {
+      L = sP[t - o];
+      hl = sH[t - o];
+      il = sI[t - o];
+      ll = sL[t - o];
+      fl = sF[t - o];
+    }
+    __syncthreads();
+    if (t >= o) {
+      if (!sH[t]) sP[t] = part_compose(L, sP[t]);
+      sH[t] |= hl;
+      sI[t] += il;
+      if (ll > sL[t]) sL[t] = ll;
+      sF[t] += fl;
+    }
+    __syncthreads();
+  }
+  Part run = t ? sP[t - 1] : part_empty();
+  long long off = t ? sI[t - 1] : 0;
+  long long lastH = t ? sL[t - 1] : -1;
+  const long long total = sI[kPlanT - 1];
+  const bool over = total + 2 > cap;
+  for (int64_t b = lo; b < hi; ++b) {
+    const SegTail T = tails[b];
+    if (T.ncross > 0 || T.opaque) {
+      if (!over) {
+        items[off++] = run_item(run);
+        if (T.opaque) {
+          items[off++] = SeedItem{b, 0, 0.0, 0, kItFine};
+        } else {
+          for (int j = 0; j < T.ncross; ++j) {
+            const SegEnt E = ents[b * kKC + j];
+            items[off++] = run_item(E.pre);
+            items[off++] = SeedItem{0, 0, E.p, 0, kItCross};
+          }
+        }
+        items[off++] = SeedItem{b, 0, 0.0, 0, kItMark};
+      }
+      run = T.opaque ? part_empty() : T.t;
+      lastH = b;
+    } else {
+      run = part_compose(run, T.t);
+    }
+    scan[b] = SegScan{run, lastH};
+  }
+  if (t == 0) {
+    if (!over) {
+      items[total] = run_item(sP[kPlanT - 1]);
+      items[total + 1] = SeedItem{0, 0, 0.0, 0, kItEnd};
+    }
+    meta[0] = total + 2;
+    meta[1] = sF[kPlanT - 1];
+    meta[2] = over ? 1 : 0;
+  }
+}
+
+// Single wave: the program from the exact c_in.  Items are read with
+// uniform addresses (scalar loads, one item ahead) and applied in uniform
+// control flow.  res[0] = running value after the shard, res[1] = 1 when
+// every item held.
+__global__ __launch_bounds__(64) void seg_eval_kernel(const double* __restrict__ dmin, int64_t n,
+                                                      double S,
+                                                      const SeedItem* __restrict__ items,
+                                                      const long long* __restrict__ meta,
+                                                      double c_in, double* __restrict__ markc,
+                                                      double* __restrict__ res) {
+  const int lane = threadIdx.x;
+  double c = c_in;
+  bool ok = meta[2] == 0;
+  const long long cnt = ok ? meta[0] : 0;
+  int64_t dummy = -1;
+  SeedItem it = cnt > 0 ? items[0] : SeedItem{0, 0, 0.0, 0, kItEnd};
+  for (long long i = 0; i < cnt; ++i) {
+    const SeedItem nx = (i + 1 < cnt) ? items[i + 1] : SeedItem{0, 0, 0.0, 0, kItEnd};
+    if (it.kind == kItEnd) break;
+    if (it.kind == kItFine) {
+      const int64_t lo = it.d0 * kSeedBlock;
+      const int64_t hi = (lo + kSeedBlock) < n ? (lo + kSeedBlock) : n;
+      c = fine_walk(dmin, S, lo, hi, c, false, 1.0, 0.0, &dummy);
+    } else if (it.kind == kItMark) {
+      if (lane == 0) markc[it.d0] = c;
+    } else if (!item_apply(it, c)) {
+      ok = false;
+      break;
+    }
+    it = nx;
+  }
+  if (lane == 0) {
+    res[0] = c;
+    res[1] = ok ? 1.0 : 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void seg_fill_kernel(const SegScan* __restrict__ scan,
+                                                       int64_t nb,
+                                                       const double* __restrict__ markc,
+                                                       const double* __restrict__ res,
+                                                       double c_in, double* __restrict__ cend) {
+  if (res[1] == 0.0) return;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const SegScan s = scan[b];
+  const double c0 = s.lh < 0 ? c_in : markc[s.lh];
+  double v = c0;
+  if (s.s.st == 1) {
+    int e;
+    long long N;
+    sp_binade(c0, e, N);
+    v = sp_value(e, N + ((N & 1) ? s.s.d1 : s.s.d0));
+  }
+  cend[b] = v;
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -756,6 +1270,38 @@ static void seed_track(Ctx& c) {
                            c.stream));
 }
 
+// NumPy's pairwise tree over m elements (np_pairwise): leaves of <= 128, split
+// at n/2 rounded down to a multiple of 8.
+static void pw_layout(int64_t off, int64_t m, std::vector<int>& leaves, std::vector<int>& post) {
+  if (m <= 128) {
+    leaves.push_back((int)off);
+    leaves.push_back((int)m);
+    post.push_back(1);
+    return;
+  }
+  int64_t m2 = m / 2;
+  m2 -= m2 % 8;
+  pw_layout(off, m2, leaves, post);
+  pw_layout(off + m2, m - m2, leaves, post);
+  post.push_back(0);
+}
+
+static void seed_tail_plan(Ctx& c, int64_t m) {
+  if (c.seed_tail_m == m) return;
+  std::vector<int> leaves, post;
+  pw_layout(0, m, leaves, post);
+  const int nl = (int)leaves.size() / 2;
+  if (nl > kTailLeaves) CDR_FAIL(CDR_ERR_UNSUPPORTED, "pairwise tail layout too large");
+  std::vector<int> plan(leaves);
+  plan.insert(plan.end(), post.begin(), post.end());
+  c.seed_tail_plan.ensure(sizeof(int) * plan.size());
+  HIP_CHECK(hipMemcpy(c.seed_tail_plan.p, plan.data(), sizeof(int) * plan.size(),
+                      hipMemcpyHostToDevice));
+  c.seed_tail_nleaves = nl;
+  c.seed_tail_npost = (int)post.size();
+  c.seed_tail_m = m;
+}
+
 void seed_update(Ctx& c, const double* cen) {
   check_points(c);
   if (!c.dmin.p) seed_reset(c);
@@ -774,53 +1320,42 @@ void seed_update(Ctx& c, const double* cen) {
   const int cidx = c.seed_count;
   if (nb > 0) {
     typedef void (*SeedFn)(const float*, int64_t, int64_t, int, const double*, double*, double*,
-                           int64_t, int32_t*, const double*, int);
-#define CDR_SU(D_) seed_update_kernel<float, D_, false>
+                           int32_t*, const double*, int);
+#define CDR_SU(D_) seed_update_kernel<float, D_>
     static const SeedFn fns[17] = {CDR_SU(0),  CDR_SU(1),  CDR_SU(2),  CDR_SU(3),  CDR_SU(4),
                                    CDR_SU(5),  CDR_SU(6),  CDR_SU(7),  CDR_SU(8),  CDR_SU(9),
                                    CDR_SU(10), CDR_SU(11), CDR_SU(12), CDR_SU(13), CDR_SU(14),
                                    CDR_SU(15), CDR_SU(16)};
 #undef CDR_SU
     const int64_t nfull = c.n / kSeedBlock;
-    const bool f32 = c.mode == CDR_MODE_F32X;
-    if (nfull > 0) {
-      if (f32)
-        hipLaunchKernelGGL(fns[c.d <= 16 ? c.d : 0], dim3(nfull), dim3(256), 0, c.stream,
-                           c.x32.as<float>(), c.n, c.n_pad, c.d, c.seed_scalar.as<double>(),
-                           c.dmin.as<double>(), c.blocksums.as<double>(), (int64_t)0, near, ccd,
-                           cidx);
-      else
-        hipLaunchKernelGGL((seed_update_kernel<double, 0, false>), dim3(nfull), dim3(256), 0,
-                           c.stream, c.x64.as<double>(), c.n, c.n_pad, c.d,
-                           c.seed_scalar.as<double>(), c.dmin.as<double>(),
-                           c.blocksums.as<double>(), (int64_t)0, near, ccd, cidx);
+    const SeedFn fn = c.d <= 16 ? fns[c.d]
+                      : c.d == 32 ? seed_update_kernel<float, 32>
+                      : c.d == 64 ? seed_update_kernel<float, 64>
+                                  : fns[0];
+    if (c.mode == CDR_MODE_F32X)
+      hipLaunchKernelGGL(fn, dim3(nb), dim3(256), 0, c.stream,
+                         c.x32.as<float>(), c.n, c.n_pad, c.d, c.seed_scalar.as<double>(),
+                         c.dmin.as<double>(), c.blocksums.as<double>(), near, ccd, cidx);
+    else
+      hipLaunchKernelGGL((seed_update_kernel<double, 0>), dim3(nb), dim3(256), 0, c.stream,
+                         c.x64.as<double>(), c.n, c.n_pad, c.d, c.seed_scalar.as<double>(),
+                         c.dmin.as<double>(), c.blocksums.as<double>(), near, ccd, cidx);
+    HIP_CHECK(hipGetLastError());
+    if (nb > nfull) {
+      seed_tail_plan(c, c.n - nfull * kSeedBlock);
+      hipLaunchKernelGGL(seed_tail_sum_kernel, dim3(1), dim3(256), 0, c.stream,
+                         c.dmin.as<double>(), nfull, c.seed_tail_plan.as<int>(),
+                         c.seed_tail_nleaves, c.seed_tail_npost, c.blocksums.as<double>());
       HIP_CHECK(hipGetLastError());
     }
-    if (nb > nfull) {
-      if (f32)
-        hipLaunchKernelGGL((seed_update_kernel<float, 0, true>), dim3(1), dim3(256), 0,
-                           c.stream, c.x32.as<float>(), c.n, c.n_pad, c.d,
-                           c.seed_scalar.as<double>(), c.dmin.as<double>(),
-                           c.blocksums.as<double>(), nfull, near, ccd, cidx);
-      else
-        hipLaunchKernelGGL((seed_update_kernel<double, 0, true>), dim3(1), dim3(256), 0,
-                           c.stream, c.x64.as<double>(), c.n, c.n_pad, c.d,
-                           c.seed_scalar.as<double>(), c.dmin.as<double>(),
-                           c.blocksums.as<double>(), nfull, near, ccd, cidx);
-    }
-    HIP_CHECK(hipGetLastError());
   }
   c.seed_count += 1;
   c.seed_scanned = false;
 }
 
-void seed_scan(Ctx& c, double total, double c_in, double* c_out) {
-  check_points(c);
+// The block-by-block walk (exact from any c_in; the fallback of the program).
+static void seed_scan_walk(Ctx& c, double total, double c_in, double* c_out) {
   const int64_t nb = c.nblocks();
-  if (nb == 0) {
-    *c_out = c_in;
-    return;
-  }
   c.xfer.ensure(sizeof(Xfer) * nb);
   c.cend.ensure(sizeof(double) * nb * 2);
   double* approx = c.cend.as<double>() + nb;
@@ -859,6 +1394,136 @@ void seed_scan(Ctx& c, double total, double c_in, double* c_out) {
   c.seed_c_in = c_in;
   c.seed_total = total;
   c.seed_scanned = true;
+}
+
+// This shard's cumsum program under the guess c_guess of the running value at
+// its first element (seg_block_kernel, seg_plan_kernel).
+static void seed_scan_program(Ctx& c, double total, double c_guess) {
+  const int64_t nb = c.nblocks();
+  c.cend.ensure(sizeof(double) * nb * 2);
+  double* approx = c.cend.as<double>() + nb;
+  c.seg_tails.ensure(sizeof(SegTail) * nb);
+  c.seg_ents.ensure(sizeof(SegEnt) * nb * kKC);
+  c.seg_scan.ensure(sizeof(SegScan) * nb);
+  c.seg_items.ensure(sizeof(SeedItem) * kItemCap);
+  c.seg_meta.ensure(sizeof(long long) * 8);
+  hipLaunchKernelGGL(approx_prefix_kernel, dim3(1), dim3(1024), 0, c.stream,
+                     c.blocksums.as<double>(), nb, total, c_guess, approx);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(seg_block_kernel, dim3((int)nb), dim3(kSegWaves * 64), 0, c.stream,
+                     c.dmin.as<double>(), c.n, total, approx, nb, c.seg_tails.as<SegTail>(),
+                     c.seg_ents.as<SegEnt>());
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(seg_plan_kernel, dim3(1), dim3(kPlanT), 0, c.stream,
+                     c.seg_tails.as<SegTail>(), c.seg_ents.as<SegEnt>(), nb,
+                     c.seg_scan.as<SegScan>(), c.seg_items.as<SeedItem>(), kItemCap,
+                     c.seg_meta.as<long long>());
+  HIP_CHECK(hipGetLastError());
+  c.seed_prog_total = total;
+  c.seed_prog_ready = true;
+}
+
+// Runs the program from the exact c_in and fills cend; false when a guess
+// failed (nothing usable written).
+static bool seed_scan_finish(Ctx& c, double c_in, double* c_out) {
+  const int64_t nb = c.nblocks();
+  double* markc = c.cend.as<double>() + nb;  // the guesses are consumed
+  double* res = reinterpret_cast<double*>(c.seg_meta.as<long long>() + 4);
+  hipLaunchKernelGGL(seg_eval_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
+                     c.seed_prog_total, c.seg_items.as<SeedItem>(), c.seg_meta.as<long long>(),
+                     c_in, markc, res);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(seg_fill_kernel, dim3((int)ceil_div(nb, 256)), dim3(256), 0, c.stream,
+                     c.seg_scan.as<SegScan>(), nb, markc, res, c_in, c.cend.as<double>());
+  HIP_CHECK(hipGetLastError());
+  double h[2];
+  HIP_CHECK(hipMemcpyAsync(h, res, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  static const bool want_stats = std::getenv("CDR_SEED_STATS") != nullptr;
+  if (want_stats) {
+    long long m[3];
+    HIP_CHECK(hipMemcpy(m, c.seg_meta.p, sizeof(m), hipMemcpyDeviceToHost));
+    fprintf(stderr, "seed program: items %lld fine %lld over %lld ok %d\n", m[0], m[1], m[2],
+            h[1] != 0.0);
+  }
+  if (h[1] == 0.0) return false;
+  *c_out = h[0];
+  return true;
+}
+
+static void seed_scan_done(Ctx& c, double total, double c_in) {
+  c.seed_c_in = c_in;
+  c.seed_total = total;
+  c.seed_scanned = true;
+  c.seed_prog_ready = false;
+}
+
+void seed_scan(Ctx& c, double total, double c_in, double* c_out) {
+  check_points(c);
+  const int64_t nb = c.nblocks();
+  if (nb == 0) {
+    *c_out = c_in;
+    return;
+  }
+  static const bool walk_only = std::getenv("CDR_SEED_WALK") != nullptr;
+  bool done = false;
+  if (!walk_only) {
+    seed_scan_program(c, total, c_in);
+    done = seed_scan_finish(c, c_in, c_out);
+    if (!done) ++c.seed_fallbacks;
+  }
+  if (!done) seed_scan_walk(c, total, c_in, c_out);
+  seed_scan_done(c, total, c_in);
+}
+
+void seed_scan_begin(Ctx& c, double total, double c_guess, int64_t* n_items, int64_t* n_fine) {
+  check_points(c);
+  const int64_t nb = c.nblocks();
+  c.seed_scanned = false;
+  if (nb == 0) {
+    *n_items = 0;
+    *n_fine = 0;
+    c.seed_prog_total = total;
+    c.seed_prog_ready = true;
+    return;
+  }
+  seed_scan_program(c, total, c_guess);
+  long long m[3];
+  HIP_CHECK(hipMemcpyAsync(m, c.seg_meta.p, sizeof(m), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  *n_items = m[2] ? -1 : m[0];
+  *n_fine = m[1];
+}
+
+void seed_scan_items(Ctx& c, cdr_seed_item* out, int64_t cap, int64_t* n_items) {
+  if (!c.seed_prog_ready) CDR_FAIL(CDR_ERR_STATE, "cdr_seed_scan_items before cdr_seed_scan_begin");
+  const int64_t nb = c.nblocks();
+  if (nb == 0) {
+    *n_items = 0;
+    return;
+  }
+  long long m[3];
+  HIP_CHECK(hipMemcpyAsync(m, c.seg_meta.p, sizeof(m), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (m[2]) CDR_FAIL(CDR_ERR_UNSUPPORTED, "seed program over its item capacity");
+  if (m[0] > cap) CDR_FAIL(CDR_ERR_ARG, "output capacity below the program's item count");
+  HIP_CHECK(hipMemcpyAsync(out, c.seg_items.p, sizeof(SeedItem) * m[0], hipMemcpyDeviceToHost,
+                           c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  *n_items = m[0];
+}
+
+void seed_scan_end(Ctx& c, double c_in, double* c_out) {
+  if (!c.seed_prog_ready) CDR_FAIL(CDR_ERR_STATE, "cdr_seed_scan_end before cdr_seed_scan_begin");
+  const double total = c.seed_prog_total;
+  const int64_t nb = c.nblocks();
+  if (nb == 0) {
+    *c_out = c_in;
+  } else if (!seed_scan_finish(c, c_in, c_out)) {
+    ++c.seed_fallbacks;
+    seed_scan_walk(c, total, c_in, c_out);
+  }
+  seed_scan_done(c, total, c_in);
 }
 
 void seed_search(Ctx& c, double c_last, double u, int64_t* idx) {
@@ -927,6 +1592,50 @@ int cdr_seed_scan(cdr_ctx* h, double total, double c_in, double* c_out) {
   if (!(total > 0.0) || std::isinf(total)) CDR_FAIL(CDR_ERR_NAN, "Probabilities contain NaN");
   HIP_CHECK(hipSetDevice(h->c.device));
   seed_scan(h->c, total, c_in, c_out);
+  CDR_CATCH
+}
+
+int cdr_seed_scan_begin(cdr_ctx* h, double total, double c_guess, int64_t* n_items,
+                        int64_t* n_fine) {
+  CDR_TRY
+  if (!h || !n_items || !n_fine) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  if (!(total > 0.0) || std::isinf(total)) CDR_FAIL(CDR_ERR_NAN, "Probabilities contain NaN");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  seed_scan_begin(h->c, total, c_guess, n_items, n_fine);
+  CDR_CATCH
+}
+
+int cdr_seed_scan_items(cdr_ctx* h, cdr_seed_item* out, int64_t cap, int64_t* n_items) {
+  CDR_TRY
+  if (!h || !n_items || (!out && cap > 0)) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  seed_scan_items(h->c, out, cap, n_items);
+  CDR_CATCH
+}
+
+int cdr_seed_scan_end(cdr_ctx* h, double c_in, double* c_out) {
+  CDR_TRY
+  if (!h || !c_out) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  seed_scan_end(h->c, c_in, c_out);
+  CDR_CATCH
+}
+
+int cdr_seed_program_eval(const cdr_seed_item* items, int64_t n_items, double c_in,
+                          double* c_out, int32_t* ok) {
+  CDR_TRY
+  if (!c_out || !ok || (!items && n_items > 0) || n_items < 0)
+    CDR_FAIL(CDR_ERR_ARG, "bad argument");
+  double c = c_in;
+  int32_t good = 1;
+  for (int64_t i = 0; i < n_items && good; ++i) {
+    SeedItem it;
+    std::memcpy(&it, items + i, sizeof(it));
+    if (it.kind == kItEnd) break;
+    if (it.kind == kItFine || !item_apply(it, c)) good = 0;
+  }
+  *c_out = c;
+  *ok = good;
   CDR_CATCH
 }
 

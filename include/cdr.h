@@ -100,6 +100,38 @@ int cdr_seed_block_sums(cdr_ctx* ctx, double* out);
  * the running value after the shard's last element.  Emulates np.cumsum
  * bit-exactly (Generator.choice, kmeans_plusplus.py:19).                   */
 int cdr_seed_scan(cdr_ctx* ctx, double total, double c_in, double* c_out);
+/* The same scan in two halves, for sharded seeding without a rank-ordered
+ * chain (cdr_dist.seed_sharded replaces kmeans_plusplus.py:19's single
+ * np.cumsum over all rows).  _begin builds this shard's cumsum program from
+ * a GUESS of the running value at its first element (the sum of the earlier
+ * shards' block sums / total); the program is the shard's exact function
+ * c_in -> c_out as long as it has no CDR_SEED_FINE item.  _items copies it
+ * out; cdr_seed_program_eval runs it on the host (no device, no context).
+ * _end takes the exact c_in, fills what cdr_seed_search needs and returns
+ * c_out — exact whatever the guess was (it falls back to the block walk).  */
+typedef struct {
+  int64_t d0, d1; /* RUN: grid steps added for an even / odd entry         */
+  double p;       /* CROSS: the element added; CONST: the value            */
+  int32_t e;      /* RUN: binade exponent                                   */
+  int32_t kind;   /* CDR_SEED_*                                             */
+} cdr_seed_item;
+enum {
+  CDR_SEED_RUN = 0,   /* c in binade e: N += (N odd ? d1 : d0), N < 2^53    */
+  CDR_SEED_CROSS = 1, /* c = fl(c + p)                                      */
+  CDR_SEED_CONST = 2, /* c = p (a shard whose c_in is known: the first)     */
+  CDR_SEED_FINE = 3,  /* element walk of block d0 (device only)             */
+  CDR_SEED_MARK = 4,  /* device bookkeeping; no-op                          */
+  CDR_SEED_END = 5,
+  CDR_SEED_SKIP = 6,  /* empty run                                          */
+  CDR_SEED_BAD = 7    /* the guess cannot hold: evaluation fails            */
+};
+int cdr_seed_scan_begin(cdr_ctx* ctx, double total, double c_guess, int64_t* n_items,
+                        int64_t* n_fine);
+int cdr_seed_scan_items(cdr_ctx* ctx, cdr_seed_item* out, int64_t cap, int64_t* n_items);
+int cdr_seed_scan_end(cdr_ctx* ctx, double c_in, double* c_out);
+/* *ok = 0 when some item does not hold for this c_in (or a FINE item).      */
+int cdr_seed_program_eval(const cdr_seed_item* items, int64_t n_items, double c_in,
+                          double* c_out, int32_t* ok);
 /* searchsorted(cumsum / c_last, u, side='right') restricted to this shard:
  * *idx = local index, or -1 when the crossing is not in this shard.        */
 int cdr_seed_search(cdr_ctx* ctx, double c_last, double u, int64_t* idx);

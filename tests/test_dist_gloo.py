@@ -1,8 +1,10 @@
 """Multi-rank protocol of cdr_dist (sharded seeding + Lloyd) on CPU, gloo,
 world_size 2.  Each rank's device shard is replaced by a test double built on
 the pinned oracle, so this checks the collective logic — 8192-row sharding,
-block-sum all-gather, the rank-ordered exact scan chain, the owner broadcast
-and the int64 all-reduce — against the single-process reference semantics."""
+block-sum all-gather, the all-gathered cumsum programs composed on every
+rank (and the rank-ordered exact scan chain they fall back to), the owner
+broadcast and the int64 all-reduce — against the single-process reference
+semantics."""
 import os
 import socket
 
@@ -11,6 +13,7 @@ import pytest
 
 from oracle import kmeans_oracle as ko
 from oracle import synth
+from seedprog_model import build_program
 
 N_TOTAL, D, K = 3 * 8192 + 1234, 4, 6
 
@@ -43,6 +46,21 @@ class OracleShard:
     def seed_scan(self, total, c_in):
         self.cum = np.cumsum(np.concatenate([[c_in], self.dmin / total]))[1:]
         return float(self.cum[-1])
+
+    # cumsum programs (cdr_seed_scan_begin / _items / _end)
+    def seed_scan_begin(self, total, c_guess):
+        self.total = total
+        self.prog = build_program(self.dmin / total, c_guess)
+        self.begun = getattr(self, "begun", 0) + 1
+        return self.prog.size, 0
+
+    def seed_scan_items(self, n):
+        assert n == self.prog.size
+        return self.prog
+
+    def seed_scan_end(self, c_in):
+        self.ended = getattr(self, "ended", 0) + 1
+        return self.seed_scan(self.total, c_in)
 
     def seed_search(self, c_last, u):
         i = int(np.searchsorted(self.cum / c_last, u, side="right"))
@@ -125,6 +143,8 @@ def _worker(rank, world, port, out_dir, empty):
     shard = OracleShard(synth.generate(N_TOTAL, begin, n_local, D, K, 9))
     comm = Comm(dist, None)
     C = seed_sharded(shard, comm, begin, N_TOTAL, K, random_state=42)
+    if rank > 0:
+        assert shard.begun == shard.ended == K - 1  # every step composed the programs
     if empty:
         C[-1] = 50.0  # far from every point: empty from the first step on
     np.random.seed(0)
@@ -162,13 +182,14 @@ def _reference_lloyd(X, C, max_iter, tol):
     return C
 
 
-@pytest.mark.parametrize("empty", [False, True], ids=["fixed-steps", "empty-cluster+tol"])
-def test_two_ranks_match_single_process(tmp_path, empty):
+@pytest.mark.parametrize("world,empty", [(2, False), (2, True), (3, False)],
+                         ids=["fixed-steps", "empty-cluster+tol", "world3"])
+def test_two_ranks_match_single_process(tmp_path, world, empty):
     """Sharded seeding + the device-loop protocol (enqueue, all-reduce,
     finalize, host take-over for an empty cluster, convergence stop) on two
-    gloo ranks equals the single-process reference."""
+    (three) gloo ranks equals the single-process reference."""
     mp = pytest.importorskip("torch.multiprocessing")
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), empty), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), empty), nprocs=world, join=True)
     X = synth.generate(N_TOTAL, 0, N_TOTAL, D, K, 9)
     C0 = ko.kmeans_plusplus_init(X, K, random_state=42)
     if empty:

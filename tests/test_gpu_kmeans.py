@@ -346,3 +346,72 @@ def test_f32x_gate_keeps_numpy_mean_exact(ctx):
         ctx.load_points(X)
         inf = ctx.info()
         assert inf["mode"] == want, (n, inf)
+
+
+@pytest.mark.parametrize("n,outlier", [(8192 * 40 + 77, False), (8192 * 25, True), (3000, False)])
+def test_seed_program_cend_exact(ctx, n, outlier):
+    """The program scan (csrc/seed.hip seg_* kernels) fills the per-block
+    running values that seed_search reads: searchsorted(cumsum / c_last, u,
+    'right') for u exactly at block ends and at random points equals NumPy's
+    (kmeans_plusplus.py:19)."""
+    import _cdr
+
+    X = synth.generate(n, 0, n, 16, 8, 4242 + n)
+    if outlier:
+        X[n // 2] = 50.0
+    ctx.load_points(X)
+    ctx.seed_reset()
+    dist = np.full(n, np.inf)
+    for c in (X[1], X[n // 3]):
+        ctx.seed_update(c)
+        dist = np.minimum(dist, np.sqrt(ko.sqdist_rows(X, c)) ** 2)
+        total = _cdr.host_seq_sum(ctx.seed_block_sums())
+        cum = np.cumsum(dist / total)
+        c_last = ctx.seed_scan(total, 0.0)
+        assert c_last == cum[-1]
+        cdf = cum / c_last
+        us = [cdf[i] for i in range(8191, n - 1, 8192)] + list(np.random.default_rng(n).random(20))
+        for u in us:
+            want = int(np.searchsorted(cdf, u, side="right"))
+            got = ctx.seed_search(c_last, float(u))
+            assert got == (want if want < n else -1), (u, got, want)
+
+
+def test_seed_programs_compose_over_shards(ctx):
+    """Sharded seeding without the rank chain: the second shard's program,
+    built from a guessed start, composed on the host from the first shard's
+    exact carry (cdr_seed_program_eval) = its exact scan (cdr_seed_scan_end)
+    = the single-shard scan."""
+    import _cdr
+
+    n, d = 8192 * 30 + 999, 8
+    X = synth.generate(n, 0, n, d, 8, 99)
+    b = _cdr.Context(ctx.device)
+    try:
+        ctx.load_points(X)
+        ctx.seed_reset()
+        ctx.seed_update(X[7])
+        tot = _cdr.host_seq_sum(ctx.seed_block_sums())
+        c_full = ctx.seed_scan(tot, 0.0)
+        for cut in (8192 * 3, 8192 * 17):
+            ctx.load_points(X[:cut])
+            b.load_points(X[cut:])
+            for s in (ctx, b):
+                s.seed_reset()
+                s.seed_update(X[7])
+            bs0, bs1 = ctx.seed_block_sums(), b.seed_block_sums()
+            assert _cdr.host_seq_sum(np.concatenate([bs0, bs1])) == tot
+            c1 = ctx.seed_scan(tot, 0.0)
+            ni, nf = b.seed_scan_begin(tot, float(np.sum(bs0)) / tot)
+            assert ni > 0 and nf == 0
+            prog = b.seed_scan_items(ni)
+            c2, ok = _cdr.seed_program_eval(prog, c1)
+            assert ok and c2 == c_full
+            assert b.seed_scan_end(c1) == c_full
+            u = 0.999
+            i1, i2 = ctx.seed_search(c_full, u), b.seed_search(c_full, u)
+            cdf = np.cumsum(np.sqrt(ko.sqdist_rows(X, X[7])) ** 2 / tot) / c_full
+            want = int(np.searchsorted(cdf, u, side="right"))
+            assert (i1 if i1 >= 0 else cut + i2) == want
+    finally:
+        b.close()
