@@ -233,7 +233,7 @@ struct Ctx {
   long long seed_fallbacks = 0;  // programs whose guess failed (block walk instead)
   DevBuf seed_tail_plan;  // pairwise layout of the partial last block (seed.hip)
   int64_t seed_tail_m = -1;
-  int seed_tail_nleaves = 0, seed_tail_npost = 0;
+  int seed_tail_nleaves = 0, seed_tail_nheights = 0;
   DevBuf seed_scalar; // small device scratch
   double seed_c_in = 0.0;
   bool seed_scanned = false;

@@ -11,7 +11,8 @@
 //
 // Pipeline (all byte work, HBM-bound, no MFMA):
 //   K8a  nl_count   one uint4 per lane, 4 KiB tiles: count record terminators
-//   K8b  hipcub exclusive scan of the tile counts + tile_total (tail record)
+//   K8b  exclusive scan of the tile counts (tile_scan_part / _mid / _out,
+//        4096 counts per workgroup) + tile_total (tail record)
 //   K8c  nl_write   K8a's per-lane masks (2 B per 16 log bytes), workgroup scan,
 //                   write each record's end index
 //   K8d  parse      64 records per workgroup (one wave; measured best of
@@ -35,8 +36,6 @@
 // Timestamps follow parse_ts_us (the regex in compute_features.py): greedy
 // digit groups are the regex's only possible match, so a left-to-right scan
 // decides it exactly.
-#include <hipcub/hipcub.hpp>
-
 #include <climits>
 #include <cstring>
 
@@ -81,6 +80,81 @@ __device__ __forceinline__ unsigned lane_mask(const uint8_t* __restrict__ b, int
   return m;
 }
 
+// Exclusive scan of one value per thread over a 256-thread workgroup (4
+// waves: shuffles inside each wave, the wave totals through LDS); *total =
+// the workgroup's sum.  Every thread of the workgroup calls it.
+__device__ __forceinline__ long long wg256_exscan(long long v, long long* total) {
+  __shared__ long long sw[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long long inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long t = __shfl_up(inc, o);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) sw[w] = inc;
+  __syncthreads();
+  long long base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i < w) base += sw[i];
+    tot += sw[i];
+  }
+  __syncthreads();  // sw is reused by the next call
+  *total = tot;
+  return base + inc - v;
+}
+
+// Exclusive scan of n counts (the tile counts): per 4096-count part the sum
+// (tile_scan_part), the parts' exclusive scan in one workgroup
+// (tile_scan_mid), then every count's offset (tile_scan_out).
+constexpr int kScanPer = 16;                // counts per thread
+constexpr int kScanPart = 256 * kScanPer;   // counts per workgroup
+__global__ __launch_bounds__(256) void tile_scan_part(const long long* __restrict__ cnt,
+                                                      int64_t n, long long* __restrict__ part) {
+  const int64_t lo = (int64_t)blockIdx.x * kScanPart + (int64_t)threadIdx.x * kScanPer;
+  long long s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j)
+    if (lo + j < n) s += cnt[lo + j];
+  long long tot;
+  wg256_exscan(s, &tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void tile_scan_mid(long long* __restrict__ part, int64_t np) {
+  const int64_t per = (np + 255) / 256;
+  const int64_t lo = (int64_t)threadIdx.x * per;
+  long long s = 0;
+  for (int64_t i = lo; i < lo + per && i < np; ++i) s += part[i];
+  long long tot;
+  long long o = wg256_exscan(s, &tot);
+  for (int64_t i = lo; i < lo + per && i < np; ++i) {
+    const long long v = part[i];
+    part[i] = o;
+    o += v;
+  }
+}
+
+__global__ __launch_bounds__(256) void tile_scan_out(const long long* __restrict__ cnt, int64_t n,
+                                                     const long long* __restrict__ part,
+                                                     long long* __restrict__ out) {
+  const int64_t lo = (int64_t)blockIdx.x * kScanPart + (int64_t)threadIdx.x * kScanPer;
+  long long v[kScanPer];
+  long long s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    v[j] = lo + j < n ? cnt[lo + j] : 0;
+    s += v[j];
+  }
+  long long tot;
+  long long o = part[blockIdx.x] + wg256_exscan(s, &tot);
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    if (lo + j < n) out[lo + j] = o;
+    o += v[j];
+  }
+}
+
 __global__ __launch_bounds__(256) void nl_count(const uint8_t* __restrict__ b,
                                                 long long* __restrict__ tile_cnt,
                                                 uint16_t* __restrict__ masks) {
@@ -88,14 +162,12 @@ __global__ __launch_bounds__(256) void nl_count(const uint8_t* __restrict__ b,
   const uint4 v = *reinterpret_cast<const uint4*>(b + base);
   const unsigned m = lane_mask(b, base, v);
   masks[(int64_t)blockIdx.x * 256 + threadIdx.x] = (uint16_t)m;  // nl_write reads these
-  int cnt = __popc(m);
-  using R = hipcub::BlockReduce<int, 256>;
-  __shared__ typename R::TempStorage tmp;
-  const int tot = R(tmp).Sum(cnt);
+  long long tot;
+  wg256_exscan(__popc(m), &tot);
   if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
 }
 
-// Record count after hipcub's scan of the tile counts: sc[0] = records
+// Record count after the scan of the tile counts: sc[0] = records
 // (terminators + the tail record), sc[5] = 1 if the last record is a last
 // line without '\n' (its end index nbytes is then written last).
 __global__ void tile_total(const long long* __restrict__ cnt, const long long* __restrict__ off,
@@ -117,11 +189,8 @@ __global__ __launch_bounds__(256) void nl_write(const uint16_t* __restrict__ mas
                                                 long long* __restrict__ ends) {
   const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x * 16;
   unsigned m = masks[(int64_t)blockIdx.x * 256 + threadIdx.x];
-  using S = hipcub::BlockScan<int, 256>;
-  __shared__ typename S::TempStorage tmp;
-  int excl;
-  S(tmp).ExclusiveSum(__popc(m), excl);
-  long long o = tile_off[blockIdx.x] + excl;
+  long long tot;
+  long long o = tile_off[blockIdx.x] + wg256_exscan(__popc(m), &tot);
   while (m) {
     const int j = __ffs(m) - 1;
     m &= m - 1;
@@ -588,11 +657,14 @@ void ingest_parse(Ctx& c, int64_t* status) {
     c.ing_mask.ensure(2 * 256 * ntiles);
     hipLaunchKernelGGL(nl_count, dim3(ntiles), dim3(256), 0, c.stream, c.ing_log.as<uint8_t>(),
                        cnt, c.ing_mask.as<uint16_t>());
-    size_t tmp = 0;
-    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, toff, (int)ntiles, c.stream));
-    c.ing_tmp.ensure(tmp + 256);
-    HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.ing_tmp.p, tmp, cnt, toff, (int)ntiles,
-                                               c.stream));
+    const int64_t nparts = ceil_div(ntiles, kScanPart);
+    c.ing_tmp.ensure(sizeof(long long) * nparts);
+    long long* part = c.ing_tmp.as<long long>();
+    hipLaunchKernelGGL(tile_scan_part, dim3(nparts), dim3(256), 0, c.stream, cnt, ntiles, part);
+    hipLaunchKernelGGL(tile_scan_mid, dim3(1), dim3(256), 0, c.stream, part, nparts);
+    hipLaunchKernelGGL(tile_scan_out, dim3(nparts), dim3(256), 0, c.stream, cnt, ntiles, part,
+                       toff);
+    HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(tile_total, dim3(1), dim3(1), 0, c.stream, cnt, toff, ntiles,
                        c.ing_log.as<uint8_t>(), nbytes, sc);
     HIP_CHECK(hipGetLastError());

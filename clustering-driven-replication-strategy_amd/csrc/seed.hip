@@ -19,6 +19,8 @@
 //   blocks are reduced in parallel; a single wave then walks the blocks,
 //   applying whole blocks inside a binade and walking element by element only
 //   across the ~log2(c_last/c_first) binade crossings.
+#include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -251,39 +253,47 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
 
 // The partial last block's pairwise sum (m < 8192 elements at base): its
 // pairwise tree depends on m alone, so the host lays it out once
-// (seed_tail_plan: the leaves' (offset, length) pairs, then the tree in
-// postfix, 1 = next leaf, 0 = add the top two); the leaves are summed in
-// parallel from global memory and one thread combines them from LDS.  Its
-// dmin values come from the seed_update_kernel launch before it (the block
-// is that grid's last workgroup, updated with the other blocks).
+// (seed_tail_plan): the leaves' (offset, length) pairs, then the internal
+// nodes grouped by height (node ids: leaves 0..L-1, internal nodes L.. in
+// height order; each internal node = (left id, right id)).  The block is
+// staged in LDS with coalesced loads, the leaves are summed in parallel, and
+// each height's nodes are added in parallel (<= 7 heights for m < 8192).
+// Its dmin values come from the seed_update_kernel launch before it (the
+// block is that grid's last workgroup, updated with the other blocks).
 constexpr int kTailLeaves = 160;
+constexpr int kTailHeights = 16;
 __global__ __launch_bounds__(256) void seed_tail_sum_kernel(const double* __restrict__ dmin,
                                                             int64_t b,
                                                             const int* __restrict__ plan,
-                                                            int nleaves, int npost,
+                                                            int nleaves, int nheights,
                                                             double* __restrict__ blocksums) {
-  __shared__ double sleaf[kTailLeaves];
-  __shared__ double sst[32];
+  __shared__ double snode[2 * kTailLeaves];
+  __shared__ double sv[kSeedBlock];
   const int64_t base = b * kSeedBlock;
   const int t = threadIdx.x;
-  if (t < nleaves) {
-    const int off = plan[2 * t], len = plan[2 * t + 1];
-    sleaf[t] = np_pw_leaf([&](int i) { return dmin[base + off + i]; }, len);
+  {
+    // the whole block, coalesced, 32 loads per thread in flight (dmin is
+    // allocated to n_pad: padding slots load, the leaves never read them)
+    double v[kSeedBlock / 256];
+#pragma unroll
+    for (int j = 0; j < kSeedBlock / 256; ++j) v[j] = dmin[base + j * 256 + t];
+#pragma unroll
+    for (int j = 0; j < kSeedBlock / 256; ++j) sv[j * 256 + t] = v[j];
   }
   __syncthreads();
-  if (t == 0) {
-    const int* post = plan + 2 * nleaves;
-    int sp = 0, li = 0;
-    for (int i = 0; i < npost; ++i) {
-      if (post[i]) {
-        sst[sp++] = sleaf[li++];
-      } else {
-        --sp;
-        sst[sp - 1] = sst[sp - 1] + sst[sp];
-      }
-    }
-    blocksums[b] = sst[0];
+  if (t < nleaves) {
+    const int off = plan[2 * t], len = plan[2 * t + 1];
+    snode[t] = np_pw_leaf([&](int i) { return sv[off + i]; }, len);
   }
+  const int* hstart = plan + 2 * nleaves;  // nheights + 1 entries
+  const int* nodes = hstart + nheights + 1;
+  for (int h = 0; h < nheights; ++h) {
+    __syncthreads();
+    const int a = hstart[h] + t;
+    if (a < hstart[h + 1]) snode[nleaves + a] = snode[nodes[2 * a]] + snode[nodes[2 * a + 1]];
+  }
+  __syncthreads();
+  if (t == 0) blocksums[b] = snode[nleaves > 1 ? nleaves + hstart[nheights] - 1 : 0];
 }
 
 // ---- cumulative-sum emulation --------------------------------------------
@@ -1167,36 +1177,70 @@ __global__ __launch_bounds__(1024) void seg_plan_kernel(const SegTail* __restric
   }
 }
 
-// Single wave: the program from the exact c_in.  Items are read with
-// uniform addresses (scalar loads, one item ahead) and applied in uniform
-// control flow.  res[0] = running value after the shard, res[1] = 1 when
-// every item held.
+// Single wave: the program from the exact c_in.  Items are staged through
+// LDS a window at a time (one round trip for the whole window); each item's
+// fields go to scalar registers (readfirstlane) so the walk over the items is
+// uniform scalar control flow with no per-item memory latency.
+// res[0] = running value after the shard, res[1] = 1 when every item held.
+constexpr int kEvalWin = 256;
+__device__ __forceinline__ long long sgpr64(long long v) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)v >> 32));
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
 __global__ __launch_bounds__(64) void seg_eval_kernel(const double* __restrict__ dmin, int64_t n,
                                                       double S,
                                                       const SeedItem* __restrict__ items,
                                                       const long long* __restrict__ meta,
                                                       double c_in, double* __restrict__ markc,
                                                       double* __restrict__ res) {
+  __shared__ SeedItem sit[kEvalWin];
   const int lane = threadIdx.x;
   double c = c_in;
   bool ok = meta[2] == 0;
   const long long cnt = ok ? meta[0] : 0;
   int64_t dummy = -1;
-  SeedItem it = cnt > 0 ? items[0] : SeedItem{0, 0, 0.0, 0, kItEnd};
-  for (long long i = 0; i < cnt; ++i) {
-    const SeedItem nx = (i + 1 < cnt) ? items[i + 1] : SeedItem{0, 0, 0.0, 0, kItEnd};
-    if (it.kind == kItEnd) break;
-    if (it.kind == kItFine) {
-      const int64_t lo = it.d0 * kSeedBlock;
-      const int64_t hi = (lo + kSeedBlock) < n ? (lo + kSeedBlock) : n;
-      c = fine_walk(dmin, S, lo, hi, c, false, 1.0, 0.0, &dummy);
-    } else if (it.kind == kItMark) {
-      if (lane == 0) markc[it.d0] = c;
-    } else if (!item_apply(it, c)) {
-      ok = false;
-      break;
+  bool end = false;
+  for (long long w0 = 0; ok && !end && w0 < cnt; w0 += kEvalWin) {
+    const int m = (int)((cnt - w0) < kEvalWin ? (cnt - w0) : kEvalWin);
+    __syncthreads();
+    {
+      const double4* src = reinterpret_cast<const double4*>(items + w0);
+      double4* dst = reinterpret_cast<double4*>(sit);
+      double4 v[kEvalWin / 64];
+#pragma unroll
+      for (int j = 0; j < kEvalWin / 64; ++j)
+        if (j * 64 + lane < m) v[j] = src[j * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < kEvalWin / 64; ++j)
+        if (j * 64 + lane < m) dst[j * 64 + lane] = v[j];
     }
-    it = nx;
+    __syncthreads();
+    for (int i = 0; i < m; ++i) {
+      const int kind = __builtin_amdgcn_readfirstlane(sit[i].kind);
+      if (kind == kItEnd) {
+        end = true;
+        break;
+      }
+      if (kind == kItFine) {
+        const int64_t lo = sgpr64(sit[i].d0) * kSeedBlock;
+        const int64_t hi = (lo + kSeedBlock) < n ? (lo + kSeedBlock) : n;
+        c = fine_walk(dmin, S, lo, hi, c, false, 1.0, 0.0, &dummy);
+      } else if (kind == kItMark) {
+        if (lane == 0) markc[sgpr64(sit[i].d0)] = c;
+      } else {
+        SeedItem it;
+        it.kind = kind;
+        it.e = __builtin_amdgcn_readfirstlane(sit[i].e);
+        it.d0 = sgpr64(sit[i].d0);
+        it.d1 = sgpr64(sit[i].d1);
+        it.p = __builtin_bit_cast(double, sgpr64(__builtin_bit_cast(long long, sit[i].p)));
+        if (!item_apply(it, c)) {
+          ok = false;
+          break;
+        }
+      }
+    }
   }
   if (lane == 0) {
     res[0] = c;
@@ -1271,34 +1315,61 @@ static void seed_track(Ctx& c) {
 }
 
 // NumPy's pairwise tree over m elements (np_pairwise): leaves of <= 128, split
-// at n/2 rounded down to a multiple of 8.
-static void pw_layout(int64_t off, int64_t m, std::vector<int>& leaves, std::vector<int>& post) {
+// at n/2 rounded down to a multiple of 8.  Returns the node's height (leaves
+// 0); internal nodes are collected as (height, left, right) with leaf ids
+// and internal ids (-1 - index into `inner`).
+static int pw_layout(int64_t off, int64_t m, std::vector<int>& leaves,
+                     std::vector<std::array<int, 3>>& inner, int& id) {
   if (m <= 128) {
+    id = (int)leaves.size() / 2;
     leaves.push_back((int)off);
     leaves.push_back((int)m);
-    post.push_back(1);
-    return;
+    return 0;
   }
   int64_t m2 = m / 2;
   m2 -= m2 % 8;
-  pw_layout(off, m2, leaves, post);
-  pw_layout(off + m2, m - m2, leaves, post);
-  post.push_back(0);
+  int l, r;
+  const int hl = pw_layout(off, m2, leaves, inner, l);
+  const int hr = pw_layout(off + m2, m - m2, leaves, inner, r);
+  const int h = 1 + (hl > hr ? hl : hr);
+  inner.push_back({h, l, r});
+  id = -(int)inner.size();  // internal node -1 - index
+  return h;
 }
 
 static void seed_tail_plan(Ctx& c, int64_t m) {
   if (c.seed_tail_m == m) return;
-  std::vector<int> leaves, post;
-  pw_layout(0, m, leaves, post);
+  std::vector<int> leaves;
+  std::vector<std::array<int, 3>> inner;
+  int root;
+  const int H = pw_layout(0, m, leaves, inner, root);
   const int nl = (int)leaves.size() / 2;
-  if (nl > kTailLeaves) CDR_FAIL(CDR_ERR_UNSUPPORTED, "pairwise tail layout too large");
+  if (nl > kTailLeaves || H > kTailHeights)
+    CDR_FAIL(CDR_ERR_UNSUPPORTED, "pairwise tail layout too large");
+  // internal nodes in height order; ids: leaves 0..nl-1, internal nl + rank
+  std::vector<int> order(inner.size()), rank(inner.size());
+  for (size_t i = 0; i < inner.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return inner[a][0] < inner[b][0]; });
+  for (size_t r = 0; r < order.size(); ++r) rank[order[r]] = (int)r;
+  auto nid = [&](int x) { return x >= 0 ? x : nl + rank[-1 - x]; };
   std::vector<int> plan(leaves);
-  plan.insert(plan.end(), post.begin(), post.end());
+  std::vector<int> hstart(H + 1, 0);
+  for (int h = 1, r = 0; h <= H; ++h) {
+    hstart[h - 1] = r;
+    while (r < (int)order.size() && inner[order[r]][0] == h) ++r;
+    hstart[h] = r;
+  }
+  plan.insert(plan.end(), hstart.begin(), hstart.end());
+  for (int r : order) {
+    plan.push_back(nid(inner[r][1]));
+    plan.push_back(nid(inner[r][2]));
+  }
   c.seed_tail_plan.ensure(sizeof(int) * plan.size());
   HIP_CHECK(hipMemcpy(c.seed_tail_plan.p, plan.data(), sizeof(int) * plan.size(),
                       hipMemcpyHostToDevice));
   c.seed_tail_nleaves = nl;
-  c.seed_tail_npost = (int)post.size();
+  c.seed_tail_nheights = H;
   c.seed_tail_m = m;
 }
 
@@ -1345,7 +1416,7 @@ void seed_update(Ctx& c, const double* cen) {
       seed_tail_plan(c, c.n - nfull * kSeedBlock);
       hipLaunchKernelGGL(seed_tail_sum_kernel, dim3(1), dim3(256), 0, c.stream,
                          c.dmin.as<double>(), nfull, c.seed_tail_plan.as<int>(),
-                         c.seed_tail_nleaves, c.seed_tail_npost, c.blocksums.as<double>());
+                         c.seed_tail_nleaves, c.seed_tail_nheights, c.blocksums.as<double>());
       HIP_CHECK(hipGetLastError());
     }
   }
