@@ -157,7 +157,7 @@ def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> N
                    "parallelism": f"files and events partitioned over {world} GPU(s), "
                                   "RCCL MAX all-reduce of the last timestamp"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": pmc_traffic("4", ne),
                      "kernel": "features group-by (csrc/groupby.hip: file-id partition + "
                                "per-bucket LDS hash), all kernels of one step",
                      "alg_bytes_per_launch": alg_bytes, "kernel_ms": gb_ms,

@@ -243,6 +243,12 @@ struct Ctx {
   // ---- medians / features scratch ----
   DevBuf med_vals, med_off, med_out, med_tmp, med_tmp2, med_hist;
   int32_t med_k = 0;  // clusters of the grouped rows (cdr_medians_group)
+  // timestamp range of the resident events (min, max, any null), computed by
+  // the producer that wrote them (events_ts_range, groupby.hip); valid for
+  // ev_tsr_n events until another writer of ev_ts clears ev_tsr_valid
+  DevBuf ev_tsr;
+  bool ev_tsr_valid = false;
+  int64_t ev_tsr_n = -1;
   DevBuf ev_file, ev_op, ev_client, ev_ts, ev_primary, ev_out, ev_scratch,
       ev_scratch2;
   DevBuf ev_part;  // int64 per ts_minmax workgroup: min, max
@@ -288,6 +294,7 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums,
 void seed_reset(Ctx& c);
 void seed_update(Ctx& c, const double* cent);
 void seed_scan(Ctx& c, double total, double c_in, double* c_out);
+void events_ts_range(Ctx& c, int64_t ne);
 void seed_scan_begin(Ctx& c, double total, double c_guess, int64_t* n_items, int64_t* n_fine);
 void seed_scan_items(Ctx& c, cdr_seed_item* out, int64_t cap, int64_t* n_items);
 void seed_scan_end(Ctx& c, double c_in, double* c_out);

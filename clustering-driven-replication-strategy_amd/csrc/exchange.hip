@@ -234,6 +234,7 @@ int cdr_features_exchange_unpack(cdr_ctx* h, const void* recv, int64_t n, int64_
   }
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.ev_n = n;
+  events_ts_range(c, n);
   c.ev_nf = nfl;
   // the packed client field must hold every received id (and the owned
   // primaries the local manifest gave: keep the wider of the two)
@@ -271,6 +272,7 @@ int cdr_features_load_events(cdr_ctx* h, int64_t n, const int32_t* file, const u
   for (int64_t i = 0; i < n; ++i) cmax = std::max(cmax, (int)client[i]);
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.ev_n = n;
+  events_ts_range(c, n);
   c.ev_nf = n_files;
   c.ev_cmax = cmax;
   CDR_CATCH

@@ -359,6 +359,7 @@ void features_aggregate(Ctx& c, int64_t ne, const int32_t* file_idx, const uint8
     HIP_CHECK(hipMemcpyAsync(c.ev_client.p, client, 4 * ne, hipMemcpyHostToDevice, c.stream));
     HIP_CHECK(hipMemcpyAsync(c.ev_ts.p, ts_us, 8 * ne, hipMemcpyHostToDevice, c.stream));
   }
+  c.ev_tsr_valid = false;  // the group-by computes the range itself
   if (n_files > 0)
     HIP_CHECK(hipMemcpyAsync(c.ev_primary.p, primary, 4 * n_files, hipMemcpyHostToDevice,
                              c.stream));
@@ -562,6 +563,7 @@ void features_generate(Ctx& c, int64_t ne, int64_t n_files, unsigned long long s
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.ev_n = ne;
+  events_ts_range(c, ne);
   c.ev_nf = n_files;
   c.ev_cmax = 2;
 }

@@ -102,6 +102,9 @@ __device__ __forceinline__ void lds_scan(const unsigned* cnt, unsigned* lp, int 
 }
 
 // ---- K1 --------------------------------------------------------------------
+// TS = false: the producer already has the timestamp range (events_ts_range),
+// only the file ids are read (4 B per event instead of 12).
+template <bool TS>
 __global__ __launch_bounds__(kGbThreads) void gb_hist1(
     const int32_t* __restrict__ file, const long long* __restrict__ ts, int64_t ne, int64_t nf,
     int shift1, int R1, unsigned* __restrict__ tilepref, unsigned* __restrict__ chunksum,
@@ -124,13 +127,14 @@ __global__ __launch_bounds__(kGbThreads) void gb_hist1(
     for (int j = 0; j < kGbPer; ++j) {
       const int64_t e = base + j * kGbThreads + tid;
       fr[j] = e < ne ? file[e] : -1;
-      tv[j] = e < ne ? ts[e] : kTsNullG;
+      tv[j] = (TS && e < ne) ? ts[e] : kTsNullG;
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kGbPer; ++j) {
       const int64_t e = base + j * kGbThreads + tid;
-      if (tv[j] == kTsNullG) {
+      if (!TS) {
+      } else if (tv[j] == kTsNullG) {
         nul |= e < ne;
       } else {
         lo = min(lo, tv[j]);
@@ -192,7 +196,8 @@ __global__ __launch_bounds__(kGbMaxBins) void gb_scan1b(unsigned* __restrict__ r
                                                         int R1, const long long* __restrict__ part,
                                                         int64_t C, unsigned* __restrict__ binbase,
                                                         int* __restrict__ tile2start,
-                                                        long long* __restrict__ res) {
+                                                        long long* __restrict__ res,
+                                                        const long long* __restrict__ tsr) {
   __shared__ long long wred[3][8];
   __shared__ unsigned wsum[8], wt[8];
   const int tid = threadIdx.x;
@@ -263,9 +268,68 @@ __global__ __launch_bounds__(kGbMaxBins) void gb_scan1b(unsigned* __restrict__ r
       hi = max(hi, wred[1][i]);
       nul |= wred[2][i];
     }
-    res[0] = lo;
-    res[1] = hi;
-    res[2] = nul;
+    res[0] = tsr ? tsr[0] : lo;
+    res[1] = tsr ? tsr[1] : hi;
+    res[2] = tsr ? tsr[2] : nul;
+  }
+}
+
+// Timestamp range of n events (min and max of the non-null ones, any null):
+// per-workgroup partials, then one workgroup.
+__global__ __launch_bounds__(256) void gb_tsr_part(const long long* __restrict__ ts, int64_t n,
+                                                   long long* __restrict__ part) {
+  long long lo = LLONG_MAX, hi = LLONG_MIN, nul = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const long long t = ts[i];
+    if (t == kTsNullG) {
+      nul = 1;
+    } else {
+      lo = min(lo, t);
+      hi = max(hi, t);
+    }
+  }
+  __shared__ long long red[3][4];
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o));
+    hi = max(hi, __shfl_xor(hi, o));
+    nul |= __shfl_xor(nul, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = lo;
+    red[1][w] = hi;
+    red[2][w] = nul;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i) {
+      lo = min(lo, red[0][i]);
+      hi = max(hi, red[1][i]);
+      nul |= red[2][i];
+    }
+    part[3 * blockIdx.x] = lo;
+    part[3 * blockIdx.x + 1] = hi;
+    part[3 * blockIdx.x + 2] = nul;
+  }
+}
+
+__global__ __launch_bounds__(64) void gb_tsr_fin(const long long* __restrict__ part, int nb,
+                                                 long long* __restrict__ out) {
+  long long lo = LLONG_MAX, hi = LLONG_MIN, nul = 0;
+  for (int b = threadIdx.x; b < nb; b += 64) {
+    lo = min(lo, part[3 * b]);
+    hi = max(hi, part[3 * b + 1]);
+    nul |= part[3 * b + 2];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o));
+    hi = max(hi, __shfl_xor(hi, o));
+    nul |= __shfl_xor(nul, o);
+  }
+  if (threadIdx.x == 0) {
+    out[0] = lo;
+    out[1] = hi;
+    out[2] = nul;
   }
 }
 
@@ -347,55 +411,52 @@ __global__ __launch_bounds__(kGbThreads) __attribute__((amdgpu_waves_per_eu(4)))
     s.cnt[tid] = 0;
     s.goff[tid] = chunkbase[c * R1 + tid] + tilepref[t * R1 + tid];
   }
-  // thread tid takes the tile's events base + 16 tid .. + 15 in two halves of
-  // 8: 16-byte loads (a wave reads 2 KiB of file ids contiguously), and the
-  // packed payload of a half is built before the next half is loaded
+  // thread tid takes the tile's event quads q = j * 512 + tid (events
+  // base + 4 q .. + 3), j = 0..3: every load instruction of a wave reads one
+  // contiguous span (file / client ids 1 KiB, timestamps 2 x 1 KiB, op bytes
+  // 256 B), so each cache line is used whole by the instruction that brings
+  // it in.  (Lane-contiguous runs of 16 events left lines half-read between
+  // instructions and, with the tile's working set over the L2, re-fetched:
+  // 29.6 B read per 17-B event.)  The order of events inside a tile does not
+  // matter to the partition.
   T val[kGbPer];
   unsigned dr[kGbPer];
-  const int64_t e0 = base + (int64_t)tid * kGbPer;
-  const bool full = e0 + kGbPer <= ne;
+  const bool full = base + kGbTile <= ne;
 #pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    constexpr int H = kGbPer / 2;
-    const int64_t eh = e0 + hf * H;
-    int fr[H], cv[H];
-    long long tv[H];
-    uint8_t ov[H];
+  for (int j = 0; j < kGbPer / 4; ++j) {
+    const int64_t q = (int64_t)j * kGbThreads + tid;
+    const int64_t eq = base + 4 * q;
+    int fr[4], cv[4];
+    long long tv[4];
+    uint8_t ov[4];
     if (full) {
-      const int4* f4 = reinterpret_cast<const int4*>(file + eh);
-      const int4* c4 = reinterpret_cast<const int4*>(client + eh);
-      const longlong2* t2 = reinterpret_cast<const longlong2*>(ts + eh);
-      const uint2 o2 = *reinterpret_cast<const uint2*>(op + eh);
+      const int4 a = reinterpret_cast<const int4*>(file + base)[q];
+      const int4 b = reinterpret_cast<const int4*>(client + base)[q];
+      const longlong2 t0 = reinterpret_cast<const longlong2*>(ts + base)[2 * q];
+      const longlong2 t1 = reinterpret_cast<const longlong2*>(ts + base)[2 * q + 1];
+      const unsigned o4 = reinterpret_cast<const unsigned*>(op + base)[q];
+      fr[0] = a.x, fr[1] = a.y, fr[2] = a.z, fr[3] = a.w;
+      cv[0] = b.x, cv[1] = b.y, cv[2] = b.z, cv[3] = b.w;
+      tv[0] = t0.x, tv[1] = t0.y, tv[2] = t1.x, tv[3] = t1.y;
 #pragma unroll
-      for (int q = 0; q < H / 4; ++q) {
-        const int4 a = f4[q], b = c4[q];
-        fr[4 * q] = a.x, fr[4 * q + 1] = a.y, fr[4 * q + 2] = a.z, fr[4 * q + 3] = a.w;
-        cv[4 * q] = b.x, cv[4 * q + 1] = b.y, cv[4 * q + 2] = b.z, cv[4 * q + 3] = b.w;
-      }
-#pragma unroll
-      for (int q = 0; q < H / 2; ++q) {
-        const longlong2 a = t2[q];
-        tv[2 * q] = a.x, tv[2 * q + 1] = a.y;
-      }
-#pragma unroll
-      for (int j = 0; j < H; ++j) ov[j] = (uint8_t)((j < 4 ? o2.x : o2.y) >> (8 * (j & 3)));
+      for (int r = 0; r < 4; ++r) ov[r] = (uint8_t)(o4 >> (8 * r));
     } else {
 #pragma unroll
-      for (int j = 0; j < H; ++j) {
-        const int64_t e = eh + j;
+      for (int r = 0; r < 4; ++r) {
+        const int64_t e = eq + r;
         const bool in = e < ne;
-        fr[j] = in ? file[e] : -1;
-        tv[j] = in ? ts[e] : 0;
-        ov[j] = in ? op[e] : 0;
-        cv[j] = in ? client[e] : -1;
+        fr[r] = in ? file[e] : -1;
+        tv[r] = in ? ts[e] : 0;
+        ov[r] = in ? op[e] : 0;
+        cv[r] = in ? client[e] : -1;
       }
     }
 #pragma unroll
-    for (int j = 0; j < H; ++j) {
-      const int o = hf * H + j;
-      dr[o] = (fr[j] >= 0 && fr[j] < nf) ? (unsigned)fr[j] >> shift1 : ~0u;
-      val[o] = gb_make<T>(p, (unsigned)((unsigned long long)(unsigned)fr[j] & p.low_mask), tv[j],
-                          ov[j], cv[j]);
+    for (int r = 0; r < 4; ++r) {
+      const int o = 4 * j + r;
+      dr[o] = (fr[r] >= 0 && fr[r] < nf) ? (unsigned)fr[r] >> shift1 : ~0u;
+      val[o] = gb_make<T>(p, (unsigned)((unsigned long long)(unsigned)fr[r] & p.low_mask), tv[r],
+                          ov[r], cv[r]);
     }
   }
   __syncthreads();
@@ -1288,6 +1349,23 @@ void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, bo
 
 }  // namespace
 
+// The resident events' timestamp range, computed once by their producer (the
+// group-by's partition then reads 4 B per event in its histogram pass
+// instead of 12).  Every writer of c.ev_ts calls this or clears
+// c.ev_tsr_valid.
+void events_ts_range(Ctx& c, int64_t ne) {
+  c.ev_tsr.ensure(sizeof(long long) * 4);
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(2048, ceil_div(ne, 256 * 16)));
+  c.gb_part.ensure(sizeof(long long) * 3 * (size_t)nb + 64);
+  hipLaunchKernelGGL(gb_tsr_part, dim3(nb), dim3(256), 0, c.stream, c.ev_ts.as<long long>(), ne,
+                     c.gb_part.as<long long>());
+  hipLaunchKernelGGL(gb_tsr_fin, dim3(1), dim3(64), 0, c.stream, c.gb_part.as<long long>(), nb,
+                     c.ev_tsr.as<long long>());
+  HIP_CHECK(hipGetLastError());
+  c.ev_tsr_valid = true;
+  c.ev_tsr_n = ne;
+}
+
 // The group-by of the events resident in c.ev_* (features_aggregate_resident's
 // hand-written path).  Returns false (nothing computed) when the shape is
 // outside what the packed payload and bucket tables can hold; the caller then
@@ -1324,9 +1402,11 @@ bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max
   // profiling: events 0 (start), 1 (partition done), 2 (buckets done)
   prof_step_begin(c);
   prof_mark(c, 0);
-  hipLaunchKernelGGL(gb_hist1, dim3(C), dim3(kGbThreads), 0, c.stream, c.ev_file.as<int32_t>(),
-                     c.ev_ts.as<long long>(), ne, nf, fbits - B1, R1,
-                     c.gb_tilepref.as<unsigned>(), c.gb_chunk.as<unsigned>(),
+  // the producer's timestamp range, when it computed one for these events
+  const bool tsr = c.ev_tsr_valid && c.ev_tsr_n == ne && !getenv("CDR_GB_TSRANGE");
+  hipLaunchKernelGGL(tsr ? gb_hist1<false> : gb_hist1<true>, dim3(C), dim3(kGbThreads), 0,
+                     c.stream, c.ev_file.as<int32_t>(), c.ev_ts.as<long long>(), ne, nf,
+                     fbits - B1, R1, c.gb_tilepref.as<unsigned>(), c.gb_chunk.as<unsigned>(),
                      c.gb_part.as<long long>());
   HIP_CHECK(hipGetLastError());
   unsigned* binbase = c.gb_small.as<unsigned>();
@@ -1337,7 +1417,7 @@ bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max
                      C, R1, c.gb_rsum.as<unsigned>());
   hipLaunchKernelGGL(gb_scan1b, dim3(1), dim3(kGbMaxBins), 0, c.stream, c.gb_rsum.as<unsigned>(),
                      G, R1, c.gb_part.as<long long>(), C, binbase, tile2start,
-                     c.gb_res.as<long long>());
+                     c.gb_res.as<long long>(), tsr ? c.ev_tsr.as<long long>() : nullptr);
   hipLaunchKernelGGL(gb_scan1c, dim3(G), dim3(kGbMaxBins), 0, c.stream, c.gb_chunk.as<unsigned>(),
                      C, R1, c.gb_rsum.as<unsigned>(), binbase);
   HIP_CHECK(hipGetLastError());

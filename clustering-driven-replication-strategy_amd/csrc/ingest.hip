@@ -635,6 +635,7 @@ void ingest_manifest(Ctx& c, int64_t n_files, const char* pbytes, const int64_t*
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.ing_nfiles = n_files;
   c.ev_n = 0;
+  c.ev_tsr_valid = false;
   c.ev_nf = 0;
 }
 
@@ -723,6 +724,7 @@ void ingest_parse(Ctx& c, int64_t* status) {
     status[5] = e[1];
   }
   c.ev_n = nrec;
+  events_ts_range(c, nrec);
   c.ev_nf = c.ing_nfiles;
   c.ev_cmax = std::max(0, c.ing_nnodes - 1);  // client ids are node ids (or < 0)
 }

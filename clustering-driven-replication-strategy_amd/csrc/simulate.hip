@@ -278,6 +278,7 @@ int64_t features_simulate(Ctx& c, int64_t nf, int64_t file_begin, double duratio
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipStreamSynchronize(c.stream));
   c.ev_n = ne;
+  events_ts_range(c, ne);
   c.ev_nf = nf;
   c.ev_cmax = n_clients - 1;
   return ne;

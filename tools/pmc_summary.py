@@ -51,6 +51,28 @@ for key in sorted(agg):
                  f" waitcnt {c.get('SQ_WAIT_ANY', 0) / w:.2f}")
     print(line)
 
+if json_cfg is not None and "--groupby" in sys.argv:
+    # config 4: HBM bytes of all group-by kernels (gb_*) of one step = their
+    # total over the run / the number of gb_hist1 launches (one per step)
+    import json
+    steps = sum(1 for k in agg if "gb_hist1" in names[k] and "FETCH_SIZE" in agg[k])
+    # gb_tsr_*: the producer's timestamp range, once per event set, not per step
+    step_k = [k for k in agg if "gb_" in names[k] and "gb_tsr" not in names[k]]
+    rb = sum(agg[k]["FETCH_SIZE"] for k in step_k if "FETCH_SIZE" in agg[k]) * 2048
+    wb = sum(agg[k]["WRITE_SIZE"] for k in step_k if "WRITE_SIZE" in agg[k]) * 1024
+    if steps:
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "profiles", "pmc_traffic.json")
+        rec = json.load(open(path)) if os.path.exists(path) else {}
+        rec[json_cfg] = {"n_local": json_n, "hbm_bytes_per_launch": (rb + wb) / steps,
+                         "read_bytes": rb / steps, "write_bytes": wb / steps, "source": root,
+                         "kernel": "all gb_* kernels of one group-by step",
+                         "note": "FETCH_SIZE KiB x2 (gfx950 half-count) + WRITE_SIZE KiB, "
+                                 "summed over the step's kernels"}
+        json.dump(rec, open(path, "w"), indent=1)
+        print("wrote", path, rec[json_cfg])
+    json_cfg = None
+
 if json_cfg is not None:
     # HBM bytes of the last steady-state (DELTA) screen32 launch: read + write
     import json
