@@ -231,6 +231,9 @@ struct Ctx {
   double seed_prog_total = 0.0;
   bool seed_prog_ready = false;
   long long seed_fallbacks = 0;  // programs whose guess failed (block walk instead)
+  DevBuf seed_x16, seed_e16, seed_mu;  // fp16-certified seeding copy (seed.hip)
+  bool seed16_valid = false;
+  std::vector<float> seed_ch_host;  // the centre in that copy's coordinates
   DevBuf seed_tail_plan;  // pairwise layout of the partial last block (seed.hip)
   int64_t seed_tail_m = -1;
   int seed_tail_nleaves = 0, seed_tail_nheights = 0;

@@ -27,6 +27,8 @@
 #include <cstring>
 #include <vector>
 
+#include <hip/hip_fp16.h>
+
 #include "cdr_internal.h"
 #include "exact_math.h"
 
@@ -231,6 +233,179 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
           }
         }
         sdm[spos(q)] = v;
+      }
+    }
+    __syncthreads();
+    if (!TAIL) {
+      const int t = threadIdx.x;
+      const int L = t >> 3, j = t & 7;
+      double r = sdm[spos(128 * L + j)];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) r = r + sdm[spos(128 * L + j + 8 * i)];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) r = r + __shfl_xor(r, o);
+      if ((t & 63) == 0) swave[t >> 6] = r;
+      __syncthreads();
+      if (t == 0) halves[h] = (swave[0] + swave[1]) + (swave[2] + swave[3]);
+      __syncthreads();
+    }
+  }
+  if (!TAIL && threadIdx.x == 0) blocksums[b] = halves[0] + halves[1];
+}
+
+// ---- fp16-certified update (F32X points, d in {8, 16, 32, 64}) --------------
+// A k-means++ step changes few minima: most points are farther from the new
+// centre than from their nearest one.  A half-size copy proves that for most
+// points without reading them in fp32: x16 = fp16 of xh = (x - mu) 2^tau
+// (tau = sigma + 14, |xh| < 2^14), grouped by 8 features, [G][n_pad] x 16 B,
+// with e16[i] >= ||xh_i - x16_i|| (computed exactly in fp64 when the copy is
+// built, rounded up).  With ch = (c - mu) 2^tau rounded to fp32 (Ec >=
+// ||ch32 - ch||), the fp32 a = ||x16_i - ch32|| has relative error below
+// (D + 8) 2^-23, so
+//     ||x_i - c|| >= (a (1 - (D + 8) 2^-23) - e16[i] - Ec) 2^-tau = r_lo,
+// and r_lo^2 >= dmin (1 + 2^-30) proves the NumPy-order distance (relative
+// error < 2^-45, as seed_prunable) is >= dmin: min(dmin, .) leaves it
+// unchanged.  Only the points it cannot prove read the fp32 row and take the
+// exact path; the triangle-inequality pruning (seed_prunable) runs first.
+constexpr int kSeed16Tau = 14;
+
+__global__ __launch_bounds__(256) void seed16_pack_kernel(const float* __restrict__ x32,
+                                                          int64_t n, int64_t n_pad, int d,
+                                                          const float* __restrict__ mu,
+                                                          double scale,
+                                                          uint4* __restrict__ x16,
+                                                          float* __restrict__ e16) {
+  const int G = (d + 7) / 8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double err = 0.0;
+    for (int g = 0; g < G; ++g) {
+      unsigned short hv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = 8 * g + j;
+        double v = 0.0;
+        if (f < d && i < n) v = ((double)x32[xidx(f, i, n_pad)] - (double)mu[f]) * scale;
+        const __half h = __float2half_rn((float)v);
+        const double dv = v - (double)__half2float(h);
+        err += dv * dv;
+        hv[j] = __half_as_ushort(h);
+      }
+      uint4 w;
+      w.x = hv[0] | ((unsigned)hv[1] << 16);
+      w.y = hv[2] | ((unsigned)hv[3] << 16);
+      w.z = hv[4] | ((unsigned)hv[5] << 16);
+      w.w = hv[6] | ((unsigned)hv[7] << 16);
+      x16[(int64_t)g * n_pad + i] = w;
+    }
+    // non-finite (an fp16 overflow) never certifies
+    const double e = sqrt(err) * (1.0 + 0x1p-20) + 0x1p-60;
+    e16[i] = isfinite(e) ? (float)e : INFINITY;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void seed_update16_kernel(
+    const float* __restrict__ X, const uint4* __restrict__ x16, const float* __restrict__ e16,
+    int64_t n, int64_t n_pad, const double* __restrict__ cen, const float* __restrict__ ch,
+    float Ec, double rscale, double* __restrict__ dmin, double* __restrict__ blocksums,
+    int32_t* __restrict__ near, const double* __restrict__ ccd, int cidx) {
+  constexpr int kHalf = 4096;
+  constexpr int G = (D + 7) / 8;
+  constexpr int Q = (D + 3) / 4;
+  constexpr int U = D <= 8 ? 4 : (D <= 32 ? 2 : 1);
+  constexpr float kRel = 1.0f - (float)(D + 8) * 0x1p-23f;
+  __shared__ double sdm[kHalf + kHalf / 16];
+  __shared__ double swave[4];
+  const int64_t b = blockIdx.x;
+  const int64_t base = b * kSeedBlock;
+  const int m = (n - base) < kSeedBlock ? (int)(n - base) : kSeedBlock;
+  const bool TAIL = m < kSeedBlock;
+  auto spos = [](int q) { return q + (q >> 4); };
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* X4 = reinterpret_cast<const f4v*>(X);
+  double halves[2] = {0.0, 0.0};
+  for (int h = 0; h < 2; ++h) {
+    for (int q0 = threadIdx.x; q0 < kHalf; q0 += U * 256) {
+      double old[U];
+      bool go[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int qi = h * kHalf + q0 + 256 * u;
+        const int64_t i = base + qi;
+        go[u] = false;
+        old[u] = 0.0;
+        if (qi < m) {
+          old[u] = dmin[i];
+          go[u] = cidx == 0 || !seed_prunable(ccd[near[i]], old[u]);
+        }
+      }
+      // the fp16 certificate
+      uint4 hv[U][G];
+      float ev[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + h * kHalf + q0 + 256 * u;
+        if (go[u]) {
+#pragma unroll
+          for (int g = 0; g < G; ++g) hv[u][g] = x16[(int64_t)g * n_pad + i];
+          ev[u] = e16[i];
+        }
+      }
+      bool need[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        need[u] = go[u];
+        if (go[u] && cidx > 0) {
+          float s = 0.0f;
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const unsigned w[4] = {hv[u][g].x, hv[u][g].y, hv[u][g].z, hv[u][g].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              if (8 * g + j < D) {
+                const float xv = __half2float(
+                    __ushort_as_half((unsigned short)(w[j >> 1] >> (16 * (j & 1)))));
+                const float t = xv - ch[8 * g + j];
+                s = fmaf(t, t, s);
+              }
+            }
+          }
+          const float lo = sqrtf(s) * kRel - ev[u] - Ec;
+          if (lo > 0.0f) {
+            const double r = (double)lo * rscale;
+            need[u] = !(r * r >= old[u] * (1.0 + 0x1p-30));
+          }
+        }
+      }
+      // the exact path for the points left
+      f4v xv[U][Q];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + h * kHalf + q0 + 256 * u;
+        if (need[u]) {
+#pragma unroll
+          for (int qq = 0; qq < Q; ++qq) xv[u][qq] = X4[(int64_t)qq * n_pad + i];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + 256 * u;
+        const int qi = h * kHalf + q;
+        double v = old[u];
+        if (need[u]) {
+          auto xf = [&](int f) { return (double)xv[u][f >> 2][f & 3]; };
+          auto cf = [&](int f) { return cen[f]; };
+          const double R = np_sqdist(xf, cf, D);
+          const double r = sqrt(R);
+          const double t = r * r;
+          if (t < old[u]) {
+            v = t;
+            dmin[base + qi] = t;
+            near[base + qi] = cidx;
+          }
+        }
+        sdm[spos(q)] = qi < m ? v : 0.0;
       }
     }
     __syncthreads();
@@ -1378,7 +1553,8 @@ void seed_update(Ctx& c, const double* cen) {
   if (!c.dmin.p) seed_reset(c);
   const int64_t nb = c.nblocks();
   c.blocksums.ensure(sizeof(double) * (nb > 0 ? nb : 1));
-  c.seed_scalar.ensure(sizeof(double) * (c.d + 8));
+  c.seed_scalar.ensure(sizeof(double) * (2 * c.d + 8));
+  c.seed_ch_host.resize(c.d);
   HIP_CHECK(hipMemcpyAsync(c.seed_scalar.p, cen, sizeof(double) * c.d, hipMemcpyHostToDevice,
                            c.stream));
   if (!c.seed_near.p) {  // dmin from an earlier session without the tracking buffers
@@ -1399,6 +1575,58 @@ void seed_update(Ctx& c, const double* cen) {
                                    CDR_SU(15), CDR_SU(16)};
 #undef CDR_SU
     const int64_t nfull = c.n / kSeedBlock;
+    static const bool no16 = std::getenv("CDR_SEED16") && std::atoi(std::getenv("CDR_SEED16")) == 0;
+    const int d = c.d;
+    if (c.mode == CDR_MODE_F32X && (d == 8 || d == 16 || d == 32 || d == 64) && !no16) {
+      const int tau = c.sigma + kSeed16Tau;
+      const int G = (d + 7) / 8;
+      if (!c.seed16_valid) {
+        c.seed_x16.ensure(sizeof(uint4) * (size_t)G * c.n_pad);
+        c.seed_e16.ensure(sizeof(float) * c.n_pad);
+        c.seed_mu.ensure(sizeof(float) * d);
+        HIP_CHECK(hipMemcpyAsync(c.seed_mu.p, c.mu.data(), sizeof(float) * d,
+                                 hipMemcpyHostToDevice, c.stream));
+        hipLaunchKernelGGL(seed16_pack_kernel, dim3(4096), dim3(256), 0, c.stream,
+                           c.x32.as<float>(), c.n, c.n_pad, d, c.seed_mu.as<float>(),
+                           std::ldexp(1.0, tau), c.seed_x16.as<uint4>(), c.seed_e16.as<float>());
+        HIP_CHECK(hipGetLastError());
+        c.seed16_valid = true;
+      }
+      // the centre in the copy's coordinates (fp32) and its rounding error
+      double ec = 0.0;
+      for (int f = 0; f < d; ++f) {
+        const double v = (cen[f] - (double)c.mu[f]) * std::ldexp(1.0, tau);
+        c.seed_ch_host[f] = (float)v;
+        const double r = v - (double)c.seed_ch_host[f];
+        ec += r * r;
+      }
+      const float Ec = (float)(std::sqrt(ec) * (1.0 + 0x1p-20) + 0x1p-60);
+      float* dch = reinterpret_cast<float*>(c.seed_scalar.as<double>() + d + 8);
+      HIP_CHECK(hipMemcpyAsync(dch, c.seed_ch_host.data(), sizeof(float) * d,
+                               hipMemcpyHostToDevice, c.stream));
+      typedef void (*S16Fn)(const float*, const uint4*, const float*, int64_t, int64_t,
+                            const double*, const float*, float, double, double*, double*,
+                            int32_t*, const double*, int);
+      const S16Fn f16 = d == 8    ? seed_update16_kernel<8>
+                        : d == 16 ? seed_update16_kernel<16>
+                        : d == 32 ? seed_update16_kernel<32>
+                                  : seed_update16_kernel<64>;
+      hipLaunchKernelGGL(f16, dim3(nb), dim3(256), 0, c.stream, c.x32.as<float>(),
+                         c.seed_x16.as<uint4>(), c.seed_e16.as<float>(), c.n, c.n_pad,
+                         c.seed_scalar.as<double>(), dch, Ec, std::ldexp(1.0, -tau),
+                         c.dmin.as<double>(), c.blocksums.as<double>(), near, ccd, cidx);
+      HIP_CHECK(hipGetLastError());
+      if (nb > nfull) {
+        seed_tail_plan(c, c.n - nfull * kSeedBlock);
+        hipLaunchKernelGGL(seed_tail_sum_kernel, dim3(1), dim3(256), 0, c.stream,
+                           c.dmin.as<double>(), nfull, c.seed_tail_plan.as<int>(),
+                           c.seed_tail_nleaves, c.seed_tail_nheights, c.blocksums.as<double>());
+        HIP_CHECK(hipGetLastError());
+      }
+      c.seed_count += 1;
+      c.seed_scanned = false;
+      return;
+    }
     const SeedFn fn = c.d <= 16 ? fns[c.d]
                       : c.d == 32 ? seed_update_kernel<float, 32>
                       : c.d == 64 ? seed_update_kernel<float, 64>
