@@ -415,3 +415,20 @@ def test_seed_programs_compose_over_shards(ctx):
             assert (i1 if i1 >= 0 else cut + i2) == want
     finally:
         b.close()
+
+
+@pytest.mark.parametrize("n,d,k", [(150_000, 64, 24), (150_000, 32, 24), (200_000, 8, 16),
+                                   (120_000, 16, 40)])
+def test_seeding_fp16_certificate_vs_oracle(ctx, n, d, k):
+    """The fp16-certified seeding update (csrc/seed.hip seed_update16_kernel):
+    minima it proves unchanged without the fp32 row must be exactly the ones
+    the reference leaves unchanged — the seeds equal the reference run's,
+    including with duplicated rows (zero distances, exact ties) and a far
+    outlier (kmeans_plusplus.py:13-20)."""
+    import kmeans_plusplus as kp
+
+    X = synth.generate(n, 0, n, d, k, 31 * n + d)
+    X[::97] = X[5]  # duplicates of one row
+    X[n // 2] = X[n // 2] + 8.0  # an outlier
+    init = kp.kmeans_plusplus_init(X, k, random_state=11, context=ctx)
+    np.testing.assert_array_equal(init, ko.kmeans_plusplus_init(X, k, random_state=11))
