@@ -293,7 +293,7 @@ def ingest_bench(args, world: int, rank: int, dist, device, json_fd: int) -> Non
                    "parallelism": f"log slices partitioned over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": "ingest (nl_count + hipcub scan + nl_write + parse), log bytes "
+                     "kernel": "ingest (nl_count + tile-count scan + nl_write + parse), log bytes "
                                "resident", "alg_bytes_per_launch": alg,
                      "kernel_ms": parse_s * 1e3},
         "log_GBps": nbytes / parse_s / 1e9,
