@@ -15,14 +15,19 @@
 //
 //   A  f64_blocksum   per 256-row block: approximate per-(cluster, feature)
 //                     sums (any order) and member counts
-//   B  f64_predict    per (cluster, feature): running approximate prefix ->
-//                     the binade the exact running value is expected to be in
+//   B  f64_predict_a/b/c  per (cluster, feature): running approximate prefix
+//                     (group sums, group prefix, in-group prefix) -> the
+//                     binade the exact running value is expected to be in
 //                     when each block starts
 //   C  f64_transfer   per (block, feature): the block's transfer for every
 //                     cluster in its predicted binade (flagged when an addend
 //                     is negative or not below the binade's top)
-//   D  f64_walk       per (cluster, feature), sequential over the blocks: the
-//                     exact running value; a block whose prediction missed,
+//   G  f64_group      per (cluster, feature) and group of 64 blocks: the
+//                     group's composed transfer when all its blocks share one
+//                     predicted binade
+//   D  f64_walk       per (cluster, feature), sequential over the groups (one
+//                     step each) and, where a group cannot be applied whole,
+//                     its blocks: the exact running value; a block whose prediction missed,
 //                     whose transfer is flagged or would leave the binade is
 //                     re-added element by element in real fp64 (so the result
 //                     is exact whatever the data; the prediction only decides
@@ -70,41 +75,70 @@ __global__ __launch_bounds__(kFB) void f64_blocksum(const double* __restrict__ X
   for (int i = threadIdx.x; i < k; i += kFB) cnt[b * k + i] = c[i];
 }
 
-// One wave per (cluster, feature): an exclusive prefix of the approximate
-// block sums, 64 blocks per round (any order is fine: it only predicts).
-__global__ __launch_bounds__(256) void f64_predict(const double* __restrict__ A,
-                                                   const unsigned* __restrict__ cnt, int64_t nb,
-                                                   int d, int k, int* __restrict__ E) {
+// The predicted binade of each block's start: an exclusive prefix of the
+// approximate block sums per (cluster, feature), any order (it only
+// predicts), in three parallel passes over groups of 64 blocks: group sums
+// (one wave per sequence and group), the groups' exclusive prefix (one wave
+// per sequence), the blocks' prefix inside each group.
+__device__ __forceinline__ int binade_e(double P) {
+  if (!(P > 0.0) || !isfinite(P)) return kENone;
+  int ex;
+  frexp(P, &ex);  // P in [2^(ex-1), 2^ex)
+  return ex - 1;
+}
+__global__ __launch_bounds__(256) void f64_predict_a(const double* __restrict__ A,
+                                                     const unsigned* __restrict__ cnt,
+                                                     int64_t nb, int d, int k, int64_t ng,
+                                                     double* __restrict__ GS) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= (int64_t)k * d * ng) return;
+  const int t = (int)(w / ng);
+  const int64_t g = w % ng;
+  const int j = t / d;
+  const int64_t b = g * 64 + lane;
+  double v = (b < nb && cnt[b * k + j]) ? A[b * k * d + t] : 0.0;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (lane == 0) GS[w] = v;
+}
+__global__ __launch_bounds__(256) void f64_predict_b(double* __restrict__ GS, int kd,
+                                                     int64_t ng) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (t >= k * d) return;
-  const int j = t / d;
+  if (t >= kd) return;
+  double* gs = GS + (int64_t)t * ng;
   double carry = 0.0;
-  // one round ahead (a single wave scans the sequence: latency-bound)
-  auto fetch = [&](int64_t b0) -> double {
-    const int64_t b = b0 + lane;
-    return (b < nb && cnt[b * k + j]) ? A[b * k * d + t] : 0.0;
-  };
-  double vn = fetch(0);
-  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
-    const int64_t b = b0 + lane;
-    const double v = vn;
-    if (b0 + 64 < nb) vn = fetch(b0 + 64);
+  for (int64_t g0 = 0; g0 < ng; g0 += 64) {
+    const int64_t g = g0 + lane;
+    const double v = g < ng ? gs[g] : 0.0;
     double inc = v;
     for (int o = 1; o < 64; o <<= 1) {
       const double u = __shfl_up(inc, o);
       if (lane >= o) inc += u;
     }
-    const double P = carry + (inc - v);
-    int e = kENone;
-    if (P > 0.0 && isfinite(P)) {
-      int ex;
-      frexp(P, &ex);  // P in [2^(ex-1), 2^ex)
-      e = ex - 1;
-    }
-    if (b < nb) E[b * k * d + t] = e;
+    if (g < ng) gs[g] = carry + (inc - v);
     carry += __shfl(inc, 63);
   }
+}
+__global__ __launch_bounds__(256) void f64_predict_c(const double* __restrict__ A,
+                                                     const unsigned* __restrict__ cnt,
+                                                     int64_t nb, int d, int k, int64_t ng,
+                                                     const double* __restrict__ GS,
+                                                     int* __restrict__ E) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= (int64_t)k * d * ng) return;
+  const int t = (int)(w / ng);
+  const int64_t g = w % ng;
+  const int j = t / d;
+  const int64_t b = g * 64 + lane;
+  const double v = (b < nb && cnt[b * k + j]) ? A[b * k * d + t] : 0.0;
+  double inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const double u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (b < nb) E[b * k * d + t] = binade_e(GS[w] + (inc - v));
 }
 
 // One thread per (block, feature); the per-cluster transfer states live in
@@ -134,9 +168,24 @@ __global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_
     me[j] = E[b * k * d + (int64_t)j * d + f];
   }
   const int64_t r0 = b * kFB, r1 = min(n, r0 + kFB);
-  for (int64_t row = r0; row < r1; ++row) {
-    const int j = labels[row];
-    const double x = X[xidx(f, row, n_pad)];
+  // rows in chunks of 16: the chunk's labels and values are loaded before
+  // the (serial, LDS-dependent) updates, so the loop does not pay a memory
+  // round trip per row
+  constexpr int kCh = 16;
+  for (int64_t rc = r0; rc < r1; rc += kCh) {
+    int lj[kCh];
+    double lx[kCh];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int64_t row = rc + u;
+      lj[u] = row < r1 ? labels[row] : -1;
+      lx[u] = row < r1 ? X[xidx(f, row, n_pad)] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+    const int j = lj[u];
+    if (j < 0) continue;
+    const double x = lx[u];
     int fl = mfl[j] | 8;
     const int e = me[j];
     if (e == kENone || !(x >= 0.0)) {
@@ -162,6 +211,7 @@ __global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_
     mdd[j] += (int)(i1 - i0);
     fl = (fl & ~3) | (int)((p0 + i0) & 1) | ((int)((p1 + i1) & 1) << 1);
     mfl[j] = fl;
+    }
   }
   for (int j = 0; j < k; ++j) {
     Xfer x;
@@ -190,6 +240,54 @@ __device__ __forceinline__ XferC xc_compose(const XferC& a, const XferC& b) {
   return r;
 }
 
+// Group transfers: one wave per (cluster, feature) and group of 64 blocks
+// (all groups in parallel): when every non-empty block of the group is
+// predicted in one binade with a usable transfer, their composition (the
+// same 6-level shuffle tree as f64_walk's) so that the walk applies the
+// whole group in one step.
+struct GXfer {
+  long long d0, d1;
+  int e;
+  int p;  // bit0 P0, bit1 P1, bit2 usable, bit3 any member
+};
+__global__ __launch_bounds__(256) void f64_group(const unsigned* __restrict__ cnt,
+                                                 const int* __restrict__ E,
+                                                 const Xfer* __restrict__ T, int64_t nb, int d,
+                                                 int k, int64_t ng, GXfer* __restrict__ G) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int kd = k * d;
+  if (w >= (int64_t)kd * ng) return;
+  const int t = (int)(w / ng);
+  const int64_t g = w % ng;
+  const int j = t / d;
+  const int64_t bl = g * 64 + lane;
+  const bool in = bl < nb;
+  const unsigned c = in ? cnt[bl * k + j] : 0u;
+  const int el = in ? E[bl * kd + t] : kENone;
+  const Xfer xl = in ? T[bl * kd + t] : Xfer{0, 0, 4};
+  const unsigned long long live = __ballot(c != 0);
+  int e0 = kENone;
+  if (live) e0 = __shfl(el, __ffsll((long long)live) - 1);
+  const bool ok = c == 0 || (e0 != kENone && el == e0 && !(xl.flags & 4));
+  const bool usable = live && __ballot(!ok) == 0ull;
+  XferC x;
+  const bool on = c != 0;
+  x.d0 = on ? xl.d0 : 0;
+  x.d1 = on ? xl.d0 + xl.dd : 0;
+  x.p = on ? (xl.flags & 3) : 2;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    XferC y;
+    y.d0 = __shfl_down(x.d0, o);
+    y.d1 = __shfl_down(x.d1, o);
+    y.p = __shfl_down(x.p, o);
+    if ((lane & (2 * o - 1)) == 0 && lane + o < 64) x = xc_compose(x, y);
+  }
+  if (lane == 0)
+    G[w] = GXfer{x.d0, x.d1, e0, (x.p & 3) | (usable ? 4 : 0) | (live ? 8 : 0)};
+}
+
 // One wave per (cluster, feature), the running value uniform across it.  The
 // lanes load 64 blocks' (count, prediction, transfer) per round; the wave
 // takes the longest run of blocks from the current one that are empty or
@@ -206,6 +304,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
                                                 const unsigned* __restrict__ cnt,
                                                 const int* __restrict__ E,
                                                 const Xfer* __restrict__ T,
+                                                const GXfer* __restrict__ G, int64_t ng,
                                                 double* __restrict__ sums,
                                                 long long* __restrict__ walked) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -248,8 +347,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
       }
     }
   };
-  // the round's (count, prediction, transfer) per lane, loaded one round ahead
-  // (a single wave walks the sequence: the load latency would set its time)
+  // a group's (count, prediction, transfer) per lane
   auto fetch = [&](int64_t b0, unsigned& c, int& el, Xfer& xl) {
     const int64_t bl = b0 + lane;
     const bool in = bl < nb;
@@ -257,64 +355,94 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
     el = in ? E[bl * k * d + t] : kENone;
     xl = in ? T[bl * k * d + t] : Xfer{0, 0, 4};
   };
-  unsigned cn;
-  int eln;
-  Xfer xn;
-  fetch(0, cn, eln, xn);
-  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
-    const unsigned c = cn;
-    const int el = eln;
-    Xfer xl = xn;
-    if (!c) xl = Xfer{0, 0, 4};
-    if (b0 + 64 < nb) fetch(b0 + 64, cn, eln, xn);
-    const unsigned long long live = __ballot(c != 0);
-    int i = 0;  // next block of this round (wave-uniform)
-    while (i < 64) {
-      const unsigned long long rest = live & (~0ull << i);
-      if (!rest) break;
-      i = __ffsll((long long)rest) - 1;  // skip empty blocks
-      int es = kENone;
-      if (s > 0.0) {
+  // Groups are read 64 at a time (one load per lane, the next 64 prefetched)
+  // and taken from registers: a group that applies in one step costs no
+  // memory round trip.  The per-block records are loaded only for a group
+  // that does not (about one per binade crossing).
+  const GXfer* Gt = G + (int64_t)t * ng;
+  auto gfetch = [&](int64_t g0) {
+    return g0 + lane < ng ? Gt[g0 + lane] : GXfer{0, 0, kENone, 0};
+  };
+  GXfer gnext = gfetch(0);
+  for (int64_t g0 = 0; g0 < ng; g0 += 64) {
+    const GXfer gl = gnext;
+    if (g0 + 64 < ng) gnext = gfetch(g0 + 64);
+    const unsigned long long gl_live = __ballot((gl.p & 8) != 0);
+    unsigned long long todo = gl_live;
+    while (todo) {
+      const int gi = __ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const int gp = __shfl(gl.p, gi);
+      if ((gp & 4) && s > 0.0) {  // the whole group in one step
+        const int ge = __shfl(gl.e, gi);
         int ex;
         frexp(s, &ex);
-        es = ex - 1;
+        if (ex - 1 == ge) {
+          const long long gd0 = __shfl(gl.d0, gi), gd1 = __shfl(gl.d1, gi);
+          const long long m = (long long)ldexp(s, 52 - ge);
+          const long long m2 = m + ((m & 1) ? gd1 : gd0);
+          if (m2 < (1ll << 53)) {
+            s = ldexp((double)m2, ge - 52);
+            continue;
+          }
+        }
       }
-      // blocks i.. that are empty or can take a transfer in binade es
-      const bool compat = c == 0 || (es != kENone && !(xl.flags & 4) && el == es);
-      const unsigned long long brk = ~__ballot(compat) & (~0ull << i);
-      const int r = brk ? __ffsll((long long)brk) - 1 : 64;  // run [i, r)
-      if (r > i + 1) {
-        XferC x;
-        const bool on = lane >= i && lane < r && c != 0;
-        x.d0 = on ? xl.d0 : 0;
-        x.d1 = on ? xl.d0 + xl.dd : 0;
-        x.p = on ? (xl.flags & 3) : 2;  // identity: P0 = 0, P1 = 1
+      const int64_t b0 = (g0 + gi) * 64;
+      unsigned c;
+      int el;
+      Xfer xl;
+      fetch(b0, c, el, xl);
+      if (!c) xl = Xfer{0, 0, 4};
+      const unsigned long long live = __ballot(c != 0);
+      int i = 0;  // next block of this group (wave-uniform)
+      while (i < 64) {
+        const unsigned long long rest = live & (~0ull << i);
+        if (!rest) break;
+        i = __ffsll((long long)rest) - 1;  // skip empty blocks
+        int es = kENone;
+        if (s > 0.0) {
+          int ex;
+          frexp(s, &ex);
+          es = ex - 1;
+        }
+        // blocks i.. that are empty or can take a transfer in binade es
+        const bool compat = c == 0 || (es != kENone && !(xl.flags & 4) && el == es);
+        const unsigned long long brk = ~__ballot(compat) & (~0ull << i);
+        const int r = brk ? __ffsll((long long)brk) - 1 : 64;  // run [i, r)
+        if (r > i + 1) {
+          XferC x;
+          const bool on = lane >= i && lane < r && c != 0;
+          x.d0 = on ? xl.d0 : 0;
+          x.d1 = on ? xl.d0 + xl.dd : 0;
+          x.p = on ? (xl.flags & 3) : 2;  // identity: P0 = 0, P1 = 1
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {  // lane 0 ends with lanes 0..63 in order
-          XferC y;
-          y.d0 = __shfl_down(x.d0, o);
-          y.d1 = __shfl_down(x.d1, o);
-          y.p = __shfl_down(x.p, o);
-          if ((lane & (2 * o - 1)) == 0 && lane + o < 64) x = xc_compose(x, y);
+          for (int o = 1; o < 64; o <<= 1) {  // lane 0 ends with lanes 0..63 in order
+            XferC y;
+            y.d0 = __shfl_down(x.d0, o);
+            y.d1 = __shfl_down(x.d1, o);
+            y.p = __shfl_down(x.p, o);
+            if ((lane & (2 * o - 1)) == 0 && lane + o < 64) x = xc_compose(x, y);
+          }
+          const long long D0 = __shfl(x.d0, 0), D1 = __shfl(x.d1, 0);
+          const long long m = (long long)ldexp(s, 52 - es);
+          const long long m2 = m + ((m & 1) ? D1 : D0);
+          if (m2 < (1ll << 53)) {
+            s = ldexp((double)m2, es - 52);
+            i = r;
+            continue;
+          }
+          // the run leaves the binade somewhere: block by block
         }
-        const long long D0 = __shfl(x.d0, 0), D1 = __shfl(x.d1, 0);
-        const long long m = (long long)ldexp(s, 52 - es);
-        const long long m2 = m + ((m & 1) ? D1 : D0);
-        if (m2 < (1ll << 53)) {
-          s = ldexp((double)m2, es - 52);
-          i = r;
-          continue;
-        }
-        // the run leaves the binade somewhere: block by block
+        const int e = __shfl(el, i);
+        const int flags = __shfl(xl.flags, i);
+        const long long d0 = __shfl(xl.d0, i);
+        const int dd = __shfl(xl.dd, i);
+        step_block(b0 + i, e, flags, d0, dd);
+        ++i;
       }
-      const int e = __shfl(el, i);
-      const int flags = __shfl(xl.flags, i);
-      const long long d0 = __shfl(xl.d0, i);
-      const int dd = __shfl(xl.dd, i);
-      step_block(b0 + i, e, flags, d0, dd);
-      ++i;
     }
   }
+
   if (lane == 0) {
     sums[(int64_t)j * d + f] = s;
     walked[t] = nwalk;
@@ -340,8 +468,15 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
                      c.x64.as<double>(), n, c.n_pad, d, k, c.labels.as<int32_t>(),
                      c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>());
   HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(f64_predict, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
-                     c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), nb, d, k,
+  const int64_t ng = ceil_div(nb, (int64_t)64);
+  c.f64x_GS.ensure(sizeof(double) * ng * kd);
+  const dim3 gwaves((unsigned)ceil_div((int64_t)kd * ng, (int64_t)4));
+  hipLaunchKernelGGL(f64_predict_a, gwaves, dim3(256), 0, c.stream, c.f64x_A.as<double>(),
+                     c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>());
+  hipLaunchKernelGGL(f64_predict_b, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
+                     c.f64x_GS.as<double>(), (int)kd, ng);
+  hipLaunchKernelGGL(f64_predict_c, gwaves, dim3(256), 0, c.stream, c.f64x_A.as<double>(),
+                     c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>(),
                      c.f64x_E.as<int>());
   HIP_CHECK(hipGetLastError());
   const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
@@ -350,10 +485,15 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
                      c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
                      c.f64x_E.as<int>(), c.f64x_T.as<Xfer>());
   HIP_CHECK(hipGetLastError());
+  c.f64x_G.ensure(sizeof(GXfer) * ng * kd);
+  hipLaunchKernelGGL(f64_group, dim3(ceil_div((int64_t)kd * ng, (int64_t)4)), dim3(256), 0,
+                     c.stream, c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(),
+                     c.f64x_T.as<Xfer>(), nb, d, k, ng, c.f64x_G.as<GXfer>());
+  HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(f64_walk, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
                      c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
-                     c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(), d_sums,
-                     c.f64x_walk.as<long long>());
+                     c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(),
+                     c.f64x_G.as<GXfer>(), ng, d_sums, c.f64x_walk.as<long long>());
   HIP_CHECK(hipGetLastError());
   return true;
 }

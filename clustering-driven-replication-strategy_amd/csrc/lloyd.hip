@@ -750,6 +750,42 @@ __global__ void assign_exact_all(const T* __restrict__ X, int64_t n, int64_t n_p
   }
 }
 
+// The same with the point's d <= 16 features loaded into registers once
+// (assign_exact_all re-reads them from memory for every centroid) and the
+// NumPy-order distance unrolled for that d; the centroid values are uniform
+// (scalar) loads.
+template <typename T, int D>
+__global__ __launch_bounds__(256) void assign_exact_d(const T* __restrict__ X, int64_t n,
+                                                      int64_t n_pad,
+                                                      const double* __restrict__ C, int k,
+                                                      int32_t* __restrict__ labels) {
+  for (int64_t pt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pt < n;
+       pt += (int64_t)gridDim.x * blockDim.x) {
+    double xr[D];
+#pragma unroll
+    for (int f = 0; f < D; ++f) xr[f] = (double)X[xidx(f, pt, n_pad)];
+    labels[pt] = exact_argmin([&](int f) { return xr[f]; }, C, k, D);
+  }
+}
+
+template <typename T>
+static void launch_assign_exact(const T* X, int64_t n, int64_t n_pad, int d, const double* C,
+                                int k, int32_t* labels, int cus, hipStream_t st) {
+  typedef void (*Fn)(const T*, int64_t, int64_t, const double*, int, int32_t*);
+#define CDR_AE(D_) assign_exact_d<T, D_>
+  static const Fn fns[17] = {nullptr,     CDR_AE(1),  CDR_AE(2),  CDR_AE(3),  CDR_AE(4),
+                             CDR_AE(5),   CDR_AE(6),  CDR_AE(7),  CDR_AE(8),  CDR_AE(9),
+                             CDR_AE(10),  CDR_AE(11), CDR_AE(12), CDR_AE(13), CDR_AE(14),
+                             CDR_AE(15),  CDR_AE(16)};
+#undef CDR_AE
+  const dim3 grid(std::max(1, (int)std::min<int64_t>(ceil_div(n, 256), (int64_t)cus * 8)));
+  if (d >= 1 && d <= 16)
+    hipLaunchKernelGGL(fns[d], grid, dim3(256), 0, st, X, n, n_pad, C, k, labels);
+  else
+    hipLaunchKernelGGL(assign_exact_all<T>, grid, dim3(256), 0, st, X, n, n_pad, d, C, k, labels);
+  HIP_CHECK(hipGetLastError());
+}
+
 // Fixed-point sums from labels (F32X shapes without the screen): LDS table per
 // workgroup, plain stores of the table, reduce_partials afterwards.
 __global__ __launch_bounds__(256) void update_from_labels_f32x(
@@ -1224,10 +1260,8 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
     c.lab8_valid = false;
     c.big_valid = false;
     // exact assignment for every point, then fixed-point sums from labels
-    hipLaunchKernelGGL(assign_exact_all<float>, dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 8))),
-                       dim3(256), 0, c.stream, c.x32.as<float>(), c.n, c.n_pad, d,
-                       c.cent64.as<double>(), k, c.labels.as<int32_t>());
-    HIP_CHECK(hipGetLastError());
+    launch_assign_exact<float>(c.x32.as<float>(), c.n, c.n_pad, d, c.cent64.as<double>(), k,
+                               c.labels.as<int32_t>(), cus, c.stream);
     const size_t lds = (size_t)len * 8;
     if (lds > 64 * 1024) CDR_FAIL(CDR_ERR_UNSUPPORTED, "k*(d+1) too large for the update table");
     int nwg = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(c.n, 256), cus * 2));
@@ -1289,13 +1323,11 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
   const int cus = lloyd_num_cus(c.device);
   upload_centroids(c, C, k);
   const bool prof = prof_step_begin(c);
-  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "assign_exact_all<double>");
+  snprintf(c.prof_kernel, sizeof(c.prof_kernel),
+           d <= 16 ? "assign_exact_d<double, %d>" : "assign_exact_all<double>", d);
   if (prof) prof_mark(c, 0);
-  hipLaunchKernelGGL(assign_exact_all<double>,
-                     dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 8))),
-                     dim3(256), 0, c.stream, c.x64.as<double>(), c.n, c.n_pad, d,
-                     c.cent64.as<double>(), k, c.labels.as<int32_t>());
-  HIP_CHECK(hipGetLastError());
+  launch_assign_exact<double>(c.x64.as<double>(), c.n, c.n_pad, d, c.cent64.as<double>(), k,
+                              c.labels.as<int32_t>(), cus, c.stream);
   if (prof) prof_mark(c, 1);
   c.f64_sums.ensure(sizeof(double) * (size_t)k * d);
   c.f64_counts.ensure(sizeof(long long) * k * 2);
