@@ -68,8 +68,19 @@ class Comm:
 
         import _cdr
 
-        uid = np.frombuffer(_cdr.comm_unique_id(), dtype=np.uint8) if self.rank == 0 \
-            else np.zeros(128, dtype=np.uint8)
+        # every rank probes librccl first and the ranks agree (MIN) before any
+        # of them enters the collective init: one rank that cannot load it
+        # must not leave the others waiting in ncclCommInitRank
+        try:
+            own = np.frombuffer(_cdr.comm_unique_id(), dtype=np.uint8)
+            ok = 1
+        except Exception:  # noqa: BLE001 - any failure means "no native comm"
+            own, ok = np.zeros(128, dtype=np.uint8), 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=self.device)
+        self.dist.all_reduce(flag, op=self.dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            return False
+        uid = own if self.rank == 0 else np.zeros(128, dtype=np.uint8)
         t = torch.from_numpy(uid.copy()).to(self.device)
         self.dist.broadcast(t, 0)
         ctx.comm_init(t.cpu().numpy().tobytes(), self.world, self.rank)
