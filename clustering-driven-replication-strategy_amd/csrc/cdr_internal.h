@@ -148,7 +148,7 @@ struct Ctx {
   DevBuf f64_sums;  // double k*d
   DevBuf f64_counts;  // int64 k
   // f64sum.hip: block sums, counts, predicted binades, transfers, walk counts
-  DevBuf f64x_A, f64x_cnt, f64x_E, f64x_T, f64x_walk, f64x_G, f64x_GS;
+  DevBuf f64x_A, f64x_cnt, f64x_E, f64x_T, f64x_walk, f64x_G, f64x_GS, f64x_prof;
   int64_t f64x_walked = -1;  // blocks re-added element-wise in the last F64 step (-1: serial)
   HostBuf h_small;  // pinned scratch for small D2H
   HostBuf h_up;     // pinned staging of the per-step screen32 upload

@@ -35,6 +35,9 @@
 //                     ~log2(n) times per sequence for non-negative data).
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "cdr_internal.h"
 
@@ -306,7 +309,8 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
                                                 const Xfer* __restrict__ T,
                                                 const GXfer* __restrict__ G, int64_t ng,
                                                 double* __restrict__ sums,
-                                                long long* __restrict__ walked) {
+                                                long long* __restrict__ walked,
+                                                long long* __restrict__ prof) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= k * d) return;
@@ -314,6 +318,8 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
   double s = 0.0;
   bool any = false;  // NumPy's reduce starts from the first selected row
   long long nwalk = 0;
+  long long pc_el = 0, pc_slow = 0, n_slow = 0;  // CDR_F64_PROF: cycles
+  const long long pc0 = prof ? (long long)clock64() : 0;
   // one block by transfer or element by element (wave-uniform b)
   auto step_block = [&](int64_t b, int e, int flags, long long d0, int dd) {
     bool ok = false;
@@ -331,6 +337,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
     }
     if (!ok) {  // element by element, in real fp64 (row order)
       ++nwalk;
+      const long long pe0 = prof ? (long long)clock64() : 0;
       const int64_t r0 = b * kFB;
       for (int q = 0; q < kFB; q += 64) {
         const int64_t row = r0 + q + lane;
@@ -338,13 +345,19 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
         const double x = mine ? X[xidx(f, row, n_pad)] : 0.0;
         unsigned long long mk = __ballot(mine);
         while (mk) {
-          const int l = __ffsll((long long)mk) - 1;
+          const int l = __builtin_amdgcn_readfirstlane(__ffsll((long long)mk) - 1);
           mk &= mk - 1;
-          const double v = __shfl(x, l);
+          const long long xb = __double_as_longlong(x);
+          const double v = __longlong_as_double(
+              (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
+                               (int)(xb >> 32), l)
+                           << 32) |
+                          (unsigned)__builtin_amdgcn_readlane((int)xb, l)));
           s = any ? s + v : v;
           any = true;
         }
       }
+      if (prof) pc_el += (long long)clock64() - pe0;
     }
   };
   // a group's (count, prediction, transfer) per lane
@@ -363,6 +376,21 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
   auto gfetch = [&](int64_t g0) {
     return g0 + lane < ng ? Gt[g0 + lane] : GXfer{0, 0, kENone, 0};
   };
+  // The running value as (binade sE, grid count sN) while groups apply whole
+  // (integer work on scalar registers: readlane, no LDS shuffles and no
+  // double <-> integer conversions per group); s is refreshed from it before
+  // a group is walked block by block, and it from s afterwards.
+  int sE = kENone;
+  long long sN = 0;
+  auto to_int = [&]() {
+    sE = kENone;
+    if (s > 0.0) {
+      int ex;
+      frexp(s, &ex);
+      sE = ex - 1;
+      sN = (long long)ldexp(s, 52 - sE);  // exact: s is on the grid
+    }
+  };
   GXfer gnext = gfetch(0);
   for (int64_t g0 = 0; g0 < ng; g0 += 64) {
     const GXfer gl = gnext;
@@ -370,23 +398,31 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
     const unsigned long long gl_live = __ballot((gl.p & 8) != 0);
     unsigned long long todo = gl_live;
     while (todo) {
-      const int gi = __ffsll((long long)todo) - 1;
+      const int gi = __builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
       todo &= todo - 1;
-      const int gp = __shfl(gl.p, gi);
-      if ((gp & 4) && s > 0.0) {  // the whole group in one step
-        const int ge = __shfl(gl.e, gi);
-        int ex;
-        frexp(s, &ex);
-        if (ex - 1 == ge) {
-          const long long gd0 = __shfl(gl.d0, gi), gd1 = __shfl(gl.d1, gi);
-          const long long m = (long long)ldexp(s, 52 - ge);
-          const long long m2 = m + ((m & 1) ? gd1 : gd0);
+      const int gp = __builtin_amdgcn_readlane(gl.p, gi);
+      if ((gp & 4) && sE != kENone) {  // the whole group in one step
+        const int ge = __builtin_amdgcn_readlane(gl.e, gi);
+        if (sE == ge) {
+          const long long gd =
+              (sN & 1) ? (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
+                                          (int)(gl.d1 >> 32), gi)
+                                      << 32) |
+                                     (unsigned)__builtin_amdgcn_readlane((int)gl.d1, gi))
+                       : (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
+                                          (int)(gl.d0 >> 32), gi)
+                                      << 32) |
+                                     (unsigned)__builtin_amdgcn_readlane((int)gl.d0, gi));
+          const long long m2 = sN + gd;
           if (m2 < (1ll << 53)) {
-            s = ldexp((double)m2, ge - 52);
+            sN = m2;
             continue;
           }
         }
       }
+      if (sE != kENone) s = ldexp((double)sN, sE - 52);  // s from the integer state
+      const long long ps0 = prof ? (long long)clock64() : 0;
+      ++n_slow;
       const int64_t b0 = (g0 + gi) * 64;
       unsigned c;
       int el;
@@ -398,7 +434,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
       while (i < 64) {
         const unsigned long long rest = live & (~0ull << i);
         if (!rest) break;
-        i = __ffsll((long long)rest) - 1;  // skip empty blocks
+        i = __builtin_amdgcn_readfirstlane(__ffsll((long long)rest) - 1);  // skip empty blocks
         int es = kENone;
         if (s > 0.0) {
           int ex;
@@ -408,39 +444,62 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
         // blocks i.. that are empty or can take a transfer in binade es
         const bool compat = c == 0 || (es != kENone && !(xl.flags & 4) && el == es);
         const unsigned long long brk = ~__ballot(compat) & (~0ull << i);
-        const int r = brk ? __ffsll((long long)brk) - 1 : 64;  // run [i, r)
+        const int r = __builtin_amdgcn_readfirstlane(brk ? __ffsll((long long)brk) - 1 : 64);  // run [i, r)
         if (r > i + 1) {
+          // inclusive ordered prefix of the run's transfers (lanes outside it
+          // are the identity), then the longest prefix that stays in the
+          // binade is applied at once and the block that leaves it is
+          // stepped alone: one scan per binade crossing, not one per block
           XferC x;
           const bool on = lane >= i && lane < r && c != 0;
           x.d0 = on ? xl.d0 : 0;
           x.d1 = on ? xl.d0 + xl.dd : 0;
           x.p = on ? (xl.flags & 3) : 2;  // identity: P0 = 0, P1 = 1
 #pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {  // lane 0 ends with lanes 0..63 in order
+          for (int o = 1; o < 64; o <<= 1) {
             XferC y;
-            y.d0 = __shfl_down(x.d0, o);
-            y.d1 = __shfl_down(x.d1, o);
-            y.p = __shfl_down(x.p, o);
-            if ((lane & (2 * o - 1)) == 0 && lane + o < 64) x = xc_compose(x, y);
+            y.d0 = __shfl_up(x.d0, o);
+            y.d1 = __shfl_up(x.d1, o);
+            y.p = __shfl_up(x.p, o);
+            if (lane >= o) x = xc_compose(y, x);
           }
-          const long long D0 = __shfl(x.d0, 0), D1 = __shfl(x.d1, 0);
           const long long m = (long long)ldexp(s, 52 - es);
-          const long long m2 = m + ((m & 1) ? D1 : D0);
-          if (m2 < (1ll << 53)) {
-            s = ldexp((double)m2, es - 52);
-            i = r;
-            continue;
+          const long long mq = m + ((m & 1) ? x.d1 : x.d0);
+          const bool inrun = lane >= i && lane < r;
+          const unsigned long long bad = __ballot(inrun && !(mq < (1ll << 53)));
+          const int L = __builtin_amdgcn_readfirstlane(bad ? __ffsll((long long)bad) - 1 : r);
+          if (L > i) {  // blocks i .. L-1 in one step
+            const long long mL =
+                (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
+                                 (int)(mq >> 32), L - 1)
+                             << 32) |
+                            (unsigned)__builtin_amdgcn_readlane((int)mq, L - 1));
+            s = ldexp((double)mL, es - 52);
+            i = L;
+            if (i >= r) continue;
           }
-          // the run leaves the binade somewhere: block by block
+          // block L leaves the binade: stepped alone below
         }
-        const int e = __shfl(el, i);
-        const int flags = __shfl(xl.flags, i);
-        const long long d0 = __shfl(xl.d0, i);
-        const int dd = __shfl(xl.dd, i);
+        const int e = __builtin_amdgcn_readlane(el, i);
+        const int flags = __builtin_amdgcn_readlane(xl.flags, i);
+        const long long d0 = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
+                                             (int)(xl.d0 >> 32), i)
+                                         << 32) |
+                                        (unsigned)__builtin_amdgcn_readlane((int)xl.d0, i));
+        const int dd = __builtin_amdgcn_readlane(xl.dd, i);
         step_block(b0 + i, e, flags, d0, dd);
         ++i;
       }
+      to_int();
+      if (prof) pc_slow += (long long)clock64() - ps0;
     }
+  }
+  if (sE != kENone) s = ldexp((double)sN, sE - 52);
+  if (prof && lane == 0) {
+    prof[4 * t] = (long long)clock64() - pc0;
+    prof[4 * t + 1] = pc_slow;
+    prof[4 * t + 2] = pc_el;
+    prof[4 * t + 3] = n_slow;
   }
 
   if (lane == 0) {
@@ -486,6 +545,8 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
                      c.f64x_E.as<int>(), c.f64x_T.as<Xfer>());
   HIP_CHECK(hipGetLastError());
   c.f64x_G.ensure(sizeof(GXfer) * ng * kd);
+  static const bool prof_on = std::getenv("CDR_F64_PROF") != nullptr;
+  if (prof_on) c.f64x_prof.ensure(sizeof(long long) * 4 * kd);
   hipLaunchKernelGGL(f64_group, dim3(ceil_div((int64_t)kd * ng, (int64_t)4)), dim3(256), 0,
                      c.stream, c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(),
                      c.f64x_T.as<Xfer>(), nb, d, k, ng, c.f64x_G.as<GXfer>());
@@ -493,7 +554,20 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
   hipLaunchKernelGGL(f64_walk, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
                      c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
                      c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(),
-                     c.f64x_G.as<GXfer>(), ng, d_sums, c.f64x_walk.as<long long>());
+                     c.f64x_G.as<GXfer>(), ng, d_sums, c.f64x_walk.as<long long>(),
+                     prof_on ? c.f64x_prof.as<long long>() : nullptr);
+  HIP_CHECK(hipGetLastError());
+  if (prof_on) {
+    std::vector<long long> h(4 * kd);
+    HIP_CHECK(hipMemcpyAsync(h.data(), c.f64x_prof.p, 8 * h.size(), hipMemcpyDeviceToHost,
+                             c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    long long mx[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i < kd; ++i)
+      for (int q = 0; q < 4; ++q) mx[q] = std::max(mx[q], h[4 * i + q]);
+    fprintf(stderr, "f64_walk max cycles: total %lld slow-groups %lld element-walks %lld; slow groups %lld\n",
+            mx[0], mx[1], mx[2], mx[3]);
+  }
   HIP_CHECK(hipGetLastError());
   return true;
 }
