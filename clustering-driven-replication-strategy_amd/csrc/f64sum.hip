@@ -74,8 +74,12 @@ __global__ __launch_bounds__(kFB) void f64_blocksum(const double* __restrict__ X
     for (int f = 0; f < d; ++f) atomicAdd(&tab[j * d + f], X[xidx(f, row, n_pad)]);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < k * d; i += kFB) A[b * k * d + i] = tab[i];
-  for (int i = threadIdx.x; i < k; i += kFB) cnt[b * k + i] = c[i];
+  // sequence-major ([cluster * d + feature][block], [cluster][block]): the
+  // later passes walk one sequence over the blocks with the lanes, so their
+  // loads are contiguous
+  const int64_t nbk = gridDim.x;
+  for (int i = threadIdx.x; i < k * d; i += kFB) A[(int64_t)i * nbk + b] = tab[i];
+  for (int i = threadIdx.x; i < k; i += kFB) cnt[(int64_t)i * nbk + b] = c[i];
 }
 
 // The predicted binade of each block's start: an exclusive prefix of the
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(256) void f64_predict_a(const double* __restrict__ 
   const int64_t g = w % ng;
   const int j = t / d;
   const int64_t b = g * 64 + lane;
-  double v = (b < nb && cnt[b * k + j]) ? A[b * k * d + t] : 0.0;
+  double v = (b < nb && cnt[(int64_t)j * nb + b]) ? A[(int64_t)t * nb + b] : 0.0;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   if (lane == 0) GS[w] = v;
 }
@@ -135,13 +139,13 @@ __global__ __launch_bounds__(256) void f64_predict_c(const double* __restrict__ 
   const int64_t g = w % ng;
   const int j = t / d;
   const int64_t b = g * 64 + lane;
-  const double v = (b < nb && cnt[b * k + j]) ? A[b * k * d + t] : 0.0;
+  const double v = (b < nb && cnt[(int64_t)j * nb + b]) ? A[(int64_t)t * nb + b] : 0.0;
   double inc = v;
   for (int o = 1; o < 64; o <<= 1) {
     const double u = __shfl_up(inc, o);
     if (lane >= o) inc += u;
   }
-  if (b < nb) E[b * k * d + t] = binade_e(GS[w] + (inc - v));
+  if (b < nb) E[(int64_t)t * nb + b] = binade_e(GS[w] + (inc - v));
 }
 
 // One thread per (block, feature); the per-cluster transfer states live in
@@ -157,6 +161,7 @@ __global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_
   int* se = sfl + (size_t)nt * k;                         // [nt][k]
   const int64_t t = (int64_t)blockIdx.x * nt + threadIdx.x;
   const bool live = t < nb * d;
+  // the d threads of one block are neighbours: they share its label stream
   const int64_t b = live ? t / d : 0;
   const int f = live ? (int)(t % d) : 0;
   long long* m0 = s0 + (size_t)threadIdx.x * k;
@@ -168,7 +173,7 @@ __global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_
     m0[j] = 0;
     mdd[j] = 0;
     mfl[j] = 2;  // P0 = 0, P1 = 1
-    me[j] = E[b * k * d + (int64_t)j * d + f];
+    me[j] = E[((int64_t)j * d + f) * nb + b];
   }
   const int64_t r0 = b * kFB, r1 = min(n, r0 + kFB);
   // rows in chunks of 16: the chunk's labels and values are loaded before
@@ -221,7 +226,7 @@ __global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_
     x.d0 = m0[j];
     x.dd = mdd[j];
     x.flags = mfl[j];
-    T[b * k * d + (int64_t)j * d + f] = x;
+    T[((int64_t)j * d + f) * nb + b] = x;
   }
 }
 
@@ -266,9 +271,9 @@ __global__ __launch_bounds__(256) void f64_group(const unsigned* __restrict__ cn
   const int j = t / d;
   const int64_t bl = g * 64 + lane;
   const bool in = bl < nb;
-  const unsigned c = in ? cnt[bl * k + j] : 0u;
-  const int el = in ? E[bl * kd + t] : kENone;
-  const Xfer xl = in ? T[bl * kd + t] : Xfer{0, 0, 4};
+  const unsigned c = in ? cnt[(int64_t)j * nb + bl] : 0u;
+  const int el = in ? E[(int64_t)t * nb + bl] : kENone;
+  const Xfer xl = in ? T[(int64_t)t * nb + bl] : Xfer{0, 0, 4};
   const unsigned long long live = __ballot(c != 0);
   int e0 = kENone;
   if (live) e0 = __shfl(el, __ffsll((long long)live) - 1);
@@ -364,9 +369,9 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
   auto fetch = [&](int64_t b0, unsigned& c, int& el, Xfer& xl) {
     const int64_t bl = b0 + lane;
     const bool in = bl < nb;
-    c = in ? cnt[bl * k + j] : 0u;
-    el = in ? E[bl * k * d + t] : kENone;
-    xl = in ? T[bl * k * d + t] : Xfer{0, 0, 4};
+    c = in ? cnt[(int64_t)j * nb + bl] : 0u;
+    el = in ? E[(int64_t)t * nb + bl] : kENone;
+    xl = in ? T[(int64_t)t * nb + bl] : Xfer{0, 0, 4};
   };
   // Groups are read 64 at a time (one load per lane, the next 64 prefetched)
   // and taken from registers: a group that applies in one step costs no
