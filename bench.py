@@ -650,6 +650,7 @@ def main() -> None:
         "fallback_frac": fb_frac,
         "queued_frac": q_frac,
         "seed_s": seed_s,
+        "seed_scans": ctx.seed_stats(),  # cumsum programs / fallbacks to the block walk
         "final_shift": st["shift"],
         "final_inertia": st["inertia"],
     }

@@ -69,6 +69,7 @@ SIGNATURES = {
     "cdr_seed_scan_items": ([_P, _P, _I64, _PI64], None),
     "cdr_seed_scan_end": ([_P, _F64, _PF64], None),
     "cdr_seed_program_eval": ([_P, _I64, _F64, _PF64, _PI32], None),
+    "cdr_seed_stats": ([_P, _PI64], None),
     "cdr_lloyd_step": ([_P, _P, _I32, _P, _I32], None),
     "cdr_lloyd_step_f64": ([_P, _P, _I32, _P, _P], None),
     "cdr_lloyd_labels": ([_P, _P], None),
@@ -337,6 +338,13 @@ class Context:
         v = _F64()
         _check(self._lib.cdr_seed_scan_end(self._h, float(c_in), ctypes.byref(v)))
         return float(v.value)
+
+    def seed_stats(self) -> dict:
+        """Cumsum scans run through a program, and those that fell back to
+        the block walk (cdr_seed_stats)."""
+        out = np.zeros(2, dtype=np.int64)
+        _check(self._lib.cdr_seed_stats(self._h, out.ctypes.data_as(_PI64)))
+        return {"programs": int(out[0]), "fallbacks": int(out[1])}
 
     def seed_search(self, c_last: float, u: float) -> int:
         v = _I64()

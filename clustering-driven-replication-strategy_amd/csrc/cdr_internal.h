@@ -230,6 +230,7 @@ struct Ctx {
   DevBuf seg_tails, seg_ents, seg_scan, seg_items, seg_meta;  // cumsum program (seed.hip)
   double seed_prog_total = 0.0;
   bool seed_prog_ready = false;
+  long long seed_programs = 0;   // scans run through a cumsum program
   long long seed_fallbacks = 0;  // programs whose guess failed (block walk instead)
   DevBuf seed_x16, seed_e16, seed_mu;  // fp16-certified seeding copy (seed.hip)
   bool seed16_valid = false;

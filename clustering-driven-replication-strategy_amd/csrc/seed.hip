@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void seed16_pack_kernel(const float* __restric
   }
 }
 
-template <int D>
+template <int D, int UU = 0>
 __global__ __launch_bounds__(256) void seed_update16_kernel(
     const float* __restrict__ X, const uint4* __restrict__ x16, const float* __restrict__ e16,
     int64_t n, int64_t n_pad, const double* __restrict__ cen, const float* __restrict__ ch,
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256) void seed_update16_kernel(
   constexpr int kHalf = 4096;
   constexpr int G = (D + 7) / 8;
   constexpr int Q = (D + 3) / 4;
-  constexpr int U = D <= 8 ? 4 : (D <= 32 ? 2 : 1);
+  constexpr int U = UU ? UU : (D <= 8 ? 4 : (D <= 32 ? 2 : 1));
   constexpr float kRel = 1.0f - (float)(D + 8) * 0x1p-23f;
   __shared__ double sdm[kHalf + kHalf / 16];
   __shared__ double swave[4];
@@ -1607,8 +1607,11 @@ void seed_update(Ctx& c, const double* cen) {
       typedef void (*S16Fn)(const float*, const uint4*, const float*, int64_t, int64_t,
                             const double*, const float*, float, double, double*, double*,
                             int32_t*, const double*, int);
+      static const int u16 = std::getenv("CDR_SEED16_U") ? std::atoi(std::getenv("CDR_SEED16_U")) : 0;
       const S16Fn f16 = d == 8    ? seed_update16_kernel<8>
-                        : d == 16 ? seed_update16_kernel<16>
+                        : d == 16 ? (u16 == 1   ? seed_update16_kernel<16, 1>
+                                     : u16 == 4 ? seed_update16_kernel<16, 4>
+                                                : seed_update16_kernel<16>)
                         : d == 32 ? seed_update16_kernel<32>
                                   : seed_update16_kernel<64>;
       hipLaunchKernelGGL(f16, dim3(nb), dim3(256), 0, c.stream, c.x32.as<float>(),
@@ -1720,6 +1723,7 @@ static void seed_scan_program(Ctx& c, double total, double c_guess) {
   HIP_CHECK(hipGetLastError());
   c.seed_prog_total = total;
   c.seed_prog_ready = true;
+  ++c.seed_programs;
 }
 
 // Runs the program from the exact c_in and fills cend; false when a guess
@@ -1917,6 +1921,14 @@ int cdr_seed_scan_end(cdr_ctx* h, double c_in, double* c_out) {
   if (!h || !c_out) CDR_FAIL(CDR_ERR_ARG, "null argument");
   HIP_CHECK(hipSetDevice(h->c.device));
   seed_scan_end(h->c, c_in, c_out);
+  CDR_CATCH
+}
+
+int cdr_seed_stats(cdr_ctx* h, int64_t* out) {
+  CDR_TRY
+  if (!h || !out) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  out[0] = h->c.seed_programs;
+  out[1] = h->c.seed_fallbacks;
   CDR_CATCH
 }
 

@@ -129,6 +129,9 @@ int cdr_seed_scan_begin(cdr_ctx* ctx, double total, double c_guess, int64_t* n_i
                         int64_t* n_fine);
 int cdr_seed_scan_items(cdr_ctx* ctx, cdr_seed_item* out, int64_t cap, int64_t* n_items);
 int cdr_seed_scan_end(cdr_ctx* ctx, double c_in, double* c_out);
+/* out[0] = scans run through a program, out[1] = of those, the ones whose
+ * guess failed and fell back to the exact block walk (same result).        */
+int cdr_seed_stats(cdr_ctx* ctx, int64_t* out);
 /* *ok = 0 when some item does not hold for this c_in (or a FINE item).      */
 int cdr_seed_program_eval(const cdr_seed_item* items, int64_t n_items, double c_in,
                           double* c_out, int32_t* ok);

@@ -361,6 +361,7 @@ def test_seed_program_cend_exact(ctx, n, outlier):
         X[n // 2] = 50.0
     ctx.load_points(X)
     ctx.seed_reset()
+    st0 = ctx.seed_stats()
     dist = np.full(n, np.inf)
     for c in (X[1], X[n // 3]):
         ctx.seed_update(c)
@@ -375,6 +376,9 @@ def test_seed_program_cend_exact(ctx, n, outlier):
             want = int(np.searchsorted(cdf, u, side="right"))
             got = ctx.seed_search(c_last, float(u))
             assert got == (want if want < n else -1), (u, got, want)
+    st = ctx.seed_stats()
+    assert st["programs"] - st0["programs"] == 2  # both scans went through programs
+    assert st["fallbacks"] == st0["fallbacks"]    # and no guess failed
 
 
 def test_seed_programs_compose_over_shards(ctx):
@@ -432,3 +436,22 @@ def test_seeding_fp16_certificate_vs_oracle(ctx, n, d, k):
     X[n // 2] = X[n // 2] + 8.0  # an outlier
     init = kp.kmeans_plusplus_init(X, k, random_state=11, context=ctx)
     np.testing.assert_array_equal(init, ko.kmeans_plusplus_init(X, k, random_state=11))
+
+
+def test_seeding_program_opaque_blocks(ctx):
+    """Blocks the cumsum program cannot summarise (csrc/seed.hip: more than
+    32 binade crossings in a block -> FINE items walked element by element):
+    a run of zero probabilities from a zero running value, and D^2 values
+    growing 4x per row.  Seeds equal the reference's (kmeans_plusplus.py:
+    13-20) on F64-mode data."""
+    import kmeans_plusplus as kp
+
+    n = 20000
+    X = np.zeros((n, 2))
+    X[8192 + 100: 8192 + 140, 0] = np.ldexp(1.0, np.arange(40) - 20)  # D^2 = 2^(2j - 40)
+    X[15000:, 1] = np.linspace(0.0, 1.0, n - 15000)
+    rs = next(r for r in range(100)
+              if not 8192 + 100 <= int(np.random.default_rng(r).integers(0, n)) < 8192 + 140)
+    for k in (2, 4, 6):
+        init = kp.kmeans_plusplus_init(X, k, random_state=rs, context=ctx)
+        np.testing.assert_array_equal(init, ko.kmeans_plusplus_init(X, k, random_state=rs))
