@@ -70,6 +70,7 @@ SIGNATURES = {
     "cdr_seed_scan_end": ([_P, _F64, _PF64], None),
     "cdr_seed_program_eval": ([_P, _I64, _F64, _PF64, _PI32], None),
     "cdr_seed_stats": ([_P, _PI64], None),
+    "cdr_seed_run": ([_P, _I64, _I32, _P, _P], None),
     "cdr_lloyd_step": ([_P, _P, _I32, _P, _I32], None),
     "cdr_lloyd_step_f64": ([_P, _P, _I32, _P, _P], None),
     "cdr_lloyd_labels": ([_P, _P], None),
@@ -338,6 +339,18 @@ class Context:
         v = _F64()
         _check(self._lib.cdr_seed_scan_end(self._h, float(c_in), ctypes.byref(v)))
         return float(v.value)
+
+    def seed_run(self, first: int, k: int, u) -> np.ndarray:
+        """k-means++ seeding of this context's points with no host round trip
+        per step (cdr_seed_run): first row index and the k - 1 uniforms of the
+        draws -> the k picked row indices."""
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        if u.size != max(k - 1, 0):
+            raise ValueError("need k - 1 uniforms")
+        picks = np.zeros(max(int(k), 1), dtype=np.int64)
+        _check(self._lib.cdr_seed_run(self._h, int(first), int(k), _ptr(u) if u.size else None,
+                                      _ptr(picks)))
+        return picks[:k]
 
     def seed_stats(self) -> dict:
         """Cumsum scans run through a program, and those that fell back to

@@ -339,6 +339,11 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
     rng = np.random.default_rng(random_state)
     C = np.empty((k, d), dtype=np.float64)
     first = int(rng.integers(0, n_total))
+    if comm.world == 1 and k > 1 and hasattr(ctx, "seed_run"):
+        # one shard: every step on the device (cdr_seed_run), one uniform per
+        # draw taken up front (:19)
+        picks = ctx.seed_run(first, k, rng.random(k - 1))
+        return np.asarray(ctx.get_rows(picks), dtype=np.float64)
     owner = _owner_of(offsets, first)
     C[0] = _fetch_row(ctx, comm, owner, first - int(offsets[owner]), d)
     if k > 1:

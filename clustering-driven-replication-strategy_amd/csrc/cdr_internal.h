@@ -234,7 +234,7 @@ struct Ctx {
   long long seed_fallbacks = 0;  // programs whose guess failed (block walk instead)
   DevBuf seed_x16, seed_e16, seed_mu;  // fp16-certified seeding copy (seed.hip)
   bool seed16_valid = false;
-  std::vector<float> seed_ch_host;  // the centre in that copy's coordinates
+  DevBuf seed_run_buf;  // seed_run: uniforms, picks, S, flags
   DevBuf seed_tail_plan;  // pairwise layout of the partial last block (seed.hip)
   int64_t seed_tail_m = -1;
   int seed_tail_nleaves = 0, seed_tail_nheights = 0;
@@ -302,6 +302,7 @@ void events_ts_range(Ctx& c, int64_t ne);
 void seed_scan_begin(Ctx& c, double total, double c_guess, int64_t* n_items, int64_t* n_fine);
 void seed_scan_items(Ctx& c, cdr_seed_item* out, int64_t cap, int64_t* n_items);
 void seed_scan_end(Ctx& c, double c_in, double* c_out);
+void seed_run(Ctx& c, int64_t first, int k, const double* u, int64_t* picks);
 void seed_search(Ctx& c, double c_last, double u, int64_t* idx);
 
 void medians_segmented(Ctx& c, const double* values, const int64_t* offsets,

@@ -304,17 +304,36 @@ __global__ __launch_bounds__(256) void seed16_pack_kernel(const float* __restric
   }
 }
 
+// The centre in the copy's coordinates: ch = fp32 of (c - mu) 2^tau and Ec >=
+// ||ch - (c - mu) 2^tau|| (rounded up), from the device copy of the centre.
+__global__ void seed_ch_kernel(const double* __restrict__ cen, const float* __restrict__ mu,
+                               int d, double scale, float* __restrict__ ch,
+                               float* __restrict__ Ec) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double ec = 0.0;
+  for (int f = 0; f < d; ++f) {
+    const double v = (cen[f] - (double)mu[f]) * scale;
+    const float h = (float)v;
+    ch[f] = h;
+    const double r = v - (double)h;
+    ec += r * r;
+  }
+  Ec[0] = (float)(sqrt(ec) * (1.0 + 0x1p-20) + 0x1p-60);
+}
+
 template <int D, int UU = 0>
 __global__ __launch_bounds__(256) void seed_update16_kernel(
     const float* __restrict__ X, const uint4* __restrict__ x16, const float* __restrict__ e16,
     int64_t n, int64_t n_pad, const double* __restrict__ cen, const float* __restrict__ ch,
-    float Ec, double rscale, double* __restrict__ dmin, double* __restrict__ blocksums,
+    const float* __restrict__ Ecp, double rscale, double* __restrict__ dmin,
+    double* __restrict__ blocksums,
     int32_t* __restrict__ near, const double* __restrict__ ccd, int cidx) {
   constexpr int kHalf = 4096;
   constexpr int G = (D + 7) / 8;
   constexpr int Q = (D + 3) / 4;
   constexpr int U = UU ? UU : (D <= 8 ? 4 : (D <= 32 ? 2 : 1));
   constexpr float kRel = 1.0f - (float)(D + 8) * 0x1p-23f;
+  const float Ec = Ecp[0];
   __shared__ double sdm[kHalf + kHalf / 16];
   __shared__ double swave[4];
   const int64_t b = blockIdx.x;
@@ -536,12 +555,27 @@ __device__ __forceinline__ double from_binade(int e, long long N) {
 // elements, then lane l walks elements [16 l, 16 l + 16) of the pass from LDS
 // (conflict-free ds_read_b64), the 64 lane transfers are composed in order and
 // the pass transfer is composed onto the block's.
+// Device-resident seeding (seed_run): the total S, the running value at the
+// shard's end and the uniform of the draw live in device memory, written by
+// the kernels before; a non-zero *gate (the program's success flag) turns the
+// block-walk fallback kernels into no-ops.  Null pointers: the by-value
+// arguments hold.
+struct SeedDev {
+  const double* S = nullptr;
+  const double* gate = nullptr;
+  const double* c_last = nullptr;
+  const double* u = nullptr;
+};
+
 constexpr int kPass = 1024;
 constexpr int kPassPad = kPass + kPass / 16;
 
 __global__ __launch_bounds__(256) void xfer_kernel(const double* __restrict__ dmin, int64_t n,
                                                    double S, const double* __restrict__ approx,
-                                                   int64_t nblocks, Xfer* __restrict__ out) {
+                                                   int64_t nblocks, Xfer* __restrict__ out,
+    SeedDev dv) {
+  if (dv.gate && dv.gate[0] != 0.0) return;
+  if (dv.S) S = dv.S[0];
   __shared__ double sbuf[4][kPassPad];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -609,7 +643,10 @@ __global__ __launch_bounds__(256) void xfer_kernel(const double* __restrict__ dm
 // approx[b] = c_in + sum_{b' < b} blocksums[b'] / S   (guesses only)
 __global__ __launch_bounds__(1024) void approx_prefix_kernel(const double* __restrict__ bs,
                                                              int64_t nb, double S, double c_in,
-                                                             double* __restrict__ approx) {
+                                                             double* __restrict__ approx,
+    SeedDev dv) {
+  if (dv.gate && dv.gate[0] != 0.0) return;
+  if (dv.S) S = dv.S[0];
   __shared__ double part[1024];
   const int t = threadIdx.x;
   const int64_t per = (nb + 1023) / 1024;
@@ -773,7 +810,10 @@ __global__ __launch_bounds__(64) void walk_kernel(const double* __restrict__ dmi
                                                   int64_t nblocks, double c_in,
                                                   double* __restrict__ cend,
                                                   double* __restrict__ c_out,
-                                                  long long* __restrict__ stats) {
+                                                  long long* __restrict__ stats,
+    SeedDev dv) {
+  if (dv.gate && dv.gate[0] != 0.0) return;
+  if (dv.S) S = dv.S[0];
   __shared__ Xfer sx[kXWin];
   const int lane = threadIdx.x;
   double c = c_in;
@@ -872,7 +912,11 @@ __global__ __launch_bounds__(64) void walk_kernel(const double* __restrict__ dmi
 __global__ __launch_bounds__(64) void search_kernel(const double* __restrict__ dmin, int64_t n,
                                                     double S, const double* __restrict__ cend,
                                                     int64_t nblocks, double c_in, double c_last,
-                                                    double u, int64_t* __restrict__ result) {
+                                                    double u, int64_t* __restrict__ result,
+    SeedDev dv) {
+  if (dv.S) S = dv.S[0];
+  if (dv.c_last) c_last = dv.c_last[0];
+  if (dv.u) u = dv.u[0];
   const int lane = threadIdx.x;
   // invariant: every block < lo misses, block hi hits (hi == nblocks: none)
   int64_t lo = 0, hi = nblocks;
@@ -1095,7 +1139,9 @@ __global__ __launch_bounds__(512) void seg_block_kernel(const double* __restrict
                                                         const double* __restrict__ approx,
                                                         int64_t nblocks,
                                                         SegTail* __restrict__ tails,
-                                                        SegEnt* __restrict__ ents) {
+                                                        SegEnt* __restrict__ ents,
+    SeedDev dv) {
+  if (dv.S) S = dv.S[0];
   __shared__ double s_sum[kSegWaves];
   __shared__ int s_m[kSegWaves], s_bad[kSegWaves], s_h[kSegWaves];
   __shared__ Part s_t[kSegWaves];
@@ -1368,7 +1414,9 @@ __global__ __launch_bounds__(64) void seg_eval_kernel(const double* __restrict__
                                                       const SeedItem* __restrict__ items,
                                                       const long long* __restrict__ meta,
                                                       double c_in, double* __restrict__ markc,
-                                                      double* __restrict__ res) {
+                                                      double* __restrict__ res,
+    SeedDev dv) {
+  if (dv.S) S = dv.S[0];
   __shared__ SeedItem sit[kEvalWin];
   const int lane = threadIdx.x;
   double c = c_in;
@@ -1441,6 +1489,70 @@ __global__ __launch_bounds__(256) void seg_fill_kernel(const SegScan* __restrict
     v = sp_value(e, N + ((N & 1) ? s.s.d1 : s.s.d0));
   }
   cend[b] = v;
+}
+
+// ---- device-resident seeding (seed_run) -----------------------------------
+
+// total = dist_sq.sum() (:18): the block sums added left to right, as the host
+// does (cdr_host_seq_sum).  A total that is not finite and positive raises
+// "Probabilities contain NaN" on the host at the end; S = 1 keeps the rest of
+// the run finite meanwhile.
+__global__ __launch_bounds__(64) void seed_total_kernel(const double* __restrict__ bs,
+                                                        int64_t nb, double* __restrict__ S,
+                                                        double* __restrict__ bad) {
+  // windows of the block sums staged in LDS by the whole wave (coalesced),
+  // then added by one lane from LDS (reads run ahead of the add chain)
+  constexpr int kWin = 4096;
+  __shared__ double2 sv[kWin / 2];
+  const int lane = threadIdx.x;
+  double s = 0.0;
+  for (int64_t w0 = 0; w0 < nb; w0 += kWin) {
+    const int m = (int)((nb - w0) < kWin ? (nb - w0) : kWin);
+    __syncthreads();
+    double* svd = reinterpret_cast<double*>(sv);
+    for (int i = lane; i < m; i += 64) svd[i] = bs[w0 + i];
+    __syncthreads();
+    if (lane == 0) {
+      int i = 0;
+      for (; i + 8 <= m; i += 8) {
+        const double2 a = sv[i / 2], b = sv[i / 2 + 1], c = sv[i / 2 + 2], d = sv[i / 2 + 3];
+        s = s + a.x;
+        s = s + a.y;
+        s = s + b.x;
+        s = s + b.y;
+        s = s + c.x;
+        s = s + c.y;
+        s = s + d.x;
+        s = s + d.y;
+      }
+      for (; i < m; ++i) s = s + svd[i];
+    }
+  }
+  if (lane == 0) {
+    const bool ok = s > 0.0 && !isinf(s);
+    S[0] = ok ? s : 1.0;
+    if (!ok) bad[0] = 1.0;
+  }
+}
+
+// The picked row (exact as fp64) into the centre slot; a missing pick (-1,
+// impossible for a finite total: cdf[-1] == 1 > u) is flagged, row 0 used.
+__global__ __launch_bounds__(64) void seed_gather_kernel(const float* __restrict__ x32,
+                                                         const double* __restrict__ x64,
+                                                         int64_t* __restrict__ pick, int d,
+                                                         int64_t n_pad,
+                                                         double* __restrict__ out,
+                                                         double* __restrict__ bad) {
+  int64_t i = pick[0];
+  if (i < 0) {
+    i = 0;
+    if (threadIdx.x == 0) {
+      bad[1] = 1.0;
+      pick[0] = 0;
+    }
+  }
+  for (int f = threadIdx.x; f < d; f += 64)
+    out[f] = x32 ? (double)x32[xidx(f, i, n_pad)] : x64[xidx(f, i, n_pad)];
 }
 
 // ---------------------------------------------------------------------------
@@ -1548,15 +1660,17 @@ static void seed_tail_plan(Ctx& c, int64_t m) {
   c.seed_tail_m = m;
 }
 
+// cen: the new centre on the host, or nullptr when seed_run has already put
+// it at the start of c.seed_scalar on the device.
 void seed_update(Ctx& c, const double* cen) {
   check_points(c);
   if (!c.dmin.p) seed_reset(c);
   const int64_t nb = c.nblocks();
   c.blocksums.ensure(sizeof(double) * (nb > 0 ? nb : 1));
   c.seed_scalar.ensure(sizeof(double) * (2 * c.d + 8));
-  c.seed_ch_host.resize(c.d);
-  HIP_CHECK(hipMemcpyAsync(c.seed_scalar.p, cen, sizeof(double) * c.d, hipMemcpyHostToDevice,
-                           c.stream));
+  if (cen)
+    HIP_CHECK(hipMemcpyAsync(c.seed_scalar.p, cen, sizeof(double) * c.d, hipMemcpyHostToDevice,
+                             c.stream));
   if (!c.seed_near.p) {  // dmin from an earlier session without the tracking buffers
     c.seed_near.ensure(sizeof(int32_t) * c.n_pad);
     HIP_CHECK(hipMemsetAsync(c.seed_near.p, 0, sizeof(int32_t) * c.n_pad, c.stream));
@@ -1593,20 +1707,14 @@ void seed_update(Ctx& c, const double* cen) {
         c.seed16_valid = true;
       }
       // the centre in the copy's coordinates (fp32) and its rounding error
-      double ec = 0.0;
-      for (int f = 0; f < d; ++f) {
-        const double v = (cen[f] - (double)c.mu[f]) * std::ldexp(1.0, tau);
-        c.seed_ch_host[f] = (float)v;
-        const double r = v - (double)c.seed_ch_host[f];
-        ec += r * r;
-      }
-      const float Ec = (float)(std::sqrt(ec) * (1.0 + 0x1p-20) + 0x1p-60);
       float* dch = reinterpret_cast<float*>(c.seed_scalar.as<double>() + d + 8);
-      HIP_CHECK(hipMemcpyAsync(dch, c.seed_ch_host.data(), sizeof(float) * d,
-                               hipMemcpyHostToDevice, c.stream));
+      float* dEc = dch + d;
+      hipLaunchKernelGGL(seed_ch_kernel, dim3(1), dim3(64), 0, c.stream,
+                         c.seed_scalar.as<double>(), c.seed_mu.as<float>(), d,
+                         std::ldexp(1.0, tau), dch, dEc);
       typedef void (*S16Fn)(const float*, const uint4*, const float*, int64_t, int64_t,
-                            const double*, const float*, float, double, double*, double*,
-                            int32_t*, const double*, int);
+                            const double*, const float*, const float*, double, double*,
+                            double*, int32_t*, const double*, int);
       static const int u16 = std::getenv("CDR_SEED16_U") ? std::atoi(std::getenv("CDR_SEED16_U")) : 0;
       const S16Fn f16 = d == 8    ? seed_update16_kernel<8>
                         : d == 16 ? (u16 == 1   ? seed_update16_kernel<16, 1>
@@ -1616,7 +1724,7 @@ void seed_update(Ctx& c, const double* cen) {
                                   : seed_update16_kernel<64>;
       hipLaunchKernelGGL(f16, dim3(nb), dim3(256), 0, c.stream, c.x32.as<float>(),
                          c.seed_x16.as<uint4>(), c.seed_e16.as<float>(), c.n, c.n_pad,
-                         c.seed_scalar.as<double>(), dch, Ec, std::ldexp(1.0, -tau),
+                         c.seed_scalar.as<double>(), dch, dEc, std::ldexp(1.0, -tau),
                          c.dmin.as<double>(), c.blocksums.as<double>(), near, ccd, cidx);
       HIP_CHECK(hipGetLastError());
       if (nb > nfull) {
@@ -1656,19 +1764,22 @@ void seed_update(Ctx& c, const double* cen) {
 }
 
 // The block-by-block walk (exact from any c_in; the fallback of the program).
-static void seed_scan_walk(Ctx& c, double total, double c_in, double* c_out) {
+// Device-resident mode (seed_run): dv carries S / gate, the running value at
+// the end goes to dres_dev, and nothing is read back (c_out == nullptr).
+static void seed_scan_walk(Ctx& c, double total, double c_in, double* c_out,
+                           const SeedDev& dv = SeedDev{}, double* dres_dev = nullptr) {
   const int64_t nb = c.nblocks();
   c.xfer.ensure(sizeof(Xfer) * nb);
   c.cend.ensure(sizeof(double) * nb * 2);
   double* approx = c.cend.as<double>() + nb;
   hipLaunchKernelGGL(approx_prefix_kernel, dim3(1), dim3(1024), 0, c.stream,
-                     c.blocksums.as<double>(), nb, total, c_in, approx);
+                     c.blocksums.as<double>(), nb, total, c_in, approx, dv);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(xfer_kernel, dim3((int)ceil_div(nb, 4)), dim3(256), 0, c.stream,
-                     c.dmin.as<double>(), c.n, total, approx, nb, c.xfer.as<Xfer>());
+                     c.dmin.as<double>(), c.n, total, approx, nb, c.xfer.as<Xfer>(), dv);
   HIP_CHECK(hipGetLastError());
-  c.seed_scalar.ensure(sizeof(double) * (c.d + 8));
-  double* dres = c.seed_scalar.as<double>() + c.d;
+  c.seed_scalar.ensure(sizeof(double) * (2 * c.d + 8));
+  double* dres = dres_dev ? dres_dev : c.seed_scalar.as<double>() + c.d;
   static const bool want_stats = std::getenv("CDR_SEED_STATS") != nullptr;
   long long* dstats = nullptr;
   if (want_stats) {
@@ -1680,7 +1791,11 @@ static void seed_scan_walk(Ctx& c, double total, double c_in, double* c_out) {
     dstats = ds;
   }
   hipLaunchKernelGGL(walk_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
-                     total, c.xfer.as<Xfer>(), nb, c_in, c.cend.as<double>(), dres, dstats);
+                     total, c.xfer.as<Xfer>(), nb, c_in, c.cend.as<double>(), dres, dstats, dv);
+  if (!c_out) {
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (want_stats) {
     long long hs[8];
     HIP_CHECK(hipMemcpyAsync(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost, c.stream));
@@ -1700,7 +1815,8 @@ static void seed_scan_walk(Ctx& c, double total, double c_in, double* c_out) {
 
 // This shard's cumsum program under the guess c_guess of the running value at
 // its first element (seg_block_kernel, seg_plan_kernel).
-static void seed_scan_program(Ctx& c, double total, double c_guess) {
+static void seed_scan_program(Ctx& c, double total, double c_guess,
+                              const SeedDev& dv = SeedDev{}) {
   const int64_t nb = c.nblocks();
   c.cend.ensure(sizeof(double) * nb * 2);
   double* approx = c.cend.as<double>() + nb;
@@ -1709,12 +1825,14 @@ static void seed_scan_program(Ctx& c, double total, double c_guess) {
   c.seg_scan.ensure(sizeof(SegScan) * nb);
   c.seg_items.ensure(sizeof(SeedItem) * kItemCap);
   c.seg_meta.ensure(sizeof(long long) * 8);
+  SeedDev dvs;  // the program is always built (no gate)
+  dvs.S = dv.S;
   hipLaunchKernelGGL(approx_prefix_kernel, dim3(1), dim3(1024), 0, c.stream,
-                     c.blocksums.as<double>(), nb, total, c_guess, approx);
+                     c.blocksums.as<double>(), nb, total, c_guess, approx, dvs);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(seg_block_kernel, dim3((int)nb), dim3(kSegWaves * 64), 0, c.stream,
                      c.dmin.as<double>(), c.n, total, approx, nb, c.seg_tails.as<SegTail>(),
-                     c.seg_ents.as<SegEnt>());
+                     c.seg_ents.as<SegEnt>(), dvs);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(seg_plan_kernel, dim3(1), dim3(kPlanT), 0, c.stream,
                      c.seg_tails.as<SegTail>(), c.seg_ents.as<SegEnt>(), nb,
@@ -1728,17 +1846,26 @@ static void seed_scan_program(Ctx& c, double total, double c_guess) {
 
 // Runs the program from the exact c_in and fills cend; false when a guess
 // failed (nothing usable written).
-static bool seed_scan_finish(Ctx& c, double c_in, double* c_out) {
+// Device-resident mode: c_out == nullptr, nothing is read back (res[0] the
+// running value, res[1] the success flag stay on the device).
+static double* seed_res(Ctx& c) {
+  return reinterpret_cast<double*>(c.seg_meta.as<long long>() + 4);
+}
+static bool seed_scan_finish(Ctx& c, double c_in, double* c_out,
+                             const SeedDev& dv = SeedDev{}) {
   const int64_t nb = c.nblocks();
   double* markc = c.cend.as<double>() + nb;  // the guesses are consumed
-  double* res = reinterpret_cast<double*>(c.seg_meta.as<long long>() + 4);
+  double* res = seed_res(c);
+  SeedDev dvs;
+  dvs.S = dv.S;
   hipLaunchKernelGGL(seg_eval_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
                      c.seed_prog_total, c.seg_items.as<SeedItem>(), c.seg_meta.as<long long>(),
-                     c_in, markc, res);
+                     c_in, markc, res, dvs);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(seg_fill_kernel, dim3((int)ceil_div(nb, 256)), dim3(256), 0, c.stream,
                      c.seg_scan.as<SegScan>(), nb, markc, res, c_in, c.cend.as<double>());
   HIP_CHECK(hipGetLastError());
+  if (!c_out) return true;
   double h[2];
   HIP_CHECK(hipMemcpyAsync(h, res, sizeof(h), hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -1840,10 +1967,76 @@ void seed_search(Ctx& c, double c_last, double u, int64_t* idx) {
   c.seed_scalar.ensure(sizeof(double) * (c.d + 8));
   int64_t* dres = reinterpret_cast<int64_t*>(c.seed_scalar.as<double>() + c.d + 1);
   hipLaunchKernelGGL(search_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
-                     c.seed_total, c.cend.as<double>(), nb, c.seed_c_in, c_last, u, dres);
+                     c.seed_total, c.cend.as<double>(), nb, c.seed_c_in, c_last, u, dres,
+                     SeedDev{});
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipMemcpyAsync(idx, dres, sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+// kmeans_plusplus_init (:3-22) on one shard with no host round trip per step:
+// every step's centre, total, cumsum program (with its fallback gated on the
+// device), draw and pick stay on the device; picks[0] = first, picks[1..k) the
+// drawn rows; u[0..k-1) the host's rng.random() draws in order.
+void seed_run(Ctx& c, int64_t first, int k, const double* u, int64_t* picks) {
+  check_points(c);
+  if (k < 1) CDR_FAIL(CDR_ERR_ARG, "k >= 1");
+  if (first < 0 || first >= c.n) CDR_FAIL(CDR_ERR_ARG, "first row out of range");
+  picks[0] = first;
+  if (k == 1) return;
+  const int64_t nb = c.nblocks();
+  // [u: k-1][picks: k][S][bad x2][pad]
+  const size_t words = (size_t)(k - 1) + (size_t)k + 8;
+  c.seed_run_buf.ensure(sizeof(double) * words);
+  double* du = c.seed_run_buf.as<double>();
+  int64_t* dpick = reinterpret_cast<int64_t*>(du + (k - 1));
+  double* dS = du + (k - 1) + k;
+  double* dbad = dS + 1;
+  HIP_CHECK(hipMemcpyAsync(du, u, sizeof(double) * (k - 1), hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(dpick, &first, sizeof(int64_t), hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemsetAsync(dbad, 0, sizeof(double) * 2, c.stream));
+  seed_reset(c);
+  c.seed_scalar.ensure(sizeof(double) * (2 * c.d + 8));
+  c.cend.ensure(sizeof(double) * nb * 2);
+  c.seg_meta.ensure(sizeof(long long) * 8);
+  static const bool walk_only = std::getenv("CDR_SEED_WALK") != nullptr;
+  const float* x32 = c.mode == CDR_MODE_F32X ? c.x32.as<float>() : nullptr;
+  const double* x64 = c.mode == CDR_MODE_F64 ? c.x64.as<double>() : nullptr;
+  for (int i = 1; i < k; ++i) {
+    hipLaunchKernelGGL(seed_gather_kernel, dim3(1), dim3(64), 0, c.stream, x32, x64,
+                       dpick + (i - 1), c.d, c.n_pad, c.seed_scalar.as<double>(), dbad);
+    HIP_CHECK(hipGetLastError());
+    seed_update(c, nullptr);
+    hipLaunchKernelGGL(seed_total_kernel, dim3(1), dim3(64), 0, c.stream,
+                       c.blocksums.as<double>(), nb, dS, dbad);
+    HIP_CHECK(hipGetLastError());
+    double* res = seed_res(c);
+    SeedDev dv;
+    dv.S = dS;
+    if (!walk_only) {
+      seed_scan_program(c, 1.0, 0.0, dv);
+      seed_scan_finish(c, 0.0, nullptr, dv);
+      dv.gate = res + 1;  // the fallback runs only when the program failed
+    } else {
+      HIP_CHECK(hipMemsetAsync(res, 0, sizeof(double) * 2, c.stream));
+    }
+    seed_scan_walk(c, 1.0, 0.0, nullptr, dv, res);
+    SeedDev ds;
+    ds.S = dS;
+    ds.c_last = res;
+    ds.u = du + (i - 1);
+    hipLaunchKernelGGL(search_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
+                       1.0, c.cend.as<double>(), nb, 0.0, 1.0, 0.5, dpick + i, ds);
+    HIP_CHECK(hipGetLastError());
+  }
+  double bad[2];
+  HIP_CHECK(hipMemcpyAsync(picks, dpick, sizeof(int64_t) * k, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(bad, dbad, sizeof(bad), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.seed_scanned = false;
+  c.seed_prog_ready = false;
+  if (bad[0] != 0.0) CDR_FAIL(CDR_ERR_NAN, "Probabilities contain NaN");
+  if (bad[1] != 0.0) CDR_FAIL(CDR_ERR_STATE, "k-means++ sampler found no index");
 }
 
 }  // namespace cdr
@@ -1921,6 +2114,14 @@ int cdr_seed_scan_end(cdr_ctx* h, double c_in, double* c_out) {
   if (!h || !c_out) CDR_FAIL(CDR_ERR_ARG, "null argument");
   HIP_CHECK(hipSetDevice(h->c.device));
   seed_scan_end(h->c, c_in, c_out);
+  CDR_CATCH
+}
+
+int cdr_seed_run(cdr_ctx* h, int64_t first, int32_t k, const double* u, int64_t* picks) {
+  CDR_TRY
+  if (!h || !picks || (k > 1 && !u)) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  seed_run(h->c, first, (int)k, u, picks);
   CDR_CATCH
 }
 

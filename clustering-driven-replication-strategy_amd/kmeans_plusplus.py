@@ -51,6 +51,16 @@ def _seed_on_device(ctx: Context, X: np.ndarray, k: int, random_state) -> np.nda
     centroids = np.empty((k, n_features), dtype=X.dtype)
     first_idx = rng.integers(0, n_samples)
     centroids[0] = X[first_idx]
+    if k > 1 and hasattr(ctx, "seed_run"):
+        # every step on the device (cdr_seed_run); rng.choice draws one
+        # uniform per step (:19), so the k - 1 draws are taken up front
+        u = rng.random(k - 1)
+        try:
+            picks = ctx.seed_run(first_idx, k, u)
+        except ValueError:
+            _nan_probabilities()
+        centroids[:] = X[picks]
+        return centroids
     if k > 1:
         ctx.seed_reset()
     for i in range(1, k):

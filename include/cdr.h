@@ -130,8 +130,15 @@ int cdr_seed_scan_begin(cdr_ctx* ctx, double total, double c_guess, int64_t* n_i
 int cdr_seed_scan_items(cdr_ctx* ctx, cdr_seed_item* out, int64_t cap, int64_t* n_items);
 int cdr_seed_scan_end(cdr_ctx* ctx, double c_in, double* c_out);
 /* out[0] = scans run through a program, out[1] = of those, the ones whose
- * guess failed and fell back to the exact block walk (same result).        */
+ * guess failed and fell back to the exact block walk (same result; counted
+ * by the per-step calls — cdr_seed_run gates its fallback on the device).  */
 int cdr_seed_stats(cdr_ctx* ctx, int64_t* out);
+/* The whole kmeans_plusplus_init (:3-22) on this context's points with no host
+ * round trip per step: first = the first row (rng.integers), u[0..k-1) = the
+ * uniforms of the k - 1 draws (rng.choice takes one rng.random() each);
+ * picks[0..k) = the chosen rows.  CDR_ERR_NAN when a total is not finite and
+ * positive ("Probabilities contain NaN").                                   */
+int cdr_seed_run(cdr_ctx* ctx, int64_t first, int32_t k, const double* u, int64_t* picks);
 /* *ok = 0 when some item does not hold for this c_in (or a FINE item).      */
 int cdr_seed_program_eval(const cdr_seed_item* items, int64_t n_items, double c_in,
                           double* c_out, int32_t* ok);
