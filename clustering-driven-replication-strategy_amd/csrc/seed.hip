@@ -321,7 +321,11 @@ __global__ void seed_ch_kernel(const double* __restrict__ cen, const float* __re
   Ec[0] = (float)(sqrt(ec) * (1.0 + 0x1p-20) + 0x1p-60);
 }
 
-template <int D, int UU = 0>
+// PR: the triangle-inequality pruning (seed_prunable) first, so that a pruned
+// point does not read its copy — worth it for wide rows; for d <= 16 the
+// dependent near / ccd loads cost more than the 32-byte copy they save, and
+// dmin and the copy are loaded together in one round trip instead.
+template <int D, int UU = 0, bool PR = (D > 16)>
 __global__ __launch_bounds__(256) void seed_update16_kernel(
     const float* __restrict__ X, const uint4* __restrict__ x16, const float* __restrict__ e16,
     int64_t n, int64_t n_pad, const double* __restrict__ cen, const float* __restrict__ ch,
@@ -348,27 +352,43 @@ __global__ __launch_bounds__(256) void seed_update16_kernel(
     for (int q0 = threadIdx.x; q0 < kHalf; q0 += U * 256) {
       double old[U];
       bool go[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int qi = h * kHalf + q0 + 256 * u;
-        const int64_t i = base + qi;
-        go[u] = false;
-        old[u] = 0.0;
-        if (qi < m) {
-          old[u] = dmin[i];
-          go[u] = cidx == 0 || !seed_prunable(ccd[near[i]], old[u]);
-        }
-      }
-      // the fp16 certificate
       uint4 hv[U][G];
       float ev[U];
+      if constexpr (PR) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t i = base + h * kHalf + q0 + 256 * u;
-        if (go[u]) {
+        for (int u = 0; u < U; ++u) {
+          const int qi = h * kHalf + q0 + 256 * u;
+          const int64_t i = base + qi;
+          go[u] = false;
+          old[u] = 0.0;
+          if (qi < m) {
+            old[u] = dmin[i];
+            go[u] = cidx == 0 || !seed_prunable(ccd[near[i]], old[u]);
+          }
+        }
+        // the fp16 certificate
 #pragma unroll
-          for (int g = 0; g < G; ++g) hv[u][g] = x16[(int64_t)g * n_pad + i];
-          ev[u] = e16[i];
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = base + h * kHalf + q0 + 256 * u;
+          if (go[u]) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) hv[u][g] = x16[(int64_t)g * n_pad + i];
+            ev[u] = e16[i];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int qi = h * kHalf + q0 + 256 * u;
+          const int64_t i = base + qi;
+          go[u] = qi < m;
+          old[u] = 0.0;
+          if (go[u]) {
+            old[u] = dmin[i];
+#pragma unroll
+            for (int g = 0; g < G; ++g) hv[u][g] = x16[(int64_t)g * n_pad + i];
+            ev[u] = e16[i];
+          }
         }
       }
       bool need[U];
@@ -1716,8 +1736,10 @@ void seed_update(Ctx& c, const double* cen) {
                             const double*, const float*, const float*, double, double*,
                             double*, int32_t*, const double*, int);
       static const int u16 = std::getenv("CDR_SEED16_U") ? std::atoi(std::getenv("CDR_SEED16_U")) : 0;
-      const S16Fn f16 = d == 8    ? seed_update16_kernel<8>
-                        : d == 16 ? (u16 == 1   ? seed_update16_kernel<16, 1>
+      static const bool pr16 = std::getenv("CDR_SEED16_PR") != nullptr;  // A/B: prune at d <= 16
+      const S16Fn f16 = d == 8    ? (pr16 ? seed_update16_kernel<8, 0, true> : seed_update16_kernel<8>)
+                        : d == 16 ? (pr16       ? seed_update16_kernel<16, 0, true>
+                                     : u16 == 1 ? seed_update16_kernel<16, 1>
                                      : u16 == 4 ? seed_update16_kernel<16, 4>
                                                 : seed_update16_kernel<16>)
                         : d == 32 ? seed_update16_kernel<32>
