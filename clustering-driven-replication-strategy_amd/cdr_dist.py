@@ -56,6 +56,7 @@ class Comm:
         self.world = dist.get_world_size() if dist else 1
         self.device = device  # torch.device for NCCL, None for gloo / single
         self.native = set()  # ids of contexts with a libcdr RCCL communicator
+        self.seed_bad = 0  # this rank's seeding consistency flag (seed_sharded)
 
     def attach_native(self, ctx) -> bool:
         """Give ``ctx`` its own RCCL communicator over the same ranks
@@ -318,8 +319,9 @@ def shard_scan(ctx, comm: Comm, parts, total: float):
         if ok:
             if rank > 0:
                 mine = ctx.seed_scan_end(c_mine)
-                if mine != seed_program_eval(prog, c_mine)[0]:
-                    raise RuntimeError("seed program and shard scan disagree")
+                # checked by every rank together with the draw's hits (a raise
+                # on one rank alone would leave the others in a collective)
+                comm.seed_bad = int(mine != seed_program_eval(prog, c_mine)[0])
             return c
     c = 0.0
     for r in range(world):  # rank-ordered chain of exact scans
@@ -354,9 +356,14 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
         total = host_seq_sum(np.concatenate(parts))
         if not (total > 0.0) or total == np.inf:
             raise ValueError("Probabilities contain NaN")
+        comm.seed_bad = 0
         c = shard_scan(ctx, comm, parts, total)
         u = rng.random()
-        hits = np.concatenate(comm.allgather(np.array([ctx.seed_search(c, u)], dtype=np.int64)))
+        got = np.stack(comm.allgather(np.array([ctx.seed_search(c, u), comm.seed_bad],
+                                               dtype=np.int64)))
+        if got[:, 1].any():
+            raise RuntimeError("a shard's cumsum program and its exact scan disagree")
+        hits = got[:, 0]
         owner = int(np.flatnonzero(hits >= 0)[0])
         C[i] = _fetch_row(ctx, comm, owner, int(hits[owner]), d)
     return C
