@@ -20,15 +20,17 @@ in total, sharded in 8192-row blocks over the N ranks (`--scaling weak`: N x
 stdout carries exactly one JSON line (rank 0): native libraries that print
 banners (RCCL) are pointed at stderr.
 
-roofline: the dominant kernel is the screen kernel (assign + fused update);
-algorithmic bytes per launch = n_local * (4*d + 4) (read the fp32 point, write
-its int32 label: SURVEY.md 8(d)), divided by its mean duration from HIP events
-recorded on the context stream around every launch of the timed region.  The
-DELTA screen streams a smaller fp16 copy of the points instead (32 bytes per
-point at d = 16 for screen32h, + a one-byte label): `kernel_bytes_per_launch`
-and `kernel_frac` state that kernel's own traffic against the same peak.  `traffic` is
-the PMC-measured HBM bytes per launch from profiles/ when a matching rocprof
-summary is committed there, else null.
+roofline: the dominant kernel is the screen kernel (assign + fused update),
+timed by HIP events on the context stream around every 4th launch of the
+timed region.  `frac` is an HBM fraction of the bytes that kernel moves: the
+PMC-measured HBM bytes per launch (`traffic`, profiles/pmc_traffic.json, when
+a rocprof pass of this kernel at this size is committed) or else the bytes it
+must move by construction (`kernel_bytes_per_launch`: the bounded screen's
+4-byte bound word per point + the hi row of each point whose bound failed),
+divided by its mean launch time and 8 TB/s.  The SURVEY.md 8(d) contract
+figure, n_local * (4*d + 4) bytes (read the fp32 point, write its int32 label),
+over the same time is `effective_achieved` / `effective_frac` — above 1,
+because the kernel does not need those bytes.
 
 cpu_baseline: the NumPy oracle (restatement of the reference, 1 core — NumPy
 ufuncs are single-threaded) timed on this host on a 1M-row sample of the
@@ -417,7 +419,11 @@ def f64_bench(args, world: int, rank: int, json_fd: int) -> None:
     ctx.close()
 
 
-def pmc_traffic(config: str, n_local: int):
+def pmc_traffic(config: str, n_local: int, kname: str | None = None):
+    """HBM bytes per launch of the config's dominant kernel from the committed
+    PMC passes (profiles/pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, the
+    MI355X_MICROARCH.md gfx950 correction), when they were taken on this size
+    and, if given, this kernel."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
@@ -426,7 +432,28 @@ def pmc_traffic(config: str, n_local: int):
     r = rec.get(config)
     if not r or int(r.get("n_local", -1)) != n_local:
         return None
+    if kname is not None and not str(r.get("kernel", "")).startswith(kname.split("<")[0] + "<"):
+        return None
     return float(r["hbm_bytes_per_launch"])
+
+
+def kernel_bytes(kname: str, n_local: int, prof: dict, steps: int) -> int:
+    """Bytes the step's screen kernel must move by construction (DESIGN.md
+    4.3c-4.3e): the fp16 hi copy + one-byte label for screen32h/p; for the
+    bounded screen32b the 4-byte bound word of every point, plus, for each
+    point whose bound failed (profile counter, per step), its hi row and its
+    new bound word."""
+    if kname.startswith("screen32b"):
+        row = 32 if kname.startswith(("screen32b<3", "screen32b<4")) else 16
+        tight = prof.get("tight_points", 0) / max(steps, 1)
+        return int(n_local * 4 + tight * (row + 4))
+    copy_b = {"screen32h1": 2 * 8, "screen32h": 2 * 16, "screen32d<1": 32, "screen32d<2": 64,
+              "screen32p<1": 2 * 8, "screen32p<2": 2 * 8, "screen32p<3": 2 * 16,
+              "screen32p<4": 2 * 16}
+    for pre, b in copy_b.items():
+        if kname.startswith(pre):
+            return n_local * (b + 1)
+    return n_local * (4 * 16 + 4)
 
 
 def spawn_ranks(n: int) -> None:
@@ -521,8 +548,11 @@ def main() -> None:
         import torch
 
         ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    g0 = time.perf_counter()
     ctx.generate_points(n_total, begin, n_local, d, k, args.seed)
     unify_points(ctx, comm, n_total)  # one scale / screen transform on every rank
+    ctx.synchronize()
+    gen_ms = (time.perf_counter() - g0) * 1e3
     native = comm.attach_native(ctx)  # each step's all-reduce issued from C (csrc/comm.hip)
     ctx.synchronize()
 
@@ -534,8 +564,11 @@ def main() -> None:
     # assign + fused update + all-reduce + means on the device
     np.random.seed(0)
     run = DeviceLloyd(ctx, C, -1.0, row_fetcher(ctx, comm, begin, d), n_total, comm)
+    w0 = time.perf_counter()
     if args.warmup:
         run.advance(args.warmup)
+    ctx.synchronize()
+    warmup_ms = (time.perf_counter() - w0) * 1e3
     # HIP events around every 4th step's kernels (an event record costs the
     # GPU a few microseconds; the kernel times are per launch either way)
     ctx.profile_reset(True, every=4)
@@ -581,16 +614,17 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    setup_ms = max(warmup_ms - args.warmup * elapsed / max(args.steps, 1) * 1e3, 0.0)
     kname = ctx.profile_kernel()
     screen_ms = prof["screen_ms"] / max(prof["steps"], 1)
     step_kernel_ms = prof["step_ms"] / max(prof["steps"], 1)
     alg_bytes = n_local * (4 * d + 4)
-    achieved = alg_bytes / (screen_ms / 1e3) / 1e9 if screen_ms > 0 else 0.0
-    traffic = pmc_traffic(args.config, n_local)
+    traffic = pmc_traffic(args.config, n_local, kname)
     value = n_total * args.steps / elapsed
     if kname.startswith("screen_big"):
         # large-k regime: the L1 screen is the dense contraction 2 n k d on
         # the matrix cores (one fp16 product per centroid block)
+        achieved = alg_bytes / (screen_ms / 1e3) / 1e9 if screen_ms > 0 else 0.0
         alg_flop = 2.0 * n_local * k * d
         tflops = alg_flop / (screen_ms / 1e3) / 1e12 if screen_ms > 0 else 0.0
         roofline = {"bound": "mfma", "achieved": tflops, "peak": MFMA_F16_PEAK_TFLOPS,
@@ -598,30 +632,30 @@ def main() -> None:
                     "kernel": kname, "alg_flop_per_launch": alg_flop, "kernel_ms": screen_ms,
                     "hbm_alg_bytes_per_launch": alg_bytes}
     else:
+        # frac is an HBM fraction of the bytes the kernel itself moves: the
+        # PMC-measured traffic per launch when a rocprof pass of this kernel
+        # and size is committed (profiles/pmc_traffic.json), else the bytes it
+        # must move by construction (kernel_bytes_per_launch).  The SURVEY 8(d)
+        # contract figure (fp32 point + int32 label per point) is kept as
+        # effective_achieved / effective_frac: it exceeds 1 because the
+        # kernels read a half-size fp16 copy and, on the bounded screen, only
+        # the points whose drift bound failed.
+        kb = kernel_bytes(kname, n_local, prof, args.steps)
+        moved = traffic if traffic else kb
+        achieved = moved / (screen_ms / 1e3) / 1e9 if screen_ms > 0 else 0.0
+        eff = alg_bytes / (screen_ms / 1e3) / 1e9 if screen_ms > 0 else 0.0
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                    "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_ms": screen_ms}
-        # the bytes this kernel itself must stream: its fp16 screen copy (hi-only
-        # screen32h / screen32h1: 2 B per padded feature; screen32d: hi + lo) and the one-byte
-        # label it compares against
-        copy_b = {"screen32h1": 2 * 8, "screen32h": 2 * 16, "screen32d<1": 32, "screen32d<2": 64,
-                  "screen32p<1": 2 * 8, "screen32p<2": 2 * 8, "screen32p<3": 2 * 16,
-                  "screen32p<4": 2 * 16}
-        for pre, b in copy_b.items():
-            if kname.startswith(pre):
-                kb = n_local * (b + 1)
-                roofline["kernel_bytes_per_launch"] = kb
-                roofline["kernel_frac"] = kb / (screen_ms / 1e3) / 1e9 / HBM_PEAK_GBPS
-                roofline["note"] = ("achieved/frac: SURVEY 8(d) bytes (fp32 point + int32 label) per "
-                                    "launch / launch time, as the contract defines them; the kernel "
-                                    "streams its fp16 copy + 1-byte label instead, so frac can exceed "
-                                    "1: its own HBM rate is kernel_bytes_per_launch / kernel_ms "
-                                    "(kernel_frac), DESIGN.md 4.3c-4.3d")
-                break
+                    "bytes_basis": "pmc" if traffic else "kernel_bytes_per_launch",
+                    "kernel": kname, "kernel_ms": screen_ms, "kernel_bytes_per_launch": kb,
+                    "alg_bytes_per_launch": alg_bytes, "effective_achieved": eff,
+                    "effective_frac": eff / HBM_PEAK_GBPS}
     # (the fallback counter accumulates over every profiled-session step)
     fb_frac = prof["fallback_points"] / max(args.steps, 1) / max(n_local, 1)
     # points the pruned screen (screen32p) handed to its k-way MFMA screen
     q_frac = prof["queued_points"] / max(args.steps, 1) / max(n_local, 1)
+    # points whose drift bound failed (screen32b), re-decided from their coordinates
+    t_frac = prof["tight_points"] / max(args.steps, 1) / max(n_local, 1)
 
     out = {
         "metric": METRIC,
@@ -649,7 +683,14 @@ def main() -> None:
         "step_kernels_ms": step_kernel_ms,
         "fallback_frac": fb_frac,
         "queued_frac": q_frac,
+        "reread_frac": t_frac,
         "seed_s": seed_s,
+        "setup_ms": setup_ms,
+        "setup_note": "one-time work outside the timed steps: device point generation + "
+                      "statistics (gen_ms), and the warmup steps' one-time copies (pre-centred, "
+                      "fp16 hi, row-major, bound words: warmup wall time minus warmup x "
+                      "ms_per_step); seeding is seed_s",
+        "gen_ms": gen_ms,
         "seed_scans": ctx.seed_stats(),  # cumsum programs / fallbacks to the block walk
         "final_shift": st["shift"],
         "final_inertia": st["inertia"],

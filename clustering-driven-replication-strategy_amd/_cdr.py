@@ -71,6 +71,10 @@ SIGNATURES = {
     "cdr_seed_program_eval": ([_P, _I64, _F64, _PF64, _PI32], None),
     "cdr_seed_stats": ([_P, _PI64], None),
     "cdr_seed_run": ([_P, _I64, _I32, _P, _P], None),
+    "cdr_seed_shard_begin": ([_P, _I64, _I64, _I32, _I32, _I64, _I32, _P, _P, _P], None),
+    "cdr_seed_shard_phase": ([_P, _I32, _P, _P], None),
+    "cdr_seed_shard_end": ([_P, _P, _P, _P, _P], None),
+    "cdr_seed_run_sharded": ([_P, _I64, _I64, _I64, _I32, _P, _P, _P, _P], None),
     "cdr_lloyd_step": ([_P, _P, _I32, _P, _I32], None),
     "cdr_lloyd_step_f64": ([_P, _P, _I32, _P, _P], None),
     "cdr_lloyd_labels": ([_P, _P], None),
@@ -91,6 +95,8 @@ SIGNATURES = {
     "cdr_comm_unique_id": ([_P], None),
     "cdr_comm_init": ([_P, _P, _I32, _I32], None),
     "cdr_comm_destroy": ([_P], None),
+    "cdr_comm_available": ([ctypes.POINTER(ctypes.c_int32)], None),
+    "cdr_comm_ranks": ([_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)], None),
     "cdr_build_id": ([], ctypes.c_char_p),
     "cdr_medians_segmented": ([_P, _P, _P, _I64, _P], None),
     "cdr_medians_by_label": ([_P, _I32, _P], None),
@@ -179,12 +185,17 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
+class NanProbabilities(ValueError):
+    """CDR_ERR_NAN: numpy Generator.choice's "Probabilities contain NaN"
+    (src/kmeans_plusplus.py:19); a ValueError like the reference's."""
+
+
 def _check(rc: int) -> None:
     if rc == CDR_OK:
         return
     msg = load_library().cdr_last_error().decode(errors="replace")
     if rc == CDR_ERR_NAN:
-        raise ValueError("Probabilities contain NaN")
+        raise NanProbabilities("Probabilities contain NaN")
     if rc == CDR_ERR_ARG:
         raise ValueError(msg)
     if rc == CDR_ERR_UNSUPPORTED:
@@ -197,6 +208,13 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     _check(lib.cdr_device_count(ctypes.byref(n)))
     return int(n.value)
+
+
+def comm_available() -> bool:
+    """librccl loads (dlopen / dlsym only; no bootstrap listener is started)."""
+    ok = ctypes.c_int32(0)
+    _check(load_library().cdr_comm_available(ctypes.byref(ok)))
+    return bool(ok.value)
 
 
 def comm_unique_id() -> bytes:
@@ -238,6 +256,7 @@ class Context:
         self._lib = lib
         self._h = h
         self.device = int(device)
+        self.restat_n = None  # n_sum of the last cdr_points_restat (cdr_dist.unify_points)
 
     # -- lifecycle -------------------------------------------------------
     def close(self) -> None:
@@ -262,10 +281,12 @@ class Context:
         X = np.ascontiguousarray(X, dtype=np.float64)
         if X.ndim != 2:
             raise ValueError("X must be 2-dimensional (n_samples, n_features)")
+        self.restat_n = None  # (cdr_dist.unify_points: not combined over shards)
         _check(self._lib.cdr_points_load_f64(self._h, _ptr(X), X.shape[0], X.shape[1]))
 
     def generate_points(self, n_total: int, row_begin: int, n_local: int, d: int,
                         n_blobs: int, seed: int) -> None:
+        self.restat_n = None
         _check(self._lib.cdr_points_generate(self._h, n_total, row_begin, n_local, d,
                                              n_blobs, ctypes.c_uint64(seed & (2**64 - 1))))
 
@@ -286,6 +307,7 @@ class Context:
         every shard (cdr_points_restat)."""
         st = np.ascontiguousarray(st, dtype=np.uint64)
         _check(self._lib.cdr_points_restat(self._h, _ptr(st), int(n_sum)))
+        self.restat_n = int(n_sum)
 
     def get_rows(self, idx) -> np.ndarray:
         idx = np.ascontiguousarray(np.atleast_1d(idx), dtype=np.int64)
@@ -352,6 +374,49 @@ class Context:
                                       _ptr(picks)))
         return picks[:k]
 
+    # -- device-resident seeding over sharded rows (include/cdr.h) -----------
+    def seed_shard_begin(self, row_begin: int, n_total: int, nranks: int, rank: int, first: int,
+                         k: int, u, red: int) -> np.ndarray:
+        """Starts the sharded device seeding; writes this rank's part of the
+        first all-reduce into the device buffer `red` (d + 4 doubles) and
+        returns the bytes per rank of the three exchanged buffers."""
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        if u.size != max(k - 1, 0):
+            raise ValueError("need k - 1 uniforms")
+        sizes = np.zeros(3, dtype=np.int64)
+        self._ss_k = int(k)
+        _check(self._lib.cdr_seed_shard_begin(self._h, int(row_begin), int(n_total), int(nranks),
+                                              int(rank), int(first), int(k),
+                                              _ptr(u) if u.size else None, _P(red), _ptr(sizes)))
+        return sizes
+
+    def seed_shard_phase(self, phase: int, buf_in: int, buf_out: int) -> None:
+        _check(self._lib.cdr_seed_shard_phase(self._h, int(phase), _P(buf_in), _P(buf_out)))
+
+    def seed_shard_end(self, red: int):
+        """(picks (k,) global rows, centres (k, d) fp64, status: 0 ok, 1 run
+        the host protocol instead, 2 Probabilities contain NaN)."""
+        k, d = self._ss_k, self.info()["d"]
+        picks = np.zeros(k, dtype=np.int64)
+        cents = np.zeros((k, d), dtype=np.float64)
+        st = ctypes.c_int32(0)
+        _check(self._lib.cdr_seed_shard_end(self._h, _P(red), _ptr(picks), _ptr(cents),
+                                            ctypes.byref(st)))
+        return picks, cents, int(st.value)
+
+    def seed_run_sharded(self, row_begin: int, n_total: int, first: int, k: int, u):
+        """Every step with the context's communicator (cdr_comm_init):
+        (picks, centres, status) as seed_shard_end."""
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        d = self.info()["d"]
+        picks = np.zeros(max(k, 1), dtype=np.int64)
+        cents = np.zeros((max(k, 1), d), dtype=np.float64)
+        st = ctypes.c_int32(0)
+        _check(self._lib.cdr_seed_run_sharded(self._h, int(row_begin), int(n_total), int(first),
+                                              int(k), _ptr(u) if u.size else None, _ptr(picks),
+                                              _ptr(cents), ctypes.byref(st)))
+        return picks[:k], cents[:k], int(st.value)
+
     def seed_stats(self) -> dict:
         """Cumsum scans run through a program, and those that fell back to
         the block walk (cdr_seed_stats)."""
@@ -407,10 +472,11 @@ class Context:
         _check(self._lib.cdr_profile_reset(self._h, max(int(every), 1) if enable else 0))
 
     def profile_read(self) -> dict:
-        out = np.zeros(5, dtype=np.float64)
+        out = np.zeros(6, dtype=np.float64)
         _check(self._lib.cdr_profile_read(self._h, _ptr(out)))
         return {"screen_ms": out[0], "steps": int(out[1]), "step_ms": out[2],
-                "fallback_points": int(out[3]), "queued_points": int(out[4])}
+                "fallback_points": int(out[3]), "queued_points": int(out[4]),
+                "tight_points": int(out[5])}
 
     def profile_kernel(self) -> str:
         buf = ctypes.create_string_buffer(96)
@@ -478,6 +544,12 @@ class Context:
 
     def comm_destroy(self) -> None:
         _check(self._lib.cdr_comm_destroy(self._h))
+
+    def comm_ranks(self) -> tuple[int, int]:
+        """(nranks, rank) of the context's communicator; nranks 0: none."""
+        nr, r = ctypes.c_int32(0), ctypes.c_int32(0)
+        _check(self._lib.cdr_comm_ranks(self._h, ctypes.byref(nr), ctypes.byref(r)))
+        return int(nr.value), int(r.value)
 
     def debug_screen(self, C: np.ndarray):
         C = np.ascontiguousarray(C, dtype=np.float64)
@@ -727,7 +799,7 @@ def loaded_library_path() -> str | None:
 
 
 __all__ = ["Context", "default_context", "load_library", "device_count", "host_seq_sum",
-           "comm_unique_id",
+           "comm_unique_id", "comm_available", "NanProbabilities",
            "MODE_F32X", "MODE_F64", "SEED_BLOCK", "SIGNATURES", "LIB_PATH"]
 
 if __name__ == "__main__":  # pragma: no cover

@@ -55,7 +55,6 @@ class Comm:
         self.rank = dist.get_rank() if dist else 0
         self.world = dist.get_world_size() if dist else 1
         self.device = device  # torch.device for NCCL, None for gloo / single
-        self.native = set()  # ids of contexts with a libcdr RCCL communicator
         self.seed_bad = 0  # this rank's seeding consistency flag (seed_sharded)
 
     def attach_native(self, ctx) -> bool:
@@ -69,24 +68,34 @@ class Comm:
 
         import _cdr
 
-        # every rank probes librccl first and the ranks agree (MIN) before any
-        # of them enters the collective init: one rank that cannot load it
-        # must not leave the others waiting in ncclCommInitRank
+        # every rank checks that librccl loads (dlopen / dlsym only) and the
+        # ranks agree (MIN) before any of them enters the collective init: one
+        # rank that cannot load it must not leave the others waiting in
+        # ncclCommInitRank.  Only rank 0 creates the unique id (each
+        # ncclGetUniqueId starts a bootstrap listener).
         try:
-            own = np.frombuffer(_cdr.comm_unique_id(), dtype=np.uint8)
-            ok = 1
+            ok = 1 if _cdr.comm_available() else 0
         except Exception:  # noqa: BLE001 - any failure means "no native comm"
-            own, ok = np.zeros(128, dtype=np.uint8), 0
+            ok = 0
+        uid = np.zeros(128, dtype=np.uint8)
+        if ok and self.rank == 0:
+            try:
+                uid = np.frombuffer(_cdr.comm_unique_id(), dtype=np.uint8).copy()
+            except Exception:  # noqa: BLE001
+                ok = 0
         flag = torch.tensor([ok], dtype=torch.int32, device=self.device)
         self.dist.all_reduce(flag, op=self.dist.ReduceOp.MIN)
         if int(flag.item()) == 0:
             return False
-        uid = own if self.rank == 0 else np.zeros(128, dtype=np.uint8)
-        t = torch.from_numpy(uid.copy()).to(self.device)
+        t = torch.from_numpy(uid).to(self.device)
         self.dist.broadcast(t, 0)
         ctx.comm_init(t.cpu().numpy().tobytes(), self.world, self.rank)
-        self.native.add(id(ctx))
         return True
+
+    def has_native(self, ctx) -> bool:
+        """ctx holds a libcdr communicator over exactly these ranks (asked of
+        the C side: a Python-side record by id() could outlive the context)."""
+        return hasattr(ctx, "comm_ranks") and ctx.comm_ranks()[0] == self.world
 
     def _t(self, arr):
         import torch
@@ -209,6 +218,32 @@ class Comm:
             t = torch.from_numpy(buf)
             self.dist.all_reduce(t)
 
+    def buffer(self, nbytes: int):
+        """(buffer, handle) of `nbytes` for a device protocol's exchanges: a
+        device uint8 tensor and its pointer under NCCL (RCCL), a host uint8
+        array (the handle itself) otherwise."""
+        return self.exchange_buffer(nbytes)
+
+    def allgather_slots(self, buf, m: int) -> None:
+        """In-place all-gather of m-byte slots: rank r's slot is bytes
+        [r m, (r + 1) m) of buf; afterwards every rank holds every slot."""
+        if not self.dist:
+            return
+        import torch
+
+        t = buf if self.device is not None else torch.from_numpy(buf)
+        src = t[self.rank * m:(self.rank + 1) * m].clone()
+        self.dist.all_gather([t[r * m:(r + 1) * m] for r in range(self.world)], src)
+
+    def allreduce_sum_f64_inplace(self, buf) -> None:
+        """SUM all-reduce of a byte buffer holding float64 values, in place."""
+        if not self.dist:
+            return
+        import torch
+
+        t = buf if self.device is not None else torch.from_numpy(buf)
+        self.dist.all_reduce(t.view(torch.float64))
+
     def bcast(self, arr: np.ndarray, src: int) -> np.ndarray:
         if not self.dist:
             return arr
@@ -235,6 +270,22 @@ def unify_points(ctx, comm: Comm | None, n_total: int) -> None:
         hi = comm.allreduce_i64(s[d:], "max")
         st = np.concatenate([lo, hi]).view(np.uint64) ^ _SIGN
     ctx.points_restat(st, n_total)
+
+
+def ensure_unified(ctx, comm: Comm | None, n_total: int) -> None:
+    """Collective guard of the sharded paths: if any rank's
+    context was not unified over n_total rows (``Context.restat_n``), every
+    rank runs unify_points; then the ranks check that they agree on the
+    storage mode and the fixed-point scale, and raise together if not."""
+    if comm is None or comm.world == 1 or not hasattr(ctx, "points_restat"):
+        return
+    need = int(getattr(ctx, "restat_n", None) != n_total)
+    if int(comm.allreduce_i64(np.array([need]), "max")[0]):
+        unify_points(ctx, comm, n_total)
+    inf = ctx.info()
+    v = np.array([inf["mode"], inf["scale_bits"], inf["d"]], dtype=np.int64)
+    if not np.array_equal(comm.allreduce_i64(v, "min"), comm.allreduce_i64(v, "max")):
+        raise RuntimeError("sharded points disagree on storage mode / scale after unify_points")
 
 
 def _fetch_row(ctx, comm: Comm, owner: int, local_idx: int, d: int) -> np.ndarray:
@@ -335,17 +386,29 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
     """kmeans_plusplus_init over the sharded rows (float64 centroids)."""
     if host_seq_sum is None:
         from _cdr import host_seq_sum
+    ensure_unified(ctx, comm, n_total)
     d = ctx.info()["d"]
     offsets = np.array([b for b in comm.allgather(np.array([row_begin], dtype=np.int64))],
                        dtype=np.int64).ravel()
     rng = np.random.default_rng(random_state)
     C = np.empty((k, d), dtype=np.float64)
     first = int(rng.integers(0, n_total))
+    # rng.choice draws one uniform per step (:19): all k - 1 taken up front
+    u = rng.random(k - 1) if k > 1 else np.zeros(0)
     if comm.world == 1 and k > 1 and hasattr(ctx, "seed_run"):
-        # one shard: every step on the device (cdr_seed_run), one uniform per
-        # draw taken up front (:19)
-        picks = ctx.seed_run(first, k, rng.random(k - 1))
+        # one shard: every step on the device (cdr_seed_run)
+        picks = ctx.seed_run(first, k, u)
         return np.asarray(ctx.get_rows(picks), dtype=np.float64)
+    if comm.world > 1 and k > 1 and hasattr(ctx, "seed_shard_begin"):
+        # sharded and device-resident: three collectives per step, no host
+        # round trip (include/cdr.h cdr_seed_shard_*); status 1 (a program
+        # that cannot be composed, seen by every rank) -> the host protocol
+        _, cents, status = seed_device_sharded(ctx, comm, row_begin, n_total, first, k, u)
+        if status == 2:
+            raise ValueError("Probabilities contain NaN")
+        if status == 0:
+            return cents
+        comm.seed_fallbacks = getattr(comm, "seed_fallbacks", 0) + 1
     owner = _owner_of(offsets, first)
     C[0] = _fetch_row(ctx, comm, owner, first - int(offsets[owner]), d)
     if k > 1:
@@ -358,8 +421,7 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
             raise ValueError("Probabilities contain NaN")
         comm.seed_bad = 0
         c = shard_scan(ctx, comm, parts, total)
-        u = rng.random()
-        got = np.stack(comm.allgather(np.array([ctx.seed_search(c, u), comm.seed_bad],
+        got = np.stack(comm.allgather(np.array([ctx.seed_search(c, u[i - 1]), comm.seed_bad],
                                                dtype=np.int64)))
         if got[:, 1].any():
             raise RuntimeError("a shard's cumsum program and its exact scan disagree")
@@ -367,6 +429,33 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
         owner = int(np.flatnonzero(hits >= 0)[0])
         C[i] = _fetch_row(ctx, comm, owner, int(hits[owner]), d)
     return C
+
+
+def seed_device_sharded(ctx, comm: Comm, row_begin: int, n_total: int, first: int, k: int, u):
+    """kmeans_plusplus_init's steps (:13-20) on sharded rows with every step on
+    the devices: with a libcdr communicator the whole run is enqueued by one C
+    call (cdr_seed_run_sharded: ncclAllGather / ncclAllReduce between the
+    kernels); otherwise the same phases are driven from here with the
+    collectives of ``comm`` on device (RCCL) or host (gloo) buffers.  Returns
+    (picks, centres (k, d), status) — status 0 ok, 1 run the host protocol,
+    2 "Probabilities contain NaN"."""
+    if comm.has_native(ctx) and hasattr(ctx, "seed_run_sharded"):
+        return ctx.seed_run_sharded(row_begin, n_total, first, k, u)
+    d = ctx.info()["d"]
+    red_b = 8 * (d + 4)
+    red, hred = comm.buffer(red_b)
+    sizes = ctx.seed_shard_begin(row_begin, n_total, comm.world, comm.rank, first, k, u, hred)
+    comm.allreduce_sum_f64_inplace(red)
+    bs, hbs = comm.buffer(comm.world * int(sizes[0]))
+    pg, hpg = comm.buffer(comm.world * int(sizes[1]))
+    for _ in range(1, k):
+        ctx.seed_shard_phase(0, hred, hbs)
+        comm.allgather_slots(bs, int(sizes[0]))
+        ctx.seed_shard_phase(1, hbs, hpg)
+        comm.allgather_slots(pg, int(sizes[1]))
+        ctx.seed_shard_phase(2, hpg, hred)
+        comm.allreduce_sum_f64_inplace(red)
+    return ctx.seed_shard_end(hred)
 
 
 LL_CHUNK_MAX = 64  # steps enqueued between two status polls (doubling from 2)
@@ -383,6 +472,7 @@ class DeviceLloyd:
                  dtype=np.float64):
         self.ctx, self.tol, self.reseed_row, self.n_total = ctx, tol, reseed_row, n_total
         self.comm, self.dtype = comm, np.dtype(dtype)
+        ensure_unified(ctx, comm, n_total)
         self.k, self.d = C.shape
         ref = np.array(C[0], dtype=np.float64)  # a data row: x - ref is exact
         x2 = ctx.points_sqdev(ref)
@@ -393,7 +483,7 @@ class DeviceLloyd:
         # steps enqueued from C (one call per chunk): a single shard, or a
         # context with its own RCCL communicator (Comm.attach_native)
         self.native = hasattr(ctx, "lloyd_enqueue_steps") and (
-            comm is None or id(ctx) in comm.native or comm.world == 1)
+            comm is None or comm.world == 1 or comm.has_native(ctx))
         if not self.native and comm is not None and comm.world > 1:
             self.buf, self.ptr = comm.lloyd_buffer(self.k * (self.d + 1))
         self.steps = 0
@@ -470,6 +560,7 @@ class ShardedLloyd:
     """Lloyd iterations over sharded F32X points with one all-reduce per step."""
 
     def __init__(self, ctx, comm: Comm, n_total: int, row_begin: int):
+        ensure_unified(ctx, comm, n_total)
         info = ctx.info()
         if info["mode"] != 1:
             raise NotImplementedError("sharded Lloyd needs F32X (grid) points")

@@ -188,6 +188,13 @@ struct Ctx {
   // certificates) instead of the k-way MFMA screen; switched off when too
   // many points of a step stay uncertified (clusters not separated)
   bool prune_on = true;
+  // bounded DELTA steps (screen32b, device loop only): per-point bound words
+  // (valid while every step since the last reset was a screen32b step whose
+  // centroid move ll_finalize32 accounted in bnd), the row-major hi copy the
+  // step gathers from, and the cumulative drifts bnd = int64 W[64] (2^-40
+  // units) | float W up [64] | float W down [64]
+  DevBuf zb, xh16, bnd, t_acc;
+  bool zb_valid = false, xh_valid = false, bnd_ok = false;
   int32_t run_k = 0;
   bool last_delta = false;
 #ifdef CDR_EXPERIMENTS
@@ -235,6 +242,12 @@ struct Ctx {
   DevBuf seed_x16, seed_e16, seed_mu;  // fp16-certified seeding copy (seed.hip)
   bool seed16_valid = false;
   DevBuf seed_run_buf;  // seed_run: uniforms, picks, S, flags
+  // device-resident seeding over sharded rows (seed.hip cdr_seed_shard_*):
+  // [u: k-1][picks: k][S, guess, c_mine, c_after, c_last, flags x4, pad]
+  DevBuf ss_buf;
+  int64_t ss_row_begin = 0, ss_n_total = 0, ss_nbmax = 0;
+  int32_t ss_nranks = 0, ss_rank = 0, ss_k = 0, ss_step = 0;
+  bool ss_on = false;
   DevBuf seed_tail_plan;  // pairwise layout of the partial last block (seed.hip)
   int64_t seed_tail_m = -1;
   int seed_tail_nleaves = 0, seed_tail_nheights = 0;
@@ -327,6 +340,10 @@ void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
 // comm.hip: SUM all-reduce of n int64 in place on the context stream over the
 // context's communicator; release of that communicator
 void comm_allreduce_i64(Ctx& c, long long* buf, size_t n);
+// SUM all-reduce of n doubles in place; in-place all-gather of `bytes` per rank
+// (this rank's part at buf + rank * bytes), both on the context stream
+void comm_allreduce_f64(Ctx& c, double* buf, size_t n);
+void comm_allgather(Ctx& c, void* buf, size_t bytes);
 void comm_release(Ctx& c);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

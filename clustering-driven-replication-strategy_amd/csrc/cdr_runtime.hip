@@ -271,6 +271,7 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   c.xt_valid = false;
   c.seed16_valid = false;
   c.xs_valid = false;
+  c.xh_valid = false;
   c.xb_valid = false;
   c.xa_valid = false;
   c.big_valid = false;
@@ -289,6 +290,7 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
   c.have_labels = false;
   c.run_valid = false;
   c.lab8_valid = false;
+  c.zb_valid = false;
   c.big_valid = false;
   c.seed_scanned = false;
 }
@@ -301,8 +303,11 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
   c.xt_valid = false;
   c.seed16_valid = false;
   c.xs16.release();
+  c.xh16.release();
+  c.zb.release();
   c.xa32.release();
   c.xs_valid = false;
+  c.xh_valid = false;
   c.xb16.release();
   c.xb_valid = false;
   c.xa_valid = false;
@@ -313,6 +318,7 @@ static void reset_points(Ctx& c, int64_t n, int32_t d) {
   c.n_pad = ceil_div(n > 0 ? n : 1, kSeedBlock) * kSeedBlock;
   c.run_valid = false;
   c.lab8_valid = false;
+  c.zb_valid = false;
   c.ll_on = false;
   c.labels.ensure(sizeof(int32_t) * c.n_pad);
   HIP_CHECK(hipMemsetAsync(c.labels.p, 0, sizeof(int32_t) * c.n_pad, c.stream));
@@ -434,7 +440,7 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.gb_p1, &c.gb_p2, &c.gb_hist2, &c.gb_list, &c.gb_slots, &c.sim_cnt, &c.sim_off,
                     &c.sim_tmp, &c.sim_ms, &c.sim_mbase, &c.x_small, &c.x_buf, &c.x_prim, &c.f64x_A, &c.f64x_cnt, &c.f64x_E,
                     &c.f64x_T, &c.f64x_walk, &c.f64x_G, &c.f64x_GS, &c.f64x_prof, &c.med_hist,
-                    &c.fb_accum, &c.q_acc, &c.xs16, &c.xa32, &c.xb16, &c.big_sums, &c.big_chunks, &c.seed_near, &c.seed_cents, &c.seed_ccd, &c.seg_tails, &c.seg_ents, &c.seg_scan, &c.seg_items, &c.seg_meta, &c.seed_tail_plan, &c.seed_x16, &c.seed_e16, &c.seed_mu, &c.seed_run_buf, &c.mv_list, &c.lab8, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
+                    &c.fb_accum, &c.q_acc, &c.xs16, &c.xa32, &c.xb16, &c.big_sums, &c.big_chunks, &c.seed_near, &c.seed_cents, &c.seed_ccd, &c.seg_tails, &c.seg_ents, &c.seg_scan, &c.seg_items, &c.seg_meta, &c.seed_tail_plan, &c.seed_x16, &c.seed_e16, &c.seed_mu, &c.seed_run_buf, &c.mv_list, &c.lab8, &c.zb, &c.xh16, &c.bnd, &c.t_acc, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
                     &c.ll_state};
   for (DevBuf* b : bufs) b->release();
   c.h_small.release();

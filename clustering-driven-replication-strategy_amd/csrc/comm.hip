@@ -29,6 +29,7 @@ struct Rccl {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) init_rank = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
 };
@@ -68,10 +69,12 @@ Rccl& rccl() {
   r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
   r.init_rank = reinterpret_cast<decltype(r.init_rank)>(dlsym(h, "ncclCommInitRank"));
   r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
+  r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
   r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(h, "ncclCommDestroy"));
   r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
-  r.ok = r.get_unique_id && r.init_rank && r.all_reduce && r.destroy && r.error_string;
-  if (!r.ok) r.why = "librccl lacks ncclGetUniqueId / ncclCommInitRank / ncclAllReduce";
+  r.ok = r.get_unique_id && r.init_rank && r.all_reduce && r.all_gather && r.destroy &&
+         r.error_string;
+  if (!r.ok) r.why = "librccl lacks ncclGetUniqueId / ncclCommInitRank / ncclAllReduce / ncclAllGather";
   return r;
 }
 
@@ -96,6 +99,26 @@ void comm_allreduce_i64(Ctx& c, long long* buf, size_t n) {
              "ncclAllReduce");
 }
 
+// SUM all-reduce of n doubles in place (seeding: the picked row, its index
+// and the flags; every other rank contributes zeros, so the sum is exact).
+void comm_allreduce_f64(Ctx& c, double* buf, size_t n) {
+  Rccl& r = need_rccl();
+  if (!c.comm) CDR_FAIL(CDR_ERR_STATE, "no communicator (cdr_comm_init)");
+  nccl_check(r.all_reduce(buf, buf, n, ncclFloat64, ncclSum, static_cast<ncclComm_t>(c.comm),
+                          c.stream),
+             "ncclAllReduce");
+}
+
+// In-place all-gather: `bytes` per rank, this rank's part at buf + rank * bytes.
+void comm_allgather(Ctx& c, void* buf, size_t bytes) {
+  Rccl& r = need_rccl();
+  if (!c.comm) CDR_FAIL(CDR_ERR_STATE, "no communicator (cdr_comm_init)");
+  unsigned char* b = static_cast<unsigned char*>(buf);
+  nccl_check(r.all_gather(b + (size_t)c.comm_rank * bytes, b, bytes, ncclUint8,
+                          static_cast<ncclComm_t>(c.comm), c.stream),
+             "ncclAllGather");
+}
+
 void comm_release(Ctx& c) {
   if (c.comm && g_rccl.ok) (void)g_rccl.destroy(static_cast<ncclComm_t>(c.comm));
   c.comm = nullptr;
@@ -108,6 +131,21 @@ void comm_release(Ctx& c) {
 using namespace cdr;
 
 extern "C" {
+
+int cdr_comm_available(int32_t* ok) {
+  CDR_TRY
+  if (!ok) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  *ok = rccl().ok ? 1 : 0;  // dlopen + dlsym only: no bootstrap listener
+  CDR_CATCH
+}
+
+int cdr_comm_ranks(cdr_ctx* h, int32_t* nranks, int32_t* rank) {
+  CDR_TRY
+  if (!h || !nranks || !rank) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  *nranks = h->c.comm ? h->c.comm_ranks : 0;  // 0: no communicator
+  *rank = h->c.comm ? h->c.comm_rank : 0;
+  CDR_CATCH
+}
 
 int cdr_comm_unique_id(void* id128) {
   CDR_TRY

@@ -1163,6 +1163,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   } else if (!exact_only && screen_supported(c, k)) {
     c.run_valid = false;  // the screen_fast / screen_kernel path keeps no running sums
     c.lab8_valid = false;
+    c.zb_valid = false;
     c.big_valid = false;
     screened = true;
     ScreenPlan pl;
@@ -1258,6 +1259,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   } else {
     c.run_valid = false;
     c.lab8_valid = false;
+    c.zb_valid = false;
     c.big_valid = false;
     // exact assignment for every point, then fixed-point sums from labels
     launch_assign_exact<float>(c.x32.as<float>(), c.n, c.n_pad, d, c.cent64.as<double>(), k,
@@ -1318,6 +1320,7 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
   if (c.mode != CDR_MODE_F64) CDR_FAIL(CDR_ERR_STATE, "lloyd_step_f64: points are not F64");
   c.run_valid = false;
   c.lab8_valid = false;
+  c.zb_valid = false;
   c.big_valid = false;
   const int d = c.d;
   const int cus = lloyd_num_cus(c.device);
@@ -1466,6 +1469,7 @@ int cdr_profile_reset(cdr_ctx* h, int32_t enable) {
   c.fb_accum.ensure(2 * sizeof(long long));
   HIP_CHECK(hipMemsetAsync(c.fb_accum.p, 0, 2 * sizeof(long long), c.stream));
   if (c.q_acc.p) HIP_CHECK(hipMemsetAsync(c.q_acc.p, 0, c.q_acc.bytes, c.stream));
+  if (c.t_acc.p) HIP_CHECK(hipMemsetAsync(c.t_acc.p, 0, c.t_acc.bytes, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
   CDR_CATCH
 }
@@ -1478,18 +1482,24 @@ int cdr_profile_read(cdr_ctx* h, double* out) {
   prof_collect(c);
   long long fb[2] = {0, 0};
   std::vector<long long> q(c.q_acc.bytes / sizeof(long long));
+  std::vector<long long> tq(c.t_acc.bytes / sizeof(long long));
   if (c.fb_accum.p)
     HIP_CHECK(hipMemcpyAsync(fb, c.fb_accum.p, std::min(c.fb_accum.bytes, sizeof(fb)),
                              hipMemcpyDeviceToHost, c.stream));
   if (!q.empty())
     HIP_CHECK(hipMemcpyAsync(q.data(), c.q_acc.p, c.q_acc.bytes, hipMemcpyDeviceToHost, c.stream));
+  if (!tq.empty())
+    HIP_CHECK(hipMemcpyAsync(tq.data(), c.t_acc.p, c.t_acc.bytes, hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
   for (long long v : q) fb[1] += v;
+  long long tight = 0;
+  for (long long v : tq) tight += v;
   out[0] = c.prof_screen_ms;
   out[1] = (double)c.prof_launches;
   out[2] = c.prof_step_ms;
   out[3] = c.prof_fb_points + (double)fb[0];
   out[4] = (double)fb[1];
+  out[5] = (double)tight;
   CDR_CATCH
 }
 

@@ -59,8 +59,25 @@ struct FinArgs {
   unsigned char* plan;
   int QH, MT;
   double sc, xxmax, l1x;
+  // screen32b's drift bounds (Ctx::bnd; null: not kept): when the centroids
+  // move, W_j += M + delta_j (int64, 2^-40 units, rounded up), with
+  // delta_j >= ||chat_j(new) - chat_j(old)|| and M = max_j delta_j; then W_j
+  // rounded up and down to fp32 for the next screen
+  long long* bnd;
   int abl;  // timing experiments only (0 in the product build)
 };
+
+// fp64 -> fp32 rounded up / down (W_j for screen32b)
+__device__ inline float f32_up(double v) {
+  float f = (float)v;
+  if ((double)f < v) f = nextafterf(f, INFINITY);
+  return f;
+}
+__device__ inline float f32_dn(double v) {
+  float f = (float)v;
+  if ((double)f > v) f = nextafterf(f, -INFINITY);
+  return f;
+}
 
 constexpr int kFinThreads = 512;
 constexpr int kFinLds = 64 * 17;  // (k, d+1) cells staged in LDS (screen32 shapes)
@@ -251,6 +268,8 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
   const double c0 = v0 ? a.C[j * d + f0] : 0.0, c1 = v1 ? a.C[j * d + f0 + 1] : 0.0;
   const double r0 = v0 ? a.ref[f0] : 0.0, r1 = v1 ? a.ref[f0 + 1] : 0.0;
   const double mu0 = v0 ? a.ref[d + f0] : 0.0, mu1 = v1 ? a.ref[d + f0 + 1] : 0.0;
+  const bool whead = a.bnd && row && (t & 7) == 0;
+  const long long w_old = whead ? a.bnd[j] : 0;
   const long long st0 = state[0];
   if (st0 == 0) return;  // uniform: the loop has stopped
   if (a.abl & 1) {
@@ -301,6 +320,18 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
       quad += (double)cnt * (ct * ct);
     }
   }
+  // how far centroid j moves (its 8 threads' features; screen32b's drift):
+  // fp64 errs by < 20 2^-53 relative here, sc is a power of two
+  double dq = 0.0;
+  if (v0) dq += (m0 - c0) * (m0 - c0);
+  if (v1) dq += (m1 - c1) * (m1 - c1);
+  dq += __shfl_xor(dq, 1);
+  dq += __shfl_xor(dq, 2);
+  dq += __shfl_xor(dq, 4);
+  const double dlt = sqrt(dq) * a.sc * (1.0 + 0x1p-45);
+  double dmx = row ? dlt : 0.0;
+#pragma unroll
+  for (int o = 32; o >= 8; o >>= 1) dmx = fmax(dmx, __shfl_xor(dmx, o));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {  // fixed pattern: deterministic
     ss += __shfl_xor(ss, o);
@@ -309,9 +340,10 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
     empty |= __shfl_xor(empty, o);
     fbv += __shfl_xor(fbv, o);
   }
-  __shared__ double r_ss[8], r_cross[8], r_quad[8];
+  __shared__ double r_ss[8], r_cross[8], r_quad[8], r_dm[8];
   __shared__ int r_empty[8], r_fb[8];
   if (lane == 0) {
+    r_dm[wv] = dmx;
     r_ss[wv] = ss;
     r_cross[wv] = cross;
     r_quad[wv] = quad;
@@ -364,6 +396,22 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
   if (!mv) return;
   if (v0) a.C[j * d + f0] = m0;
   if (v1) a.C[j * d + f0 + 1] = m1;
+  if (whead) {  // screen32b's drift bounds of this move
+    double M = 0.0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) M = fmax(M, r_dm[w]);
+    double inc = (M + dlt) * (1.0 + 0x1p-50);
+    if (!(inc < 0x1p10)) inc = 0x1p10;  // (NaN too)
+    // saturating: past 2^52 units the fp64 value is no longer exact and every
+    // bound test fails from then on (W up = inf)
+    const long long wn =
+        w_old >= (1LL << 60) ? w_old : w_old + (long long)ceil(ldexp(inc, 40));
+    a.bnd[j] = wn;
+    const double wvv = ldexp((double)wn, -40);
+    float* wf = reinterpret_cast<float*>(a.bnd + 64);
+    wf[j] = wn < (1LL << 52) ? f32_up(wvv) : INFINITY;
+    wf[64 + j] = f32_dn(wvv);
+  }
   if (!a.plan || reason != kLLRun || (a.abl & 2)) return;
   // ---- the next step's plan (plan32_build, per element) ----
   unsigned char* __restrict__ plan = a.plan;
@@ -628,6 +676,11 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   c.ll_sums.ensure(sizeof(long long) * (size_t)k * (d + 1));
   c.ll_ref.ensure(sizeof(double) * 2 * d);
   c.ll_state.ensure(sizeof(long long) * kLLState);
+  // screen32b's drift bounds (kept by ll_finalize32 only)
+  const bool fin_old = std::getenv("CDR_FIN_OLD") && std::atoi(std::getenv("CDR_FIN_OLD"));
+  c.bnd_ok = c.ll_devplan && !fin_old;
+  c.bnd.ensure(sizeof(long long) * 64 + 2 * sizeof(float) * 64);
+  HIP_CHECK(hipMemsetAsync(c.bnd.p, 0, c.bnd.bytes, c.stream));
   std::vector<double> rm(2 * d);
   for (int f = 0; f < d; ++f) {
     rm[f] = ref[f];
@@ -646,6 +699,7 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   // the first step recomputes the running sums from scratch (see resume)
   c.run_valid = false;
   c.lab8_valid = false;
+  c.zb_valid = false;
   c.big_valid = false;
   if (c.ll_devplan) ll_plan(c);
   if (c.ll_devbig) ll_plan_big(c);
@@ -733,6 +787,7 @@ static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
   a.sc = std::ldexp(1.0, c.sigma);
   a.xxmax = c.ll_xxmax;
   a.l1x = c.ll_l1x;
+  a.bnd = c.bnd_ok ? c.bnd.as<long long>() : nullptr;
   a.abl = 0;
 #ifdef CDR_EXPERIMENTS
   if (const char* e = std::getenv("CDR_FIN_ABL")) a.abl = std::atoi(e);
@@ -856,6 +911,7 @@ int cdr_lloyd_resume(cdr_ctx* h, const double* C, int32_t add_steps, int32_t hos
   // among them never zeroed and rebuilt them.  The next step starts afresh.
   c.run_valid = false;
   c.lab8_valid = false;
+  c.zb_valid = false;
   c.big_valid = false;
   CDR_CATCH
 }

@@ -960,7 +960,14 @@ struct FixArgs {
   int ho;
   const float* ms;  // -mu_f 2^sigma
   float sig;
+  // screen32b's per-point bound words (null otherwise): a label change here
+  // leaves the point's word "no bound" with its new label
+  uint32_t* zb;
 };
+
+// screen32b's bound word of a point whose bound is unknown (a quiet NaN: the
+// bound test fails) — the low 6 bits carry the label
+constexpr unsigned kZbStale = 0x7FC00000u;
 
 // Workgroup b applies the lists of screen32d waves FR b .. FR b + FR - 1 (a region
 // spread over the whole workgroup) to an LDS table (rows padded to 65: the
@@ -1274,6 +1281,7 @@ __device__ __forceinline__ void fixup_regions(const FixArgs& a, int r0, int FR, 
         if (jmin != old && !(a.abl & 32)) {
           a.labels[own] = jmin;
           a.lab8[own] = (uint8_t)jmin;
+          if (a.zb) a.zb[own] = kZbStale | (unsigned)jmin;  // (screen32b: bound unknown)
 #pragma unroll
           for (int f = 0; f < DM; ++f) {
             if (f < d) {
@@ -1716,6 +1724,439 @@ __global__ __launch_bounds__(256, 5) void screen32p(S32PArgs a) {
   }
   fixup_regions<Q, MT>(a.fx, blockIdx.x * 4, 4, blockIdx.x % kRunSlices, L, FixPlan{sA, sC});
 }
+
+// ---------------------------------------------------------------------------
+// Bounded DELTA screen: screen32b (device loop; d <= 16, k <= 64: configs 2, 3).
+//
+// screen32p still reads every point's 32-byte hi copy every step.  After the
+// first steps almost every point keeps its label by a wide margin and the
+// centroids move little, so a point's distances can be bounded across steps
+// instead of recomputed (Hamerly's bounds, SURVEY.md §7 hard parts (c): exact,
+// the same labels, less work).  With t_j(s) = ||xhat - chat_j(s)|| (the
+// reference's distance up to 2^sigma) and the centroid drifts
+// delta_j(s) >= ||chat_j(s) - chat_j(s - 1)||, M(s) = max_j delta_j(s):
+//   t_a(t) <= t_a(t0) + sum_{t0 < s <= t} delta_a(s),
+//   min_{j != a} t_j(t) >= min_{j != a} t_j(t0) - sum_{t0 < s <= t} M(s).
+// ll_finalize32 keeps the cumulative W_j(t) = sum_{s <= t} (M(s) + delta_j(s))
+// as exact int64 multiples of 2^-40 (every increment rounded up) and hands
+// this step W_j rounded up and down to fp32 (wup / wdn).  A point whose label
+// a was decided at step t0 with rigorous bounds u0 >= t_a(t0) and
+// l0 <= min_{j != a} t_j(t0) stores ONE word
+//   Z = l0 (1 - 2^-20) - u0 + wdn_a(t0)     (rounded down; low 6 bits: a)
+// and keeps a at step t when Z > wup_a(t): then
+//   min_{j != a} t_j(t) > t_a(t) + 2^-20 l0 > t_a(t) (1 + 2^-22),
+// far above the reference's fp64 rounding (< 2^-45), so np.argmin of the
+// reference's norms is a (src/kmeans_plusplus.py:33-34) and the point's
+// coordinates are not read at all.
+//
+// Per wave: phase 1 streams the bound words (4 per lane, 1 KiB per load, four
+// chunks in flight) and lists the points that fail in LDS; phase 2 gathers
+// those points' hi rows (AoS copy XH, one line per point) 64 at a time, one
+// batch ahead, and decides them exactly as screen32p does (triangle test
+// against c32_a, else screen32h's k-way screen and hi-only certificate, else
+// the exact fallback of the fused fixup), writing the point's new word:
+//   triangle kept:  u0 = ub_a, l0 = h_a (1 - 2^-22) - ub_a;
+//   k-way certified (label b, keys vb <= vs):
+//     u0 = sqrt(vb (1 + 2^-16) + thr0 + ||h||^2_up - D_lo) (1 + 2^-19) + dn,
+//     l0 = sqrt(vs - thr0 - D_hi + ||h||^2_lo) (1 - 2^-19) - dn
+//     (|S_j - exact| <= E < thr0 / 2: thr0 also covers the fp32 rounding of
+//     these sums; every other key is >= vs);
+//   uncertified: "no bound" (kZbStale | old label; the fixup rewrites the
+//     label if the exact decision moves the point).
+// Moves and fallbacks go to the same per-wave lists as screen32p's, and the
+// fused fixup finishes the step, so labels and int64 running sums are those
+// of the full screen.
+// ---------------------------------------------------------------------------
+constexpr int kBChunk = 256;  // points per wave-chunk of the bound stream (4 per lane)
+constexpr int kBList = 512;   // per-wave LDS list of the points whose bound failed
+constexpr int kBPD = 4;       // chunks in flight per wave (phase 1)
+
+struct S32BArgs {
+  S32PArgs p;                // the pruned screen's plan, lists and fused fixup
+  const unsigned char* XH;   // AoS hi-only copy: 2 x 16 B (d <= 8: 2 x 8 B) per point
+  uint32_t* zb;              // per point: Z bits | label (n_pad words)
+  const float* wup;          // [64] W_j of this step's centroids, rounded up
+  const float* wdn;          // [64] rounded down
+  int64_t nchunks;           // n_pad / kBChunk
+  long long* t_acc;          // profiling: points whose bound failed, per wave (null: off)
+  int dbg;                   // tests only (CDR_BOUNDS_DBG): 1 = every bound fails
+};
+
+// The stored word of bounds (l0, u0) and W_a rounded down (see above):
+// Z = l0 (1 - 2^-20) - u0 + w minus 2^-21 (|l0| + u0 + w), which covers the
+// three fp32 roundings of the sum; no usable bound -> -1 (the test fails).
+__device__ __forceinline__ unsigned zb_pack(float l0, float u0, float w, unsigned label) {
+  if (!(l0 > 0.0f) || !(u0 >= 0.0f) || !(w >= 0.0f)) return 0xBF800000u | label;
+  l0 = fminf(l0, 0x1p60f) * (1.0f - 0x1p-20f);
+  const float s = (l0 - u0) + w;
+  const float m = 0x1p-21f * ((l0 + u0) + w);
+  const float z = s - m;
+  return (z > 0.0f ? (__float_as_uint(z) & ~63u) : 0xBF800000u) | label;
+}
+
+template <int Q, int MT>
+__global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
+  const S32PArgs& a = B.p;
+  constexpr int QH = FixDims<Q>::QH;
+  if (a.gate && a.gate[0] == 0) return;
+  constexpr bool H1 = QH == 1;
+  constexpr int kTile = H1 ? 512 : 1024;  // bytes per 32-point tile of the queue
+  constexpr int kHalf = kTile / 2;
+  constexpr int kPB = H1 ? 8 : 16;        // bytes per (point, half)
+  constexpr int NWH = kPB / 4;            // dwords per point half
+  constexpr int kRow = 2 * kPB;           // bytes per point in XH
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float c32s[64 * kPrStr + 128];
+  float* const eb = c32s + 64 * kPrStr;  // E_j
+  float* const hc = eb + 64;             // h_j
+  // per wave: the k-way queue (screen32p's ring) and, after the last drain,
+  // the fused fixup's table (FixLds)
+  constexpr size_t kQBytes = 4 * 2 * 2 * kTile + 4 * 128 * sizeof(int2);
+  __shared__ __attribute__((aligned(16))) unsigned char qlds[kQBytes > kFixLdsBytes ? kQBytes : kFixLdsBytes];
+  typedef unsigned char QRow[2][2 * kTile];
+  QRow* qd = reinterpret_cast<QRow*>(qlds);
+  int2 (*qm)[128] = reinterpret_cast<int2 (*)[128]>(qlds + 4 * 2 * 2 * kTile);
+  // per wave: points whose bound failed, (chunk iteration << 14 | offset << 6 | label)
+  __shared__ unsigned flist[4][kBList];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = t >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
+  const int nwaves = gridDim.x * 4;
+  const int64_t nchunks = B.nchunks;
+
+  // ---- phase 1 loads: the first chunks overlap the prologue ----
+  // Ordinary loads (the compiler's s_waitcnt counts them): every iteration
+  // issues exactly one, a chunk past the end reloads the last one, so the
+  // counts are the same on every path and kBPD - 1 chunks stay in flight.
+  auto zload = [&](u4v& z, int64_t ci) __attribute__((always_inline)) {
+    const int64_t cc = ci < nchunks ? ci : nchunks - 1;  // past the end: reload the last
+    z = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(B.zb + cc * kBChunk) + lane);
+  };
+  u4v zc[kBPD];
+#pragma unroll
+  for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], wave + (int64_t)i * nwaves);
+
+  // ---- the plan (screen32p's staging, one round trip) ----
+  __shared__ h8 sA[MT * 2 * 64];
+  __shared__ __attribute__((aligned(16))) float sC[MT * 4 * 2 * 4];
+  constexpr int kPr4 = (64 * kPrStr + 128) / 4;
+  static_assert(kPr4 <= 512 && MT * 2 * 64 <= 256, "prologue: two float4 per thread");
+  const f4* prune4 = reinterpret_cast<const f4*>(a.prune);
+  const f4 pv0 = prune4[t];
+  const f4 pv1 = t + 256 < kPr4 ? prune4[t + 256] : f4{0.f, 0.f, 0.f, 0.f};
+  h8 av = {};
+  if (t < MT * 2 * 64) av = a.frag[t];
+  float cv = 0.0f;
+  const int cm = t >> 5, ci4 = (t >> 3) & 3, chh = (t >> 2) & 1, cc = t & 3;
+  if (t < MT * 32) cv = a.cinit[(cm * 16 + ci4 * 4 + cc) * 64 + chh * 32];
+  const float wup_l = B.wup[lane], wdn_l = B.wdn[lane];  // lane j: W_j (k <= 64)
+  const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
+  const float Dv = a.thr_dev ? a.thr_dev[1] : a.Dv;
+  const float Dlo = Dv * (1.0f - 0x1p-19f), Dhi = Dv * (1.0f + 0x1p-19f);  // D_lo < D < D_hi
+  reinterpret_cast<f4*>(c32s)[t] = pv0;
+  if (t + 256 < kPr4) reinterpret_cast<f4*>(c32s)[t + 256] = pv1;
+  if (t < MT * 2 * 64) sA[t] = av;
+  if (t < MT * 32) sC[t] = cv;
+  __syncthreads();
+
+  int2* fb_region = a.fb_list + (size_t)wave * a.cap;
+  int2* mv_region = a.mv_list + (size_t)wave * a.cap;
+  int fb_used = 0, mv_used = 0;
+  struct Row {
+    unsigned w[2 * NWH];  // the point's hi row: half 0 then half 1 (packed fp16 pairs)
+  };
+  // q = ||h - c32_j||^2 (screen32p's dist2)
+  auto dist2 = [&](const Row& b, int j) __attribute__((always_inline)) -> float {
+    const f4* c4 = reinterpret_cast<const f4*>(c32s + j * kPrStr);
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 acc = {0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < NWH; ++q) {
+      const f4 cq = c4[q];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = 2 * q + u;
+        const f2 df = {mix_sub_lo(b.w[i], cq[2 * u]), mix_sub_hi(b.w[i], cq[2 * u + 1])};
+        acc = __builtin_elementwise_fma(df, df, acc);
+      }
+    }
+    return acc.x + acc.y;
+  };
+  // (best, runner-up) keys of one 32-point tile of queued points (screen32p's tile)
+  auto tile = [&](const u4v& v, unsigned& bk, unsigned& sk, float& hp) __attribute__((always_inline)) {
+    const h8 BH = __builtin_bit_cast(h8, v);
+    hp = 0.0f;
+#pragma unroll
+    for (int i = 0; i < (H1 ? 4 : 8); i += 2)
+      hp = __builtin_amdgcn_fdot2(h2{BH[i], BH[i + 1]}, h2{BH[i], BH[i + 1]}, hp, false);
+    unsigned b = 0xFFFFFFFFu, s = 0xFFFFFFFFu;
+#pragma nounroll
+    for (int m = 0; m < MT; ++m) {
+      h8 A0 = sA[(m * 2 + 0) * 64 + lane];
+      const h8 A1 = sA[(m * 2 + 1) * 64 + lane];
+      if constexpr (H1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A0[4 + i] = A1[i];
+      f16v acc;
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const f4 c4v = *reinterpret_cast<const f4*>(sC + ((m * 4 + i4) * 2 + (lane >> 5)) * 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * i4 + i] = c4v[i];
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, BH, acc, 0, 0, 0);
+      if constexpr (!H1) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, BH, acc, 0, 0, 0);
+      const unsigned rb = 32u * (unsigned)m;
+      auto key = [&](int i) {
+        return (__float_as_uint(acc[i]) & ~63u) | (rb + (unsigned)(8 * (i >> 2) + (i & 3)));
+      };
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        const unsigned x = key(q), y = key(q + 1);
+        unsigned tq;
+        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(tq) : "v"(b), "v"(x), "v"(y));
+        asm("v_min3_u32 %0, %1, %2, %3" : "=v"(b) : "v"(b), "v"(x), "v"(y));
+        s = min(s, tq);
+      }
+    }
+    bk = b | ((unsigned)(lane >> 5) << 2);
+    sk = s | ((unsigned)(lane >> 5) << 2);
+  };
+  // the k-way screen of queue block qb (nvalid entries), its lists and bound words
+  auto drain = [&](int qb, int nvalid) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's queue writes
+    const unsigned char* src = qd[wv][qb];
+    u4v v[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      if constexpr (H1) {
+        const uint2 x = *reinterpret_cast<const uint2*>(src + tt * kTile + lane * kPB);
+        v[tt] = u4v{x.x, x.y, x.x, x.y};
+      } else {
+        v[tt] = *reinterpret_cast<const u4v*>(src + tt * kTile + lane * kPB);
+      }
+    }
+    const int2 meta = qm[wv][qb * 64 + lane];  // lane l owns entry l after the swap
+    unsigned bA = 0, sA_ = 0, bB = 0, sB = 0;
+    float hA = 0.0f, hB = 0.0f;
+#pragma nounroll
+    for (int tt = 0; tt < 2; ++tt) {
+      unsigned bk, sk;
+      float hp;
+      tile(tt == 0 ? v[0] : v[1], bk, sk, hp);
+      if (tt == 0) {
+        bA = bk;
+        sA_ = sk;
+        hA = hp;
+      } else {
+        bB = bk;
+        sB = sk;
+        hB = hp;
+      }
+    }
+    swap32(bA, bB);
+    swap32(sA_, sB);
+    merge_top2(bA, sA_, bB, sB);
+    const int label = (int)(bA & 63u);
+    const float vb = __uint_as_float(bA & ~63u);
+    const float vs = __uint_as_float(sA_ & ~63u);
+    float thr = fmaf(vb, thr_rel, thr0);
+    unsigned ua = __float_as_uint(hA), ub = __float_as_uint(hB);
+    swap32(ua, ub);
+    const float hsum = __uint_as_float(ua) + __uint_as_float(ub);
+    const float hh = fmaf(hsum, 1.0f + 0x1p-18f, 0x1p-20f);  // >= ||h||^2
+    const float hl = hsum * (1.0f - 0x1p-18f);               // <= ||h||^2
+    const float dn = fmaf(0x1p-11f * (1.0f + 0x1p-9f), __builtin_amdgcn_sqrtf(hh), 0x1p-23f);
+    {  // the hi-only certificate (screen32d)
+      const float K = thr0 + hh - Dlo;
+      const float Gs = fmaxf(vs + K, 0x1p-100f), Gb = fmaxf(fmaf(vb, thr_rel, K), 0x1p-100f);
+      thr += 2.0f * (1.0f + 0x1p-19f) * dn * (__builtin_amdgcn_sqrtf(Gs) + __builtin_amdgcn_sqrtf(Gb));
+    }
+    const bool valid = lane < nvalid;
+    const bool cert = vs > thr;  // NaN: never certified
+    const int pt = meta.x, ob = meta.y;
+    const bool moved = valid && cert && label != ob;
+    if (moved) {
+      a.labels[pt] = label;
+      a.lab8[pt] = (uint8_t)label;
+    }
+    // the point's bound word: from its best and runner-up keys, or "no bound"
+    const float gb = fmaf(vb, thr_rel, thr0 + hh - Dlo);
+    const float gs = vs - ((thr0 + Dhi) - hl);
+    const float u0 = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gb, 0.0f)), 1.0f + 0x1p-19f, dn);
+    const float l0 = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gs, 0.0f)), 1.0f - 0x1p-19f, -dn);
+    const float wl = __shfl(wdn_l, label);
+    if (valid) B.zb[pt] = cert ? zb_pack(l0, u0, wl, (unsigned)label) : (kZbStale | (unsigned)ob);
+    const bool unc = valid && !cert;
+    const unsigned long long mv = __ballot(moved);
+    const unsigned long long need = __ballot(unc);
+    const int rm = __builtin_amdgcn_mbcnt_hi((unsigned)(mv >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((unsigned)mv, 0u));
+    const int rn = __builtin_amdgcn_mbcnt_hi((unsigned)(need >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((unsigned)need, 0u));
+    if (moved) mv_region[mv_used + rm] = int2{pt, ob | (label << 16)};
+    if (unc) fb_region[fb_used + rn] = int2{pt, ob};
+    mv_used += __popcll(mv);
+    fb_used += __popcll(need);
+  };
+  int qh = 0, qn = 0;  // k-way queue head (next slot, mod 128) and length: wave-uniform
+  int qtot = 0, ttot = 0;
+  // one gathered point per lane: the triangle test, else the k-way queue
+  auto process = [&](const Row& b, bool valid, int pt, int ao) __attribute__((always_inline)) {
+    const float qa = dist2(b, ao);
+    const float uba = fmaf(__builtin_amdgcn_sqrtf(qa), 1.0f + 0x1p-18f, eb[ao]);
+    const float l0 = fmaf(hc[ao], 1.0f - 0x1p-22f, -uba);
+    const bool keep = l0 > uba * (1.0f + 0x1p-20f);
+    if (valid && keep) B.zb[pt] = zb_pack(l0, uba, __shfl(wdn_l, ao), (unsigned)ao);
+    const bool q = valid && !keep;
+    const unsigned long long m = __ballot(q);
+    if (m) {
+      if (q) {
+        const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        const int slot = (qh + r) & 127;
+        const int e = slot & 63;
+        unsigned char* dst = qd[wv][slot >> 6] + (e >> 5) * kTile + (e & 31) * kPB;
+        if constexpr (H1) {
+          *reinterpret_cast<uint2*>(dst) = uint2{b.w[0], b.w[1]};
+          *reinterpret_cast<uint2*>(dst + kHalf) = uint2{b.w[2], b.w[3]};
+        } else {
+          *reinterpret_cast<uint4*>(dst) = uint4{b.w[0], b.w[1], b.w[2], b.w[3]};
+          *reinterpret_cast<uint4*>(dst + kHalf) = uint4{b.w[4], b.w[5], b.w[6], b.w[7]};
+        }
+        qm[wv][slot] = int2{pt, ao};
+      }
+      const int c = __popcll(m);
+      qh = (qh + c) & 127;
+      qn += c;
+      qtot += c;
+      if (qn >= 64) {
+        drain(((qh - qn) & 127) >> 6, 64);
+        qn -= 64;
+      }
+    }
+  };
+  // ---- phase 2: the listed points, 64 per batch, the next batch's rows in flight ----
+  // The gathers are ordinary loads too: a load issued from inline asm leaves
+  // a register the allocator may copy (at a join, around a call-sized block)
+  // before the data lands, which the compiler's own counts never do.
+  unsigned* const fl = flist[wv];
+  struct GB {
+    Row r;
+    int pt, ao;
+    bool valid;
+  };
+  auto gload = [&](GB& g, int b, int cnt) __attribute__((always_inline)) {
+    const int e = 64 * b + lane;
+    g.valid = e < cnt;
+    const unsigned ent = fl[g.valid ? e : 64 * b];  // (entry 64 b exists)
+    const int64_t ci = wave + (int64_t)(ent >> 14) * nwaves;
+    const int64_t pt = ci * kBChunk + ((ent >> 6) & 255);
+    g.pt = (int)pt;
+    g.ao = (int)(ent & 63);
+    const u4v* src = reinterpret_cast<const u4v*>(B.XH + pt * kRow);
+    const u4v q0 = __builtin_nontemporal_load(src);
+    g.r.w[0] = q0.x; g.r.w[1] = q0.y; g.r.w[2] = q0.z; g.r.w[3] = q0.w;
+    if constexpr (!H1) {
+      const u4v q1 = __builtin_nontemporal_load(src + 1);
+      g.r.w[4] = q1.x; g.r.w[5] = q1.y; g.r.w[6] = q1.z; g.r.w[7] = q1.w;
+    }
+  };
+  // every full batch of the list (all of it when `last`); a partial batch
+  // stays at the front for the next call
+  auto phase2 = [&](int& cnt, bool last) __attribute__((always_inline)) {
+    const int nb = last ? (cnt + 63) >> 6 : cnt >> 6;
+    if (nb == 0) return;
+    ttot += last ? cnt : nb * 64;
+    GB g;
+    gload(g, 0, cnt);
+    for (int b = 0; b < nb; ++b) {
+      const GB cur = g;
+      if (b + 1 < nb) gload(g, b + 1, cnt);
+      process(cur.r, cur.valid, cur.pt, cur.ao);
+    }
+    const int done = nb * 64;
+    const int rem = last ? 0 : cnt - done;
+    if (rem > 0) {
+      const unsigned v = lane < rem ? fl[done + lane] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < rem) fl[lane] = v;
+    }
+    cnt = rem;
+  };
+
+  // ---- phase 1: the bound words, 4 points per lane per chunk ----
+  int cnt = 0;  // listed points (wave-uniform)
+  int64_t it = 0;
+  for (int64_t C0 = wave; C0 < nchunks; C0 += (int64_t)kBPD * nwaves) {
+#pragma unroll
+    for (int i = 0; i < kBPD; ++i, ++it) {
+      const int64_t Ci = C0 + (int64_t)i * nwaves;
+      if (Ci >= nchunks) break;
+      zload(zc[(i + kBPD - 1) % kBPD], Ci + (int64_t)(kBPD - 1) * nwaves);
+      const u4v z = zc[i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const unsigned w = z[u];
+        const unsigned lab = w & 63u;
+        const bool fail = !(__uint_as_float(w & ~63u) > __shfl(wup_l, (int)lab)) || (B.dbg & 1);
+        const unsigned long long m = __ballot(fail);
+        if (m) {
+          if (fail) {
+            const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            fl[cnt + r] = (unsigned)it << 14 | (unsigned)(4 * lane + u) << 6 | lab;
+          }
+          cnt += __popcll(m);
+        }
+      }
+      if (cnt > kBList - kBChunk) phase2(cnt, false);
+    }
+  }
+  phase2(cnt, true);
+  if (qn > 0) drain(((qh - qn) & 127) >> 6, qn);  // the partial queue block
+  if (lane == 0) {
+    a.fb_count[wave] = fb_used;
+    a.mv_count[wave] = mv_used;
+    if (a.q_acc) a.q_acc[wave] += qtot;
+    if (B.t_acc) B.t_acc[wave] += ttot;
+  }
+  if (!a.fuse) return;
+  __syncthreads();  // every queue drained (its LDS becomes the table); lists written
+  const FixLds L(qlds);
+  if (lane == 0) {
+    L.s_mv[wv + 1] = mv_used;
+    L.s_fb[wv + 1] = fb_used;
+  }
+  fixup_regions<Q, MT>(a.fx, blockIdx.x * 4, 4, blockIdx.x % kRunSlices, L, FixPlan{sA, sC});
+}
+
+// Bound words before the first bounded step of a run of them: every real
+// point "no bound" with its current label (lab8), padding rows "always keep".
+__global__ void zb_reset_kernel(const uint8_t* __restrict__ lab8, uint32_t* __restrict__ zb,
+                                int64_t n, int64_t n_pad, const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad;
+       i += (int64_t)gridDim.x * blockDim.x)
+    zb[i] = i < n ? (kZbStale | lab8[i]) : 0x7F000000u;  // (2^127: above any W)
+}
+
+// The hi-only screen copy row by row (XH: screen32b's gathers read one line
+// per point), from the tiled copy: tile of 32 points [2 halves][32][kPB].
+template <int kPB>
+__global__ void aos_hi_kernel(const unsigned char* __restrict__ xs, int64_t n_pad,
+                              unsigned char* __restrict__ xh) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_pad * 2;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pt = t >> 1;
+    const int hh = (int)(t & 1);
+    const unsigned char* s = xs + (pt >> 5) * (64 * kPB) + hh * (32 * kPB) + (pt & 31) * kPB;
+    unsigned char* d = xh + pt * (2 * kPB) + hh * kPB;
+    if constexpr (kPB == 16) *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+    else *reinterpret_cast<uint2*>(d) = *reinterpret_cast<const uint2*>(s);
+  }
+}
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -1985,6 +2426,30 @@ static void screen32p_launch(int Q, int MT, int PD, dim3 grid, hipStream_t s,
 #undef CDR_S32P_GO
 }
 
+#define CDR_S32B_ALL(X) X(1, 1) X(1, 2) X(2, 1) X(2, 2) X(3, 1) X(3, 2) X(4, 1) X(4, 2)
+
+static int screen32b_blocks_per_cu(int Q, int MT) {
+  static int cache[4][2] = {};
+  int& nb = cache[Q - 1][MT - 1];
+  if (!nb) {
+    hipError_t e = hipErrorInvalidValue;
+#define CDR_S32B_OCC(Q_, M_) \
+    if (Q == Q_ && MT == M_) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32b<Q_, M_>, 256, 0);
+    CDR_S32B_ALL(CDR_S32B_OCC)
+#undef CDR_S32B_OCC
+    if (e != hipSuccess || nb < 1) nb = 2;
+    if (nb > 8) nb = 8;
+  }
+  return nb;
+}
+
+static void screen32b_launch(int Q, int MT, dim3 grid, hipStream_t s, const S32BArgs& p) {
+#define CDR_S32B_GO(Q_, M_) \
+  if (Q == Q_ && MT == M_) hipLaunchKernelGGL((screen32b<Q_, M_>), grid, dim3(256), 0, s, p);
+  CDR_S32B_ALL(CDR_S32B_GO)
+#undef CDR_S32B_GO
+}
+
 // Prefetch depth of screen32d: CDR_S32D_PD=2|3|4 (comparisons), else the
 // measured default per shape.
 static int s32d_depth(int QH) {
@@ -2016,9 +2481,17 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   // the fixup fused into screen32p's tail (CDR_PRUNE_FUSE=0: a separate fixup32)
   static const bool fuse_env =
       !std::getenv("CDR_PRUNE_FUSE") || std::atoi(std::getenv("CDR_PRUNE_FUSE"));
+  // bounded screen (screen32b) in the device loop, where ll_finalize32 keeps
+  // the drift bounds of every centroid move (CDR_BOUNDS=0 turns it off)
+  const bool bnd_env = std::getenv("CDR_BOUNDS") && std::atoi(std::getenv("CDR_BOUNDS"));
+  const bool BND = PR && bnd_env && gate && dthr && c.ll_on && c.bnd_ok &&
+                   c.n_pad < (int64_t(1) << 31);
+  if (!BND) c.zb_valid = false;  // another path decides this step's labels
   int bpc;
   const int PD = PR ? PPD : LRn ? LRn : s32d_depth(QH);
-  if (PR) {
+  if (BND) {
+    bpc = screen32b_blocks_per_cu(PQ, MT);
+  } else if (PR) {
     bpc = screen32p_blocks_per_cu(PQ, MT, PPD);
     static const int bpc_env = std::getenv("CDR_S32P_BPC") ? std::atoi(std::getenv("CDR_S32P_BPC")) : 0;
     if (bpc_env >= 1 && bpc_env < bpc) bpc = bpc_env;
@@ -2050,10 +2523,13 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     else if (MT == 1) bpc = s32d_blocks_per_cu<2, 1, 2>();
     else bpc = s32d_blocks_per_cu<2, 2, 2>();
   }
-  int nwg = (int)std::min<int64_t>(ceil_div(groups, 4), (int64_t)cus * bpc);
+  // (screen32b: a wave's unit is a chunk of kBChunk points, not a 64-point group)
+  const int64_t units = BND ? c.n_pad / kBChunk : groups;
+  const int unit_pts = BND ? kBChunk : 64;
+  int nwg = (int)std::min<int64_t>(ceil_div(units, 4), (int64_t)cus * bpc);
   if (nwg < 1) nwg = 1;
   const int nwaves = nwg * 4;
-  const int cap = (int)(ceil_div(groups, nwaves) * 64);
+  const int cap = (int)(ceil_div(units, nwaves) * unit_pts);
   c.fb_list.ensure(sizeof(int2) * (size_t)nwaves * cap);
   c.mv_list.ensure(sizeof(int2) * (size_t)nwaves * cap);
   c.mv_count.ensure(sizeof(int32_t) * (size_t)nwaves);
@@ -2116,6 +2592,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   f.ho = HO;
   f.ms = c.mu_s.as<float>();
   f.sig = (float)std::ldexp(1.0, c.sigma);
+  f.zb = nullptr;
 #ifdef CDR_EXPERIMENTS
   if (const char* e = std::getenv("CDR_FIX_ABL")) f.abl = std::atoi(e);
 #endif
@@ -2156,10 +2633,52 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     p.fx = f;
     p.fx.fr = 4;
     p.fuse = fused ? 1 : 0;
+    if (BND) {
+      // bound words: reset (every point "no bound", labels from lab8) at the
+      // first bounded step of a run; the row-major hi copy once per point set
+      c.zb.ensure(sizeof(uint32_t) * (size_t)c.n_pad);
+      if (!c.zb_valid) {
+        hipLaunchKernelGGL(zb_reset_kernel, dim3(2048), dim3(256), 0, c.stream,
+                           c.lab8.as<uint8_t>(), c.zb.as<uint32_t>(), c.n, c.n_pad, gate);
+        HIP_CHECK(hipGetLastError());
+      }
+      if (!c.xh_valid) {
+        c.xh16.ensure((size_t)c.n_pad * (QH == 1 ? 16 : 32));
+        if (QH == 1)
+          hipLaunchKernelGGL(aos_hi_kernel<8>, dim3(4096), dim3(256), 0, c.stream,
+                             c.xs16.as<unsigned char>(), c.n_pad, c.xh16.as<unsigned char>());
+        else
+          hipLaunchKernelGGL(aos_hi_kernel<16>, dim3(4096), dim3(256), 0, c.stream,
+                             c.xs16.as<unsigned char>(), c.n_pad, c.xh16.as<unsigned char>());
+        HIP_CHECK(hipGetLastError());
+        c.xh_valid = true;
+      }
+      if (c.prof_on && c.t_acc.bytes < sizeof(long long) * nwaves) {  // (zeroed when grown)
+        c.t_acc.ensure(sizeof(long long) * nwaves);
+        HIP_CHECK(hipMemsetAsync(c.t_acc.p, 0, c.t_acc.bytes, c.stream));
+      }
+      S32BArgs b;
+      f.zb = c.zb.as<uint32_t>();  // (the separate fixup32, CDR_PRUNE_FUSE=0)
+      b.p = p;
+      b.p.fx.zb = c.zb.as<uint32_t>();
+      b.XH = c.xh16.as<unsigned char>();
+      b.zb = c.zb.as<uint32_t>();
+      b.wup = reinterpret_cast<const float*>(c.bnd.as<long long>() + 64);
+      b.wdn = b.wup + 64;
+      b.nchunks = c.n_pad / kBChunk;
+      b.t_acc = c.prof_on ? c.t_acc.as<long long>() : nullptr;
+      b.dbg = std::getenv("CDR_BOUNDS_DBG") ? std::atoi(std::getenv("CDR_BOUNDS_DBG")) : 0;
+      c.zb_valid = true;
+      snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32b<%d,%d>%s", PQ, MT,
+               fused ? "+fixup" : "");
+      if (prof) prof_mark(c, 0);
+      screen32b_launch(PQ, MT, grid, c.stream, b);
+    } else {
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32p<%d,%d,%d>%s", PQ, MT, PPD,
              fused ? "+fixup" : "");
     if (prof) prof_mark(c, 0);
     screen32p_launch(PQ, MT, PPD, grid, c.stream, p);
+    }
   } else {
   if (LRn)
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>lds", MT, PD);

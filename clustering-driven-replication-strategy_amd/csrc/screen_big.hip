@@ -1636,6 +1636,7 @@ static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* th
   c.big_k = k;
   c.run_valid = false;
   c.lab8_valid = false;
+  c.zb_valid = false;
   return true;
 }
 

@@ -585,6 +585,7 @@ struct SeedDev {
   const double* gate = nullptr;
   const double* c_last = nullptr;
   const double* u = nullptr;
+  const double* c_in = nullptr;  // (sharded device seeding: the shard's exact start)
 };
 
 constexpr int kPass = 1024;
@@ -667,6 +668,7 @@ __global__ __launch_bounds__(1024) void approx_prefix_kernel(const double* __res
     SeedDev dv) {
   if (dv.gate && dv.gate[0] != 0.0) return;
   if (dv.S) S = dv.S[0];
+  if (dv.c_in) c_in = dv.c_in[0];
   __shared__ double part[1024];
   const int t = threadIdx.x;
   const int64_t per = (nb + 1023) / 1024;
@@ -937,6 +939,7 @@ __global__ __launch_bounds__(64) void search_kernel(const double* __restrict__ d
   if (dv.S) S = dv.S[0];
   if (dv.c_last) c_last = dv.c_last[0];
   if (dv.u) u = dv.u[0];
+  if (dv.c_in) c_in = dv.c_in[0];
   const int lane = threadIdx.x;
   // invariant: every block < lo misses, block hi hits (hi == nblocks: none)
   int64_t lo = 0, hi = nblocks;
@@ -1437,6 +1440,7 @@ __global__ __launch_bounds__(64) void seg_eval_kernel(const double* __restrict__
                                                       double* __restrict__ res,
     SeedDev dv) {
   if (dv.S) S = dv.S[0];
+  if (dv.c_in) c_in = dv.c_in[0];
   __shared__ SeedItem sit[kEvalWin];
   const int lane = threadIdx.x;
   double c = c_in;
@@ -1495,8 +1499,10 @@ __global__ __launch_bounds__(256) void seg_fill_kernel(const SegScan* __restrict
                                                        int64_t nb,
                                                        const double* __restrict__ markc,
                                                        const double* __restrict__ res,
-                                                       double c_in, double* __restrict__ cend) {
+                                                       double c_in, double* __restrict__ cend,
+                                                       const double* __restrict__ c_in_dev) {
   if (res[1] == 0.0) return;
+  if (c_in_dev) c_in = c_in_dev[0];
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nb) return;
   const SegScan s = scan[b];
@@ -1849,6 +1855,7 @@ static void seed_scan_program(Ctx& c, double total, double c_guess,
   c.seg_meta.ensure(sizeof(long long) * 8);
   SeedDev dvs;  // the program is always built (no gate)
   dvs.S = dv.S;
+  dvs.c_in = dv.c_in;
   hipLaunchKernelGGL(approx_prefix_kernel, dim3(1), dim3(1024), 0, c.stream,
                      c.blocksums.as<double>(), nb, total, c_guess, approx, dvs);
   HIP_CHECK(hipGetLastError());
@@ -1880,12 +1887,13 @@ static bool seed_scan_finish(Ctx& c, double c_in, double* c_out,
   double* res = seed_res(c);
   SeedDev dvs;
   dvs.S = dv.S;
+  dvs.c_in = dv.c_in;
   hipLaunchKernelGGL(seg_eval_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
                      c.seed_prog_total, c.seg_items.as<SeedItem>(), c.seg_meta.as<long long>(),
                      c_in, markc, res, dvs);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(seg_fill_kernel, dim3((int)ceil_div(nb, 256)), dim3(256), 0, c.stream,
-                     c.seg_scan.as<SegScan>(), nb, markc, res, c_in, c.cend.as<double>());
+                     c.seg_scan.as<SegScan>(), nb, markc, res, c_in, c.cend.as<double>(), dv.c_in);
   HIP_CHECK(hipGetLastError());
   if (!c_out) return true;
   double h[2];
@@ -2061,6 +2069,374 @@ void seed_run(Ctx& c, int64_t first, int k, const double* u, int64_t* picks) {
   if (bad[1] != 0.0) CDR_FAIL(CDR_ERR_STATE, "k-means++ sampler found no index");
 }
 
+// ---- device-resident seeding over sharded rows ------------------------------
+//
+// kmeans_plusplus_init (:3-22) with the rows sharded over nranks ranks (whole
+// 8192-row blocks each, so every shard block is a global block) and no host
+// round trip per step.  One step = three phases with a collective after each:
+//   phase 0: the previous pick's row (from the SUM all-reduce: its owner sent
+//            it, every other rank zeros) becomes the new centre; dmin update;
+//            this shard's block sums into its slot of [nranks][nbmax]
+//            -> all-gather
+//   phase 1: the total = every global block sum left to right (zero padding
+//            adds nothing), exactly the host's dist_sq.sum(); this shard's
+//            cumsum program from a guessed start (the earlier shards' sums /
+//            total), packed into its slot of [nranks][kShardProgCap] items
+//            -> all-gather
+//   phase 2: every rank composes the programs in rank order (its exact start
+//            c_mine and the global c_last), runs its own program from c_mine
+//            (checked against the composition), searches u c_last in its
+//            shard and sends {row, global index + 1, flags} if it holds the
+//            pick, zeros otherwise
+//            -> SUM all-reduce
+// The steps' picks stay on the device; one readback at the end.  A program
+// that cannot be composed (over capacity, opaque blocks, a wrong guess) or a
+// program / scan mismatch on any rank sets a flag that every rank sees in the
+// all-reduce; the host then runs the host protocol instead (cdr_dist.py).
+constexpr int kShardProgCap = 1024;  // program items per rank (item 0: the header)
+constexpr int kShardRed = 4;         // red buffer: row (d) | index + 1 | fail | nan | pad
+enum : int { kSsS = 0, kSsGuess, kSsMine, kSsAfter, kSsLast, kSsFail, kSsNan, kSsNoHit, kSsWords };
+
+// phase 0: the centre (and the previous pick) from the all-reduced buffer
+__global__ __launch_bounds__(64) void shard_center_kernel(const double* __restrict__ red, int d,
+                                                          double* __restrict__ centre,
+                                                          int64_t* __restrict__ pick,
+                                                          double* __restrict__ sc) {
+  for (int f = threadIdx.x; f < d; f += 64) centre[f] = red[f];
+  if (threadIdx.x == 0) {
+    const double g1 = red[d];  // global index + 1 (0: nobody held it)
+    pick[0] = g1 >= 1.0 ? (int64_t)g1 - 1 : 0;
+    if (!(g1 >= 1.0)) sc[kSsNoHit] = 1.0;
+    if (red[d + 1] != 0.0) sc[kSsFail] = 1.0;
+    if (red[d + 2] != 0.0) sc[kSsNan] = 1.0;
+  }
+}
+
+// this shard's block sums into its slot, zero padded to nbmax
+__global__ __launch_bounds__(256) void shard_bs_kernel(const double* __restrict__ bs, int64_t nb,
+                                                       int64_t nbmax, double* __restrict__ out) {
+  for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < nbmax; b += (int64_t)gridDim.x * 256)
+    out[b] = b < nb ? bs[b] : 0.0;
+}
+
+// phase 1: the guessed start of this shard (earlier shards' sums / total;
+// any order: only a guess) — exactly 0 on rank 0
+__global__ __launch_bounds__(256) void shard_guess_kernel(const double* __restrict__ gbs,
+                                                          int64_t before,
+                                                          double* __restrict__ sc) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < before; i += 256) s += gbs[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sc[kSsGuess] = before ? red[0] / sc[kSsS] : 0.0;
+}
+
+// this shard's program into its slot: item 0 = {count, 0, 0, 0, 0} (count -1
+// when it cannot be composed elsewhere: over capacity or opaque blocks)
+__global__ __launch_bounds__(256) void shard_pack_kernel(const SeedItem* __restrict__ items,
+                                                         const long long* __restrict__ meta,
+                                                         SeedItem* __restrict__ out) {
+  const long long cnt = meta[0];
+  const bool ok = meta[2] == 0 && meta[1] == 0 && cnt <= kShardProgCap - 1;
+  if (threadIdx.x == 0) out[0] = SeedItem{ok ? cnt : -1, 0, 0.0, 0, kItSkip};
+  if (!ok) return;
+  for (long long i = threadIdx.x; i < cnt; i += 256) out[1 + i] = items[i];
+}
+
+// phase 2: compose every rank's program in rank order from 0 (one wave; a
+// rank's items staged in LDS, then walked in scalar registers)
+__global__ __launch_bounds__(64) void shard_compose_kernel(const SeedItem* __restrict__ progs,
+                                                           int nranks, int rank,
+                                                           double* __restrict__ sc) {
+  __shared__ SeedItem sit[kShardProgCap];
+  const int lane = threadIdx.x;
+  double c = 0.0, mine = 0.0, after = 0.0;
+  bool ok = sc[kSsFail] == 0.0;
+  for (int r = 0; r < nranks && ok; ++r) {
+    const SeedItem* P = progs + (size_t)r * kShardProgCap;
+    const long long cnt = sgpr64(P[0].d0);
+    if (cnt < 0) {
+      ok = false;
+      break;
+    }
+    __syncthreads();
+    for (long long i = lane; i < cnt; i += 64) sit[i] = P[1 + i];
+    __syncthreads();
+    if (r == rank) mine = c;
+    for (long long i = 0; i < cnt; ++i) {
+      SeedItem it;
+      it.kind = __builtin_amdgcn_readfirstlane(sit[i].kind);
+      if (it.kind == kItEnd) break;
+      it.e = __builtin_amdgcn_readfirstlane(sit[i].e);
+      it.d0 = sgpr64(sit[i].d0);
+      it.d1 = sgpr64(sit[i].d1);
+      it.p = __builtin_bit_cast(double, sgpr64(__builtin_bit_cast(long long, sit[i].p)));
+      if (!item_apply(it, c)) {
+        ok = false;
+        break;
+      }
+    }
+    if (r == rank) after = c;
+  }
+  if (lane == 0) {
+    sc[kSsMine] = mine;
+    sc[kSsAfter] = after;
+    sc[kSsLast] = c;
+    if (!ok) sc[kSsFail] = 1.0;
+  }
+}
+
+// phase 2 end: this rank's part of the SUM all-reduce — the picked row, its
+// global index + 1 and the flags (own program vs the composition, a failed
+// composition, a bad total) when it holds the pick or sees a problem
+__global__ __launch_bounds__(64) void shard_red_kernel(const float* __restrict__ x32,
+                                                       const double* __restrict__ x64,
+                                                       const int64_t* __restrict__ hit, int d,
+                                                       int64_t n_pad, int64_t row_begin,
+                                                       const double* __restrict__ res,
+                                                       const double* __restrict__ bad,
+                                                       const double* __restrict__ sc, int rank,
+                                                       const double* __restrict__ u,
+                                                       double* __restrict__ red) {
+  // the shard's search gives its first element whose running value exceeds
+  // u c_last; when that is its first element, the pick belongs to this shard
+  // only if the running value before it (the shard start) does not already
+  // exceed it — else an earlier shard holds the pick (searchsorted 'right')
+  int64_t i = hit[0];
+  if (i == 0 && u && sc[kSsMine] / sc[kSsLast] > u[0]) i = -1;
+  for (int f = threadIdx.x; f < d; f += 64)
+    red[f] = i < 0 ? 0.0 : x32 ? (double)x32[xidx(f, i, n_pad)] : x64[xidx(f, i, n_pad)];
+  if (threadIdx.x == 0) {
+    red[d] = i < 0 ? 0.0 : (double)(row_begin + i + 1);
+    // own program run from the composed start must end where the composition did
+    const bool mism = res[1] == 0.0 || res[0] != sc[kSsAfter];
+    red[d + 1] = (sc[kSsFail] != 0.0 || mism) ? 1.0 : 0.0;
+    red[d + 2] = (rank == 0 && bad[0] != 0.0) ? 1.0 : 0.0;
+    red[d + 3] = 0.0;
+  }
+}
+
+static void ss_require(const Ctx& c) {
+  if (!c.ss_on) CDR_FAIL(CDR_ERR_STATE, "cdr_seed_shard_begin first");
+}
+static double* ss_sc(Ctx& c) {
+  return c.ss_buf.as<double>() + (c.ss_k - 1) + c.ss_k;
+}
+
+// Sizes of the exchanged buffers (in bytes per rank): block sums, programs,
+// the all-reduced record.
+static void ss_sizes(const Ctx& c, int64_t* sizes) {
+  sizes[0] = (int64_t)sizeof(double) * c.ss_nbmax;
+  sizes[1] = (int64_t)sizeof(SeedItem) * kShardProgCap;
+  sizes[2] = (int64_t)sizeof(double) * (c.d + kShardRed);
+}
+
+void seed_shard_begin(Ctx& c, int64_t row_begin, int64_t n_total, int nranks, int rank,
+                      int64_t first, int k, const double* u, double* red_out, int64_t* sizes) {
+  check_points(c);
+  if (k < 1 || nranks < 1 || rank < 0 || rank >= nranks) CDR_FAIL(CDR_ERR_ARG, "bad k / ranks");
+  if (first < 0 || first >= n_total) CDR_FAIL(CDR_ERR_ARG, "first row out of range");
+  if (row_begin % kSeedBlock != 0 && c.n > 0)
+    CDR_FAIL(CDR_ERR_ARG, "shards must start on an 8192-row block");
+  c.ss_row_begin = row_begin;
+  c.ss_n_total = n_total;
+  c.ss_nranks = nranks;
+  c.ss_rank = rank;
+  c.ss_k = k;
+  c.ss_step = 1;
+  // every shard but the last holds whole blocks: nbmax = the first shard's
+  c.ss_nbmax = ceil_div(ceil_div(n_total, kSeedBlock), nranks);
+  if (c.nblocks() > c.ss_nbmax) CDR_FAIL(CDR_ERR_ARG, "shard larger than n_total / nranks blocks");
+  const size_t words = (size_t)(k - 1) + (size_t)k + kSsWords + 8;
+  c.ss_buf.ensure(sizeof(double) * words);
+  double* du = c.ss_buf.as<double>();
+  if (k > 1)
+    HIP_CHECK(hipMemcpyAsync(du, u, sizeof(double) * (k - 1), hipMemcpyHostToDevice, c.stream));
+  double* sc = du + (k - 1) + k;
+  HIP_CHECK(hipMemsetAsync(sc, 0, sizeof(double) * (kSsWords + 8), c.stream));
+  seed_reset(c);
+  c.seed_scalar.ensure(sizeof(double) * (2 * c.d + 8));
+  c.cend.ensure(sizeof(double) * (c.nblocks() > 0 ? c.nblocks() : 1) * 2);
+  c.seg_meta.ensure(sizeof(long long) * 8);
+  c.ss_on = true;
+  ss_sizes(c, sizes);
+  // the first centre: its owner sends the row (the red buffer after the SUM)
+  int64_t hit = first - row_begin;
+  if (hit < 0 || hit >= c.n) hit = -1;
+  c.seed_run_buf.ensure(sizeof(double) * 8);
+  int64_t* dhit = reinterpret_cast<int64_t*>(c.seed_run_buf.as<double>());
+  double* zres = c.seed_run_buf.as<double>() + 2;  // {c_after, ok}: no mismatch
+  HIP_CHECK(hipMemcpyAsync(dhit, &hit, sizeof(hit), hipMemcpyHostToDevice, c.stream));
+  const double zr[4] = {0.0, 1.0, 0.0, 0.0};
+  HIP_CHECK(hipMemcpyAsync(zres, zr, sizeof(zr), hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(shard_red_kernel, dim3(1), dim3(64), 0, c.stream,
+                     c.mode == CDR_MODE_F32X ? c.x32.as<float>() : nullptr,
+                     c.mode == CDR_MODE_F64 ? c.x64.as<double>() : nullptr, dhit, c.d, c.n_pad,
+                     row_begin, zres, zres + 2, sc, rank, nullptr, red_out);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipStreamSynchronize(c.stream));  // hit and zr live on this stack
+}
+
+// phase p of the current step (see above); in / out: device buffers
+void seed_shard_phase(Ctx& c, int phase, const void* in, void* out) {
+  ss_require(c);
+  if (c.ss_step >= c.ss_k) CDR_FAIL(CDR_ERR_STATE, "seeding: every step done");
+  const int d = c.d, rank = c.ss_rank;
+  const int64_t nb = c.nblocks();
+  double* du = c.ss_buf.as<double>();
+  int64_t* dpick = reinterpret_cast<int64_t*>(du + (c.ss_k - 1));
+  double* sc = ss_sc(c);
+  if (phase == 0) {
+    hipLaunchKernelGGL(shard_center_kernel, dim3(1), dim3(64), 0, c.stream,
+                       static_cast<const double*>(in), d, c.seed_scalar.as<double>(),
+                       dpick + (c.ss_step - 1), sc);
+    HIP_CHECK(hipGetLastError());
+    seed_update(c, nullptr);
+    double* slot = static_cast<double*>(out) + (size_t)rank * c.ss_nbmax;
+    if (nb > 0)
+      hipLaunchKernelGGL(shard_bs_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(c.ss_nbmax, 256), 1024)),
+                         dim3(256), 0, c.stream, c.blocksums.as<double>(), nb, c.ss_nbmax, slot);
+    else
+      HIP_CHECK(hipMemsetAsync(slot, 0, sizeof(double) * c.ss_nbmax, c.stream));
+    HIP_CHECK(hipGetLastError());
+  } else if (phase == 1) {
+    const double* gbs = static_cast<const double*>(in);
+    double* bad = sc + kSsWords;  // {bad total, no index}
+    hipLaunchKernelGGL(seed_total_kernel, dim3(1), dim3(64), 0, c.stream, gbs,
+                       (int64_t)c.ss_nranks * c.ss_nbmax, sc + kSsS, bad);
+    hipLaunchKernelGGL(shard_guess_kernel, dim3(1), dim3(256), 0, c.stream, gbs,
+                       (int64_t)rank * c.ss_nbmax, sc);
+    HIP_CHECK(hipGetLastError());
+    SeedItem* slot = static_cast<SeedItem*>(out) + (size_t)rank * kShardProgCap;
+    if (nb > 0) {
+      SeedDev dv;
+      dv.S = sc + kSsS;
+      dv.c_in = sc + kSsGuess;
+      seed_scan_program(c, 1.0, 0.0, dv);
+      hipLaunchKernelGGL(shard_pack_kernel, dim3(1), dim3(256), 0, c.stream,
+                         c.seg_items.as<SeedItem>(), c.seg_meta.as<long long>(), slot);
+    } else {  // an empty shard: the identity program
+      const SeedItem hdr[2] = {SeedItem{1, 0, 0.0, 0, kItSkip}, SeedItem{0, 0, 0.0, 0, kItEnd}};
+      HIP_CHECK(hipMemcpyAsync(slot, hdr, sizeof(hdr), hipMemcpyHostToDevice, c.stream));
+      HIP_CHECK(hipStreamSynchronize(c.stream));
+    }
+    HIP_CHECK(hipGetLastError());
+  } else if (phase == 2) {
+    hipLaunchKernelGGL(shard_compose_kernel, dim3(1), dim3(64), 0, c.stream,
+                       static_cast<const SeedItem*>(in), c.ss_nranks, rank, sc);
+    HIP_CHECK(hipGetLastError());
+    double* res = seed_res(c);
+    c.seed_run_buf.ensure(sizeof(double) * 8);
+    int64_t* dhit = reinterpret_cast<int64_t*>(c.seed_run_buf.as<double>());
+    if (nb > 0) {
+      SeedDev dv;
+      dv.S = sc + kSsS;
+      dv.c_in = sc + kSsMine;
+      seed_scan_finish(c, 0.0, nullptr, dv);
+      SeedDev ds;
+      ds.S = sc + kSsS;
+      ds.c_last = sc + kSsLast;
+      ds.u = du + (c.ss_step - 1);
+      ds.c_in = sc + kSsMine;
+      hipLaunchKernelGGL(search_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
+                         1.0, c.cend.as<double>(), nb, 0.0, 1.0, 0.5, dhit, ds);
+    } else {
+      const int64_t none = -1;
+      HIP_CHECK(hipMemcpyAsync(dhit, &none, sizeof(none), hipMemcpyHostToDevice, c.stream));
+      // (no own program: the composition's "after" is the start itself)
+      HIP_CHECK(hipMemcpyAsync(res, sc + kSsAfter, sizeof(double), hipMemcpyDeviceToDevice,
+                               c.stream));
+      const double one = 1.0;
+      HIP_CHECK(hipMemcpyAsync(res + 1, &one, sizeof(one), hipMemcpyHostToDevice, c.stream));
+      HIP_CHECK(hipStreamSynchronize(c.stream));
+    }
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(shard_red_kernel, dim3(1), dim3(64), 0, c.stream,
+                       c.mode == CDR_MODE_F32X ? c.x32.as<float>() : nullptr,
+                       c.mode == CDR_MODE_F64 ? c.x64.as<double>() : nullptr, dhit, d, c.n_pad,
+                       c.ss_row_begin, res, sc + kSsWords, sc, rank, du + (c.ss_step - 1),
+                       static_cast<double*>(out));
+    HIP_CHECK(hipGetLastError());
+    c.ss_step += 1;
+  } else {
+    CDR_FAIL(CDR_ERR_ARG, "phase 0, 1 or 2");
+  }
+}
+
+// The last step's pick from the final all-reduced buffer; picks (k global row
+// indices) and the status: 0 ok, 1 the host protocol must redo the seeding
+// (a program could not be composed or disagreed with its scan), 2 a total
+// was not finite and positive (Probabilities contain NaN).
+void seed_shard_end(Ctx& c, const double* red, int64_t* picks, double* cents, int32_t* status) {
+  ss_require(c);
+  if (c.ss_step != c.ss_k) CDR_FAIL(CDR_ERR_STATE, "seeding: steps left");
+  double* du = c.ss_buf.as<double>();
+  int64_t* dpick = reinterpret_cast<int64_t*>(du + (c.ss_k - 1));
+  double* sc = ss_sc(c);
+  hipLaunchKernelGGL(shard_center_kernel, dim3(1), dim3(64), 0, c.stream, red, c.d,
+                     c.seed_scalar.as<double>(), dpick + (c.ss_k - 1), sc);
+  HIP_CHECK(hipGetLastError());
+  double flags[kSsWords];
+  HIP_CHECK(hipMemcpyAsync(picks, dpick, sizeof(int64_t) * c.ss_k, hipMemcpyDeviceToHost, c.stream));
+  // the centres: the k - 1 the updates used (seed_track's list, in order) and
+  // the last pick's row (just written to seed_scalar)
+  const size_t d = (size_t)c.d;
+  if (c.ss_k > 1)
+    HIP_CHECK(hipMemcpyAsync(cents, c.seed_cents.p, sizeof(double) * d * (c.ss_k - 1),
+                             hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(cents + d * (c.ss_k - 1), c.seed_scalar.p, sizeof(double) * d,
+                           hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(flags, sc, sizeof(flags), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.ss_on = false;
+  c.seed_scanned = false;
+  c.seed_prog_ready = false;
+  *status = flags[kSsFail] != 0.0 ? 1 : flags[kSsNan] != 0.0 ? 2 : flags[kSsNoHit] != 0.0 ? 1 : 0;
+}
+
+// Every step with the context's communicator (csrc/comm.hip): the same phases,
+// the collectives enqueued from C between them.
+void seed_run_sharded(Ctx& c, int64_t row_begin, int64_t n_total, int64_t first, int k,
+                      const double* u, int64_t* picks, double* cents, int32_t* status) {
+  if (!c.comm) CDR_FAIL(CDR_ERR_STATE, "no communicator (cdr_comm_init)");
+  int64_t sizes[3];
+  DevBuf bufs;
+  // (sizes depend on the shard layout: computed by begin, buffers after it)
+  c.ss_nbmax = ceil_div(ceil_div(n_total, kSeedBlock), c.comm_ranks);
+  const size_t bs_b = sizeof(double) * c.ss_nbmax, pg_b = sizeof(SeedItem) * kShardProgCap,
+               rd_b = sizeof(double) * (c.d + kShardRed);
+  const size_t R = (size_t)c.comm_ranks;
+  bufs.ensure(R * bs_b + R * pg_b + rd_b);
+  unsigned char* base = static_cast<unsigned char*>(bufs.p);
+  double* gbs = reinterpret_cast<double*>(base);
+  SeedItem* progs = reinterpret_cast<SeedItem*>(base + R * bs_b);
+  double* red = reinterpret_cast<double*>(base + R * bs_b + R * pg_b);
+  try {
+    seed_shard_begin(c, row_begin, n_total, c.comm_ranks, c.comm_rank, first, k, u, red, sizes);
+    comm_allreduce_f64(c, red, c.d + kShardRed);
+    for (int i = 1; i < k; ++i) {
+      seed_shard_phase(c, 0, red, gbs);
+      comm_allgather(c, gbs, bs_b);
+      seed_shard_phase(c, 1, gbs, progs);
+      comm_allgather(c, progs, pg_b);
+      seed_shard_phase(c, 2, progs, red);
+      comm_allreduce_f64(c, red, c.d + kShardRed);
+    }
+    seed_shard_end(c, red, picks, cents, status);
+  } catch (...) {
+    (void)hipStreamSynchronize(c.stream);
+    bufs.release();
+    c.ss_on = false;
+    throw;
+  }
+  bufs.release();
+}
+
 }  // namespace cdr
 
 using namespace cdr;
@@ -2144,6 +2520,42 @@ int cdr_seed_run(cdr_ctx* h, int64_t first, int32_t k, const double* u, int64_t*
   if (!h || !picks || (k > 1 && !u)) CDR_FAIL(CDR_ERR_ARG, "null argument");
   HIP_CHECK(hipSetDevice(h->c.device));
   seed_run(h->c, first, (int)k, u, picks);
+  CDR_CATCH
+}
+
+int cdr_seed_shard_begin(cdr_ctx* h, int64_t row_begin, int64_t n_total, int32_t nranks,
+                         int32_t rank, int64_t first, int32_t k, const double* u, double* red,
+                         int64_t* sizes) {
+  CDR_TRY
+  if (!h || !red || !sizes || (k > 1 && !u)) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  seed_shard_begin(h->c, row_begin, n_total, nranks, rank, first, (int)k, u, red, sizes);
+  CDR_CATCH
+}
+
+int cdr_seed_shard_phase(cdr_ctx* h, int32_t phase, const void* in, void* out) {
+  CDR_TRY
+  if (!h || !in || !out) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  seed_shard_phase(h->c, phase, in, out);
+  CDR_CATCH
+}
+
+int cdr_seed_shard_end(cdr_ctx* h, const double* red, int64_t* picks, double* cents,
+                       int32_t* status) {
+  CDR_TRY
+  if (!h || !red || !picks || !cents || !status) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  seed_shard_end(h->c, red, picks, cents, status);
+  CDR_CATCH
+}
+
+int cdr_seed_run_sharded(cdr_ctx* h, int64_t row_begin, int64_t n_total, int64_t first, int32_t k,
+                         const double* u, int64_t* picks, double* cents, int32_t* status) {
+  CDR_TRY
+  if (!h || !picks || !cents || !status || (k > 1 && !u)) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  seed_run_sharded(h->c, row_begin, n_total, first, (int)k, u, picks, cents, status);
   CDR_CATCH
 }
 

