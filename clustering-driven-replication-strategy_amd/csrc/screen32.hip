@@ -2069,12 +2069,19 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
     const int nb = last ? (cnt + 63) >> 6 : cnt >> 6;
     if (nb == 0) return;
     ttot += last ? cnt : nb * 64;
-    GB g;
-    gload(g, 0, cnt);
-    for (int b = 0; b < nb; ++b) {
-      const GB cur = g;
-      if (b + 1 < nb) gload(g, b + 1, cnt);
-      process(cur.r, cur.valid, cur.pt, cur.ao);
+    // three batches in flight: every slot is reloaded unconditionally (past
+    // the end: the last batch again, not processed), so the compiler's
+    // counts let the two later batches stay in flight while one is decided
+    GB g[3];
+    gload(g[0], 0, cnt);
+    gload(g[1], nb > 1 ? 1 : 0, cnt);
+    for (int b = 0; b < nb; b += 3) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int nx = b + i + 2;
+        gload(g[(i + 2) % 3], nx < nb ? nx : nb - 1, cnt);
+        if (b + i < nb) process(g[i].r, g[i].valid, g[i].pt, g[i].ao);
+      }
     }
     const int done = nb * 64;
     const int rem = last ? 0 : cnt - done;
@@ -2483,7 +2490,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       !std::getenv("CDR_PRUNE_FUSE") || std::atoi(std::getenv("CDR_PRUNE_FUSE"));
   // bounded screen (screen32b) in the device loop, where ll_finalize32 keeps
   // the drift bounds of every centroid move (CDR_BOUNDS=0 turns it off)
-  const bool bnd_env = std::getenv("CDR_BOUNDS") && std::atoi(std::getenv("CDR_BOUNDS"));
+  const bool bnd_env = !std::getenv("CDR_BOUNDS") || std::atoi(std::getenv("CDR_BOUNDS"));
   const bool BND = PR && bnd_env && gate && dthr && c.ll_on && c.bnd_ok &&
                    c.n_pad < (int64_t(1) << 31);
   if (!BND) c.zb_valid = false;  // another path decides this step's labels

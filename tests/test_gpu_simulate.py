@@ -85,3 +85,44 @@ def test_groupby_of_simulated_log_matches_oracle(ctx):
     np.testing.assert_array_equal(got, exp)
     assert mx == emx
     assert got[:, 5].max() >= 3  # hot files have seconds with several events
+
+
+def test_config4_full_size_groupby(ctx):
+    """the bench's exact config-4 workload (744K files x
+    600 s x 3 datanodes, ~125M events from the device simulator, seed 0x5EED,
+    the two-pass partition + gb_bucket_wave4 path: L = 2, 4-byte payload)
+    against independent bincount / sort counters at full size
+    (src/compute_features.py:31-46)."""
+    nf, dur, ncl = 744_000, 600.0, 3  # bench.py FEATURES_CFG
+    ne = ctx.features_simulate(nf, dur, ncl, seed=0x5EED)
+    got, mx = ctx.features_aggregate_resident()
+    info = ctx.features_groupby_info()
+    assert info["hand"] == 1 and info["L"] == 2 and info["passes"] == 2 and info["dense"] == 1
+    assert info["payload_bytes"] == 4 and info["big_buckets"] == 0
+    f, op, cl, ts, pr = ctx.features_events_read()
+    assert ne == f.size and ne > 100_000_000
+    f64 = f.astype(np.int64)
+    cnt = np.bincount(f64, minlength=nf)
+    np.testing.assert_array_equal(got[:, 0], cnt)
+    np.testing.assert_array_equal(got[:, 4], cnt)
+    np.testing.assert_array_equal(got[:, 1], np.bincount(f64[op == 1], minlength=nf))
+    np.testing.assert_array_equal(got[:, 2], np.bincount(f64[op == 2], minlength=nf))
+    np.testing.assert_array_equal(got[:, 3], np.bincount(f64[cl == pr[f]], minlength=nf))
+    del cl, op
+    # max over seconds of the (file, second) count: sort (file, second) keys,
+    # run lengths, then the largest run of each file
+    sec = ts // 1_000_000  # floor(ts_us / 1e6) for ts >= 0 (Spark's second)
+    s0 = int(sec.min())
+    span = int(sec.max()) - s0 + 1
+    key = f64 * span + (sec - s0)
+    del sec, f64
+    key.sort()
+    starts = np.flatnonzero(np.concatenate([[True], key[1:] != key[:-1]]))
+    runs = np.diff(np.append(starts, key.size))
+    files = key[starts] // span
+    del key
+    fst = np.flatnonzero(np.concatenate([[True], files[1:] != files[:-1]]))
+    conc = np.zeros(nf, dtype=np.int64)
+    conc[files[fst]] = np.maximum.reduceat(runs, fst)
+    np.testing.assert_array_equal(got[:, 5], conc)
+    assert mx == int(ts.max())

@@ -86,6 +86,7 @@ if json_cfg is not None:
         rec = json.load(open(path)) if os.path.exists(path) else {}
         rec[json_cfg] = {"n_local": json_n, "hbm_bytes_per_launch": rb + wb, "read_bytes": rb,
                          "write_bytes": wb, "source": root,
+                         "kernel": names[max(f, key=lambda k: k[1])],
                          "note": "FETCH_SIZE KiB x2 (gfx950 half-count) + WRITE_SIZE KiB"}
         json.dump(rec, open(path, "w"), indent=1)
         print("wrote", path, rec[json_cfg])
