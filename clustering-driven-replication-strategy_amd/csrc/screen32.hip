@@ -2009,7 +2009,11 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
     const float l0 = fmaf(hc[ao], 1.0f - 0x1p-22f, -uba);
     const bool keep = l0 > uba * (1.0f + 0x1p-20f);
     if (valid && keep) B.zb[pt] = zb_pack(l0, uba, __shfl(wdn_l, ao), (unsigned)ao);
+#ifdef CDR_EXPERIMENTS
+    const bool q = valid && !keep && !(B.dbg & 8);  // (timing: no k-way screen)
+#else
     const bool q = valid && !keep;
+#endif
     const unsigned long long m = __ballot(q);
     if (m) {
       if (q) {
@@ -2069,6 +2073,12 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
     const int nb = last ? (cnt + 63) >> 6 : cnt >> 6;
     if (nb == 0) return;
     ttot += last ? cnt : nb * 64;
+#ifdef CDR_EXPERIMENTS
+    if (B.dbg & 4) {  // timing experiments only: the listed points are not decided
+      cnt = 0;
+      return;
+    }
+#endif
     // three batches in flight: every slot is reloaded unconditionally (past
     // the end: the last batch again, not processed), so the compiler's
     // counts let the two later batches stay in flight while one is decided
@@ -2107,7 +2117,12 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
       for (int u = 0; u < 4; ++u) {
         const unsigned w = z[u];
         const unsigned lab = w & 63u;
+#ifdef CDR_EXPERIMENTS
+        const bool fail = (!(__uint_as_float(w & ~63u) > __shfl(wup_l, (int)lab)) || (B.dbg & 1)) &&
+                          !(B.dbg & 16);  // (timing: the stream alone)
+#else
         const bool fail = !(__uint_as_float(w & ~63u) > __shfl(wup_l, (int)lab)) || (B.dbg & 1);
+#endif
         const unsigned long long m = __ballot(fail);
         if (m) {
           if (fail) {
@@ -2129,6 +2144,9 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
     if (a.q_acc) a.q_acc[wave] += qtot;
     if (B.t_acc) B.t_acc[wave] += ttot;
   }
+#ifdef CDR_EXPERIMENTS
+  if (B.dbg & 2) return;  // (timing: no fused fixup)
+#endif
   if (!a.fuse) return;
   __syncthreads();  // every queue drained (its LDS becomes the table); lists written
   const FixLds L(qlds);
@@ -2675,6 +2693,9 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       b.nchunks = c.n_pad / kBChunk;
       b.t_acc = c.prof_on ? c.t_acc.as<long long>() : nullptr;
       b.dbg = std::getenv("CDR_BOUNDS_DBG") ? std::atoi(std::getenv("CDR_BOUNDS_DBG")) : 0;
+#ifndef CDR_EXPERIMENTS
+      b.dbg &= 1;  // (the other bits are timing experiments: experiments build only)
+#endif
       c.zb_valid = true;
       snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32b<%d,%d>%s", PQ, MT,
                fused ? "+fixup" : "");

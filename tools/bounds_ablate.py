@@ -1,0 +1,38 @@
+"""In-process timing of the bounded screen (screen32b) with parts switched off
+(CDR_BOUNDS_DBG bits, experiments build only: 2 no fused fixup, 4 listed
+points not decided, 8 no k-way screen, 16 stream only).  Results are garbage
+while a bit is set; diagnostic tool, not a test.
+    CDR_LIB=.../libcdr_exp.so python tools/bounds_ablate.py [n] [d] [k] [masks]"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "clustering-driven-replication-strategy_amd"), REPO]
+import _cdr  # noqa: E402
+from cdr_dist import Comm, DeviceLloyd, seed_sharded  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
+d = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+k = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+masks = [int(m) for m in (sys.argv[4].split(",") if len(sys.argv) > 4 else "0,2,4,8,16,6".split(","))]
+ctx = _cdr.Context(0)
+ctx.generate_points(n, 0, n, d, k, 0x5EED)
+C = seed_sharded(ctx, Comm(), 0, n, k, random_state=42)
+np.random.seed(0)
+run = DeviceLloyd(ctx, C, -1.0, lambda g: ctx.get_rows([g])[0], n)
+run.advance(6)
+res = {m: [] for m in masks}
+for rnd in range(3):
+    for m in masks:
+        os.environ["CDR_BOUNDS_DBG"] = str(m)
+        ctx.profile_reset(True)
+        run.advance(4, chunk=4, chunk_max=4)
+        p = ctx.profile_read()
+        res[m].append(p["screen_ms"] / max(p["steps"], 1))
+        ctx.profile_reset(False)
+os.environ["CDR_BOUNDS_DBG"] = "0"
+for m in masks:
+    print(f"mask {m:3d}: screen32b {np.median(res[m]) * 1e3:8.1f} us  (rounds {[round(x * 1e3, 1) for x in res[m]]})")
+run.finish()
