@@ -35,6 +35,8 @@
 #include <cstdio>
 #include <cmath>
 #include <cstring>
+#include <algorithm>
+#include <vector>
 
 #include "cdr_internal.h"
 #include "exact_math.h"
@@ -1780,6 +1782,7 @@ struct S32BArgs {
   int64_t nchunks;           // n_pad / kBChunk
   long long* t_acc;          // profiling: points whose bound failed, per wave (null: off)
   int dbg;                   // tests only (CDR_BOUNDS_DBG): 1 = every bound fails
+  unsigned long long* tprof; // experiments build only: per-wave timestamps (null: off)
 };
 
 // The stored word of bounds (l0, u0) and W_a rounded down (see above):
@@ -2157,6 +2160,568 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
   fixup_regions<Q, MT>(a.fx, blockIdx.x * 4, 4, blockIdx.x % kRunSlices, L, FixPlan{sA, sC});
 }
 
+// ---------------------------------------------------------------------------
+// screen32bs: the bounded screen deciding in registers (device loop; d <= 16,
+// k <= 64).  Phase 1 is screen32b's.  Phase 2 gathers the listed points' fp32
+// rows (XA: one 64-byte line per point at d = 16, the same memory
+// transactions as screen32b's 32-byte hi row) and decides each batch of 64
+// without a queue, a list or a fixup pass:
+//   * xhat32 = fma(x, 2^sigma, -mu 2^sigma) (split_copy_kernel's values) and
+//     the triangle test against c32_a with q = ||xhat32 - c32_a||^2 (the same
+//     rounding count as screen32p's; E_a >= dn + ec covers ||xhat32 - xhat||
+//     + ||c32_a - chat_a||, as it covers the fp16 row);
+//   * when any lane of the batch fails it, the SPLIT screen of the whole batch
+//     (screen32d's 2-3 MFMA per centroid tile on the hi / lo halves of
+//     xhat32, formed in registers: one permlane32 swap per operand dword turns
+//     the lanes' own rows into both 32-point B operands) and screen32d's
+//     certificate vs > vb thr_rel + thr0, the K-case bounds from (vb, vs)
+//     relative to xhat32 (|S_j - (D + ||chat_j||^2 - 2 chat_j . xhat32)| <= E
+//     <= thr0 / 2), then the rounding of xhat32 (dn32 <= 2^-24 ||xhat32||);
+//   * when any lane is not certified (near ties), fixup_regions' candidate set
+//     (every key within the threshold of the best) evaluated in exact fp64
+//     NumPy order: np.argmin of the reference's norms
+//     (src/kmeans_plusplus.py:33-34); such a point keeps "no bound".
+// Moves go into a per-workgroup int64 table in LDS ([k][d + 1], run_sums'
+// layout) flushed into one run_sums slice at the end when the workgroup moved
+// anything.  The split screen is ~2^8 tighter than the hi-only one, so almost
+// no point needs the exact fp64 pass.
+// ---------------------------------------------------------------------------
+template <int Q, int MT>
+__global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
+  const S32PArgs& a = B.p;
+  const FixArgs& F = a.fx;
+#ifdef CDR_EXPERIMENTS
+  unsigned long long tp[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
+#define CDR_TP(i) tp[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define CDR_TP(i)
+#endif
+  constexpr int QH = FixDims<Q>::QH;
+  constexpr int DM = FixDims<Q>::DM;
+  if (a.gate && a.gate[0] == 0) return;
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) float c32s[64 * kPrStr + 128];
+  float* const eb = c32s + 64 * kPrStr;  // E_j
+  float* const hc = eb + 64;             // h_j
+  // per wave: points whose bound failed (screen32b's entries); room for the
+  // kBPD chunks streamed between two phase-2 passes, so phase 2 has one call
+  // site (code size: the decision is inlined once)
+  constexpr int kSList = kBPD * kBChunk + 256;
+  __shared__ unsigned flist[4][kSList];
+  __shared__ unsigned long long mtab[64 * 17];  // this workgroup's moves, [k][d + 1]
+  __shared__ float msl[16];                     // -mu_f 2^sigma
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = t >> 6;
+  const int h = lane >> 5, p = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
+  const int nwaves = gridDim.x * 4;
+  const int64_t nchunks = B.nchunks;
+  const int k = a.k, d = a.d, d1 = d + 1;
+
+  // ---- phase 1 loads (screen32b's) ----
+  auto zload = [&](u4v& z, int64_t ci) __attribute__((always_inline)) {
+    const int64_t cc = ci < nchunks ? ci : nchunks - 1;
+    z = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(B.zb + cc * kBChunk) + lane);
+  };
+  u4v zc[kBPD];
+#pragma unroll
+  for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], wave + (int64_t)i * nwaves);
+
+  // ---- the plan ----
+  __shared__ h8 sA[MT * 2 * 64];
+  __shared__ __attribute__((aligned(16))) float sC[MT * 4 * 2 * 4];
+  constexpr int kPr4 = (64 * kPrStr + 128) / 4;
+  static_assert(kPr4 <= 512 && MT * 2 * 64 <= 256, "prologue: two float4 per thread");
+  const f4* prune4 = reinterpret_cast<const f4*>(a.prune);
+  const f4 pv0 = prune4[t];
+  const f4 pv1 = t + 256 < kPr4 ? prune4[t + 256] : f4{0.f, 0.f, 0.f, 0.f};
+  h8 av = {};
+  if (t < MT * 2 * 64) av = a.frag[t];
+  float cv = 0.0f;
+  const int cm = t >> 5, ci4 = (t >> 3) & 3, chh = (t >> 2) & 1, cc = t & 3;
+  if (t < MT * 32) cv = a.cinit[(cm * 16 + ci4 * 4 + cc) * 64 + chh * 32];
+  const float wup_l = B.wup[lane], wdn_l = B.wdn[lane];  // lane j: W_j (k <= 64)
+  const float msv = lane < d ? F.ms[lane] : 0.0f;        // lane f: -mu_f 2^sigma
+  const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
+  const float Dv = a.thr_dev ? a.thr_dev[1] : a.Dv;
+  const float Dlo = Dv * (1.0f - 0x1p-19f), Dhi = Dv * (1.0f + 0x1p-19f);
+  const float sig = F.sig;
+  reinterpret_cast<f4*>(c32s)[t] = pv0;
+  if (t + 256 < kPr4) reinterpret_cast<f4*>(c32s)[t + 256] = pv1;
+  if (t < MT * 2 * 64) sA[t] = av;
+  if (t < MT * 32) sC[t] = cv;
+  for (int e = t; e < 64 * 17; e += 256) mtab[e] = 0ull;
+  if (t < 16) msl[t] = msv;
+  __syncthreads();
+  CDR_TP(1);
+
+  int fb_used = 0, mv_used = 0, qtot = 0, ttot = 0;
+  const f4* XA4 = reinterpret_cast<const f4*>(F.XA);  // point i: XA4[i * Q + q]
+
+  // (best, runner-up) keys of one 32-point tile of the split screen
+  auto screen_m = [&](int m, const u4v (&v)[QH]) __attribute__((always_inline)) -> f16v {
+    asm volatile("" ::: "memory");  // the plan is read here, not held in registers
+    const h8 A0 = sA[(m * 2 + 0) * 64 + lane];
+    const h8 A1 = sA[(m * 2 + 1) * 64 + lane];
+    f16v acc;
+#pragma unroll
+    for (int i4 = 0; i4 < 4; ++i4) {
+      const f4 c4v = *reinterpret_cast<const f4*>(sC + ((m * 4 + i4) * 2 + h) * 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[4 * i4 + i] = c4v[i];
+    }
+    const h8 BH = __builtin_bit_cast(h8, v[0]);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, BH, acc, 0, 0, 0);
+    if constexpr (QH == 2) {
+      const h8 BL = __builtin_bit_cast(h8, v[QH - 1]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, BL, acc, 0, 0, 0);
+    }
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, BH, acc, 0, 0, 0);
+  };
+  auto tile = [&](const u4v (&v)[QH], unsigned& bk, unsigned& sk) __attribute__((always_inline)) {
+    unsigned b = 0xFFFFFFFFu, s = 0xFFFFFFFFu;
+#pragma nounroll
+    for (int m = 0; m < MT; ++m) {
+      const f16v acc = screen_m(m, v);
+      const unsigned rb = 32u * (unsigned)m;
+      auto key = [&](int i) {
+        return (__float_as_uint(acc[i]) & ~63u) | (rb + (unsigned)(8 * (i >> 2) + (i & 3)));
+      };
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        const unsigned x = key(q), y = key(q + 1);
+        unsigned tq;
+        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(tq) : "v"(b), "v"(x), "v"(y));
+        asm("v_min3_u32 %0, %1, %2, %3" : "=v"(b) : "v"(b), "v"(x), "v"(y));
+        s = min(s, tq);
+      }
+    }
+    bk = b | ((unsigned)h << 2);
+    sk = s | ((unsigned)h << 2);
+  };
+  // candidate rows of tile v for the point of this lane's column (threshold
+  // tau of that point): bit 16 m + i = value i of centroid tile m in half h
+  auto cmask = [&](const u4v (&v)[QH], float tau) __attribute__((always_inline)) -> unsigned {
+    unsigned r = 0;
+#pragma nounroll
+    for (int m = 0; m < MT; ++m) {
+      const f16v acc = screen_m(m, v);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float kv = __uint_as_float(__float_as_uint(acc[i]) & ~63u);
+        if (!(kv > tau)) r |= 1u << (16 * m + i);  // (NaN: a candidate)
+      }
+    }
+    return r;
+  };
+  // q = ||xhat32 - c32_j||^2 in fp32: one rounding per difference, two fma
+  // chains of <= 8 and one add, every term >= 0, so |q - exact| <= 2^-20 q
+  // and |sqrt(q) - ||xhat32 - c32_j||| <= 2^-19 sqrt(q) (v_sqrt_f32: 1 ulp)
+  auto q32 = [&](const float (&xh)[DM], int j) __attribute__((always_inline)) -> float {
+    const f4* c4 = reinterpret_cast<const f4*>(c32s + j * kPrStr);
+    f2 acc = {0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const f4 cq = c4[q];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const f2 df = {xh[4 * q + 2 * u] - cq[2 * u], xh[4 * q + 2 * u + 1] - cq[2 * u + 1]};
+        acc = __builtin_elementwise_fma(df, df, acc);
+      }
+    }
+    return acc.x + acc.y;
+  };
+  struct GB {
+    f4 x[Q];  // the point's fp32 row
+    int pt, ao;
+    bool valid;
+  };
+  // the split screen operands of the wave's 64 rows (lane l: point l): the
+  // hi / lo halves of xhat32; lanes 0-31 keep their own half 0 for tile 0 and
+  // receive lane 32 + p's half 0 for tile 1, lanes 32-63 receive lane p's
+  // half 1 for tile 0 and keep their own half 1 for tile 1
+  auto split_tiles = [&](const float (&xh)[DM], u4v (&T0)[QH], u4v (&T1)[QH]) __attribute__((always_inline)) {
+    unsigned hw[4 * QH], lw[4 * QH];
+#pragma unroll
+    for (int qq = 0; qq < 2 * QH; ++qq) {
+      f4 xt = {0.f, 0.f, 0.f, 0.f};
+      if (qq < Q) xt = f4{xh[4 * qq], xh[4 * qq + 1], xh[4 * qq + 2], xh[4 * qq + 3]};
+      split4(xt, hw[2 * qq], hw[2 * qq + 1], lw[2 * qq], lw[2 * qq + 1]);
+    }
+    unsigned ad[4 * QH], bd[4 * QH];  // quads 0 .. QH-1 | quads QH .. 2QH-1
+    if constexpr (QH == 1) {  // [hi(q), lo(q)]
+      ad[0] = hw[0]; ad[1] = hw[1]; ad[2] = lw[0]; ad[3] = lw[1];
+      bd[0] = hw[2]; bd[1] = hw[3]; bd[2] = lw[2]; bd[3] = lw[3];
+    } else {  // [hi(q0), hi(q1)], [lo(q0), lo(q1)]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ad[i] = hw[i];
+        ad[4 + i] = lw[i];
+        bd[i] = hw[4 + i];
+        bd[4 + i] = lw[4 + i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * QH; ++i) swap32(ad[i], bd[i]);
+#pragma unroll
+    for (int u = 0; u < QH; ++u) {
+      T0[u] = u4v{ad[4 * u], ad[4 * u + 1], ad[4 * u + 2], ad[4 * u + 3]};
+      T1[u] = u4v{bd[4 * u], bd[4 * u + 1], bd[4 * u + 2], bd[4 * u + 3]};
+    }
+  };
+  // (best, runner-up) keys of this lane's point over both tiles and halves
+  auto keys = [&](const u4v (&T0)[QH], const u4v (&T1)[QH], unsigned& b, unsigned& s) __attribute__((always_inline)) {
+    unsigned bB, sB;
+    tile(T0, b, s);
+    tile(T1, bB, sB);
+    swap32(b, bB);
+    swap32(s, sB);
+    merge_top2(b, s, bB, sB);
+  };
+  auto rowhat = [&](const f4 (&x)[Q], float (&xh)[DM]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int f = 0; f < DM; ++f) xh[f] = f < d ? fmaf(x[f >> 2][f & 3], sig, msl[f]) : 0.0f;
+  };
+  // a point leaving cluster ao for lab: labels and this workgroup's table
+  // (row: the point's row when the caller holds it, else read again)
+  auto move = [&](bool live, int pt, int ao, int lab, const f4* row) __attribute__((always_inline)) {
+    const bool moved = live && lab != ao;
+    const unsigned long long mm = __ballot(moved);
+    if (!mm) return;
+    if (moved) {
+      a.labels[pt] = lab;
+      a.lab8[pt] = (uint8_t)lab;
+      f4 xr[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) xr[q] = row ? row[q] : XA4[(int64_t)pt * Q + q];
+#pragma unroll
+      for (int f = 0; f < DM; ++f) {
+        if (f < d) {
+          const long long v = __double2ll_rn((double)xr[f >> 2][f & 3] * F.fx);
+          atomicAdd(&mtab[lab * d1 + f], (unsigned long long)v);
+          atomicAdd(&mtab[ao * d1 + f], (unsigned long long)-v);
+        }
+      }
+      atomicAdd(&mtab[lab * d1 + d], 1ull);
+      atomicAdd(&mtab[ao * d1 + d], ~0ull);
+    }
+    mv_used += __popcll(mm);
+  };
+  int2* fb_region = a.fb_list + (size_t)wave * a.cap;
+  // one gathered batch: lane l decides point l
+  auto decide = [&](const GB& g) __attribute__((always_inline)) {
+    const bool valid = g.valid;
+    const int pt = g.pt, ao = g.ao;
+    float xh[DM];
+    rowhat(g.x, xh);
+    // triangle test: q = ||xhat32 - c32_a||^2
+    const float qa = q32(xh, ao);
+    const float uba = fmaf(__builtin_amdgcn_sqrtf(qa), 1.0f + 0x1p-18f, eb[ao]);
+    const float l0P = fmaf(hc[ao], 1.0f - 0x1p-22f, -uba);
+    const bool keep = l0P > uba * (1.0f + 0x1p-20f);
+    const float w_ao = __shfl(wdn_l, ao);
+    if (valid && keep) B.zb[pt] = zb_pack(l0P, uba, w_ao, (unsigned)ao);
+    const bool need = valid && !keep;
+    const unsigned long long nm = __ballot(need);
+    if (!nm) return;
+    qtot += __popcll(nm);
+#ifdef CDR_EXPERIMENTS
+    if (B.dbg & 8) return;  // (timing: no k-way screen)
+#endif
+    // ||xhat32||^2 (fp32, 16 roundings at most: relative 2^-19 covers them)
+    float xx;
+    {
+      f2 acc = {0.0f, 0.0f};
+#pragma unroll
+      for (int f = 0; f < DM; f += 2) {
+        const f2 v = {xh[f], xh[f + 1]};
+        acc = __builtin_elementwise_fma(v, v, acc);
+      }
+      xx = acc.x + acc.y;
+    }
+    unsigned bA, sA_;
+    u4v T0[QH], T1[QH];
+    split_tiles(xh, T0, T1);
+    keys(T0, T1, bA, sA_);
+    const int label = (int)(bA & 63u);
+    const float vb = __uint_as_float(bA & ~63u);
+    const float vs = __uint_as_float(sA_ & ~63u);
+    const bool cert = vs > fmaf(vb, thr_rel, thr0);  // NaN: never certified
+    const bool unc = need && !cert;
+    const float w_lab = __shfl(wdn_l, label);
+    // K-case: the point's bound word from its split keys
+    if (need && cert) {
+      const float xu = fmaf(xx, 1.0f + 0x1p-19f, 0x1p-120f);  // >= ||xhat32||^2
+      const float xl = xx * (1.0f - 0x1p-19f);               // <= ||xhat32||^2
+      const float dn32 = fmaf(0x1p-24f * (1.0f + 0x1p-20f), __builtin_amdgcn_sqrtf(xu), 0x1p-120f);
+      const float gb = fmaf(vb, thr_rel, thr0 + xu - Dlo);
+      const float gs = vs - ((thr0 + Dhi) - xl);
+      const float u0 = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gb, 0.0f)), 1.0f + 0x1p-19f, dn32);
+      const float l0 = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gs, 0.0f)), 1.0f - 0x1p-19f, -dn32);
+      B.zb[pt] = zb_pack(l0, u0, w_lab, (unsigned)label);
+    }
+    // uncertified (near ties): the wave's list {point, best key}, resolved
+    // after the workgroup's last batch
+    const unsigned long long um = __ballot(unc);
+    if (um) {
+      if (unc) {
+        const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(um >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((unsigned)um, 0u));
+        fb_region[fb_used + r] = int2{pt, (int)bA};
+      }
+      fb_used += __popcll(um);
+    }
+    move(need && cert, pt, ao, label, nullptr);
+  };
+
+  // ---- phase 2: the listed points, 64 per batch, two batches in flight ----
+  unsigned* const fl = flist[wv];
+  auto gload = [&](GB& g, int b, int cnt) __attribute__((always_inline)) {
+    const int e = 64 * b + lane;
+    g.valid = e < cnt;
+    const unsigned ent = fl[g.valid ? e : 64 * b];  // (entry 64 b exists)
+    const int64_t ci = wave + (int64_t)(ent >> 14) * nwaves;
+    const int64_t pt = ci * kBChunk + ((ent >> 6) & 255);
+    g.pt = (int)pt;
+    g.ao = (int)(ent & 63);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) g.x[q] = __builtin_nontemporal_load(XA4 + pt * Q + q);
+  };
+  auto phase2 = [&](int& cnt, bool last) __attribute__((always_inline)) {
+    const int nb = last ? (cnt + 63) >> 6 : cnt >> 6;
+    if (nb == 0) return;
+    ttot += last ? cnt : nb * 64;
+#ifdef CDR_EXPERIMENTS
+    if (B.dbg & 4) {  // (timing: the listed points are not decided)
+      cnt = 0;
+      return;
+    }
+#endif
+    // the next batch's rows load while one is decided (past the end: the
+    // last batch again, not decided); the copy waits for them after it
+    GB cur, nxt;
+    gload(cur, 0, cnt);
+#pragma nounroll
+    for (int b = 0; b < nb; ++b) {
+      gload(nxt, b + 1 < nb ? b + 1 : nb - 1, cnt);
+      decide(cur);
+      cur = nxt;
+    }
+    const int done = nb * 64;
+    const int rem = last ? 0 : cnt - done;
+    if (rem > 0) {
+      const unsigned v = lane < rem ? fl[done + lane] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < rem) fl[lane] = v;
+    }
+    cnt = rem;
+  };
+
+  // ---- phase 1: the bound words, 4 points per lane per chunk ----
+  int cnt = 0;
+  int64_t it = 0;
+  for (int64_t C0 = wave;; C0 += (int64_t)kBPD * nwaves) {
+    const bool more = C0 < nchunks;  // (wave-uniform)
+    if (more) {
+#pragma unroll
+    for (int i = 0; i < kBPD; ++i, ++it) {
+      const int64_t Ci = C0 + (int64_t)i * nwaves;
+      if (Ci >= nchunks) break;
+      zload(zc[(i + kBPD - 1) % kBPD], Ci + (int64_t)(kBPD - 1) * nwaves);
+      const u4v z = zc[i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const unsigned w = z[u];
+        const unsigned lab = w & 63u;
+#ifdef CDR_EXPERIMENTS
+        const bool fail = (!(__uint_as_float(w & ~63u) > __shfl(wup_l, (int)lab)) || (B.dbg & 1)) &&
+                          !(B.dbg & 16);  // (timing: the stream alone)
+#else
+        const bool fail = !(__uint_as_float(w & ~63u) > __shfl(wup_l, (int)lab)) || (B.dbg & 1);
+#endif
+        const unsigned long long m = __ballot(fail);
+        if (m) {
+          if (fail) {
+            const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            fl[cnt + r] = (unsigned)it << 14 | (unsigned)(4 * lane + u) << 6 | lab;
+          }
+          cnt += __popcll(m);
+        }
+      }
+    }
+    }
+    if (!more || cnt > kSList - kBPD * kBChunk) phase2(cnt, !more);
+    if (!more) break;
+  }
+  // ---- the uncertified points: the same split screen again (the same values),
+  // every centroid whose key is within the threshold of the best is a
+  // candidate (|S_j - T_j| <= E: the reference's argmin is among them), and
+  // the candidates in exact fp64 NumPy order (fixup_regions' decision) from
+  // an LDS copy of the step's centroids (the lists' LDS, free now) ----
+  CDR_TP(2);
+#ifdef CDR_EXPERIMENTS
+  if (B.dbg & 2) fb_used = 0;  // (timing: no exact pass)
+#endif
+  {
+    const double* cs = F.cent;
+    for (int e0 = 0; e0 < fb_used; e0 += 64) {
+      const int e = e0 + lane;
+      const bool live = e < fb_used;
+      const int2 rec = fb_region[live ? e : e0];
+      const int pt = rec.x;
+      const int ao = a.lab8[pt];  // (unchanged until this pass decides the point)
+      f4 xr[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) xr[q] = XA4[(int64_t)pt * Q + q];
+      float xh[DM];
+      rowhat(xr, xh);
+      u4v T0[QH], T1[QH];
+      split_tiles(xh, T0, T1);
+      const float tau = fmaf(__uint_as_float((unsigned)rec.y & ~63u), thr_rel, thr0);
+      // tile tt's column p is the point of lane 32 tt + p, which holds its tau
+      unsigned mine[2], other[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const float tau_t = __shfl(tau, 32 * tt + p);
+        const unsigned r = cmask(tt == 0 ? T0 : T1, tau_t);
+        mine[tt] = r;
+        other[tt] = (unsigned)__shfl_xor((int)r, 32);
+      }
+      int lab = ao;
+      bool c2 = false;  // decided by the direct fp32 distances
+      float u0 = 0.0f, l0 = 0.0f;
+      if (live) {
+        unsigned long long cand = 0;
+        const unsigned mh0 = h == 0 ? mine[0] : other[1], mh1 = h == 0 ? other[0] : mine[1];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          unsigned mmk = hh ? mh1 : mh0;  // rows of half hh of this lane's tile
+          while (mmk) {
+            const int bb = __builtin_ctz(mmk);
+            mmk &= mmk - 1;
+            const int m = bb >> 4, i = bb & 15;
+            cand |= 1ull << (32 * m + 8 * (i >> 2) + 4 * hh + (i & 3));
+          }
+        }
+        if (k < 64) cand &= (1ull << k) - 1;
+        // the candidates' direct fp32 distances (c32 in LDS): t_j = ||xhat -
+        // chat_j|| lies within sqrt(q_j) (1 -+ 2^-19) -+ (dn32 + ec_j), where
+        // dn32 >= ||xhat32 - xhat|| and ec_j >= ||c32_j - chat_j||: c32 is
+        // the fp32 rounding of chat_j in fp64, so ec_j <= (2^-24 + 2^-51)
+        // ||chat_j|| <= 2^-24 (1 + 2^-18) ||c32_j||
+        float xx;
+        {
+          f2 acc = {0.0f, 0.0f};
+#pragma unroll
+          for (int f = 0; f < DM; f += 2) {
+            const f2 v = {xh[f], xh[f + 1]};
+            acc = __builtin_elementwise_fma(v, v, acc);
+          }
+          xx = acc.x + acc.y;
+        }
+        const float xu = fmaf(xx, 1.0f + 0x1p-19f, 0x1p-120f);
+        const float xl = xx * (1.0f - 0x1p-19f);
+        const float dn32 = fmaf(0x1p-24f * (1.0f + 0x1p-20f), __builtin_amdgcn_sqrtf(xu), 0x1p-120f);
+        float ub = INFINITY, lo_other = INFINITY, lb_best = INFINITY, rbest = INFINITY;
+        int jb = 0;
+        bool bad = false;  // a NaN distance: the exact pass decides
+        unsigned long long cm2 = cand;
+        while (cm2) {  // increasing j
+          const int j = __builtin_ctzll(cm2);
+          cm2 &= cm2 - 1;
+          float nc;
+          {
+            const float zr[DM] = {};
+            nc = q32(zr, j);  // ||c32_j||^2 (the same rounding bound)
+          }
+          const float ec = fmaf(0x1p-24f * (1.0f + 0x1p-18f),
+                                __builtin_amdgcn_sqrtf(nc * (1.0f + 0x1p-19f)), 0x1p-120f);
+          const float e2 = (dn32 + ec) * (1.0f + 0x1p-20f);
+          const float r = __builtin_amdgcn_sqrtf(q32(xh, j));
+          const float U = fmaf(r, 1.0f + 0x1p-19f, e2), L = fmaf(r, 1.0f - 0x1p-19f, -e2);
+          bad = bad || !(U == U) || !(L == L);
+          if (r < rbest) {
+            lo_other = fminf(lo_other, lb_best);
+            rbest = r;
+            ub = U;
+            lb_best = L;
+            jb = j;
+          } else {
+            lo_other = fminf(lo_other, L);
+          }
+        }
+        // every other centroid's key is above tau: its distance is at least
+        const float gs = tau - ((thr0 + Dhi) - xl);
+        const float lnc = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gs, 0.0f)), 1.0f - 0x1p-19f, -dn32);
+        c2 = !bad && rbest < INFINITY && lo_other > ub * (1.0f + 0x1p-20f);
+        if (c2) {
+          lab = jb;
+          u0 = ub;
+          l0 = fminf(lo_other, lnc);
+        } else {
+        float x[16];  // fp32 data, converted exactly where used
+#pragma unroll
+        for (int f = 0; f < 16; ++f) x[f] = f < DM ? xr[f >> 2][f & 3] : 0.0f;
+        double sb = INFINITY, rb = INFINITY;
+        int jmin = 0x7fffffff;
+        while (cand) {  // increasing j
+          const int j = __builtin_ctzll(cand);
+          cand &= cand - 1;
+          const double sq = np_sqdist16(x, cs + j * d, d);
+          if (sq < sb) {  // sqrt is monotone: only a smaller square gives a smaller root
+            const double rt = sqrt(sq);
+            sb = sq;
+            if (rt < rb) {
+              rb = rt;
+              jmin = j;
+            }
+          }
+        }
+        lab = jmin >= k ? 0 : jmin;  // every root NaN: np.argmin of all-NaN is 0
+        }
+      }
+      const float w_lab = __shfl(wdn_l, lab);
+      if (live)  // the direct bounds, or none (decided again next step)
+        B.zb[pt] = c2 ? zb_pack(l0, u0, w_lab, (unsigned)lab) : (kZbStale | (unsigned)lab);
+#ifdef CDR_EXPERIMENTS
+      if (B.dbg & 64) continue;  // (timing: no moves from this pass)
+      const unsigned long long tm0 = __builtin_amdgcn_s_memrealtime();
+      tp[6] += 1;
+      tp[7] += __popcll(__ballot(live && lab != ao));
+#endif
+      move(live, pt, ao, lab, xr);
+#ifdef CDR_EXPERIMENTS
+      tp[5] += __builtin_amdgcn_s_memrealtime() - tm0;
+#endif
+    }
+  }
+  CDR_TP(3);
+  if (lane == 0) {
+    a.fb_count[wave] = fb_used;
+    a.mv_count[wave] = mv_used;
+    if (a.q_acc) a.q_acc[wave] += qtot;
+    if (B.t_acc) B.t_acc[wave] += ttot;
+  }
+  // this workgroup's moves into one run_sums slice (nothing to do: no atomics)
+  if (__syncthreads_or(mv_used)) {
+    const int cells = k * d1;
+    unsigned long long* out = F.run_sums + (size_t)(blockIdx.x % kRunSlices) * cells;
+    for (int e = t; e < cells; e += 256) {
+      const unsigned long long v = mtab[e];
+      if (v) atomicAdd(&out[e], v);
+    }
+  }
+#ifdef CDR_EXPERIMENTS
+  CDR_TP(4);
+  if (B.tprof && lane == 0)
+    for (int q = 0; q < 8; ++q) B.tprof[(size_t)wave * 8 + q] = tp[q];
+#endif
+#undef CDR_TP
+}
+
 // Bound words before the first bounded step of a run of them: every real
 // point "no bound" with its current label (lab8), padding rows "always keep".
 __global__ void zb_reset_kernel(const uint8_t* __restrict__ lab8, uint32_t* __restrict__ zb,
@@ -2475,6 +3040,28 @@ static void screen32b_launch(int Q, int MT, dim3 grid, hipStream_t s, const S32B
 #undef CDR_S32B_GO
 }
 
+static int screen32bs_blocks_per_cu(int Q, int MT) {
+  static int cache[4][2] = {};
+  int& nb = cache[Q - 1][MT - 1];
+  if (!nb) {
+    hipError_t e = hipErrorInvalidValue;
+#define CDR_S32BS_OCC(Q_, M_) \
+    if (Q == Q_ && MT == M_) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32bs<Q_, M_>, 256, 0);
+    CDR_S32B_ALL(CDR_S32BS_OCC)
+#undef CDR_S32BS_OCC
+    if (e != hipSuccess || nb < 1) nb = 2;
+    if (nb > 8) nb = 8;
+  }
+  return nb;
+}
+
+static void screen32bs_launch(int Q, int MT, dim3 grid, hipStream_t s, const S32BArgs& p) {
+#define CDR_S32BS_GO(Q_, M_) \
+  if (Q == Q_ && MT == M_) hipLaunchKernelGGL((screen32bs<Q_, M_>), grid, dim3(256), 0, s, p);
+  CDR_S32B_ALL(CDR_S32BS_GO)
+#undef CDR_S32BS_GO
+}
+
 // Prefetch depth of screen32d: CDR_S32D_PD=2|3|4 (comparisons), else the
 // measured default per shape.
 static int s32d_depth(int QH) {
@@ -2511,10 +3098,15 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   const bool bnd_env = !std::getenv("CDR_BOUNDS") || std::atoi(std::getenv("CDR_BOUNDS"));
   const bool BND = PR && bnd_env && gate && dthr && c.ll_on && c.bnd_ok &&
                    c.n_pad < (int64_t(1) << 31);
+  // the bounded screen deciding in registers (screen32bs; CDR_S32B_SPLIT=0:
+  // screen32b with its queue and fused fixup)
+  const bool BS = BND && (!std::getenv("CDR_S32B_SPLIT") || std::atoi(std::getenv("CDR_S32B_SPLIT")));
   if (!BND) c.zb_valid = false;  // another path decides this step's labels
   int bpc;
   const int PD = PR ? PPD : LRn ? LRn : s32d_depth(QH);
-  if (BND) {
+  if (BS) {
+    bpc = screen32bs_blocks_per_cu(PQ, MT);
+  } else if (BND) {
     bpc = screen32b_blocks_per_cu(PQ, MT);
   } else if (PR) {
     bpc = screen32p_blocks_per_cu(PQ, MT, PPD);
@@ -2556,7 +3148,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   const int nwaves = nwg * 4;
   const int cap = (int)(ceil_div(units, nwaves) * unit_pts);
   c.fb_list.ensure(sizeof(int2) * (size_t)nwaves * cap);
-  c.mv_list.ensure(sizeof(int2) * (size_t)nwaves * cap);
+  if (!BS) c.mv_list.ensure(sizeof(int2) * (size_t)nwaves * cap);  // (screen32bs: no move list)
   c.mv_count.ensure(sizeof(int32_t) * (size_t)nwaves);
   if (c.fb_count.bytes < sizeof(int32_t) * (nwaves + 3) || c.fb_layout != nwaves) {
     c.fb_count.ensure(sizeof(int32_t) * (nwaves + 3));
@@ -2667,7 +3259,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
                            c.lab8.as<uint8_t>(), c.zb.as<uint32_t>(), c.n, c.n_pad, gate);
         HIP_CHECK(hipGetLastError());
       }
-      if (!c.xh_valid) {
+      if (!BS && !c.xh_valid) {
         c.xh16.ensure((size_t)c.n_pad * (QH == 1 ? 16 : 32));
         if (QH == 1)
           hipLaunchKernelGGL(aos_hi_kernel<8>, dim3(4096), dim3(256), 0, c.stream,
@@ -2697,10 +3289,66 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       b.dbg &= 1;  // (the other bits are timing experiments: experiments build only)
 #endif
       c.zb_valid = true;
-      snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32b<%d,%d>%s", PQ, MT,
-               fused ? "+fixup" : "");
-      if (prof) prof_mark(c, 0);
-      screen32b_launch(PQ, MT, grid, c.stream, b);
+      b.tprof = nullptr;
+#ifdef CDR_EXPERIMENTS
+      static unsigned long long* tprof_buf = nullptr;
+      const bool tprof_on = BS && std::getenv("CDR_S32BS_TPROF");
+      if (tprof_on) {
+        if (!tprof_buf) HIP_CHECK(hipMalloc(&tprof_buf, sizeof(unsigned long long) * 8 * 65536));
+        b.tprof = tprof_buf;
+      }
+#endif
+      if (BS) {
+        snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32bs<%d,%d>", PQ, MT);
+        if (prof) prof_mark(c, 0);
+        screen32bs_launch(PQ, MT, grid, c.stream, b);
+#ifdef CDR_EXPERIMENTS
+        if (tprof_on) {  // per-wave phase times (100 MHz counter), to stderr
+          std::vector<unsigned long long> h((size_t)nwaves * 8);
+          HIP_CHECK(hipStreamSynchronize(c.stream));
+          HIP_CHECK(hipMemcpy(h.data(), tprof_buf, h.size() * 8, hipMemcpyDeviceToHost));
+          unsigned long long t0 = ~0ull, t4 = 0;
+          double sum[6] = {}, mx[6] = {}, mv = 0, nb = 0, mvt = 0;
+          for (int w = 0; w < nwaves; ++w) {
+            const unsigned long long* r = &h[(size_t)w * 8];
+            t0 = std::min(t0, r[0]);
+            t4 = std::max(t4, r[4]);
+          }
+          for (int w = 0; w < nwaves; ++w) {
+            const unsigned long long* r = &h[(size_t)w * 8];
+            const double v[6] = {double(r[0] - t0), double(r[1] - r[0]), double(r[2] - r[1]),
+                                 double(r[3] - r[2]), double(r[4] - r[3]), double(t4 - r[4])};
+            for (int q = 0; q < 6; ++q) {
+              sum[q] += v[q];
+              mx[q] = std::max(mx[q], v[q]);
+            }
+            mvt += double(r[5]);
+            nb += double(r[6]);
+            mv += double(r[7]);
+          }
+          if (const char* path = std::getenv("CDR_S32BS_TPROF_FILE")) {  // raw, appended
+            if (FILE* fo = std::fopen(path, "ab")) {
+              std::fwrite(h.data(), 8, h.size(), fo);
+              std::fclose(fo);
+            }
+          }
+          std::fprintf(stderr,
+                       "TPROF waves %d span %.1f us | avg/max us: start %.1f/%.1f prologue %.1f/%.1f "
+                       "phases %.1f/%.1f tail %.1f/%.1f flush %.1f/%.1f idle-end %.1f/%.1f | "
+                       "tail batches/wave %.2f tail moves/wave %.1f tail move us/wave %.2f\n",
+                       nwaves, (t4 - t0) / 100.0, sum[0] / nwaves / 100, mx[0] / 100,
+                       sum[1] / nwaves / 100, mx[1] / 100, sum[2] / nwaves / 100, mx[2] / 100,
+                       sum[3] / nwaves / 100, mx[3] / 100, sum[4] / nwaves / 100, mx[4] / 100,
+                       sum[5] / nwaves / 100, mx[5] / 100, nb / nwaves, mv / nwaves,
+                       mvt / nwaves / 100);
+        }
+#endif
+      } else {
+        snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32b<%d,%d>%s", PQ, MT,
+                 fused ? "+fixup" : "");
+        if (prof) prof_mark(c, 0);
+        screen32b_launch(PQ, MT, grid, c.stream, b);
+      }
     } else {
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32p<%d,%d,%d>%s", PQ, MT, PPD,
              fused ? "+fixup" : "");
@@ -2743,7 +3391,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   static const int fr_env = std::getenv("CDR_FIX_FR") ? std::atoi(std::getenv("CDR_FIX_FR")) : 8;
   f.fr = fr_env >= 1 && fr_env <= kFixMaxR ? fr_env : 8;
   const dim3 fgrid((nwaves + f.fr - 1) / f.fr);
-  if (!fused) switch (d4_of(c.d) / 4) {
+  if (!fused && !BS) switch (d4_of(c.d) / 4) {  // (screen32bs applies its own moves)
 #define CDR_FIX(Q_)                                                                  \
   case Q_:                                                                           \
     if (MT == 1) hipLaunchKernelGGL((fixup32<Q_, 1>), fgrid, blk, 0, c.stream, f);    \

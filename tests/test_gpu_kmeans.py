@@ -186,10 +186,14 @@ def test_full_size_properties_config2(ctx):
     sample = np.sort(rng.choice(n, 20000, replace=False))
     Xs = ctx.get_rows(sample)
     np.testing.assert_array_equal(lab[sample], ko.assign(Xs, C))
-    # sums are consistent with labels: recompute one cluster exactly on host
+    # the int64 sums of one whole cluster recomputed on the host from its rows
+    # (the points are multiples of 2^-S: exact)
+    S = ctx.info()["scale_bits"]
     j = int(np.argmax(out[:, d]))
-    idx = np.flatnonzero(lab == j)[:200000]
-    assert idx.size > 0
+    idx = np.flatnonzero(lab == j)
+    assert idx.size == out[j, d] > 0
+    rows = ctx.get_rows(idx)
+    np.testing.assert_array_equal(np.ldexp(rows, S).astype(np.int64).sum(axis=0), out[j, :d])
     assert ctx.fallback_count() < n // 50
 
 

@@ -422,7 +422,9 @@ def _mirrored(n, d, k, seed):
 @pytest.mark.parametrize("n,d,k,kind", [(200_000, 16, 64, "blobs"), (150_000, 16, 64, "uniform"),
                                         (150_000, 8, 16, "uniform"), (100_000, 5, 40, "uniform"),
                                         (120_000, 13, 50, "blobs"), (90_000, 3, 7, "uniform"),
-                                        (160_000, 16, 64, "mirror"), (100_000, 8, 32, "mirror")])
+                                        (160_000, 16, 64, "mirror"), (100_000, 8, 32, "mirror"),
+                                        (160_000, 16, 64, "mirror-queue"),
+                                        (150_000, 8, 16, "uniform-queue")])
 def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     """screen32b: after the bound rebuild a point keeps its
     label without its coordinates being read when its stored drift bound
@@ -430,8 +432,12 @@ def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     data (every step moves points across slowly moving boundaries) and on
     mirrored data with exact and near ties: labels and centroids equal the
     oracle's every time, and the bounded steps re-read fewer points than
-    they kept."""
+    they kept.  The default kernel decides in registers (screen32bs); the
+    "-queue" cases run screen32b (LDS queue + fused fixup, CDR_S32B_SPLIT=0)."""
     monkeypatch.setenv("CDR_BOUNDS", "1")
+    queue = kind.endswith("-queue")
+    kind = kind.replace("-queue", "")
+    monkeypatch.setenv("CDR_S32B_SPLIT", "0" if queue else "1")
     if kind == "blobs":
         X = synth.generate(n, 0, n, d, k, 17 * n + d)
     elif kind == "uniform":
@@ -451,7 +457,8 @@ def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     C, st = _loop(ctx, C0, steps, -1.0, X)
     prof = ctx.profile_read()
     ctx.profile_reset(False)
-    assert ctx.profile_kernel().startswith("screen32b"), ctx.profile_kernel()
+    assert ctx.profile_kernel().startswith("screen32b<" if queue else "screen32bs<"), \
+        ctx.profile_kernel()
     np.random.seed(3)
     C_ref, lab_ref, _, _ = ko.lloyd(X, C0, steps, -1.0)
     np.testing.assert_array_equal(ctx.labels(), lab_ref)

@@ -16,7 +16,9 @@ from cdr_dist import Comm, DeviceLloyd, seed_sharded  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 k = int(sys.argv[3]) if len(sys.argv) > 3 else 64
-masks = [int(m) for m in (sys.argv[4].split(",") if len(sys.argv) > 4 else "0,2,4,8,16,6".split(","))]
+# a mask "F<n>" sets CDR_FIX_ABL=n instead (the fused fixup's parts: 1 no moves,
+# 2 no fallback, 4 no flush) with every bound part on
+masks = sys.argv[4].split(",") if len(sys.argv) > 4 else "0,2,4,8,16,6".split(",")
 ctx = _cdr.Context(0)
 ctx.generate_points(n, 0, n, d, k, 0x5EED)
 C = seed_sharded(ctx, Comm(), 0, n, k, random_state=42)
@@ -26,13 +28,19 @@ run.advance(6)
 res = {m: [] for m in masks}
 for rnd in range(3):
     for m in masks:
-        os.environ["CDR_BOUNDS_DBG"] = str(m)
+        fix = m.startswith("F")
+        os.environ["CDR_BOUNDS_DBG"] = "0" if fix else m
+        os.environ["CDR_FIX_ABL"] = m[1:] if fix else "0"
         ctx.profile_reset(True)
         run.advance(4, chunk=4, chunk_max=4)
         p = ctx.profile_read()
         res[m].append(p["screen_ms"] / max(p["steps"], 1))
+        if not m.startswith("F") and int(m) & 128:  # candidates of the exact pass (high word)
+            print(f"mask {m}: steps {p['steps']} tight {p['tight_points'] & 0xFFFFFFFF} "
+                  f"candidates {p['tight_points'] >> 32} profile {p}")
         ctx.profile_reset(False)
 os.environ["CDR_BOUNDS_DBG"] = "0"
+os.environ["CDR_FIX_ABL"] = "0"
 for m in masks:
-    print(f"mask {m:3d}: screen32b {np.median(res[m]) * 1e3:8.1f} us  (rounds {[round(x * 1e3, 1) for x in res[m]]})")
+    print(f"mask {m:>4}: screen32b {np.median(res[m]) * 1e3:8.1f} us  (rounds {[round(x * 1e3, 1) for x in res[m]]})")
 run.finish()
