@@ -77,6 +77,8 @@ SIGNATURES = {
     "cdr_seed_run_sharded": ([_P, _I64, _I64, _I64, _I32, _P, _P, _P, _P], None),
     "cdr_lloyd_step": ([_P, _P, _I32, _P, _I32], None),
     "cdr_lloyd_step_f64": ([_P, _P, _I32, _P, _P], None),
+    "cdr_lloyd_step_f32r": ([_P, _P, _I32, _P, _P], None),
+    "cdr_f32r_seed_update": ([_P, _P, _I32, _P], None),
     "cdr_lloyd_labels": ([_P, _P], None),
     "cdr_lloyd_stats": ([_P, _PI64], None),
     "cdr_debug_screen": ([_P, _P, _I32, _P, _P], None),
@@ -450,6 +452,28 @@ class Context:
         counts = np.empty(k, dtype=np.int64)
         _check(self._lib.cdr_lloyd_step_f64(self._h, _ptr(C), k, _ptr(sums), _ptr(counts)))
         return sums, counts
+
+    def lloyd_step_f32r(self, C: np.ndarray):
+        """The reference's float32 step: (sequential fp32 sums as float64
+        (k, d), counts (k,)); labels from the fp32 norms."""
+        C = np.ascontiguousarray(C, dtype=np.float32)
+        k, d = C.shape
+        sums = np.empty((k, d), dtype=np.float64)
+        counts = np.empty(k, dtype=np.int64)
+        _check(self._lib.cdr_lloyd_step_f32r(self._h, _ptr(C), k, _ptr(sums), _ptr(counts)))
+        return sums, counts
+
+    def f32r_seed_update(self, c: np.ndarray, reset: bool) -> float:
+        """The reference's float32 seeding step; returns dist_sq.sum() (fp32)
+        and stages fp32(dist_sq / total) for seed_scan(1.0, ...)."""
+        c = np.ascontiguousarray(c, dtype=np.float32).ravel()
+        tot = ctypes.c_float()
+        code = self._lib.cdr_f32r_seed_update(self._h, _ptr(c), 1 if reset else 0,
+                                              ctypes.byref(tot))
+        if code == CDR_ERR_NAN:
+            raise NanProbabilities("Probabilities contain NaN")
+        _check(code)
+        return float(np.float32(tot.value))
 
     def f64_walked(self) -> int:
         """Blocks the last F64 step re-added element-wise (-1: serial kernel)."""

@@ -138,6 +138,7 @@ struct Ctx {
 
   // ---- Lloyd ----
   DevBuf labels;    // int32[n_pad]
+  DevBuf cent32r;   // float[k*d]: the float32 reference runs' centroids
   DevBuf cent64;    // double[k*d]
   DevBuf frag;      // fp16 MFMA A-operand fragments
   DevBuf partials;  // int64 per workgroup k*(d+1)
@@ -224,6 +225,7 @@ struct Ctx {
 
   // ---- seeding ----
   DevBuf dmin;        // double[n_pad]
+  DevBuf dmin32, bs32;  // float32 reference runs: fp32 dist_sq [n_pad], chunk sums
   // exact pruning of the seeding update (seed.hip seed_prunable): the index
   // of each point's nearest centre so far, the centres, their distances to
   // the newest one
@@ -310,6 +312,9 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums,
 
 void seed_reset(Ctx& c);
 void seed_update(Ctx& c, const double* cent);
+void f32r_seed_update(Ctx& c, const float* cen, int reset, float* total);
+void lloyd_step_f32r(Ctx& c, const float* C, int32_t k, double* sums, int64_t* counts);
+bool f32_sums_parallel(Ctx& c, int k, double* d_sums);
 void seed_scan(Ctx& c, double total, double c_in, double* c_out);
 void events_ts_range(Ctx& c, int64_t ne);
 void seed_scan_begin(Ctx& c, double total, double c_guess, int64_t* n_items, int64_t* n_fine);

@@ -49,13 +49,29 @@ constexpr int kFB = 256;               // rows per block
 constexpr int kFMaxK = 64;             // clusters handled here (LDS state)
 constexpr int kENone = -100000;        // no prediction (no member before the block)
 
+// The summed type T: double (F64 mode) or float (the reference's float32
+// runs: the same algorithm on a 24-bit significand).  MB = significand bits
+// after the point; binades below kMinE are subnormal (no fixed grid): those
+// blocks are re-added element by element.
+template <typename T>
+struct SumTraits {
+  static constexpr int MB = 52;
+  static constexpr int kMinE = -1022;
+};
+template <>
+struct SumTraits<float> {
+  static constexpr int MB = 23;
+  static constexpr int kMinE = -126;
+};
+
 struct Xfer {
   long long d0;  // grid steps added for an even entry
   int dd;        // d1 - d0
   int flags;     // bit0 P0, bit1 P1 (exit parities), bit2 invalid, bit3 members
 };
 
-__global__ __launch_bounds__(kFB) void f64_blocksum(const double* __restrict__ X, int64_t n,
+template <typename T>
+__global__ __launch_bounds__(kFB) void f64_blocksum(const T* __restrict__ X, int64_t n,
                                                     int64_t n_pad, int d, int k,
                                                     const int32_t* __restrict__ labels,
                                                     double* __restrict__ A,
@@ -71,7 +87,7 @@ __global__ __launch_bounds__(kFB) void f64_blocksum(const double* __restrict__ X
   if (row < n) {
     const int j = labels[row];
     atomicAdd(&c[j], 1u);
-    for (int f = 0; f < d; ++f) atomicAdd(&tab[j * d + f], X[xidx(f, row, n_pad)]);
+    for (int f = 0; f < d; ++f) atomicAdd(&tab[j * d + f], (double)X[xidx(f, row, n_pad)]);
   }
   __syncthreads();
   // sequence-major ([cluster * d + feature][block], [cluster][block]): the
@@ -150,7 +166,8 @@ __global__ __launch_bounds__(256) void f64_predict_c(const double* __restrict__ 
 
 // One thread per (block, feature); the per-cluster transfer states live in
 // LDS ([thread][cluster]).
-__global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_pad, int d,
+template <typename TA, typename S>
+__global__ void f64_transfer(const S* __restrict__ X, int64_t n, int64_t n_pad, int d,
                              int k, int64_t nb, const int32_t* __restrict__ labels,
                              const int* __restrict__ E, Xfer* __restrict__ T) {
   extern __shared__ unsigned char smem[];
@@ -187,7 +204,7 @@ __global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_
     for (int u = 0; u < kCh; ++u) {
       const int64_t row = rc + u;
       lj[u] = row < r1 ? labels[row] : -1;
-      lx[u] = row < r1 ? X[xidx(f, row, n_pad)] : 0.0;
+      lx[u] = row < r1 ? (double)X[xidx(f, row, n_pad)] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kCh; ++u) {
@@ -196,12 +213,12 @@ __global__ void f64_transfer(const double* __restrict__ X, int64_t n, int64_t n_
     const double x = lx[u];
     int fl = mfl[j] | 8;
     const int e = me[j];
-    if (e == kENone || !(x >= 0.0)) {
+    if (e == kENone || e < SumTraits<TA>::kMinE || !(x >= 0.0)) {
       mfl[j] = fl | 4;
       continue;
     }
-    const double y = ldexp(x, 52 - e);  // exact: a power-of-two scaling
-    if (!(y < 9007199254740992.0)) {    // x not below the binade's top
+    const double y = ldexp(x, SumTraits<TA>::MB - e);  // exact: a power-of-two scaling
+    if (!(y < (double)(1ll << (SumTraits<TA>::MB + 1)))) {  // x not below the binade's top
       mfl[j] = fl | 4;
       continue;
     }
@@ -306,7 +323,8 @@ __global__ __launch_bounds__(256) void f64_group(const unsigned* __restrict__ cn
 // binade is applied block by block, re-adding a block element by element in
 // real fp64 whenever its transfer cannot be used.  (Stepping every block
 // through the transfer one at a time cost 8 ms at 10M x 5, k = 16.)
-__global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, int64_t n,
+template <typename TA, typename S>
+__global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t n,
                                                 int64_t n_pad, int d, int k, int64_t nb,
                                                 const int32_t* __restrict__ labels,
                                                 const unsigned* __restrict__ cnt,
@@ -320,7 +338,9 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
   const int lane = threadIdx.x & 63;
   if (t >= k * d) return;
   const int j = t / d, f = t % d;
-  double s = 0.0;
+  constexpr int MB = SumTraits<TA>::MB, kMinE = SumTraits<TA>::kMinE;
+  constexpr long long kTop = 1ll << (MB + 1);
+  double s = 0.0;  // (a T value)
   bool any = false;  // NumPy's reduce starts from the first selected row
   long long nwalk = 0;
   long long pc_el = 0, pc_slow = 0, n_slow = 0;  // CDR_F64_PROF: cycles
@@ -331,11 +351,11 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
     if (!(flags & 4) && s > 0.0) {
       int ex;
       frexp(s, &ex);
-      if (ex - 1 == e) {
-        const long long m = (long long)ldexp(s, 52 - e);  // exact: s is on the grid
+      if (ex - 1 == e && e >= kMinE) {
+        const long long m = (long long)ldexp(s, MB - e);  // exact: s is on the grid
         const long long m2 = m + ((m & 1) ? d0 + dd : d0);
-        if (m2 < (1ll << 53)) {
-          s = ldexp((double)m2, e - 52);
+        if (m2 < kTop) {
+          s = ldexp((double)m2, e - MB);
           ok = true;
         }
       }
@@ -347,7 +367,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
       for (int q = 0; q < kFB; q += 64) {
         const int64_t row = r0 + q + lane;
         const bool mine = row < n && labels[row] == j;
-        const double x = mine ? X[xidx(f, row, n_pad)] : 0.0;
+        const double x = mine ? (double)X[xidx(f, row, n_pad)] : 0.0;
         unsigned long long mk = __ballot(mine);
         while (mk) {
           const int l = __builtin_amdgcn_readfirstlane(__ffsll((long long)mk) - 1);
@@ -358,7 +378,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
                                (int)(xb >> 32), l)
                            << 32) |
                           (unsigned)__builtin_amdgcn_readlane((int)xb, l)));
-          s = any ? s + v : v;
+          s = any ? (double)((TA)s + (TA)v) : v;  // (TA arithmetic: one rounding)
           any = true;
         }
       }
@@ -392,8 +412,10 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
     if (s > 0.0) {
       int ex;
       frexp(s, &ex);
-      sE = ex - 1;
-      sN = (long long)ldexp(s, 52 - sE);  // exact: s is on the grid
+      if (ex - 1 >= kMinE) {
+        sE = ex - 1;
+        sN = (long long)ldexp(s, MB - sE);  // exact: s is on the grid
+      }
     }
   };
   GXfer gnext = gfetch(0);
@@ -419,13 +441,13 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
                                       << 32) |
                                      (unsigned)__builtin_amdgcn_readlane((int)gl.d0, gi));
           const long long m2 = sN + gd;
-          if (m2 < (1ll << 53)) {
+          if (m2 < kTop) {
             sN = m2;
             continue;
           }
         }
       }
-      if (sE != kENone) s = ldexp((double)sN, sE - 52);  // s from the integer state
+      if (sE != kENone) s = ldexp((double)sN, sE - MB);  // s from the integer state
       const long long ps0 = prof ? (long long)clock64() : 0;
       ++n_slow;
       const int64_t b0 = (g0 + gi) * 64;
@@ -444,7 +466,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
         if (s > 0.0) {
           int ex;
           frexp(s, &ex);
-          es = ex - 1;
+          if (ex - 1 >= kMinE) es = ex - 1;
         }
         // blocks i.. that are empty or can take a transfer in binade es
         const bool compat = c == 0 || (es != kENone && !(xl.flags & 4) && el == es);
@@ -468,10 +490,10 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
             y.p = __shfl_up(x.p, o);
             if (lane >= o) x = xc_compose(y, x);
           }
-          const long long m = (long long)ldexp(s, 52 - es);
+          const long long m = (long long)ldexp(s, MB - es);
           const long long mq = m + ((m & 1) ? x.d1 : x.d0);
           const bool inrun = lane >= i && lane < r;
-          const unsigned long long bad = __ballot(inrun && !(mq < (1ll << 53)));
+          const unsigned long long bad = __ballot(inrun && !(mq < kTop));
           const int L = __builtin_amdgcn_readfirstlane(bad ? __ffsll((long long)bad) - 1 : r);
           if (L > i) {  // blocks i .. L-1 in one step
             const long long mL =
@@ -479,7 +501,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
                                  (int)(mq >> 32), L - 1)
                              << 32) |
                             (unsigned)__builtin_amdgcn_readlane((int)mq, L - 1));
-            s = ldexp((double)mL, es - 52);
+            s = ldexp((double)mL, es - MB);
             i = L;
             if (i >= r) continue;
           }
@@ -499,7 +521,7 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
       if (prof) pc_slow += (long long)clock64() - ps0;
     }
   }
-  if (sE != kENone) s = ldexp((double)sN, sE - 52);
+  if (sE != kENone) s = ldexp((double)sN, sE - MB);
   if (prof && lane == 0) {
     prof[4 * t] = (long long)clock64() - pc0;
     prof[4 * t + 1] = pc_slow;
@@ -518,7 +540,9 @@ __global__ __launch_bounds__(256) void f64_walk(const double* __restrict__ X, in
 // sums (k, d) on the device, exact sequential row-order fp64 sums; returns
 // false when the shape is not covered (d < 2, k > 64): the caller runs the
 // serial kernel.
-bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
+// TA: the summed (arithmetic) type; S: the storage type of X
+template <typename TA, typename S>
+static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums) {
   const int d = c.d;
   if (d < 2 || k < 1 || k > kFMaxK || c.n < 1) return false;
   const int64_t n = c.n, nb = ceil_div(n, kFB);
@@ -528,8 +552,8 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
   c.f64x_E.ensure(sizeof(int) * nb * kd);
   c.f64x_T.ensure(sizeof(Xfer) * nb * kd);
   c.f64x_walk.ensure(sizeof(long long) * kd);
-  hipLaunchKernelGGL(f64_blocksum, dim3(nb), dim3(kFB), sizeof(double) * kd + 4 * k, c.stream,
-                     c.x64.as<double>(), n, c.n_pad, d, k, c.labels.as<int32_t>(),
+  hipLaunchKernelGGL(f64_blocksum<S>, dim3(nb), dim3(kFB), sizeof(double) * kd + 4 * k, c.stream,
+                     X, n, c.n_pad, d, k, c.labels.as<int32_t>(),
                      c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>());
   HIP_CHECK(hipGetLastError());
   const int64_t ng = ceil_div(nb, (int64_t)64);
@@ -545,8 +569,8 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
   HIP_CHECK(hipGetLastError());
   const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
   const size_t lds = (size_t)nt * k * (8 + 4 + 4 + 4);
-  hipLaunchKernelGGL(f64_transfer, dim3(ceil_div(nb * d, nt)), dim3(nt), lds, c.stream,
-                     c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
+  hipLaunchKernelGGL((f64_transfer<TA, S>), dim3(ceil_div(nb * d, nt)), dim3(nt), lds, c.stream,
+                     X, n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
                      c.f64x_E.as<int>(), c.f64x_T.as<Xfer>());
   HIP_CHECK(hipGetLastError());
   c.f64x_G.ensure(sizeof(GXfer) * ng * kd);
@@ -556,8 +580,8 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
                      c.stream, c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(),
                      c.f64x_T.as<Xfer>(), nb, d, k, ng, c.f64x_G.as<GXfer>());
   HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(f64_walk, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
-                     c.x64.as<double>(), n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
+  hipLaunchKernelGGL((f64_walk<TA, S>), dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
+                     X, n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
                      c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(),
                      c.f64x_G.as<GXfer>(), ng, d_sums, c.f64x_walk.as<long long>(),
                      prof_on ? c.f64x_prof.as<long long>() : nullptr);
@@ -575,6 +599,16 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
   }
   HIP_CHECK(hipGetLastError());
   return true;
+}
+
+bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
+  return sums_parallel<double, double>(c, c.x64.as<double>(), k, d_sums);
+}
+// The reference's float32 runs: sequential fp32 sums of fp32 points (X:
+// F32X storage, or F64 storage holding fp32 values), returned as doubles.
+bool f32_sums_parallel(Ctx& c, int k, double* d_sums) {
+  if (c.mode == CDR_MODE_F32X) return sums_parallel<float, float>(c, c.x32.as<float>(), k, d_sums);
+  return sums_parallel<float, double>(c, c.x64.as<double>(), k, d_sums);
 }
 
 }  // namespace cdr

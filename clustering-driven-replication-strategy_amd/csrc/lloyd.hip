@@ -1370,6 +1370,149 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
   c.last_fallback = c.n;
 }
 
+// ---------------------------------------------------------------------------
+// The reference's float32 runs (X float32 keeps its dtype,
+// src/kmeans_plusplus.py:6): distances are float32 norms in NumPy order with
+// one rounded sqrt, np.argmin takes the first of equal float32 norms (:33-34),
+// and X[mask].mean(axis=0) is a sequential float32 sum over the rows divided
+// (in fp64, cast to fp32 by the caller) by the count (:41).
+// ---------------------------------------------------------------------------
+template <typename S, int D>
+__global__ __launch_bounds__(256) void f32r_assign_kernel(const S* __restrict__ X, int64_t n,
+                                                          int64_t n_pad, int d,
+                                                          const float* __restrict__ C, int k,
+                                                          int32_t* __restrict__ labels) {
+  const int dd = D ? D : d;
+  for (int64_t pt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pt < n;
+       pt += (int64_t)gridDim.x * blockDim.x) {
+    float xr[D ? D : 1];
+    if constexpr (D > 0) {
+#pragma unroll
+      for (int f = 0; f < D; ++f) xr[f] = (float)X[xidx(f, pt, n_pad)];
+    }
+    auto xv = [&](int f) { return D ? xr[D ? f : 0] : (float)X[xidx(f, pt, n_pad)]; };
+    float Rb = INFINITY, rb = INFINITY;
+    int jb = 0;
+    for (int j = 0; j < k; ++j) {
+      const float* cj = C + (size_t)j * dd;
+      auto cv = [&](int f) { return cj[f]; };
+      const float R = np_sqdist<decltype(xv), decltype(cv), float>(xv, cv, dd);
+      if (R < Rb) {  // sqrt is monotone: only a smaller square can give a smaller norm
+        const float r = (float)sqrt((double)R);  // the correctly rounded fp32 sqrt
+        Rb = R;
+        if (r < rb) {
+          rb = r;
+          jb = j;
+        }
+      }
+    }
+    labels[pt] = jb;
+  }
+}
+
+// Serial form (k > 64 or d == 1): one thread per (cluster, feature); d == 1
+// follows NumPy's contiguous reduction (8192-blocked pairwise, fp32).
+template <typename S>
+__global__ void f32r_seq_sums(const S* __restrict__ X, int64_t n, int64_t n_pad, int d, int k,
+                              const int32_t* __restrict__ labels,
+                              const long long* __restrict__ counts_in,
+                              double* __restrict__ sums) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= k * d) return;
+  const int j = t / d, f = t % d;
+  auto col = [&](int64_t i) { return (float)X[xidx(f, i, n_pad)]; };
+  if (d >= 2) {
+    float s = 0.0f;
+    bool any = false;
+    for (int64_t i = 0; i < n; ++i)
+      if (labels[i] == j) {
+        s = any ? s + col(i) : col(i);
+        any = true;
+      }
+    sums[(size_t)j * d + f] = (double)s;
+    return;
+  }
+  const long long m = counts_in[j];
+  int64_t cursor = 0;
+  auto next = [&](int64_t) -> float {
+    while (labels[cursor] != j) ++cursor;
+    return col(cursor++);
+  };
+  float res = 0.0f;
+  for (long long done = 0; done < m; done += kSeedBlock) {
+    const long long blk = (m - done) < kSeedBlock ? (m - done) : kSeedBlock;
+    res = res + np_pairwise<decltype(next), float>(next, blk);
+  }
+  sums[j] = (double)res;
+}
+
+void lloyd_step_f32r(Ctx& c, const float* C, int32_t k, double* sums, int64_t* counts) {
+  check_k(c, k);
+  c.run_valid = false;
+  c.lab8_valid = false;
+  c.zb_valid = false;
+  c.big_valid = false;
+  const int d = c.d;
+  const int cus = lloyd_num_cus(c.device);
+  c.cent32r.ensure(sizeof(float) * (size_t)k * d);
+  HIP_CHECK(hipMemcpyAsync(c.cent32r.p, C, sizeof(float) * (size_t)k * d, hipMemcpyHostToDevice,
+                           c.stream));
+  const bool prof = prof_step_begin(c);
+  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "f32r_assign_kernel<%d>", d);
+  if (prof) prof_mark(c, 0);
+  const dim3 grid(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), (int64_t)cus * 8)));
+  const float* dC = c.cent32r.as<float>();
+  int32_t* lab = c.labels.as<int32_t>();
+#define CDR_F32R_AS(S_, X_)                                                                      \
+  switch (d) {                                                                                  \
+    case 2: hipLaunchKernelGGL((f32r_assign_kernel<S_, 2>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dC, k, lab); break; \
+    case 5: hipLaunchKernelGGL((f32r_assign_kernel<S_, 5>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dC, k, lab); break; \
+    case 8: hipLaunchKernelGGL((f32r_assign_kernel<S_, 8>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dC, k, lab); break; \
+    case 16: hipLaunchKernelGGL((f32r_assign_kernel<S_, 16>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dC, k, lab); break; \
+    default: hipLaunchKernelGGL((f32r_assign_kernel<S_, 0>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dC, k, lab); \
+  }
+  if (c.mode == CDR_MODE_F32X) {
+    CDR_F32R_AS(float, c.x32.as<float>())
+  } else {
+    CDR_F32R_AS(double, c.x64.as<double>())
+  }
+#undef CDR_F32R_AS
+  HIP_CHECK(hipGetLastError());
+  if (prof) prof_mark(c, 1);
+  c.f64_sums.ensure(sizeof(double) * (size_t)k * d);
+  c.f64_counts.ensure(sizeof(long long) * k * 2);
+  long long* cnt_pre = c.f64_counts.as<long long>() + k;
+  HIP_CHECK(hipMemsetAsync(cnt_pre, 0, sizeof(long long) * k, c.stream));
+  hipLaunchKernelGGL(count_labels, dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 2))),
+                     dim3(256), k <= kCountLds ? sizeof(unsigned) * 4 * k : 0, c.stream,
+                     c.labels.as<int32_t>(), c.n, k, reinterpret_cast<unsigned long long*>(cnt_pre));
+  HIP_CHECK(hipGetLastError());
+  if (!getenv("CDR_F64_SERIAL") && f32_sums_parallel(c, k, c.f64_sums.as<double>())) {
+    c.f64x_walked = 0;
+  } else {
+    const int threads = k * d;
+    if (c.mode == CDR_MODE_F32X)
+      hipLaunchKernelGGL(f32r_seq_sums<float>, dim3((threads + 63) / 64), dim3(64), 0, c.stream,
+                         c.x32.as<float>(), c.n, c.n_pad, d, k, c.labels.as<int32_t>(), cnt_pre,
+                         c.f64_sums.as<double>());
+    else
+      hipLaunchKernelGGL(f32r_seq_sums<double>, dim3((threads + 63) / 64), dim3(64), 0, c.stream,
+                         c.x64.as<double>(), c.n, c.n_pad, d, k, c.labels.as<int32_t>(), cnt_pre,
+                         c.f64_sums.as<double>());
+    HIP_CHECK(hipGetLastError());
+    c.f64x_walked = -1;
+  }
+  if (prof) prof_mark(c, 2);
+  HIP_CHECK(hipMemcpyAsync(sums, c.f64_sums.p, sizeof(double) * (size_t)k * d,
+                           hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(counts, cnt_pre, sizeof(long long) * k, hipMemcpyDeviceToHost,
+                           c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.last_k = k;
+  c.have_labels = true;
+  c.last_fallback = c.n;
+}
+
 __global__ void labels_to_i64(const int32_t* __restrict__ a, int64_t n, long long* __restrict__ b) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -1397,6 +1540,14 @@ int cdr_lloyd_step_f64(cdr_ctx* h, const double* C, int32_t k, double* sums,
   if (!h || !C || !sums || !counts) CDR_FAIL(CDR_ERR_ARG, "null argument");
   HIP_CHECK(hipSetDevice(h->c.device));
   lloyd_step_f64(h->c, C, k, sums, counts);
+  CDR_CATCH
+}
+
+int cdr_lloyd_step_f32r(cdr_ctx* h, const float* C, int32_t k, double* sums, int64_t* counts) {
+  CDR_TRY
+  if (!h || !C || !sums || !counts) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  lloyd_step_f32r(h->c, C, k, sums, counts);
   CDR_CATCH
 }
 

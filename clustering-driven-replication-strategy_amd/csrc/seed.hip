@@ -2441,6 +2441,144 @@ void seed_run_sharded(Ctx& c, int64_t row_begin, int64_t n_total, int64_t first,
 
 using namespace cdr;
 
+namespace cdr {
+
+// ---------------------------------------------------------------------------
+// The reference's float32 runs (X float32 keeps its dtype:
+// src/kmeans_plusplus.py:6): dist_sq, its sum and the probabilities are
+// float32 arrays there.
+//   t       = np.linalg.norm(X - c, axis=2)   fp32 NumPy order, one rounded sqrt (:15)
+//   dist_sq = min(dist_sq, t ** 2)            fp32 square; np.min keeps NaN (:14)
+//   total   = dist_sq.sum()                   fp32: 8192-element chunks pairwise,
+//                                             chunks added left to right (:18)
+//   probs   = dist_sq / total                 fp32 (:18)
+// and Generator.choice converts p to float64 before its cumsum (:19), so the
+// exact cumsum scan (seed_scan) runs unchanged on p as doubles with S = 1.
+// ---------------------------------------------------------------------------
+template <typename S, int D>
+__global__ __launch_bounds__(256) void f32r_min_kernel(const S* __restrict__ X, int64_t n,
+                                                       int64_t n_pad, int d,
+                                                       const float* __restrict__ cen,
+                                                       float* __restrict__ dmin32) {
+  const int dd = D ? D : d;
+  for (int64_t pt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pt < n;
+       pt += (int64_t)gridDim.x * blockDim.x) {
+    auto xv = [&](int f) { return (float)X[xidx(f, pt, n_pad)]; };  // exact: fp32 values
+    auto cv = [&](int f) { return cen[f]; };
+    const float R = np_sqdist<decltype(xv), decltype(cv), float>(xv, cv, dd);
+    const float t = (float)sqrt((double)R);  // = the correctly rounded fp32 sqrt
+    const float t2 = t * t;
+    const float m = dmin32[pt];
+    dmin32[pt] = (m != m || t2 != t2) ? NAN : (t2 < m ? t2 : m);
+  }
+}
+__global__ void f32r_fill_kernel(float* __restrict__ p, int64_t n_pad, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = i < n ? INFINITY : 0.0f;
+}
+// fp32 pairwise sum of each 8192-element chunk: a full chunk is the perfect
+// tree over 64 leaves of 128 (lane l: leaf l, combined left + right by
+// shuffles); the partial last chunk runs the whole recursion on one lane.
+__global__ __launch_bounds__(64) void f32r_block_kernel(const float* __restrict__ dmin32,
+                                                        int64_t n, float* __restrict__ bs32) {
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t base = b * kSeedBlock;
+  if (base + kSeedBlock <= n) {
+    const float* src = dmin32 + base + lane * 128;
+    auto leaf = [&](int i) { return src[i]; };
+    float v = np_pw_leaf<decltype(leaf), float>(leaf, 128);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float r = __shfl_down(v, o);
+      if ((lane & (2 * o - 1)) == 0) v = v + r;
+    }
+    if (lane == 0) bs32[b] = v;
+  } else if (lane == 0) {
+    auto all = [&](int64_t i) { return dmin32[base + i]; };
+    bs32[b] = np_pairwise<decltype(all), float>(all, n - base);
+  }
+}
+// p = fl32(dist_sq / total) as doubles (the scan's dmin, rows >= n zero) and
+// each chunk's sum in any order (the scan's binade guesses only)
+__global__ __launch_bounds__(256) void f32r_prob_kernel(const float* __restrict__ dmin32,
+                                                        int64_t n, float total,
+                                                        double* __restrict__ dmin,
+                                                        double* __restrict__ bs) {
+  __shared__ double red[4];
+  const int64_t b = blockIdx.x;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < kSeedBlock; i += 256) {
+    const int64_t pt = b * kSeedBlock + i;
+    // fp32 division via fp64: fl32(fl64(a / b)) = fl32(a / b) for fp32 a, b
+    const double p = pt < n ? (double)(float)((double)dmin32[pt] / (double)total) : 0.0;
+    dmin[pt] = p;
+    acc += p;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) bs[b] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+void f32r_seed_update(Ctx& c, const float* cen, int reset, float* total_out) {
+  check_points(c);
+  const int64_t nb = c.nblocks();
+  c.dmin32.ensure(sizeof(float) * (size_t)(c.n_pad > 0 ? c.n_pad : 1));
+  c.dmin.ensure(sizeof(double) * (size_t)(c.n_pad > 0 ? c.n_pad : 1));
+  c.blocksums.ensure(sizeof(double) * (nb > 0 ? nb : 1));
+  c.bs32.ensure(sizeof(float) * (nb > 0 ? nb : 1));
+  c.seed_scalar.ensure(sizeof(double) * (2 * c.d + 8));
+  if (reset) {
+    hipLaunchKernelGGL(f32r_fill_kernel, dim3(2048), dim3(256), 0,
+                       c.stream, c.dmin32.as<float>(), c.n_pad, c.n);
+    HIP_CHECK(hipGetLastError());
+  }
+  float* dcen = reinterpret_cast<float*>(c.seed_scalar.p);
+  HIP_CHECK(hipMemcpyAsync(dcen, cen, sizeof(float) * c.d, hipMemcpyHostToDevice, c.stream));
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(c.n, 256), 4096)));
+  const int d = c.d;
+#define CDR_F32R_MIN(S_, X_)                                                                \
+  switch (d) {                                                                             \
+    case 2: hipLaunchKernelGGL((f32r_min_kernel<S_, 2>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); break; \
+    case 5: hipLaunchKernelGGL((f32r_min_kernel<S_, 5>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); break; \
+    case 8: hipLaunchKernelGGL((f32r_min_kernel<S_, 8>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); break; \
+    case 16: hipLaunchKernelGGL((f32r_min_kernel<S_, 16>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); break; \
+    default: hipLaunchKernelGGL((f32r_min_kernel<S_, 0>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); \
+  }
+  if (c.mode == CDR_MODE_F32X) {
+    CDR_F32R_MIN(float, c.x32.as<float>())
+  } else {
+    CDR_F32R_MIN(double, c.x64.as<double>())
+  }
+#undef CDR_F32R_MIN
+  HIP_CHECK(hipGetLastError());
+  float total = 0.0f;
+  if (nb > 0) {
+    hipLaunchKernelGGL(f32r_block_kernel, dim3((unsigned)nb), dim3(64), 0, c.stream,
+                       c.dmin32.as<float>(), c.n, c.bs32.as<float>());
+    HIP_CHECK(hipGetLastError());
+    std::vector<float> bs((size_t)nb);
+    HIP_CHECK(hipMemcpyAsync(bs.data(), c.bs32.p, sizeof(float) * nb, hipMemcpyDeviceToHost,
+                             c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    for (float v : bs) total = total + v;  // NumPy: the chunks from 0, left to right (fp32)
+  }
+  *total_out = total;
+  if (!(total > 0.0f) || std::isinf(total)) CDR_FAIL(CDR_ERR_NAN, "Probabilities contain NaN");
+  if (nb > 0) {
+    hipLaunchKernelGGL(f32r_prob_kernel, dim3((unsigned)nb), dim3(256), 0, c.stream,
+                       c.dmin32.as<float>(), c.n, total, c.dmin.as<double>(),
+                       c.blocksums.as<double>());
+    HIP_CHECK(hipGetLastError());
+  }
+  c.seed_scanned = false;
+  c.seed_prog_ready = false;
+}
+
+}  // namespace cdr
+
 extern "C" {
 
 int cdr_seed_reset(cdr_ctx* h) {
@@ -2448,6 +2586,14 @@ int cdr_seed_reset(cdr_ctx* h) {
   if (!h) CDR_FAIL(CDR_ERR_ARG, "null ctx");
   HIP_CHECK(hipSetDevice(h->c.device));
   seed_reset(h->c);
+  CDR_CATCH
+}
+
+int cdr_f32r_seed_update(cdr_ctx* h, const float* c, int32_t reset, float* total) {
+  CDR_TRY
+  if (!h || !c || !total) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  f32r_seed_update(h->c, c, reset, total);
   CDR_CATCH
 }
 

@@ -15,9 +15,11 @@ reference (src/kmeans_plusplus.py)  here
 :19     rng.choice(n, p=probs)      host rng.random() + cdr_seed_scan/search
                                     (bit-exact sequential cumsum emulation)
 :33-34  norm + argmin               cdr_lloyd_step: certified MFMA screen +
-                                    exact fp64 fallback (identical labels)
+                                    exact fp64 fallback (identical labels);
+                                    float32 X: cdr_lloyd_step_f32r (fp32 norms)
 :37-41  X[mask].mean(axis=0)        fused int64 fixed-point sums (F32X) or
-                                    row-ordered fp64 sums (F64) / host divide
+                                    row-ordered fp64 sums (F64) / host divide;
+                                    float32 X: row-ordered fp32 sums
 :43     np.random.randint reseed    host (global legacy RNG, j order)
 :45-48  norm(new - old) < tol       host NumPy (same BLAS call)
 =================================  ==========================================
@@ -78,12 +80,42 @@ def _seed_on_device(ctx: Context, X: np.ndarray, k: int, random_state) -> np.nda
     return centroids
 
 
+def _seed_f32r(ctx: Context, X: np.ndarray, k: int, random_state) -> np.ndarray:
+    """The reference's seeding on a float32 X (:6, 14-19 in float32): the
+    device forms fp32 dist_sq, its fp32 total and fp32 probabilities
+    (cdr_f32r_seed_update), then the exact float64 cumsum scan and search of
+    Generator.choice run as in the float64 case with S = 1."""
+    rng = np.random.default_rng(random_state)
+    n_samples, n_features = X.shape
+    centroids = np.empty((k, n_features), dtype=X.dtype)
+    first_idx = rng.integers(0, n_samples)
+    centroids[0] = X[first_idx]
+    for i in range(1, k):
+        try:
+            ctx.f32r_seed_update(centroids[i - 1], reset=(i == 1))
+        except NanProbabilities:
+            _nan_probabilities()
+        c_last = ctx.seed_scan(1.0, 0.0)
+        u = rng.random()
+        next_idx = ctx.seed_search(c_last, u)
+        if next_idx < 0:  # cannot happen: cdf[-1] == 1.0 > u
+            raise RuntimeError("k-means++ sampler found no index")
+        centroids[i] = X[next_idx]
+    return centroids
+
+
+def _seed(ctx: Context, X: np.ndarray, k: int, random_state) -> np.ndarray:
+    if X.dtype == np.float32:
+        return _seed_f32r(ctx, X, k, random_state)
+    return _seed_on_device(ctx, X, k, random_state)
+
+
 def kmeans_plusplus_init(X, k, random_state=None, *, context: Context | None = None):
     """D^2 seeding (reference src/kmeans_plusplus.py:3-22)."""
     X = np.asarray(X)
     ctx = context if context is not None else default_context()
     ctx.load_points(X)
-    return _seed_on_device(ctx, X, k, random_state)
+    return _seed(ctx, X, k, random_state)
 
 
 def _cluster_means(ctx: Context, C: np.ndarray, mode: int, scale_bits: int):
@@ -112,13 +144,35 @@ def kmeans(X, k, number_of_files=100, tol=1e-4, random_state=None, *,
     n_samples = X.shape[0]
     ctx = context if context is not None else default_context()
     ctx.load_points(X)
-    centroids = _seed_on_device(ctx, X, k, random_state)
+    centroids = _seed(ctx, X, k, random_state)
 
     if max_iter is None:
         max_iter = max(100, number_of_files / 100)
     iters = range(max_iter)  # the reference's TypeError for a float max_iter (:29-31)
     info = ctx.info()
     mode, scale_bits = info["mode"], info["scale_bits"]
+
+    if X.dtype == np.float32:
+        # the reference's float32 arithmetic (:6, 33-34, 41): fp32 norms and
+        # argmin, sequential fp32 cluster sums; np.mean divides in fp64 (the
+        # intp count promotes) and casts the quotient to float32
+        ran = False
+        for _ in iters:
+            ran = True
+            sums, counts = ctx.lloyd_step_f32r(centroids)
+            with np.errstate(invalid="ignore", divide="ignore"):
+                means = sums / counts[:, None].astype(np.float64)
+            new_centroids = np.empty_like(centroids)
+            new_centroids[...] = means
+            for j in np.flatnonzero(counts == 0):  # j order, as the reference draws (:43)
+                new_centroids[j] = X[np.random.randint(0, n_samples)]
+            shift = np.linalg.norm(new_centroids - centroids)
+            centroids = new_centroids
+            if shift < tol:
+                break
+        if not ran:
+            raise UnboundLocalError("local variable 'labels' referenced before assignment")
+        return centroids, ctx.labels()
 
     if mode == MODE_F32X and centroids.dtype in (np.float64, np.float32) and len(iters) > 0:
         # device-resident loop: means, shift and convergence on the device,

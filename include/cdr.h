@@ -92,6 +92,14 @@ int cdr_seed_reset(cdr_ctx* ctx);
  * dist_sq (NumPy's blocked add.reduce, used by dist_sq.sum() at :18).  c is
  * one float64 row of length d.                                              */
 int cdr_seed_update(cdr_ctx* ctx, const double* c);
+/* The reference's float32 seeding step (src/kmeans_plusplus.py:14-18 on a
+ * float32 X): dist_sq = min(dist_sq, fp32(norm(X - c))**2) with c float32
+ * (reset != 0: dist_sq starts at +inf), *total = dist_sq.sum() in fp32
+ * (NumPy's 8192-chunk pairwise order), and the probabilities fp32(dist_sq /
+ * total) staged as doubles for cdr_seed_scan(ctx, 1.0, ...) and
+ * cdr_seed_search, which then give rng.choice's pick.  CDR_ERR_NAN when the
+ * total is not positive and finite.                                        */
+int cdr_f32r_seed_update(cdr_ctx* ctx, const float* c, int32_t reset, float* total);
 /* Number of 8192-element blocks of this shard and their pairwise sums.     */
 int cdr_seed_num_blocks(cdr_ctx* ctx, int64_t* nblocks);
 int cdr_seed_block_sums(cdr_ctx* ctx, double* out);
@@ -186,6 +194,14 @@ int cdr_lloyd_step(cdr_ctx* ctx, const double* C, int32_t k, int64_t* out,
  * order exactly like X[labels == j].mean(axis=0)'s sum; counts (k).        */
 int cdr_lloyd_step_f64(cdr_ctx* ctx, const double* C, int32_t k, double* sums,
                        int64_t* counts);
+/* The reference's float32 runs (X float32 keeps its dtype,
+ * src/kmeans_plusplus.py:6, 33-34, 41): float32 norms in NumPy order, argmin
+ * of the fp32 norms, sums (k, d) = the SEQUENTIAL float32 sums of each
+ * cluster's rows (returned as doubles holding fp32 values; the caller
+ * divides in fp64 and casts to fp32, as np.mean does); counts (k).
+ * C: k x d float32.  Points loaded from a float32 array (either mode).  */
+int cdr_lloyd_step_f32r(cdr_ctx* ctx, const float* C, int32_t k, double* sums,
+                        int64_t* counts);
 /* F64 mode, d >= 2, k <= 64: the sums are formed in parallel (csrc/f64sum.hip:
  * per-block parity transfers inside one binade, exact); *walked = blocks of
  * (cluster, feature) sequences re-added element by element in the last step,

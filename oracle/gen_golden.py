@@ -243,12 +243,56 @@ def float32_cases():
     np.savez_compressed(os.path.join(GOLD, "kmeans_f32_cases.npz"), **out)
 
 
+F32_HARD = [  # name, n, d, k, rs, np_seed, transform
+    ("big", 2_400_000, 2, 2, 5, 21, "synth"),       # two ~1.2M-point clusters
+    ("coarse", 6000, 3, 12, 9, 22, "grid8"),        # values on a 2^-8 grid: ties
+    ("near", 5000, 4, 10, 4, 23, "near20"),         # offsets of 2^-20 around 0.5
+]
+
+
+def float32_hard_cases():
+    """The reference on float32 X where its float32 arithmetic matters
+    (VERDICT r3 item 6): a ~1.2M-point cluster (sequential fp32 mean drift),
+    data on a coarse grid (exact distance ties) and offsets of 2^-20 around
+    0.5 (fp32 norms tie where fp64 norms do not).  Stored: parameters, the
+    float32 and float64 runs' seeds and centroids, labels bit-packed (k = 2,
+    np.packbits) or as uint8, and whether the two runs differ."""
+    ref = load_ref("kmeans_plusplus")
+    out = {}
+    for i, (name, n, d, k, rs, nps, tr) in enumerate(F32_HARD):
+        X = synth.f32_hard_data(n, d, k, tr, 1000 + i)
+        runs = {}
+        for tag, Xc in (("f32", X), ("f64", X.astype(np.float64))):
+            np.random.seed(nps)
+            init = ref.kmeans_plusplus_init(Xc, k, random_state=rs)
+            np.random.seed(nps)
+            C, labels = ref.kmeans(Xc, k, number_of_files=100, random_state=rs)
+            runs[tag] = (init, C, labels)
+            out[f"h{i}_{tag}_init"] = init
+            out[f"h{i}_{tag}_centroids"] = C
+            if tag == "f32":  # (the float64 run's labels: only whether they differ)
+                out[f"h{i}_{tag}_labels"] = (np.packbits(labels.astype(np.uint8)) if k == 2
+                                             else labels.astype(np.uint8))
+        diff = [int(not np.array_equal(runs["f32"][0].astype(np.float64), runs["f64"][0])),
+                int(not np.array_equal(runs["f32"][2], runs["f64"][2])),
+                int(np.abs(runs["f32"][1].astype(np.float64) - runs["f64"][1]).max() /
+                    np.abs(runs["f64"][1]).max() > 2.0 ** -22)]
+        print(name, "f32 vs f64 differ (init, labels, centroids):", diff,
+              "max rel", np.abs(runs["f32"][1].astype(np.float64) - runs["f64"][1]).max() /
+              np.abs(runs["f64"][1]).max())
+        out[f"h{i}_meta"] = np.array([n, d, k, rs, nps, 1000 + i] + diff, dtype=np.int64)
+        out[f"h{i}_name"] = np.array(name + ":" + tr)
+    np.savez_compressed(os.path.join(GOLD, "kmeans_f32_hard.npz"), **out)
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
     if "--only-f32" in sys.argv:
         float32_cases()
+        float32_hard_cases()
         return
     float32_cases()
+    float32_hard_cases()
     cases, terr = kmeans_cases()
     save_kmeans(cases, terr)
     scoring_cases()

@@ -114,7 +114,7 @@ def kmeans_plusplus_init(X, k, random_state=None):
     centroids = np.empty((k, n_features), dtype=X.dtype)
     first_idx = rng.integers(0, n_samples)
     centroids[0] = X[first_idx]
-    dist_sq = np.full(n_samples, np.inf)
+    dist_sq = np.full(n_samples, np.inf, dtype=X.dtype)  # float32 X: fp32 sum and probs (:14-18)
     for i in range(1, k):
         t = np.sqrt(sqdist_rows(X, centroids[i - 1])) ** 2
         dist_sq = np.minimum(dist_sq, t)

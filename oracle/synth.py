@@ -49,3 +49,18 @@ def generate(n_total: int, row_begin: int, n_local: int, d: int, n_blobs: int,
             u = np.clip(center + 13 * (s - 131070), 0, 0xFFFFFF)
             out[:, f] = u.astype(np.float64) / 16777216.0
     return out
+
+
+def f32_hard_data(n: int, d: int, k: int, transform: str, seed: int) -> np.ndarray:
+    """Inputs of the hard float32 k-means fixtures (oracle/gen_golden.py
+    float32_hard_cases; the tests re-create them from these parameters):
+    "synth" the blobs as they are, "grid8" on a 2^-8 grid (distance ties),
+    "near20" offsets of 2^-20 around 0.5 plus a spread fifth."""
+    X = generate(n, 0, n, d, max(k, 2), seed)
+    if transform == "grid8":
+        X = np.floor(X * 256.0) / 256.0
+    elif transform == "near20":
+        q = np.floor(X * 8.0) - 4.0  # -4 .. 3
+        X = 0.5 + np.ldexp(q, -20)
+        X[: n // 5] = generate(n, 0, n // 5, d, 3, seed + 1)
+    return X.astype(np.float32)
