@@ -66,8 +66,9 @@ def test_loop_empty_cluster_far_centroid_and_convergence(ctx):
 
 
 def test_loop_float32_points_round_means(ctx):
-    """X float32: the centroids keep X's dtype (np.empty_like), as the
-    drop-in's host loop always did."""
+    """X float32: the reference's float32 arithmetic (float32 seeding, norms
+    and sequential float32 means; the centroids keep X's dtype) — the oracle
+    on the same float32 X, bit for bit."""
     import kmeans_plusplus as kp
 
     n, d, k = 30000, 8, 12
@@ -75,22 +76,27 @@ def test_loop_float32_points_round_means(ctx):
     np.random.seed(1)
     C, lab = kp.kmeans(X, k, random_state=3, max_iter=6, context=ctx)
     assert C.dtype == np.float32
-    X64 = X.astype(np.float64)
-    # the drop-in seeds in fp64 on float32 data: rows of X
-    Cr = ko.kmeans_plusplus_init(X64, k, random_state=3).astype(np.float32)
     np.random.seed(1)
-    for _ in range(6):
-        labr = ko.assign(X64, Cr.astype(np.float64))
-        new = np.empty_like(Cr)
-        for j in range(k):
-            m = labr == j
-            new[j] = X64[m].mean(axis=0) if m.any() else X[np.random.randint(0, n)]
-        shift = np.linalg.norm(new - Cr)
-        Cr = new
-        if shift < 1e-4:
-            break
+    Cr, labr = ko.kmeans(X, k, random_state=3, max_iter=6)
+    assert Cr.dtype == np.float32
     np.testing.assert_array_equal(C, Cr)
     np.testing.assert_array_equal(lab, labr)
+
+
+@pytest.mark.parametrize("n,d,k", [(40000, 1, 5), (30000, 3, 70), (20000, 20, 9)])
+def test_float32_serial_shapes_vs_oracle(ctx, n, d, k):
+    """The float32 path's shapes outside the parallel sequential sums (d = 1:
+    NumPy's blocked pairwise mean; k > 64: the serial kernel) and d > 16
+    (the generic distance kernel), against the oracle on float32 X."""
+    import kmeans_plusplus as kp
+
+    X = synth.generate(n, 0, n, d, min(k, 40), 91 + d).astype(np.float32)
+    np.random.seed(4)
+    C, lab = kp.kmeans(X, k, random_state=8, max_iter=4, context=ctx)
+    np.random.seed(4)
+    Cr, labr = ko.kmeans(X, k, random_state=8, max_iter=4)
+    np.testing.assert_array_equal(lab, labr)
+    np.testing.assert_array_equal(C, Cr)
 
 
 def _config_common(ctx, n, d, k, steps, sample, seed=0x5EED):
