@@ -150,6 +150,12 @@ struct Ctx {
   DevBuf f64_counts;  // int64 k
   // f64sum.hip: block sums, counts, predicted binades, transfers, walk counts
   DevBuf f64x_A, f64x_cnt, f64x_E, f64x_T, f64x_walk, f64x_G, f64x_GS, f64x_prof;
+  // f64_step_fused: the binade predictions of the last F64 step (two buffers:
+  // the one the current transfers use, the next step's), valid for (k, blocks)
+  DevBuf f64x_E2;
+  bool f64x_e_ok = false;
+  int f64x_e_cur = 0, f64x_e_k = 0;
+  int64_t f64x_e_nb = 0;
   int64_t f64x_walked = -1;  // blocks re-added element-wise in the last F64 step (-1: serial)
   HostBuf h_small;  // pinned scratch for small D2H
   HostBuf h_up;     // pinned staging of the per-step screen32 upload
@@ -337,7 +343,9 @@ void features_aggregate(Ctx& c, int64_t n_events, const int32_t* file_idx,
 bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max_ts);
 // exact sequential-order F64 centroid sums in parallel (f64sum.hip); false =
 // shape not covered (d < 2 or k > 64)
-bool f64_sums_parallel(Ctx& c, int k, double* d_sums);
+bool f64_sums_parallel(Ctx& c, int k, double* d_sums, bool pre = false);
+bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
+                    unsigned long long* d_counts, bool prof);
 void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
                        const double* creation_s, double observation_end,
                        double* out);

@@ -131,4 +131,27 @@ __device__ R np_pairwise(AF a, int64_t n) {
   return ret;
 }
 
+// np.argmin of the fp64 NumPy-order norms (src/kmeans_plusplus.py:33-34):
+// the first index of the smallest correctly rounded root; a root is taken
+// only for a smaller square (sqrt is monotone).
+template <typename XF>
+__device__ __forceinline__ int exact_argmin(XF xv, const double* __restrict__ C, int k,
+                                            int d) {
+  double Rb = INFINITY, rb = INFINITY;
+  int jb = 0;
+  for (int j = 0; j < k; ++j) {
+    const double* cj = C + (size_t)j * d;
+    const double R = np_sqdist(xv, [&](int f) { return cj[f]; }, d);
+    if (R < Rb) {
+      const double r = sqrt(R);
+      if (r < rb) {
+        rb = r;
+        Rb = R;
+        jb = j;
+      }
+    }
+  }
+  return jb;
+}
+
 }  // namespace cdr

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "cdr_internal.h"
+#include "exact_math.h"
 
 namespace cdr {
 
@@ -69,6 +70,50 @@ struct Xfer {
   int dd;        // d1 - d0
   int flags;     // bit0 P0, bit1 P1 (exit parities), bit2 invalid, bit3 members
 };
+
+// One element x >= 0 of a (cluster, feature) sequence added to a transfer
+// state (m0: grid steps for an even entry, mdd: odd - even, mfl: bit0 P0,
+// bit1 P1, bit2 invalid, bit3 members) under the predicted binade e.  With
+// x = mx 2^ex (integer significand), y = x / 2^(e - MB) = mx 2^-sh: q =
+// mx >> sh and the rounding of the fraction from the shifted-out bits — the
+// same q and fraction as ldexp / floor in fp64, in integer instructions.
+template <typename TA>
+__device__ __forceinline__ void xfer_add(double x, int e, long long& m0, int& mdd, int& mfl) {
+  constexpr int MB = SumTraits<TA>::MB;
+  int fl = mfl | 8;
+  if (e == kENone || e < SumTraits<TA>::kMinE || !(x >= 0.0)) {
+    mfl = fl | 4;
+    return;
+  }
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(x) & 0x7FFFFFFFFFFFFFFFull;
+  const int er = (int)(bits >> 52);
+  const unsigned long long mx = er ? ((bits & 0xFFFFFFFFFFFFFull) | (1ull << 52)) : bits;
+  const int sh = e - MB - ((er ? er : 1) - 1075);
+  long long qi = 0;
+  bool up = false, tie = false;
+  if (er == 0x7FF || (sh < 0 && mx != 0)) {  // infinite, or not below the binade's top
+    mfl = fl | 4;
+    return;
+  } else if (sh <= 0) {
+    qi = (long long)mx;
+  } else if (sh < 64) {
+    qi = (long long)(mx >> sh);
+    const unsigned long long rem = mx & ((1ull << sh) - 1ull), half = 1ull << (sh - 1);
+    up = rem > half;
+    tie = rem == half;
+  }  // (sh >= 64: y < 2^-11, q = 0, below one half)
+  if (!(qi < (1ll << (MB + 1)))) {
+    mfl = fl | 4;
+    return;
+  }
+  const int p0 = fl & 1;
+  const long long i0 = qi + (up ? 1 : (tie ? ((p0 + qi) & 1) : 0));
+  const int p1 = (fl >> 1) & 1;
+  const long long i1 = qi + (up ? 1 : (tie ? ((p1 + qi) & 1) : 0));
+  m0 += i0;
+  mdd += (int)(i1 - i0);
+  mfl = (fl & ~3) | (int)((p0 + i0) & 1) | ((int)((p1 + i1) & 1) << 1);
+}
 
 template <typename T>
 __global__ __launch_bounds__(kFB) void f64_blocksum(const T* __restrict__ X, int64_t n,
@@ -210,32 +255,7 @@ __global__ void f64_transfer(const S* __restrict__ X, int64_t n, int64_t n_pad, 
     for (int u = 0; u < kCh; ++u) {
     const int j = lj[u];
     if (j < 0) continue;
-    const double x = lx[u];
-    int fl = mfl[j] | 8;
-    const int e = me[j];
-    if (e == kENone || e < SumTraits<TA>::kMinE || !(x >= 0.0)) {
-      mfl[j] = fl | 4;
-      continue;
-    }
-    const double y = ldexp(x, SumTraits<TA>::MB - e);  // exact: a power-of-two scaling
-    if (!(y < (double)(1ll << (SumTraits<TA>::MB + 1)))) {  // x not below the binade's top
-      mfl[j] = fl | 4;
-      continue;
-    }
-    const double q = floor(y);
-    const double r = y - q;
-    const long long qi = (long long)q;
-    const bool up = r > 0.5, tie = r == 0.5;
-    // even-entry path
-    const int p0 = fl & 1;
-    const long long i0 = qi + (up ? 1 : (tie ? ((p0 + qi) & 1) : 0));
-    // odd-entry path
-    const int p1 = (fl >> 1) & 1;
-    const long long i1 = qi + (up ? 1 : (tie ? ((p1 + qi) & 1) : 0));
-    m0[j] += i0;
-    mdd[j] += (int)(i1 - i0);
-    fl = (fl & ~3) | (int)((p0 + i0) & 1) | ((int)((p1 + i1) & 1) << 1);
-    mfl[j] = fl;
+    xfer_add<TA>(lx[u], me[j], m0[j], mdd[j], mfl[j]);
     }
   }
   for (int j = 0; j < k; ++j) {
@@ -364,10 +384,21 @@ __global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t
       ++nwalk;
       const long long pe0 = prof ? (long long)clock64() : 0;
       const int64_t r0 = b * kFB;
-      for (int q = 0; q < kFB; q += 64) {
-        const int64_t row = r0 + q + lane;
-        const bool mine = row < n && labels[row] == j;
-        const double x = mine ? (double)X[xidx(f, row, n_pad)] : 0.0;
+      // the block's labels and values all issued first (independent loads:
+      // one memory round trip, not two per 64 rows)
+      static_assert(kFB == 256, "four rows per lane");
+      int lj[4];
+      double lx[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = r0 + 64 * q + lane;
+        lj[q] = row < n ? labels[row] : -1;
+        lx[q] = row < n ? (double)X[xidx(f, row, n_pad)] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool mine = lj[q] == j;
+        const double x = lx[q];
         unsigned long long mk = __ballot(mine);
         while (mk) {
           const int l = __builtin_amdgcn_readfirstlane(__ffsll((long long)mk) - 1);
@@ -535,14 +566,167 @@ __global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t
   }
 }
 
+// F64 mode, the assignment fused with the block pass (one workgroup per
+// block of kFB rows): labels (exact_argmin, src/kmeans_plusplus.py:33-34),
+// the block's approximate sums and exact counts in f64_blocksum's layout,
+// and (XF) the block's transfers under Eprev, the previous step's predicted
+// binades — labels change little between Lloyd steps, so they are mostly
+// right, and a wrong one only makes f64_walk re-add that block element by
+// element (exact either way).  The rows are staged in LDS; thread (j, f)
+// walks its sequence's members in row order.  D <= 16, k <= 64.
+template <int D, bool XF>
+__global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict__ X, int64_t n,
+                                                        int64_t n_pad,
+                                                        const double* __restrict__ C, int k,
+                                                        int32_t* __restrict__ labels,
+                                                        double* __restrict__ A,
+                                                        unsigned* __restrict__ cnt,
+                                                        const int* __restrict__ Eprev,
+                                                        Xfer* __restrict__ T) {
+  __shared__ double tab[kFMaxK * D];
+  __shared__ unsigned cc[kFMaxK];
+  __shared__ double sx[XF ? D * kFB : 1];
+  __shared__ int sj[XF ? kFB : 1];
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  for (int i = threadIdx.x; i < k * D; i += kFB) tab[i] = 0.0;
+  if (threadIdx.x < kFMaxK) cc[threadIdx.x] = 0u;
+  const int64_t row = b * kFB + threadIdx.x;
+  double xr[D];
+  int j = -1;
+  if (row < n) {
+#pragma unroll
+    for (int f = 0; f < D; ++f) xr[f] = X[xidx(f, row, n_pad)];
+    j = exact_argmin([&](int f) { return xr[f]; }, C, k, D);
+    labels[row] = j;
+  }
+  if constexpr (XF) {
+    sj[threadIdx.x] = j;
+#pragma unroll
+    for (int f = 0; f < D; ++f) sx[f * kFB + threadIdx.x] = j >= 0 ? xr[f] : 0.0;
+  }
+  __syncthreads();
+  if (j >= 0) {
+    atomicAdd(&cc[j], 1u);
+#pragma unroll
+    for (int f = 0; f < D; ++f) atomicAdd(&tab[j * D + f], xr[f]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k * D; i += kFB) A[(int64_t)i * nb + b] = tab[i];
+  for (int i = threadIdx.x; i < k; i += kFB) cnt[(int64_t)i * nb + b] = cc[i];
+  if constexpr (XF) {
+    for (int pr = threadIdx.x; pr < k * D; pr += kFB) {
+      const int jj = pr / D, f = pr - jj * D;
+      const int e = Eprev[(int64_t)pr * nb + b];
+      long long m0 = 0;
+      int mdd = 0, mfl = 2;  // P0 = 0, P1 = 1
+      if (cc[jj]) {
+        for (int r = 0; r < kFB; ++r)
+          if (sj[r] == jj) xfer_add<double>(sx[f * kFB + r], e, m0, mdd, mfl);
+      }
+      T[(int64_t)pr * nb + b] = Xfer{m0, mdd, mfl};
+    }
+  }
+}
+
+// The transfers with one workgroup per block (f64_transfer's results): the
+// block's rows and labels are staged in LDS with coalesced loads, then thread
+// (j, f) walks its sequence's members in row order with its state in
+// registers.  (f64_transfer, one thread per (block, feature) with k states
+// in LDS each, ran at low occupancy: 0.24 ms at 10M x 5, k = 16.)
+template <typename TA, typename S>
+__global__ __launch_bounds__(kFB) void f64_transfer_block(const S* __restrict__ X, int64_t n,
+                                                          int64_t n_pad, int d, int k,
+                                                          const int32_t* __restrict__ labels,
+                                                          const unsigned* __restrict__ cnt,
+                                                          const int* __restrict__ E,
+                                                          Xfer* __restrict__ T) {
+  // [d][kFB] values, then int order[kFB], off[65], wcnt[4][64]
+  extern __shared__ double tsx[];
+  int* order = reinterpret_cast<int*>(tsx + (size_t)d * kFB);
+  int* off = order + kFB;
+  int* wcnt = off + 65;
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t row = b * kFB + t;
+  const bool in = row < n;
+  const int lj = in ? labels[row] : -1;
+  for (int f = 0; f < d; ++f) tsx[f * kFB + t] = in ? (double)X[xidx(f, row, n_pad)] : 0.0;
+  wcnt[t] = 0;  // (4 x 64 = kFB)
+  if (t < k) off[t + 1] = (int)cnt[(int64_t)t * nb + b];
+  __syncthreads();
+  // the rows of each cluster in row order: a row's rank among its wave's
+  // rows of the same cluster (one ballot per cluster present), plus the
+  // earlier waves' counts of that cluster, plus the cluster's offset
+  int rank = 0;
+  {
+    unsigned long long todo = __ballot(lj >= 0);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    while (todo) {
+      const int l0 = __builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
+      const int lab = __builtin_amdgcn_readlane(lj, l0);
+      const unsigned long long m = __ballot(lj == lab);
+      if (lj == lab) rank = __popcll(m & below);
+      if (lane == 0) wcnt[w * 64 + lab] = __popcll(m);
+      todo &= ~m;
+    }
+  }
+  if (t == 0) {
+    off[0] = 0;
+    for (int j = 1; j <= k; ++j) off[j] += off[j - 1];
+  }
+  __syncthreads();
+  if (lj >= 0) {
+    int base = off[lj];
+    for (int ww = 0; ww < w; ++ww) base += wcnt[ww * 64 + lj];
+    order[base + rank] = t;
+  }
+  __syncthreads();
+  for (int pr = t; pr < k * d; pr += kFB) {
+    const int jj = pr / d, f = pr - jj * d;
+    long long m0 = 0;
+    int mdd = 0, mfl = 2;  // P0 = 0, P1 = 1
+    const int o0 = off[jj], o1 = off[jj + 1];
+    if (o1 > o0) {
+      const int e = E[(int64_t)pr * nb + b];
+      for (int o = o0; o < o1; ++o) xfer_add<TA>(tsx[f * kFB + order[o]], e, m0, mdd, mfl);
+    }
+    T[(int64_t)pr * nb + b] = Xfer{m0, mdd, mfl};
+  }
+}
+
+// counts[j] += the sum over a slice of blocks of cnt[j][b] (grid (k,
+// slices); counts zeroed first)
+__global__ __launch_bounds__(256) void count_total_kernel(const unsigned* __restrict__ cnt,
+                                                          int64_t nb,
+                                                          unsigned long long* __restrict__ counts) {
+  __shared__ unsigned long long red[4];
+  const int j = blockIdx.x;
+  unsigned long long s = 0;
+  for (int64_t b = (int64_t)blockIdx.y * 256 + threadIdx.x; b < nb; b += (int64_t)gridDim.y * 256)
+    s += cnt[(int64_t)j * nb + b];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long v = (red[0] + red[1]) + (red[2] + red[3]);
+    if (v) atomicAdd(&counts[j], v);
+  }
+}
+
 }  // namespace
 
 // sums (k, d) on the device, exact sequential row-order fp64 sums; returns
 // false when the shape is not covered (d < 2, k > 64): the caller runs the
 // serial kernel.
-// TA: the summed (arithmetic) type; S: the storage type of X
 template <typename TA, typename S>
-static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums) {
+static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
+                             const int* Ewalk, bool have_T);
+
+// TA: the summed (arithmetic) type; S: the storage type of X.  pre: the
+// block sums and counts (f64x_A, f64x_cnt) were already written by the
+// assignment (assign_blocksum_f64, lloyd.hip).
+template <typename TA, typename S>
+static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums, bool pre = false) {
   const int d = c.d;
   if (d < 2 || k < 1 || k > kFMaxK || c.n < 1) return false;
   const int64_t n = c.n, nb = ceil_div(n, kFB);
@@ -552,10 +736,24 @@ static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums) {
   c.f64x_E.ensure(sizeof(int) * nb * kd);
   c.f64x_T.ensure(sizeof(Xfer) * nb * kd);
   c.f64x_walk.ensure(sizeof(long long) * kd);
-  hipLaunchKernelGGL(f64_blocksum<S>, dim3(nb), dim3(kFB), sizeof(double) * kd + 4 * k, c.stream,
-                     X, n, c.n_pad, d, k, c.labels.as<int32_t>(),
-                     c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>());
-  HIP_CHECK(hipGetLastError());
+  if (!pre) {
+    hipLaunchKernelGGL(f64_blocksum<S>, dim3(nb), dim3(kFB), sizeof(double) * kd + 4 * k, c.stream,
+                       X, n, c.n_pad, d, k, c.labels.as<int32_t>(),
+                       c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>());
+    HIP_CHECK(hipGetLastError());
+  }
+  return sums_after_block<TA, S>(c, X, k, d_sums, c.f64x_E.as<int>(), c.f64x_E.as<int>(), false);
+}
+
+// After the block pass: the binade predictions into Enew; the transfers under
+// Enew unless have_T (already formed under Ewalk by f64_assign_block); the
+// group compositions and the walk under Ewalk.
+template <typename TA, typename S>
+static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
+                             const int* Ewalk, bool have_T) {
+  const int d = c.d;
+  const int64_t n = c.n, nb = ceil_div(n, kFB);
+  const size_t kd = (size_t)k * d;
   const int64_t ng = ceil_div(nb, (int64_t)64);
   c.f64x_GS.ensure(sizeof(double) * ng * kd);
   const dim3 gwaves((unsigned)ceil_div((int64_t)kd * ng, (int64_t)4));
@@ -564,25 +762,36 @@ static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums) {
   hipLaunchKernelGGL(f64_predict_b, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
                      c.f64x_GS.as<double>(), (int)kd, ng);
   hipLaunchKernelGGL(f64_predict_c, gwaves, dim3(256), 0, c.stream, c.f64x_A.as<double>(),
-                     c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>(),
-                     c.f64x_E.as<int>());
+                     c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>(), Enew);
   HIP_CHECK(hipGetLastError());
   const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
   const size_t lds = (size_t)nt * k * (8 + 4 + 4 + 4);
-  hipLaunchKernelGGL((f64_transfer<TA, S>), dim3(ceil_div(nb * d, nt)), dim3(nt), lds, c.stream,
-                     X, n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
-                     c.f64x_E.as<int>(), c.f64x_T.as<Xfer>());
-  HIP_CHECK(hipGetLastError());
+  // (CDR_F64_TBLOCK=1: the one-workgroup-per-block transfer; measured slower
+  // at 10M x 5, k = 16: 0.25-0.30 ms against f64_transfer's 0.24 ms)
+  static const bool tb_env = std::getenv("CDR_F64_TBLOCK") && std::atoi(std::getenv("CDR_F64_TBLOCK"));
+  if (!have_T && tb_env && d <= 32) {
+    hipLaunchKernelGGL((f64_transfer_block<TA, S>), dim3((unsigned)nb), dim3(kFB),
+                       sizeof(double) * d * kFB + sizeof(int) * (2 * kFB + 65), c.stream, X, n,
+                       c.n_pad, d, k,
+                       c.labels.as<int32_t>(), c.f64x_cnt.as<unsigned>(), Ewalk,
+                       c.f64x_T.as<Xfer>());
+    HIP_CHECK(hipGetLastError());
+  } else if (!have_T) {
+    hipLaunchKernelGGL((f64_transfer<TA, S>), dim3(ceil_div(nb * d, nt)), dim3(nt), lds, c.stream,
+                       X, n, c.n_pad, d, k, nb, c.labels.as<int32_t>(), Ewalk,
+                       c.f64x_T.as<Xfer>());
+    HIP_CHECK(hipGetLastError());
+  }
   c.f64x_G.ensure(sizeof(GXfer) * ng * kd);
   static const bool prof_on = std::getenv("CDR_F64_PROF") != nullptr;
   if (prof_on) c.f64x_prof.ensure(sizeof(long long) * 4 * kd);
   hipLaunchKernelGGL(f64_group, dim3(ceil_div((int64_t)kd * ng, (int64_t)4)), dim3(256), 0,
-                     c.stream, c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(),
+                     c.stream, c.f64x_cnt.as<unsigned>(), Ewalk,
                      c.f64x_T.as<Xfer>(), nb, d, k, ng, c.f64x_G.as<GXfer>());
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL((f64_walk<TA, S>), dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
                      X, n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
-                     c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(),
+                     c.f64x_cnt.as<unsigned>(), Ewalk, c.f64x_T.as<Xfer>(),
                      c.f64x_G.as<GXfer>(), ng, d_sums, c.f64x_walk.as<long long>(),
                      prof_on ? c.f64x_prof.as<long long>() : nullptr);
   HIP_CHECK(hipGetLastError());
@@ -601,8 +810,91 @@ static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums) {
   return true;
 }
 
-bool f64_sums_parallel(Ctx& c, int k, double* d_sums) {
-  return sums_parallel<double, double>(c, c.x64.as<double>(), k, d_sums);
+bool f64_sums_parallel(Ctx& c, int k, double* d_sums, bool pre) {
+  return sums_parallel<double, double>(c, c.x64.as<double>(), k, d_sums, pre);
+}
+// The F64 step's assignment and sums as one pipeline: f64_assign_block
+// (labels, block sums, counts and — when the previous step left binade
+// predictions for this (k, n) — the transfers), the cluster counts, the new
+// predictions, the transfers otherwise, groups and walk.  false: shape not
+// covered (d > 16, d < 2, k > 64), nothing launched.
+bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
+                    unsigned long long* d_counts, bool prof) {
+  const int d = c.d;
+  if (d < 2 || d > 16 || k < 1 || k > kFMaxK || c.n < 1) return false;
+  const int64_t n = c.n, nb = ceil_div(n, kFB);
+  const size_t kd = (size_t)k * d;
+  c.f64x_A.ensure(sizeof(double) * nb * kd);
+  c.f64x_cnt.ensure(sizeof(unsigned) * nb * k);
+  c.f64x_E.ensure(sizeof(int) * nb * kd);
+  c.f64x_E2.ensure(sizeof(int) * nb * kd);
+  c.f64x_T.ensure(sizeof(Xfer) * nb * kd);
+  c.f64x_walk.ensure(sizeof(long long) * kd);
+  // transfers under the previous step's predictions (CDR_F64_CARRY=1): right
+  // only near convergence — between early steps 8-25 % of the blocks' binades
+  // move and every such block is re-added element by element — so off by default
+  static const bool carry = std::getenv("CDR_F64_CARRY") && std::atoi(std::getenv("CDR_F64_CARRY"));
+  const bool xf = carry && c.f64x_e_ok && c.f64x_e_k == k && c.f64x_e_nb == nb;
+  int* Ecur = (c.f64x_e_cur ? c.f64x_E2 : c.f64x_E).as<int>();
+  int* Eoth = (c.f64x_e_cur ? c.f64x_E : c.f64x_E2).as<int>();
+  typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
+                     unsigned*, const int*, Xfer*);
+#define CDR_FAB(D_) f64_assign_block<D_, false>, f64_assign_block<D_, true>
+  static const Fn fns[17][2] = {{nullptr, nullptr}, {CDR_FAB(1)},  {CDR_FAB(2)},  {CDR_FAB(3)},
+                                {CDR_FAB(4)},       {CDR_FAB(5)},  {CDR_FAB(6)},  {CDR_FAB(7)},
+                                {CDR_FAB(8)},       {CDR_FAB(9)},  {CDR_FAB(10)}, {CDR_FAB(11)},
+                                {CDR_FAB(12)},      {CDR_FAB(13)}, {CDR_FAB(14)}, {CDR_FAB(15)},
+                                {CDR_FAB(16)}};
+#undef CDR_FAB
+  hipLaunchKernelGGL(fns[d][xf ? 1 : 0], dim3((unsigned)nb), dim3(kFB), 0, c.stream,
+                     c.x64.as<double>(), n, c.n_pad, dC, k, c.labels.as<int32_t>(),
+                     c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), Ecur, c.f64x_T.as<Xfer>());
+  HIP_CHECK(hipGetLastError());
+  if (prof) prof_mark(c, 1);
+  HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(unsigned long long) * k, c.stream));
+  hipLaunchKernelGGL(count_total_kernel,
+                     dim3(k, (unsigned)std::min<int64_t>(64, ceil_div(nb, (int64_t)256))),
+                     dim3(256), 0, c.stream, c.f64x_cnt.as<unsigned>(), nb, d_counts);
+  HIP_CHECK(hipGetLastError());
+  // with transfers formed under Ecur: predict into the other buffer, walk
+  // under Ecur; else predict into Ecur and form the transfers under it
+  int* Enew = xf ? Eoth : Ecur;
+  sums_after_block<double, double>(c, c.x64.as<double>(), k, d_sums, Enew, xf ? Ecur : Enew, xf);
+  static const bool xcheck = std::getenv("CDR_F64_XCHECK") != nullptr;
+  if (xcheck && xf) {  // (diagnostics) the fused transfers vs f64_transfer under the same E
+    DevBuf t2;
+    t2.ensure(sizeof(Xfer) * nb * kd);
+    const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
+    hipLaunchKernelGGL((f64_transfer<double, double>), dim3(ceil_div(nb * d, nt)), dim3(nt),
+                       (size_t)nt * k * 20, c.stream, c.x64.as<double>(), n, c.n_pad, d, k, nb,
+                       c.labels.as<int32_t>(), Ecur, t2.as<Xfer>());
+    std::vector<Xfer> a(nb * kd), b(nb * kd);
+    std::vector<int> e0(nb * kd), e1(nb * kd);
+    HIP_CHECK(hipMemcpyAsync(a.data(), c.f64x_T.p, sizeof(Xfer) * a.size(), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(b.data(), t2.p, sizeof(Xfer) * b.size(), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(e0.data(), Ecur, sizeof(int) * e0.size(), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(e1.data(), Enew, sizeof(int) * e1.size(), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    size_t bad = 0, ediff = 0, inval = 0;
+    for (size_t i = 0; i < a.size(); ++i) {
+      if (a[i].d0 != b[i].d0 || a[i].dd != b[i].dd || a[i].flags != b[i].flags) {
+        if (bad < 4)
+          fprintf(stderr, "xcheck T[%zu]: fused (%lld,%d,%d) ref (%lld,%d,%d)\n", i, a[i].d0,
+                  a[i].dd, a[i].flags, b[i].d0, b[i].dd, b[i].flags);
+        ++bad;
+      }
+      ediff += e0[i] != e1[i];
+      inval += (b[i].flags & 4) != 0;
+    }
+    fprintf(stderr, "xcheck: %zu of %zu transfers differ; E prev vs new differ %zu; ref invalid %zu\n",
+            bad, a.size(), ediff, inval);
+    t2.release();
+  }
+  if (xf) c.f64x_e_cur ^= 1;  // the new predictions are the next step's
+  c.f64x_e_ok = true;
+  c.f64x_e_k = k;
+  c.f64x_e_nb = nb;
+  return true;
 }
 // The reference's float32 runs: sequential fp32 sums of fp32 points (X:
 // F32X storage, or F64 storage holding fp32 values), returned as doubles.

@@ -599,25 +599,6 @@ __global__ __launch_bounds__(256) void reduce_partials(const long long* __restri
 // Exact NumPy-order argmin over k centroids (row-major fp64 C).  sqrt is only
 // evaluated when the squared distance drops, which keeps first-index ties of
 // the *square roots* exactly as np.argmin(np.linalg.norm(...)) sees them.
-template <typename XF>
-__device__ __forceinline__ int exact_argmin(XF xv, const double* __restrict__ C, int k,
-                                            int d) {
-  double Rb = INFINITY, rb = INFINITY;
-  int jb = 0;
-  for (int j = 0; j < k; ++j) {
-    const double* cj = C + (size_t)j * d;
-    const double R = np_sqdist(xv, [&](int f) { return cj[f]; }, d);
-    if (R < Rb) {
-      const double r = sqrt(R);
-      if (r < rb) {
-        rb = r;
-        Rb = R;
-        jb = j;
-      }
-    }
-  }
-  return jb;
-}
 
 // Wave-wide minimum, result in every lane: row_ror 8/4/2/1 inside each row of
 // 16 lanes (DPP), then the permlane16 / permlane32 swaps across rows.
@@ -1326,15 +1307,41 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
   const int cus = lloyd_num_cus(c.device);
   upload_centroids(c, C, k);
   const bool prof = prof_step_begin(c);
+  c.f64_sums.ensure(sizeof(double) * (size_t)k * d);
+  c.f64_counts.ensure(sizeof(long long) * k * 2);
+  long long* cnt_pre = c.f64_counts.as<long long>() + k;
+  // the fused pipeline (f64sum.hip: assignment + block pass, transfers from
+  // the previous step's binade predictions; CDR_F64_FUSE=0: separate passes)
+  static const bool fuse_env = !getenv("CDR_F64_FUSE") || atoi(getenv("CDR_F64_FUSE"));
+  if (fuse_env && !getenv("CDR_F64_SERIAL")) {
+    snprintf(c.prof_kernel, sizeof(c.prof_kernel), "f64_assign_block<%d>", d);
+    if (prof) prof_mark(c, 0);
+    if (f64_step_fused(c, k, c.cent64.as<double>(), c.f64_sums.as<double>(),
+                       reinterpret_cast<unsigned long long*>(c.f64_counts.as<long long>()),
+                       prof)) {
+      if (prof) prof_mark(c, 2);
+      std::vector<long long> w((size_t)k * d);
+      HIP_CHECK(hipMemcpyAsync(w.data(), c.f64x_walk.p, sizeof(long long) * w.size(),
+                               hipMemcpyDeviceToHost, c.stream));
+      HIP_CHECK(hipMemcpyAsync(sums, c.f64_sums.p, sizeof(double) * (size_t)k * d,
+                               hipMemcpyDeviceToHost, c.stream));
+      HIP_CHECK(hipMemcpyAsync(counts, c.f64_counts.p, sizeof(long long) * k,
+                               hipMemcpyDeviceToHost, c.stream));
+      HIP_CHECK(hipStreamSynchronize(c.stream));
+      c.f64x_walked = 0;
+      for (long long v : w) c.f64x_walked += v;
+      c.last_k = k;
+      c.have_labels = true;
+      c.last_fallback = c.n;
+      return;
+    }
+  }
   snprintf(c.prof_kernel, sizeof(c.prof_kernel),
            d <= 16 ? "assign_exact_d<double, %d>" : "assign_exact_all<double>", d);
   if (prof) prof_mark(c, 0);
   launch_assign_exact<double>(c.x64.as<double>(), c.n, c.n_pad, d, c.cent64.as<double>(), k,
                               c.labels.as<int32_t>(), cus, c.stream);
   if (prof) prof_mark(c, 1);
-  c.f64_sums.ensure(sizeof(double) * (size_t)k * d);
-  c.f64_counts.ensure(sizeof(long long) * k * 2);
-  long long* cnt_pre = c.f64_counts.as<long long>() + k;
   HIP_CHECK(hipMemsetAsync(cnt_pre, 0, sizeof(long long) * k, c.stream));
   hipLaunchKernelGGL(count_labels, dim3(std::max(1, (int)std::min<int64_t>(ceil_div(c.n, 256), cus * 2))),
                      dim3(256), k <= kCountLds ? sizeof(unsigned) * 4 * k : 0, c.stream,
