@@ -443,6 +443,10 @@ def kernel_bytes(kname: str, n_local: int, prof: dict, steps: int) -> int:
     bounded screen32b the 4-byte bound word of every point, plus, for each
     point whose bound failed (profile counter, per step), its hi row and its
     new bound word."""
+    if kname.startswith("screen32bs<"):  # the fp32 row (16 Q bytes) of each re-read point
+        q = int(kname[len("screen32bs<"):].split(",")[0])
+        tight = prof.get("tight_points", 0) / max(steps, 1)
+        return int(n_local * 4 + tight * (16 * q + 4))
     if kname.startswith("screen32b"):
         row = 32 if kname.startswith(("screen32b<3", "screen32b<4")) else 16
         tight = prof.get("tight_points", 0) / max(steps, 1)
