@@ -1769,6 +1769,12 @@ __global__ __launch_bounds__(256, 5) void screen32p(S32PArgs a) {
 // fused fixup finishes the step, so labels and int64 running sums are those
 // of the full screen.
 // ---------------------------------------------------------------------------
+#ifndef CDR_S32BS_DEPTH
+#define CDR_S32BS_DEPTH 2  // gathered batches in flight in screen32bs's phase 2 (experiments: 3)
+#endif
+#ifndef CDR_S32BS_LAZY
+#define CDR_S32BS_LAZY 1  // screen32bs: phase 2 interleaved with the stream (0: in bursts)
+#endif
 constexpr int kBChunk = 256;  // points per wave-chunk of the bound stream (4 per lane)
 constexpr int kBList = 512;   // per-wave LDS list of the points whose bound failed
 constexpr int kBPD = 4;       // chunks in flight per wave (phase 1)
@@ -2501,6 +2507,18 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #endif
     // the next batch's rows load while one is decided (past the end: the
     // last batch again, not decided); the copy waits for them after it
+#if CDR_S32BS_DEPTH >= 3
+    GB cur, nxt, nx2;
+    gload(cur, 0, cnt);
+    gload(nxt, nb > 1 ? 1 : 0, cnt);
+#pragma nounroll
+    for (int b = 0; b < nb; ++b) {
+      gload(nx2, b + 2 < nb ? b + 2 : nb - 1, cnt);
+      decide(cur);
+      cur = nxt;
+      nxt = nx2;
+    }
+#else
     GB cur, nxt;
     gload(cur, 0, cnt);
 #pragma nounroll
@@ -2509,6 +2527,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       decide(cur);
       cur = nxt;
     }
+#endif
     const int done = nb * 64;
     const int rem = last ? 0 : cnt - done;
     if (rem > 0) {
@@ -2518,6 +2537,57 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     }
     cnt = rem;
   };
+
+#if CDR_S32BS_LAZY
+  // Phase 2 interleaved with the stream: after every kBPD chunks the batch
+  // whose rows were gathered one group of chunks earlier is decided and the
+  // next 64 listed points' rows are gathered, so a batch's gather latency
+  // hides behind the stream instead of stalling the wave.  Only when the
+  // list would overflow (steps where most bounds fail) are batches decided
+  // back to back.
+  GB cur;
+  bool pend = false;
+  int head = 0;  // listed entries before head are gathered (wave-uniform)
+  auto step2 = [&](int& cnt, bool last) __attribute__((always_inline)) {
+    constexpr int kRoom = kBPD * kBChunk;
+    for (;;) {
+      if (pend) {
+        decide(cur);
+        pend = false;
+      }
+      const int avail = cnt - head;
+      if (avail >= 64 || (last && avail > 0)) {
+        const int e = head + lane;
+        cur.valid = e < cnt;
+        const unsigned ent = fl[cur.valid ? e : head];
+        const int64_t ci = wave + (int64_t)(ent >> 14) * nwaves;
+        const int64_t pt = ci * kBChunk + ((ent >> 6) & 255);
+        cur.pt = (int)pt;
+        cur.ao = (int)(ent & 63);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) cur.x[q] = __builtin_nontemporal_load(XA4 + pt * Q + q);
+        const int take = avail < 64 ? avail : 64;
+        head += take;
+        ttot += take;
+        pend = true;
+      }
+      if (head > 0 && !last && cnt + kRoom > kSList) {  // compact [head, cnt) to the front
+        const int m = cnt - head;
+        for (int o = 0; o < m; o += 64) {  // (writes stay below the reads still to come)
+          const int e2 = o + lane;
+          const unsigned v = e2 < m ? fl[head + e2] : 0u;
+          __builtin_amdgcn_wave_barrier();
+          if (e2 < m) fl[e2] = v;
+          __builtin_amdgcn_wave_barrier();
+        }
+        cnt = m;
+        head = 0;
+      }
+      const bool again = last ? (pend || cnt > head) : (cnt - head + kRoom > kSList);
+      if (!again) break;
+    }
+  };
+#endif
 
   // ---- phase 1: the bound words, 4 points per lane per chunk ----
   int cnt = 0;
@@ -2553,7 +2623,11 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       }
     }
     }
+#if CDR_S32BS_LAZY
+    step2(cnt, !more);
+#else
     if (!more || cnt > kSList - kBPD * kBChunk) phase2(cnt, !more);
+#endif
     if (!more) break;
   }
   // ---- the uncertified points: the same split screen again (the same values),
