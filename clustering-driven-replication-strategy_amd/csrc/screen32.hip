@@ -1789,6 +1789,11 @@ struct S32BArgs {
   long long* t_acc;          // profiling: points whose bound failed, per wave (null: off)
   int dbg;                   // tests only (CDR_BOUNDS_DBG): 1 = every bound fails
   unsigned long long* tprof; // experiments build only: per-wave timestamps (null: off)
+  // screen32bs: chunk shares per CU slot (the workgroups blockIdx / slot_wg
+  // = s share chunks [R_s, R_s+1) in proportion wsl[s]); slot_wg 0: one
+  // strided split over all waves
+  int slot_wg;
+  int wsl[4];
 };
 
 // The stored word of bounds (l0, u0) and W_a rounded down (see above):
@@ -2231,9 +2236,29 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     const int64_t cc = ci < nchunks ? ci : nchunks - 1;
     z = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(B.zb + cc * kBChunk) + lane);
   };
+  // this wave's chunks: wbase + i wstride below wend
+  int64_t wbase = wave, wend = nchunks;
+  int wstride = nwaves;
+  if (B.slot_wg > 0) {
+    // Workgroups of one CU slot (launch generation) share a region in
+    // proportion to its weight: the later generations on a CU get fewer
+    // issue slots (oldest-first) and otherwise finish last.
+    const int ns = (int)gridDim.x / B.slot_wg;
+    const int sl = (int)blockIdx.x / B.slot_wg;
+    int wsum = 0, wpre = 0;
+    for (int q = 0; q < ns; ++q) {
+      wsum += B.wsl[q];
+      if (q < sl) wpre += B.wsl[q];
+    }
+    const int64_t R0 = nchunks * wpre / wsum, R1 = nchunks * (wpre + B.wsl[sl]) / wsum;
+    wstride = B.slot_wg * 4;
+    wbase = R0 + (int64_t)((int)blockIdx.x - sl * B.slot_wg) * 4 + wv;
+    wend = R1;
+  }
+  wbase = __builtin_amdgcn_readfirstlane((int)wbase);
   u4v zc[kBPD];
 #pragma unroll
-  for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], wave + (int64_t)i * nwaves);
+  for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], wbase + (int64_t)i * wstride);
 
   // ---- the plan ----
   __shared__ h8 sA[MT * 2 * 64];
@@ -2488,7 +2513,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     const int e = 64 * b + lane;
     g.valid = e < cnt;
     const unsigned ent = fl[g.valid ? e : 64 * b];  // (entry 64 b exists)
-    const int64_t ci = wave + (int64_t)(ent >> 14) * nwaves;
+    const int64_t ci = wbase + (int64_t)(ent >> 14) * wstride;
     const int64_t pt = ci * kBChunk + ((ent >> 6) & 255);
     g.pt = (int)pt;
     g.ao = (int)(ent & 63);
@@ -2560,7 +2585,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
         const int e = head + lane;
         cur.valid = e < cnt;
         const unsigned ent = fl[cur.valid ? e : head];
-        const int64_t ci = wave + (int64_t)(ent >> 14) * nwaves;
+        const int64_t ci = wbase + (int64_t)(ent >> 14) * wstride;
         const int64_t pt = ci * kBChunk + ((ent >> 6) & 255);
         cur.pt = (int)pt;
         cur.ao = (int)(ent & 63);
@@ -2592,14 +2617,14 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   // ---- phase 1: the bound words, 4 points per lane per chunk ----
   int cnt = 0;
   int64_t it = 0;
-  for (int64_t C0 = wave;; C0 += (int64_t)kBPD * nwaves) {
-    const bool more = C0 < nchunks;  // (wave-uniform)
+  for (int64_t C0 = wbase;; C0 += (int64_t)kBPD * wstride) {
+    const bool more = C0 < wend;  // (wave-uniform)
     if (more) {
 #pragma unroll
     for (int i = 0; i < kBPD; ++i, ++it) {
-      const int64_t Ci = C0 + (int64_t)i * nwaves;
-      if (Ci >= nchunks) break;
-      zload(zc[(i + kBPD - 1) % kBPD], Ci + (int64_t)(kBPD - 1) * nwaves);
+      const int64_t Ci = C0 + (int64_t)i * wstride;
+      if (Ci >= wend) break;
+      zload(zc[(i + kBPD - 1) % kBPD], Ci + (int64_t)(kBPD - 1) * wstride);
       const u4v z = zc[i];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -3364,6 +3389,28 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
 #endif
       c.zb_valid = true;
       b.tprof = nullptr;
+      b.slot_wg = 0;
+      // chunk shares of screen32bs's 4 launch generations (workgroups per CU):
+      // one region per generation, equal by default (A/B at 100M: 180 -> 166
+      // us against one strided split; speed-proportional weights 100,82,68,61
+      // 166 us); CDR_S32BS_W="w0,w1,w2,w3" sets them, CDR_S32BS_W=0 the split
+      if (BS) {
+        static int wenv[4] = {-1, 0, 0, 0};
+        if (wenv[0] < 0) {
+          for (int q = 0; q < 4; ++q) wenv[q] = 100;
+          if (const char* e = std::getenv("CDR_S32BS_W")) {
+            wenv[0] = 0;
+            int v[4] = {0, 0, 0, 0};
+            if (std::sscanf(e, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 &&
+                v[1] > 0 && v[2] > 0 && v[3] > 0)
+              for (int q = 0; q < 4; ++q) wenv[q] = v[q];
+          }
+        }
+        if (wenv[0] > 0 && nwg == cus * bpc && bpc == 4) {
+          b.slot_wg = cus;
+          for (int q = 0; q < 4; ++q) b.wsl[q] = wenv[q];
+        }
+      }
 #ifdef CDR_EXPERIMENTS
       static unsigned long long* tprof_buf = nullptr;
       const bool tprof_on = BS && std::getenv("CDR_S32BS_TPROF");
