@@ -153,6 +153,7 @@ struct Ctx {
   // f64_step_fused: the binade predictions of the last F64 step (two buffers:
   // the one the current transfers use, the next step's), valid for (k, blocks)
   DevBuf f64x_E2;
+  DevBuf f64x_ord;  // f64_step_fused: each block's rows in cluster order (uint8 offsets)
   bool f64x_e_ok = false;
   int f64x_e_cur = 0, f64x_e_k = 0;
   int64_t f64x_e_nb = 0;

@@ -582,9 +582,12 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
                                                         double* __restrict__ A,
                                                         unsigned* __restrict__ cnt,
                                                         const int* __restrict__ Eprev,
-                                                        Xfer* __restrict__ T) {
+                                                        Xfer* __restrict__ T,
+                                                        unsigned char* __restrict__ ordr) {
   __shared__ double tab[kFMaxK * D];
   __shared__ unsigned cc[kFMaxK];
+  __shared__ int coff[kFMaxK];
+  __shared__ int wcnt[kFB / 64][kFMaxK];
   __shared__ double sx[XF ? D * kFB : 1];
   __shared__ int sj[XF ? kFB : 1];
   const int64_t b = blockIdx.x, nb = gridDim.x;
@@ -610,9 +613,43 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
 #pragma unroll
     for (int f = 0; f < D; ++f) atomicAdd(&tab[j * D + f], xr[f]);
   }
+  // the block's rows in cluster order, row order inside a cluster (ordr: the
+  // transfer pass walks each (cluster, feature) sequence through it): a
+  // row's rank among its wave's rows of its cluster (one ballot per cluster
+  // present), the earlier waves' counts, the cluster's offset
+  int rank = 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (ordr) {
+    for (int i = lane; i < kFMaxK; i += 64) wcnt[w][i] = 0;
+    unsigned long long todo = __ballot(j >= 0);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    while (todo) {
+      const int l0 = __builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
+      const int lab = __builtin_amdgcn_readlane(j, l0);
+      const unsigned long long m = __ballot(j == lab);
+      if (j == lab) rank = __popcll(m & below);
+      if (lane == 0) wcnt[w][lab] = __popcll(m);
+      todo &= ~m;
+    }
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < k * D; i += kFB) A[(int64_t)i * nb + b] = tab[i];
   for (int i = threadIdx.x; i < k; i += kFB) cnt[(int64_t)i * nb + b] = cc[i];
+  if (ordr) {
+    if (threadIdx.x == 0) {
+      int o = 0;
+      for (int q = 0; q < k; ++q) {
+        coff[q] = o;
+        o += (int)cc[q];
+      }
+    }
+    __syncthreads();
+    if (j >= 0) {
+      int pos = coff[j] + rank;
+      for (int ww = 0; ww < w; ++ww) pos += wcnt[ww][j];
+      ordr[b * kFB + pos] = (unsigned char)threadIdx.x;
+    }
+  }
   if constexpr (XF) {
     for (int pr = threadIdx.x; pr < k * D; pr += kFB) {
       const int jj = pr / D, f = pr - jj * D;
@@ -694,6 +731,65 @@ __global__ __launch_bounds__(kFB) void f64_transfer_block(const S* __restrict__ 
   }
 }
 
+// The transfers from the rows in cluster order (ordr, written by
+// f64_assign_block): one thread per (block, feature) as f64_transfer, but a
+// cluster's members are consecutive, so the running state lives in registers
+// and is written out at the end of each run (f64_transfer keeps k states per
+// thread in LDS, which capped it at 1-2 waves per SIMD: 0.24 ms at 10M x 5,
+// k = 16).  Rows are read 16 at a time (one 16-byte load of their offsets,
+// then the 16 values together).
+template <typename TA, typename S>
+__global__ __launch_bounds__(256) void f64_transfer_sorted(const S* __restrict__ X, int64_t n,
+                                                           int64_t n_pad, int d, int k, int64_t nb,
+                                                           const unsigned* __restrict__ cnt,
+                                                           const int* __restrict__ E,
+                                                           const unsigned char* __restrict__ ordr,
+                                                           Xfer* __restrict__ T) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb * d) return;
+  const int64_t b = t / d;
+  const int f = (int)(t % d);
+  const int64_t r0 = b * kFB;
+  const int nrow = (int)((n - r0) < kFB ? (n - r0) : kFB);
+  // the first non-empty cluster and its run
+  int jj = -1, left = 0;
+  auto next_run = [&]() {
+    while (left == 0 && jj + 1 < k) {
+      ++jj;
+      left = (int)cnt[(int64_t)jj * nb + b];
+      if (left == 0) T[((int64_t)jj * d + f) * nb + b] = Xfer{0, 0, 2};
+    }
+  };
+  next_run();
+  long long m0 = 0;
+  int mdd = 0, mfl = 2;  // P0 = 0, P1 = 1
+  int e = left ? E[((int64_t)jj * d + f) * nb + b] : kENone;
+  const uint4* ob = reinterpret_cast<const uint4*>(ordr + r0);
+  for (int c0 = 0; c0 < nrow; c0 += 16) {
+    const uint4 oq = ob[c0 >> 4];
+    double xv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const unsigned word = u < 4 ? oq.x : u < 8 ? oq.y : u < 12 ? oq.z : oq.w;
+      const int r = (int)((word >> (8 * (u & 3))) & 255u);
+      xv[u] = c0 + u < nrow ? (double)X[xidx(f, r0 + r, n_pad)] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (c0 + u >= nrow || left == 0) break;
+      xfer_add<TA>(xv[u], e, m0, mdd, mfl);
+      if (--left == 0) {  // the run ends: its transfer, then the next run's state
+        T[((int64_t)jj * d + f) * nb + b] = Xfer{m0, mdd, mfl};
+        m0 = 0;
+        mdd = 0;
+        mfl = 2;
+        next_run();
+        if (left) e = E[((int64_t)jj * d + f) * nb + b];
+      }
+    }
+  }
+}
+
 // counts[j] += the sum over a slice of blocks of cnt[j][b] (grid (k,
 // slices); counts zeroed first)
 __global__ __launch_bounds__(256) void count_total_kernel(const unsigned* __restrict__ cnt,
@@ -720,7 +816,7 @@ __global__ __launch_bounds__(256) void count_total_kernel(const unsigned* __rest
 // serial kernel.
 template <typename TA, typename S>
 static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
-                             const int* Ewalk, bool have_T);
+                             const int* Ewalk, bool have_T, const unsigned char* ordr = nullptr);
 
 // TA: the summed (arithmetic) type; S: the storage type of X.  pre: the
 // block sums and counts (f64x_A, f64x_cnt) were already written by the
@@ -750,7 +846,7 @@ static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums, bool pre = 
 // group compositions and the walk under Ewalk.
 template <typename TA, typename S>
 static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
-                             const int* Ewalk, bool have_T) {
+                             const int* Ewalk, bool have_T, const unsigned char* ordr) {
   const int d = c.d;
   const int64_t n = c.n, nb = ceil_div(n, kFB);
   const size_t kd = (size_t)k * d;
@@ -769,7 +865,12 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
   // (CDR_F64_TBLOCK=1: the one-workgroup-per-block transfer; measured slower
   // at 10M x 5, k = 16: 0.25-0.30 ms against f64_transfer's 0.24 ms)
   static const bool tb_env = std::getenv("CDR_F64_TBLOCK") && std::atoi(std::getenv("CDR_F64_TBLOCK"));
-  if (!have_T && tb_env && d <= 32) {
+  if (!have_T && ordr) {
+    hipLaunchKernelGGL((f64_transfer_sorted<TA, S>), dim3((unsigned)ceil_div(nb * d, (int64_t)256)),
+                       dim3(256), 0, c.stream, X, n, c.n_pad, d, k, nb, c.f64x_cnt.as<unsigned>(),
+                       Ewalk, ordr, c.f64x_T.as<Xfer>());
+    HIP_CHECK(hipGetLastError());
+  } else if (!have_T && tb_env && d <= 32) {
     hipLaunchKernelGGL((f64_transfer_block<TA, S>), dim3((unsigned)nb), dim3(kFB),
                        sizeof(double) * d * kFB + sizeof(int) * (2 * kFB + 65), c.stream, X, n,
                        c.n_pad, d, k,
@@ -837,8 +938,17 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   const bool xf = carry && c.f64x_e_ok && c.f64x_e_k == k && c.f64x_e_nb == nb;
   int* Ecur = (c.f64x_e_cur ? c.f64x_E2 : c.f64x_E).as<int>();
   int* Eoth = (c.f64x_e_cur ? c.f64x_E : c.f64x_E2).as<int>();
+  // the rows in cluster order per block and f64_transfer_sorted (CDR_F64_SORTED=1;
+  // measured slower at 10M x 5, k = 16: 0.43 ms against f64_transfer's 0.24 ms,
+  // the order itself +0.04 ms in the assignment)
+  static const bool sorted_env = std::getenv("CDR_F64_SORTED") && std::atoi(std::getenv("CDR_F64_SORTED"));
+  unsigned char* ordr = nullptr;
+  if (sorted_env && !xf) {
+    c.f64x_ord.ensure((size_t)nb * kFB);
+    ordr = c.f64x_ord.as<unsigned char>();
+  }
   typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
-                     unsigned*, const int*, Xfer*);
+                     unsigned*, const int*, Xfer*, unsigned char*);
 #define CDR_FAB(D_) f64_assign_block<D_, false>, f64_assign_block<D_, true>
   static const Fn fns[17][2] = {{nullptr, nullptr}, {CDR_FAB(1)},  {CDR_FAB(2)},  {CDR_FAB(3)},
                                 {CDR_FAB(4)},       {CDR_FAB(5)},  {CDR_FAB(6)},  {CDR_FAB(7)},
@@ -848,7 +958,8 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
 #undef CDR_FAB
   hipLaunchKernelGGL(fns[d][xf ? 1 : 0], dim3((unsigned)nb), dim3(kFB), 0, c.stream,
                      c.x64.as<double>(), n, c.n_pad, dC, k, c.labels.as<int32_t>(),
-                     c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), Ecur, c.f64x_T.as<Xfer>());
+                     c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), Ecur, c.f64x_T.as<Xfer>(),
+                     ordr);
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
   HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(unsigned long long) * k, c.stream));
@@ -859,7 +970,8 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   // with transfers formed under Ecur: predict into the other buffer, walk
   // under Ecur; else predict into Ecur and form the transfers under it
   int* Enew = xf ? Eoth : Ecur;
-  sums_after_block<double, double>(c, c.x64.as<double>(), k, d_sums, Enew, xf ? Ecur : Enew, xf);
+  sums_after_block<double, double>(c, c.x64.as<double>(), k, d_sums, Enew, xf ? Ecur : Enew, xf,
+                                   ordr);
   static const bool xcheck = std::getenv("CDR_F64_XCHECK") != nullptr;
   if (xcheck && xf) {  // (diagnostics) the fused transfers vs f64_transfer under the same E
     DevBuf t2;
