@@ -86,6 +86,16 @@ def _record_start(fh, x: int, size: int) -> int:
         chunk = fh.read(1 << 16)
         if not chunk:
             return size
+        if not inq and b'"' not in chunk:
+            # no quote: every newline ends a record and only "at a field
+            # start" carries over (bytes.find, not a Python loop per byte)
+            if pos + len(chunk) >= x:
+                i = chunk.find(b"\n", max(0, x - pos - 1))
+                if i >= 0:
+                    return pos + i + 1
+            fstart = chunk[-1] in (_C, _NL, 13)
+            pos += len(chunk)
+            continue
         for i, c in enumerate(chunk):
             if inq:
                 if qpend:

@@ -231,3 +231,59 @@ def test_sharded_features_equal_single_process(tmp_path, world, quoted):
     exp_paths, exp_table, _, _ = fo.compute(man, log)
     assert [p or "" for p in exp_paths] == [p or "" for p in paths]
     np.testing.assert_array_equal(table, exp_table)
+
+
+def _record_start_bytewise(data: bytes, x: int) -> int:
+    """The csv.reader record-start scan byte by byte (the form features_dist
+    used before its quote-free fast path): the checker of test below."""
+    if x <= 0:
+        return 0
+    if x >= len(data):
+        return len(data)
+    inq = qpend = False
+    fstart = True
+    for i, c in enumerate(data):
+        if inq:
+            if qpend:
+                qpend = False
+                if c == 34:
+                    continue
+                inq = False
+            elif c == 34:
+                qpend = True
+                continue
+            else:
+                continue
+        if c == 34 and fstart:
+            inq, fstart = True, False
+        elif c == 44:
+            fstart = True
+        elif c == 10:
+            fstart = True
+            if i + 1 >= x:
+                return i + 1
+        else:
+            fstart = c == 13
+    return len(data)
+
+
+def test_record_start_fast_path_matches_bytewise(tmp_path):
+    """quote-free 64 KiB chunks skip the per-byte loop; the
+    cut points equal the byte-by-byte scan on logs with sparse and dense
+    quoting, quoted newlines, doubled quotes and CRs."""
+    import random
+
+    from features_dist import _record_start
+
+    rng = random.Random(5)
+    alphabet = [b"a", b"b", b"1", b",", b"\n", b"\r", b'"', b" "]
+    for trial in range(6):
+        weights = [30, 30, 20, 10, 6, 1, 1 if trial % 2 else 8, 4]
+        n = 200_000 if trial < 3 else 3000
+        data = b"".join(rng.choices(alphabet, weights=weights, k=n))
+        p = tmp_path / f"log{trial}.csv"
+        p.write_bytes(data)
+        with open(p, "rb") as fh:
+            for x in [0, 1, 2, 65535, 65536, 65537, n // 3, n // 2, n - 2, n - 1, n] + \
+                     [rng.randrange(n) for _ in range(20)]:
+                assert _record_start(fh, x, n) == _record_start_bytewise(data, x), (trial, x)
