@@ -100,3 +100,18 @@ def test_kmeans_2m_minmax_features_bit_exact(ctx):
     step = (time.perf_counter() - t1) / 5
     print(f"\nF64 2M x 5 k=8: kmeans {dt:.2f} s, one step {step * 1e3:.2f} ms, "
           f"walked blocks {ctx.f64_walked()}")
+
+
+@pytest.mark.parametrize("n,d,k", [(120_000, 16, 64), (80_000, 20, 10), (60_000, 6, 70),
+                                   (50_000, 2, 3), (70_001, 9, 33)])
+def test_step_shapes_fused_and_separate(ctx, monkeypatch, n, d, k):
+    """The fused assignment + block pass (d <= 16, k <= 64: f64_step_fused),
+    the separate passes (d > 16) and the serial sums (k > 64), at ragged n:
+    labels = the oracle's, sums = NumPy's sequential sums, = the serial kernel."""
+    rng = np.random.default_rng(10 + d + k)
+    X = _minmax(rng, n, d)
+    C = X[rng.choice(n, k, replace=False)].copy()
+    _check_step(ctx, X, C, monkeypatch)
+    # a second step from moved centroids (the predictions of the first are not reused)
+    C2 = C * 0.75 + 0.125
+    _check_step(ctx, X, C2, monkeypatch)
