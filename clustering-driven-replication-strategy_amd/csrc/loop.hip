@@ -292,9 +292,19 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
   long long* cnt_out = reinterpret_cast<long long*>(Cnew + (size_t)k * d);
   if (row && (t & 7) == 0) cnt_out[j] = cnt;
   // the per-wave fallback counts (the step's total: the decision sync below)
+  // (eight loads in flight per thread: a rolled loop waited for each one)
   int fbv = 0;
-  if (a.fbc)
-    for (int i = t; i < a.nwaves; i += blockDim.x) fbv += a.fbc[i];
+  if (a.fbc) {
+    int acc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = t + u * (int)blockDim.x;
+      acc[u] = i < a.nwaves ? a.fbc[i] : 0;
+    }
+    for (int i = t + 8 * (int)blockDim.x; i < a.nwaves; i += blockDim.x) acc[0] += a.fbc[i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fbv += acc[u];
+  }
   // the host's np.ldexp(acc.astype(float64), -S) / counts (kmeans_plusplus.py)
   const double sj0 = ldexp((double)S0, -a.sbits), sj1 = ldexp((double)S1, -a.sbits);
   double m0 = sj0 / (double)cnt, m1 = sj1 / (double)cnt;

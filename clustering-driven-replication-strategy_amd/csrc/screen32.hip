@@ -559,18 +559,22 @@ __global__ __launch_bounds__(256) void publish32(const long long* __restrict__ o
                                                  int* __restrict__ fbc, int nwaves,
                                                  long long* __restrict__ fb_acc,
                                                  const long long* __restrict__ gate) {
+  // (one cell per thread over as many workgroups as needed: a single
+  // workgroup looping over the cells paid one memory round trip per pass)
   if (gate && gate[0] == 0) {  // a stopped loop contributes nothing to the all-reduce
     if (dout)
-      for (int i = threadIdx.x; i < cells; i += blockDim.x) dout[i] = 0;
+      for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += gridDim.x * blockDim.x)
+        dout[i] = 0;
     return;
   }
-  for (int i = threadIdx.x; i < cells; i += blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += gridDim.x * blockDim.x) {
     long long v = 0;
+#pragma unroll
     for (int sl = 0; sl < kRunSlices; ++sl) v += out[(size_t)sl * cells + i];
     if (dout) dout[i] = v;
     if (hout) hout[i] = v;
   }
-  if (fbc) {  // (uniform)
+  if (fbc && blockIdx.x == 0) {  // (uniform)
     const int fb = block_sum_counts(fbc, nwaves);
     if (threadIdx.x == 0) {
       fbc[nwaves] = 0;
@@ -3532,7 +3536,8 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   }
   c.fb_accum.ensure(2 * sizeof(long long));
   if (dout || hout_dev || !gate) {
-    hipLaunchKernelGGL(publish32, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(),
+    hipLaunchKernelGGL(publish32, dim3((unsigned)std::max(1, (len + 255) / 256)), dim3(256), 0,
+                       c.stream, c.run_sums.as<long long>(),
                        len, dout, hout_dev, gate ? nullptr : c.fb_count.as<int32_t>(), nwaves,
                        c.prof_on ? c.fb_accum.as<long long>() : nullptr, gate);
     HIP_CHECK(hipGetLastError());
@@ -3720,7 +3725,8 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   if (dout || hout_dev || !gate) {
     // (device loop with no all-reduce buffer: ll_finalize reads the slices and
     // moves the fallback counter itself)
-    hipLaunchKernelGGL(publish32, dim3(1), dim3(256), 0, c.stream, c.run_sums.as<long long>(),
+    hipLaunchKernelGGL(publish32, dim3((unsigned)std::max(1, (len + 255) / 256)), dim3(256), 0,
+                       c.stream, c.run_sums.as<long long>(),
                        len, dout, hout_dev, gate ? nullptr : c.fb_count.as<int32_t>(), nwaves,
                        c.prof_on ? c.fb_accum.as<long long>() : nullptr, gate);
     HIP_CHECK(hipGetLastError());
