@@ -470,17 +470,24 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
   }
   const double ec = plan32_prune_ec(e2, s);
   double sm = INFINITY;  // smallest squared distance of c32_j to another c32
-  if (row && !(a.abl & 4))
+  if (row && !(a.abl & 4)) {
+    // own row in registers, four partial sums per pair (a short dependency
+    // chain; every term >= 0 and at most 6 roundings on any path, within
+    // plan32_prune_h's 2^-44 margin)
+    float cj[16];
+#pragma unroll
+    for (int f = 0; f < 16; ++f) cj[f] = c32[j * 16 + f];
     for (int jj = t & 7; jj < k; jj += 8) {
       if (jj == j) continue;
-      double s2 = 0.0;
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int f = 0; f < 16; ++f) {
-        const double df = (double)c32[j * 16 + f] - (double)c32[jj * 16 + f];
-        s2 += df * df;
+        const double df = (double)cj[f] - (double)c32[jj * 16 + f];  // exact
+        acc[f & 3] += df * df;
       }
-      sm = fmin(sm, s2);
+      sm = fmin(sm, (acc[0] + acc[1]) + (acc[2] + acc[3]));
     }
+  }
   sm = fmin(sm, __shfl_xor(sm, 1));
   sm = fmin(sm, __shfl_xor(sm, 2));
   sm = fmin(sm, __shfl_xor(sm, 4));
