@@ -39,7 +39,11 @@ Spark semantics kept (Spark 3.5, docker/docker-compose.yml:67):
     then age-row order); an empty path is null and joins nothing (age 0).
     The reference's generators never write either case: parity unpinned.
   * doubles written like Java's ``Double.toString`` (decimal in [1e-3, 1e7),
-    otherwise ``d.dddE<exp>``), longs as integers.
+    otherwise ``d.dddE<exp>``), longs as integers.  The digits are those of
+    the JDK that runs Spark: apache/spark:3.5.2 ships a pre-19 JDK, whose
+    ``FloatingDecimal`` does not always print the shortest digits
+    (``java_double_legacy``, the default).  ``CDR_JAVA_DOUBLE=19`` selects the
+    JDK 19+ shortest-digit layout (``java_double``).
 """
 from __future__ import annotations
 
@@ -48,6 +52,7 @@ import csv
 import math
 import os
 import re
+import struct
 import time
 import uuid
 from decimal import Decimal
@@ -112,7 +117,7 @@ def _days_from_civil(y: int, m: int, d: int) -> int:
 
 
 def java_double(x: float) -> str:
-    """Java ``Double.toString`` layout of the shortest round-trip digits."""
+    """``Double.toString`` of JDK 19+: the shortest round-trip digits."""
     x = float(x)
     if x != x:
         return "NaN"
@@ -148,6 +153,153 @@ def java_double(x: float) -> str:
         return f"{sign}{ip}.{fp}"
     mant = digits[0] + "." + (digits[1:] or "0")
     return f"{sign}{mant}E{exp10}"
+
+
+# ---- pre-JDK-19 Double.toString -------------------------------------------
+# Restated from the published algorithm of OpenJDK's
+# jdk.internal.math.FloatingDecimal.BinaryToASCIIBuffer (JDK 8 to 18; the JDK is
+# not part of the reference, which reaches it through Spark's CSV writer,
+# src/compute_features.py:96): Steele & White digit generation with a symmetric
+# half-ulp stopping test, a decimal-exponent estimate from a linear fit of
+# log10, a direct path for integers below 2^63 that keeps all their digits up
+# to a power-of-two-derived rounding position, and at least two digits in
+# E-notation.  Pinned by the outputs JDK bug 4511638 lists (tests/test_host_logic.py).
+
+_N5_BITS = [(5 ** i).bit_length() for i in range(27)]  # bit length of 5^i
+_POW2_DEC_DIGITS = [len(str(1 << p)) - 1 for p in range(64)]  # floor(log10(2^p))
+
+
+def _wrap(v: int, bits: int) -> int:
+    """Two's-complement wrap (the int / long arithmetic of the fast paths)."""
+    v &= (1 << bits) - 1
+    return v - (1 << bits) if v >> (bits - 1) else v
+
+
+def _legacy_digits(bin_exp: int, fract: int, n_sig: int):
+    """Digits and decimal exponent (value = 0.d1d2... x 10^exp) of
+    fract * 2^(bin_exp - 52), fract normalised to 53 bits."""
+    tail = (fract & -fract).bit_length() - 1
+    n_fract = 53 - tail  # significant bits
+    n_tiny = max(0, n_fract - bin_exp - 1)  # bits right of the binary point
+    if n_tiny == 0 and -21 <= bin_exp <= 62:
+        # an integer: all its digits, rounded (half up) at 10^i where 2^p
+        # has i + 1 digits and p = bin_exp - n_sig - 1
+        p = bin_exp - n_sig - 1
+        drop = _POW2_DEC_DIGITS[p] if bin_exp > n_sig and 1 < p < 64 else 0
+        v = fract << (bin_exp - 52) if bin_exp >= 52 else fract >> (52 - bin_exp)
+        if drop:
+            v, rem = divmod(v, 10 ** drop)
+            v += rem >= (10 ** drop) >> 1
+        txt = str(v)
+        return [int(c) for c in txt.rstrip("0")], drop + len(txt)
+    mant = struct.unpack("<d", struct.pack("<Q", 0x3FF0000000000000 | (fract & ((1 << 52) - 1))))[0]
+    dec = math.floor((mant - 1.5) * 0.289529654 + 0.176091259 + bin_exp * 0.301029995663981)
+    b5 = max(0, -dec)
+    b2 = b5 + n_tiny + bin_exp
+    s5 = max(0, dec)
+    s2 = s5 + n_tiny
+    m5, m2 = b5, b2 - n_sig
+    fract >>= tail
+    b2 -= n_fract - 1
+    common = min(b2, s2)
+    b2, s2, m2 = b2 - common, s2 - common, m2 - common
+    if n_fract == 1:  # a power of two: the gap below is half as wide
+        m2 -= 1
+    if m2 < 0:
+        b2, s2, m2 = b2 - m2, s2 - m2, 0
+    b_bits = n_fract + b2 + (_N5_BITS[b5] if b5 < 27 else 3 * b5)
+    ts_bits = s2 + 1 + (_N5_BITS[s5 + 1] if s5 + 1 < 27 else 3 * (s5 + 1))
+    digits = []
+    if b_bits < 64 and ts_bits < 64:
+        # int (both < 32 bits) or long arithmetic; m may overflow as in Java
+        w = 32 if b_bits < 32 and ts_bits < 32 else 64
+        b = _wrap((fract * 5 ** b5) << b2, w)
+        s = _wrap(5 ** s5 << s2, w)
+        m = _wrap(5 ** m5 << m2, w)
+        ts = _wrap(s * 10, w)
+        q, b, m = b // s, _wrap(10 * (b % s), w), _wrap(m * 10, w)
+        low, high = b < m, _wrap(b + m, w) > ts
+        if q == 0 and not high:
+            dec -= 1
+        else:
+            digits.append(q)
+        if dec < -3 or dec >= 8:
+            low = high = False
+        while not low and not high:
+            q, b, m = b // s, _wrap(10 * (b % s), w), _wrap(m * 10, w)
+            if m > 0:
+                low, high = b < m, _wrap(b + m, w) > ts
+            else:
+                low = high = True
+            digits.append(q)
+        tie = _wrap(_wrap(b << 1, w) - ts, w)
+    else:
+        s = 5 ** s5 << s2
+        m = 5 ** (m5 + 1) << (m2 + 1)
+        ts = 10 * s
+        q, r = divmod((fract * 5 ** b5) << b2, s)
+        b = 10 * r
+        low, high = b < m, ts <= b + m
+        if q == 0 and not high:
+            dec -= 1
+        else:
+            digits.append(q)
+        if dec < -3 or dec >= 8:
+            low = high = False
+        while not low and not high:
+            q, r = divmod(b, s)
+            b, m = 10 * r, m * 10
+            low, high = b < m, ts <= b + m
+            digits.append(q)
+        tie = (2 * b > ts) - (2 * b < ts) if high and low else 0
+    exp = dec + 1
+    if high and (not low or tie > 0 or (tie == 0 and digits[-1] & 1)):
+        i = len(digits) - 1
+        while digits[i] == 9 and i > 0:
+            digits[i] = 0
+            i -= 1
+        if digits[i] == 9:  # 9...9 -> 10...0
+            digits[0] = 1
+            exp += 1
+        else:
+            digits[i] += 1
+    return digits, exp
+
+
+def java_double_legacy(x: float) -> str:
+    """``Double.toString`` of a JDK 8-18 (the JVM of apache/spark:3.5.2,
+    docker/docker-compose.yml:67), e.g. 2e23 -> ``1.9999999999999998E23``."""
+    x = float(x)
+    if x != x:
+        return "NaN"
+    if math.isinf(x):
+        return "Infinity" if x > 0 else "-Infinity"
+    bits = struct.unpack("<Q", struct.pack("<d", x))[0]
+    sign = "-" if bits >> 63 else ""
+    fract, be = bits & ((1 << 52) - 1), (bits >> 52) & 0x7FF
+    if be == 0:
+        if fract == 0:
+            return sign + "0.0"
+        shift = 53 - fract.bit_length()
+        fract, be, n_sig = fract << shift, 1 - shift, fract.bit_length()
+    else:
+        fract, n_sig = fract | (1 << 52), 53
+    digits, exp = _legacy_digits(be - 1023, fract, n_sig)
+    d = "".join(map(str, digits))
+    if 0 < exp < 8:
+        if len(d) <= exp:
+            return f"{sign}{d.ljust(exp, '0')}.0"
+        return f"{sign}{d[:exp]}.{d[exp:]}"
+    if -3 < exp <= 0:
+        return f"{sign}0.{'0' * -exp}{d}"
+    return f"{sign}{d[0]}.{d[1:] or '0'}E{exp - 1}"
+
+
+def _double_formatter():
+    mode = os.environ.get("CDR_JAVA_DOUBLE", "legacy")
+    if mode not in ("legacy", "19"):
+        raise ValueError(f"CDR_JAVA_DOUBLE={mode!r}: expected 'legacy' or '19'")
+    return java_double if mode == "19" else java_double_legacy
 
 
 def load_manifest(path: str):
@@ -292,8 +444,10 @@ def compute_features(manifest: str, access_log: str, ctx: Context | None = None)
     return paths, table
 
 
-def write_spark_csv(out_dir: str, paths, table) -> str:
-    """One part file with a header, like ``coalesce(1).write.csv`` (:96)."""
+def write_spark_csv(out_dir: str, paths, table, fmt=None) -> str:
+    """One part file with a header, like ``coalesce(1).write.csv`` (:96).
+    ``fmt`` formats the doubles (default: ``CDR_JAVA_DOUBLE``, see above)."""
+    fmt = fmt or _double_formatter()
     out_dir = _strip_scheme(out_dir)
     if os.path.isdir(out_dir):  # mode("overwrite")
         for name in os.listdir(out_dir):
@@ -307,7 +461,7 @@ def write_spark_csv(out_dir: str, paths, table) -> str:
             row = [pth]
             for j, col in enumerate(OUT_COLUMNS[1:]):
                 v = table[i, j]
-                row.append(str(int(v)) if col in LONG_COLUMNS else java_double(v))
+                row.append(str(int(v)) if col in LONG_COLUMNS else fmt(v))
             w.writerow(row)
     open(os.path.join(out_dir, "_SUCCESS"), "w").close()
     return part

@@ -32,6 +32,68 @@ def test_java_double_layout():
         assert float(java_double(v).replace("E", "e")) == v
 
 
+def test_java_double_legacy_pre_jdk19_digits():
+    """apache/spark:3.5.2 (docker/docker-compose.yml:67) runs a pre-19 JDK, whose
+    Double.toString is not always shortest.  Pinned by the outputs JDK bug 4511638
+    lists for JDK <= 18, and by hand derivations of the integer path."""
+    from compute_features import java_double, java_double_legacy
+
+    pinned = [(2.82879384806159e17, "2.82879384806159008E17"),
+              (1.387364135037754e18, "1.38736413503775411E18"),
+              (1.45800632428665e17, "1.45800632428664992E17"),
+              (5.684341886080802e-14, "5.6843418860808015E-14"),
+              (8.41e21, "8.409999999999999E21"),
+              (1.9400994884341945e25, "1.9400994884341944E25"),
+              (2e23, "1.9999999999999998E23"),
+              # integers below 2^63 keep their digits down to 10^i, i + 1 = the digit
+              # count of 2^(binExp - 54), rounded half up: 2^60 = 1152921504606846976,
+              # 2^6 = 64 -> drop one digit -> ...697|6 -> ...698
+              (2.0 ** 60, "1.15292150460684698E18"),
+              (2.0 ** 62, "4.6116860184273879E18"),  # 2^8 = 256 -> drop two digits: ...879|04 -> ...879
+              (2.0 ** 63, "9.223372036854776E18"),  # binExp 63 > 62: digit generation
+              (2.0 ** 53, "9.007199254740992E15"),
+              (5e-324, "4.9E-324"), (1.7976931348623157e308, "1.7976931348623157E308")]
+    for v, s in pinned:
+        assert java_double_legacy(v) == s, (v, java_double_legacy(v))
+        assert java_double_legacy(-v) == "-" + s
+    # the layout is the same as JDK 19+ wherever the digits agree
+    for v, s in [(0.0, "0.0"), (-0.0, "-0.0"), (1.0, "1.0"), (0.5, "0.5"), (100.0, "100.0"),
+                 (1e7, "1.0E7"), (1e-3, "0.001"), (9.99e-4, "9.99E-4"), (1e-5, "1.0E-5"),
+                 (9999999.5, "9999999.5"), (0.1 + 0.2, "0.30000000000000004"), (-2.5e-7, "-2.5E-7"),
+                 (float("nan"), "NaN"), (float("inf"), "Infinity"), (float("-inf"), "-Infinity"),
+                 (1.0 / 3, "0.3333333333333333"), (123456789.0, "1.23456789E8"),
+                 (1234567.0, "1234567.0"), (12277768.082999945, "1.2277768082999945E7")]:
+        assert java_double_legacy(v) == s, (v, java_double_legacy(v))
+    # every output reads back as the same double, and is never shorter than the
+    # shortest digits; both formats agree on most values
+    rng = random.Random(7)
+    same = 0
+    for _ in range(4000):
+        v = rng.uniform(-1, 1) * 10 ** rng.randint(-30, 30)
+        if rng.random() < 0.2:
+            v = float(rng.getrandbits(rng.randint(1, 63)))
+        a, b = java_double_legacy(v), java_double(v)
+        assert float(a.replace("E", "e")) == v, (v, a)
+        assert len(a.lstrip("-").split("E")[0]) >= len(b.lstrip("-").split("E")[0]), (v, a, b)
+        same += a == b
+    assert same > 3000
+
+
+def test_spark_csv_double_format_switch(tmp_path, monkeypatch):
+    from compute_features import write_spark_csv
+
+    table = np.full((1, 10), 2e23)
+    monkeypatch.delenv("CDR_JAVA_DOUBLE", raising=False)
+    with open(write_spark_csv(str(tmp_path / "a"), ["/p"], table)) as fh:
+        assert "1.9999999999999998E23" in fh.read()
+    monkeypatch.setenv("CDR_JAVA_DOUBLE", "19")
+    with open(write_spark_csv(str(tmp_path / "b"), ["/p"], table)) as fh:
+        assert "2.0E23" in fh.read()
+    monkeypatch.setenv("CDR_JAVA_DOUBLE", "17")
+    with pytest.raises(ValueError):
+        write_spark_csv(str(tmp_path / "c"), ["/p"], table)
+
+
 def test_iso_timestamp_parsing_matches_pandas():
     from compute_features import parse_ts_us
 
@@ -70,6 +132,8 @@ def test_pipeline_features_csv_roundtrip(tmp_path):
     part = write_spark_csv(str(tmp_path / "out"), list(df["path"]), z["table"])
     assert os.path.basename(part).startswith("part-00000")
     assert os.path.exists(str(tmp_path / "out" / "_SUCCESS"))
+    with open(part) as a, open(os.path.join(pdir, "features_out", "part-00000-golden-c000.csv")) as b:
+        assert a.read() == b.read()  # pre-JDK-19 digits; none of these values differ
     back = pd.read_csv(part, float_precision="round_trip")
     np.testing.assert_array_equal(back[OUT_COLUMNS[1:]].to_numpy(dtype=np.float64), z["table"])
 
