@@ -77,42 +77,51 @@ struct Xfer {
 // x = mx 2^ex (integer significand), y = x / 2^(e - MB) = mx 2^-sh: q =
 // mx >> sh and the rounding of the fraction from the shifted-out bits — the
 // same q and fraction as ldexp / floor in fp64, in integer instructions.
+// Split in two so that a thread can run the part that does not depend on
+// the state (xfer_pre: q, the rounding of the fraction, validity) for a whole
+// chunk of rows as independent, branch-free work before the short serial
+// updates (xfer_apply) — f64_transfer was bound by the dependent latency of
+// the branchy combined form at two waves per SIMD.
+struct XPre {
+  long long q;
+  int r;  // bit0 fraction above one half, bit1 exactly one half, bit2 invalid
+};
 template <typename TA>
-__device__ __forceinline__ void xfer_add(double x, int e, long long& m0, int& mdd, int& mfl) {
+__device__ __forceinline__ XPre xfer_pre(double x, int e) {
   constexpr int MB = SumTraits<TA>::MB;
-  int fl = mfl | 8;
-  if (e == kENone || e < SumTraits<TA>::kMinE || !(x >= 0.0)) {
-    mfl = fl | 4;
-    return;
-  }
   const unsigned long long bits = (unsigned long long)__double_as_longlong(x) & 0x7FFFFFFFFFFFFFFFull;
   const int er = (int)(bits >> 52);
   const unsigned long long mx = er ? ((bits & 0xFFFFFFFFFFFFFull) | (1ull << 52)) : bits;
   const int sh = e - MB - ((er ? er : 1) - 1075);
-  long long qi = 0;
-  bool up = false, tie = false;
-  if (er == 0x7FF || (sh < 0 && mx != 0)) {  // infinite, or not below the binade's top
-    mfl = fl | 4;
-    return;
-  } else if (sh <= 0) {
-    qi = (long long)mx;
-  } else if (sh < 64) {
-    qi = (long long)(mx >> sh);
-    const unsigned long long rem = mx & ((1ull << sh) - 1ull), half = 1ull << (sh - 1);
-    up = rem > half;
-    tie = rem == half;
-  }  // (sh >= 64: y < 2^-11, q = 0, below one half)
-  if (!(qi < (1ll << (MB + 1)))) {
-    mfl = fl | 4;
-    return;
-  }
-  const int p0 = fl & 1;
-  const long long i0 = qi + (up ? 1 : (tie ? ((p0 + qi) & 1) : 0));
-  const int p1 = (fl >> 1) & 1;
-  const long long i1 = qi + (up ? 1 : (tie ? ((p1 + qi) & 1) : 0));
-  m0 += i0;
-  mdd += (int)(i1 - i0);
-  mfl = (fl & ~3) | (int)((p0 + i0) & 1) | ((int)((p1 + i1) & 1) << 1);
+  // sh >= 64: y < 2^-11, q = 0 and below one half, as with a shift of 63
+  const int sc = sh < 0 ? 0 : (sh > 63 ? 63 : sh);
+  const long long qi = (long long)(mx >> sc);
+  const unsigned long long rem = mx & ((1ull << sc) - 1ull);
+  const unsigned long long half = sc ? (1ull << (sc - 1)) : 0ull;
+  const bool bad = e == kENone || e < SumTraits<TA>::kMinE || !(x >= 0.0) || er == 0x7FF ||
+                   (sh < 0 && mx != 0) || !(qi < (1ll << (MB + 1)));
+  return XPre{qi, (sc > 0 && rem > half ? 1 : 0) | (sc > 0 && rem == half ? 2 : 0) | (bad ? 4 : 0)};
+}
+__device__ __forceinline__ void xfer_apply(XPre p, long long& m0, int& mdd, int& mfl) {
+  const int fl = mfl | 8;
+  const int p0 = fl & 1, p1 = (fl >> 1) & 1;
+  const long long i0 = p.q + ((p.r & 1) ? 1 : ((p.r & 2) ? ((p0 + p.q) & 1) : 0));
+  const long long i1 = p.q + ((p.r & 1) ? 1 : ((p.r & 2) ? ((p1 + p.q) & 1) : 0));
+  const bool bad = p.r & 4;
+  m0 += bad ? 0 : i0;
+  mdd += bad ? 0 : (int)(i1 - i0);
+  mfl = bad ? (fl | 4) : ((fl & ~3) | (int)((p0 + i0) & 1) | ((int)((p1 + i1) & 1) << 1));
+}
+
+// One element x >= 0 of a (cluster, feature) sequence added to a transfer
+// state (m0: grid steps for an even entry, mdd: odd - even, mfl: bit0 P0,
+// bit1 P1, bit2 invalid, bit3 members) under the predicted binade e.  With
+// x = mx 2^ex (integer significand), y = x / 2^(e - MB) = mx 2^-sh: q =
+// mx >> sh and the rounding of the fraction from the shifted-out bits — the
+// same q and fraction as ldexp / floor in fp64, in integer instructions.
+template <typename TA>
+__device__ __forceinline__ void xfer_add(double x, int e, long long& m0, int& mdd, int& mfl) {
+  xfer_apply(xfer_pre<TA>(x, e), m0, mdd, mfl);
 }
 
 template <typename T>
@@ -210,59 +219,100 @@ __global__ __launch_bounds__(256) void f64_predict_c(const double* __restrict__ 
 }
 
 // One thread per (block, feature); the per-cluster transfer states live in
-// LDS ([thread][cluster]).
+// LDS, cluster-major ([cluster][thread]): a lane's state for cluster j sits
+// at j * nt + lane, so the lanes of a wave hit distinct banks whatever
+// clusters their rows belong to (thread-major rows k * 8 bytes apart put
+// every other lane on the same bank).
 template <typename TA, typename S>
-__global__ void f64_transfer(const S* __restrict__ X, int64_t n, int64_t n_pad, int d,
+__global__ __launch_bounds__(256) void f64_transfer(const S* __restrict__ X, int64_t n, int64_t n_pad, int d,
                              int k, int64_t nb, const int32_t* __restrict__ labels,
                              const int* __restrict__ E, Xfer* __restrict__ T) {
   extern __shared__ unsigned char smem[];
   const int nt = blockDim.x;
-  long long* s0 = reinterpret_cast<long long*>(smem);   // [nt][k]
-  int* sdd = reinterpret_cast<int*>(s0 + (size_t)nt * k);  // [nt][k]
-  int* sfl = sdd + (size_t)nt * k;                        // [nt][k]
-  int* se = sfl + (size_t)nt * k;                         // [nt][k]
+  long long* s0 = reinterpret_cast<long long*>(smem);   // [k][nt]
+  int* sdd = reinterpret_cast<int*>(s0 + (size_t)nt * k);  // [k][nt]
+  int* sfl = sdd + (size_t)nt * k;                        // [k][nt]
+  int* se = sfl + (size_t)nt * k;                         // [k][nt]
   const int64_t t = (int64_t)blockIdx.x * nt + threadIdx.x;
   const bool live = t < nb * d;
   // the d threads of one block are neighbours: they share its label stream
   const int64_t b = live ? t / d : 0;
   const int f = live ? (int)(t % d) : 0;
-  long long* m0 = s0 + (size_t)threadIdx.x * k;
-  int* mdd = sdd + (size_t)threadIdx.x * k;
-  int* mfl = sfl + (size_t)threadIdx.x * k;
-  int* me = se + (size_t)threadIdx.x * k;
+  long long* m0 = s0 + threadIdx.x;  // [j * nt]
+  int* mdd = sdd + threadIdx.x;
+  int* mfl = sfl + threadIdx.x;
+  int* me = se + threadIdx.x;
   if (!live) return;
   for (int j = 0; j < k; ++j) {
-    m0[j] = 0;
-    mdd[j] = 0;
-    mfl[j] = 2;  // P0 = 0, P1 = 1
-    me[j] = E[((int64_t)j * d + f) * nb + b];
+    m0[j * nt] = 0;
+    mdd[j * nt] = 0;
+    mfl[j * nt] = 2;  // P0 = 0, P1 = 1
+    me[j * nt] = E[((int64_t)j * d + f) * nb + b];
   }
   const int64_t r0 = b * kFB, r1 = min(n, r0 + kFB);
-  // rows in chunks of 16: the chunk's labels and values are loaded before
-  // the (serial, LDS-dependent) updates, so the loop does not pay a memory
-  // round trip per row
+  // rows in chunks of 16, the next chunk's labels and values loaded while
+  // the current one goes through the (serial, LDS-dependent) updates: at two
+  // waves per SIMD (LDS-bound) the memory latency is not hidden otherwise
+  // (0.27 ms at 10M x 5, k = 16 with the loads of a chunk issued only at its start)
   constexpr int kCh = 16;
+  int lj[kCh], nj[kCh];
+  double lx[kCh], nx[kCh];
+  auto load = [&](int64_t rc, int* jj, double* xx) {
+    if (rc + kCh <= r1) {  // (all but the last chunk of the last block)
+#pragma unroll
+      for (int u = 0; u < kCh; ++u) {
+        jj[u] = labels[rc + u];
+        xx[u] = (double)X[xidx(f, rc + u, n_pad)];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kCh; ++u) {
+        const int64_t row = rc + u;
+        jj[u] = row < r1 ? labels[row] : -1;
+        xx[u] = row < r1 ? (double)X[xidx(f, row, n_pad)] : 0.0;
+      }
+    }
+  };
+  load(r0, lj, lx);
   for (int64_t rc = r0; rc < r1; rc += kCh) {
-    int lj[kCh];
-    double lx[kCh];
+    if (rc + kCh < r1) load(rc + kCh, nj, nx);
+    // the chunk's binades (read-only), then its state-free parts, then the
+    // serial state updates
+    int le[kCh];
 #pragma unroll
     for (int u = 0; u < kCh; ++u) {
-      const int64_t row = rc + u;
-      lj[u] = row < r1 ? labels[row] : -1;
-      lx[u] = row < r1 ? (double)X[xidx(f, row, n_pad)] : 0.0;
+      const int ev = me[(lj[u] < 0 ? 0 : lj[u]) * nt];
+      le[u] = lj[u] >= 0 ? ev : kENone;
+    }
+    XPre pr[kCh];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) pr[u] = xfer_pre<TA>(lx[u], le[u]);
+    // branch-free (a row past the end rewrites cluster 0's state unchanged),
+    // the row's three state words read together before its writes
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const bool live_row = lj[u] >= 0;
+      const int o = (live_row ? lj[u] : 0) * nt;
+      long long a = m0[o];
+      int b = mdd[o], c = mfl[o];
+      const long long a0 = a;
+      const int b0 = b, c0 = c;
+      xfer_apply(pr[u], a, b, c);
+      m0[o] = live_row ? a : a0;
+      mdd[o] = live_row ? b : b0;
+      mfl[o] = live_row ? c : c0;
     }
 #pragma unroll
     for (int u = 0; u < kCh; ++u) {
-    const int j = lj[u];
-    if (j < 0) continue;
-    xfer_add<TA>(lx[u], me[j], m0[j], mdd[j], mfl[j]);
+      lj[u] = nj[u];
+      lx[u] = nx[u];
     }
   }
   for (int j = 0; j < k; ++j) {
     Xfer x;
-    x.d0 = m0[j];
-    x.dd = mdd[j];
-    x.flags = mfl[j];
+    x.d0 = m0[j * nt];
+    x.dd = mdd[j * nt];
+    x.flags = mfl[j * nt];
     T[((int64_t)j * d + f) * nb + b] = x;
   }
 }
