@@ -640,7 +640,14 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
   __shared__ int wcnt[kFB / 64][kFMaxK];
   __shared__ double sx[XF ? D * kFB : 1];
   __shared__ int sj[XF ? kFB : 1];
-  const int64_t b = blockIdx.x, nb = gridDim.x;
+  // Workgroups are dealt round-robin over the 8 XCDs; XCD x takes the
+  // contiguous block range x * (nb / 8) + min(x, nb % 8) + [0, its share), so
+  // the 8-byte writes of consecutive blocks into the sequence-major A and cnt
+  // rows meet in one L2 and leave it as whole lines (with blockIdx.x as the
+  // block, neighbouring blocks sit in different L2s and every write is partial)
+  const int64_t nb = gridDim.x;
+  const int64_t bq = nb >> 3, brm = nb & 7, bx = blockIdx.x & 7;
+  const int64_t b = bx * bq + (bx < brm ? bx : brm) + (blockIdx.x >> 3);
   for (int i = threadIdx.x; i < k * D; i += kFB) tab[i] = 0.0;
   if (threadIdx.x < kFMaxK) cc[threadIdx.x] = 0u;
   const int64_t row = b * kFB + threadIdx.x;
