@@ -679,8 +679,13 @@ def main() -> None:
                                   f"k x (d+1) int64 per step" + (
                                       " (ncclAllReduce enqueued from libcdr between the "
                                       "step's kernels)" if native else " (none at 1 GPU)"),
-                   "screen": "fp16 hi/lo split MFMA (certified) + exact fp64 fallback; "
-                             "int64 fixed-point sums (results bit-identical to fp64 NumPy)",
+                   "screen": "exact drift-bound pruning (Hamerly bounds: a 4-byte bound word per "
+                             "point, coordinates re-read only where the bound fails), labels "
+                             "bit-identical; re-read points decided by a certified fp16 hi/lo "
+                             "split MFMA screen + exact fp64 fallback; int64 fixed-point sums "
+                             "(results bit-identical to fp64 NumPy)" if kname.startswith("screen32b")
+                             else "fp16 hi/lo split MFMA (certified) + exact fp64 fallback; int64 "
+                                  "fixed-point sums (results bit-identical to fp64 NumPy)",
                    "loop": "device-resident (means, shift, convergence test on the device; "
                            "host polls once per timed region)"},
         "roofline": roofline,
@@ -690,6 +695,9 @@ def main() -> None:
         "reread_frac": t_frac,
         "seed_s": seed_s,
         "setup_ms": setup_ms,
+        # wall time per Lloyd step from the first step to the last (warmup
+        # steps with their one-time copies and the bound rebuild included)
+        "run_ms_per_step": (warmup_ms + elapsed * 1e3) / max(args.warmup + args.steps, 1),
         "setup_note": "one-time work outside the timed steps: device point generation + "
                       "statistics (gen_ms), and the warmup steps' one-time copies (pre-centred, "
                       "fp16 hi, row-major, bound words: warmup wall time minus warmup x "

@@ -84,6 +84,7 @@ SIGNATURES = {
     "cdr_debug_screen": ([_P, _P, _I32, _P, _P], None),
     "cdr_profile_reset": ([_P, _I32], None),
     "cdr_profile_read": ([_P, _P], None),
+    "cdr_profile_read_sub": ([_P, _P], None),
     "cdr_profile_kernel": ([_P, _P, _I32], None),
     "cdr_points_sqdev": ([_P, _P, _PF64], None),
     "cdr_lloyd_begin": ([_P, _P, _I32, _F64, _I32, _P, _F64], None),
@@ -274,6 +275,12 @@ class Context:
 
     def set_stream(self, stream_handle: int | None) -> None:
         _check(self._lib.cdr_set_stream(self._h, _P(stream_handle or 0)))
+        self._stream = int(stream_handle) if stream_handle else None
+
+    def stream_handle(self) -> int | None:
+        """The caller's HIP stream this context enqueues on (set_stream), or
+        None while it uses its own stream."""
+        return getattr(self, "_stream", None)
 
     def synchronize(self) -> None:
         _check(self._lib.cdr_synchronize(self._h))
@@ -501,6 +508,13 @@ class Context:
         return {"screen_ms": out[0], "steps": int(out[1]), "step_ms": out[2],
                 "fallback_points": int(out[3]), "queued_points": int(out[4]),
                 "tight_points": int(out[5])}
+
+    def profile_read_sub(self) -> dict:
+        """Steps whose screen ran as two kernels (the split bounded screen):
+        time from the step start to the end of the first kernel (screen32bz)."""
+        out = np.zeros(2, dtype=np.float64)
+        _check(self._lib.cdr_profile_read_sub(self._h, _ptr(out)))
+        return {"first_ms": out[0], "steps": int(out[1])}
 
     def profile_kernel(self) -> str:
         buf = ctypes.create_string_buffer(96)

@@ -97,6 +97,28 @@ class Comm:
         the C side: a Python-side record by id() could outlive the context)."""
         return hasattr(ctx, "comm_ranks") and ctx.comm_ranks()[0] == self.world
 
+    def fenced(self, ctx, fn, *args):
+        """Run the collective fn(*args) on device buffers that ctx's kernels
+        write before it and read after it.  torch.distributed runs it on
+        torch's current stream; when ctx enqueues on another stream (its own,
+        unless ctx.set_stream(torch's current stream) was called), wait for
+        ctx's queued kernels before the collective and for the collective
+        before ctx's next kernels (otherwise the two streams race
+        and the results are silently wrong).  Host buffers (gloo) need none."""
+        if self.device is None or not self.dist:
+            return fn(*args)
+        import torch
+
+        cur = torch.cuda.current_stream(self.device)
+        sh = getattr(ctx, "stream_handle", None)
+        same = sh is not None and sh() == cur.cuda_stream
+        if not same:
+            ctx.synchronize()
+        r = fn(*args)
+        if not same:
+            cur.synchronize()
+        return r
+
     def _t(self, arr):
         import torch
 
@@ -381,6 +403,25 @@ def shard_scan(ctx, comm: Comm, parts, total: float):
     return c
 
 
+def device_seed_layout_ok(offsets, n_total: int, world: int) -> bool:
+    """Whether the ranks' row layout fits the device-resident protocol
+    (csrc/seed.hip seed_shard_begin): shards in rank order from row 0, every
+    start on an 8192-row block, and no shard over ceil(blocks / world) blocks
+    (the [nranks][nbmax] block-sum slots).  Decided from the all-gathered
+    offsets, so every rank takes the same branch: a layout the device
+    protocol cannot hold runs the host protocol on all ranks instead of
+    raising on some of them while the others wait in a collective."""
+    off = [int(o) for o in np.asarray(offsets, dtype=np.int64).ravel()]
+    if len(off) != world or off[0] != 0:
+        return False
+    ends = off[1:] + [int(n_total)]
+    nbmax = -(-(-(-int(n_total) // 8192)) // world)
+    for b, e in zip(off, ends):
+        if e < b or (b % 8192 != 0 and e > b) or -(-(e - b) // 8192) > nbmax:
+            return False
+    return True
+
+
 def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_state=None,
                  host_seq_sum=None) -> np.ndarray:
     """kmeans_plusplus_init over the sharded rows (float64 centroids)."""
@@ -399,7 +440,8 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
         # one shard: every step on the device (cdr_seed_run)
         picks = ctx.seed_run(first, k, u)
         return np.asarray(ctx.get_rows(picks), dtype=np.float64)
-    if comm.world > 1 and k > 1 and hasattr(ctx, "seed_shard_begin"):
+    if comm.world > 1 and k > 1 and hasattr(ctx, "seed_shard_begin") and \
+            device_seed_layout_ok(offsets, n_total, comm.world):
         # sharded and device-resident: three collectives per step, no host
         # round trip (include/cdr.h cdr_seed_shard_*); status 1 (a program
         # that cannot be composed, seen by every rank) -> the host protocol
@@ -445,16 +487,16 @@ def seed_device_sharded(ctx, comm: Comm, row_begin: int, n_total: int, first: in
     red_b = 8 * (d + 4)
     red, hred = comm.buffer(red_b)
     sizes = ctx.seed_shard_begin(row_begin, n_total, comm.world, comm.rank, first, k, u, hred)
-    comm.allreduce_sum_f64_inplace(red)
+    comm.fenced(ctx, comm.allreduce_sum_f64_inplace, red)
     bs, hbs = comm.buffer(comm.world * int(sizes[0]))
     pg, hpg = comm.buffer(comm.world * int(sizes[1]))
     for _ in range(1, k):
         ctx.seed_shard_phase(0, hred, hbs)
-        comm.allgather_slots(bs, int(sizes[0]))
+        comm.fenced(ctx, comm.allgather_slots, bs, int(sizes[0]))
         ctx.seed_shard_phase(1, hbs, hpg)
-        comm.allgather_slots(pg, int(sizes[1]))
+        comm.fenced(ctx, comm.allgather_slots, pg, int(sizes[1]))
         ctx.seed_shard_phase(2, hpg, hred)
-        comm.allreduce_sum_f64_inplace(red)
+        comm.fenced(ctx, comm.allreduce_sum_f64_inplace, red)
     return ctx.seed_shard_end(hred)
 
 
@@ -497,7 +539,7 @@ class DeviceLloyd:
         for _ in range(m):
             self.ctx.lloyd_enqueue_assign(self.ptr)
             if self.buf is not None:
-                self.comm.allreduce_inplace(self.buf)
+                self.comm.fenced(self.ctx, self.comm.allreduce_inplace, self.buf)
             self.ctx.lloyd_enqueue_finalize(self.ptr)
 
     def advance(self, max_steps: int, chunk: int = 2, chunk_max: int = LL_CHUNK_MAX) -> int:
@@ -639,7 +681,7 @@ def sharded_medians(ctx, comm: Comm, k: int) -> np.ndarray:
         ctx.medians_pass_hist(p, handle)
         if comm.dist:
             if comm.device is not None:
-                comm.dist.all_reduce(buf)
+                comm.fenced(ctx, comm.dist.all_reduce, buf)
             else:
                 import torch
 

@@ -171,10 +171,13 @@ struct Ctx {
   int prof_period = 1;     // profile every prof_period-th step (event records
   int64_t prof_seen = 0;   // cost the GPU a few us each)
   std::vector<hipEvent_t> prof_pool;
-  size_t prof_used = 0;  // events of this profiling session (triples)
+  size_t prof_used = 0;  // events of this profiling session (4 per step)
   int64_t prof_cur = -1; // first event of the current step's triple, -1 none
   double prof_screen_ms = 0.0, prof_step_ms = 0.0, prof_fb_points = 0.0;
   int64_t prof_launches = 0;
+  std::vector<char> prof_sub;  // per recorded step: event 3 (prof_mark_sub) recorded
+  double prof_sub_ms = 0.0;    // start -> event 3, summed over those steps
+  int64_t prof_sub_launches = 0;
   DevBuf fb_accum;  // int64: fallback points summed over the steps (publish32)
   DevBuf q_acc;     // int64 per screen32p wave: points queued for the k-way screen (profiling)
   char prof_kernel[96] = {0};  // name of the last screen kernel launched
@@ -202,6 +205,7 @@ struct Ctx {
   // step gathers from, and the cumulative drifts bnd = int64 W[64] (2^-40
   // units) | float W up [64] | float W down [64]
   DevBuf zb, xh16, bnd, t_acc;
+  DevBuf zl, zn;  // split bounded screen: per-wave lists of failed points (screen32bz), lengths
   bool zb_valid = false, xh_valid = false, bnd_ok = false;
   int32_t run_k = 0;
   bool last_delta = false;
@@ -364,9 +368,11 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Profiling (lloyd.hip): prof_step_begin starts a profiled step when
 // profiling is on (false otherwise); prof_mark(c, i) records event i of it
-// (0 start, 1 after the screen kernel, 2 end).
+// (0 start, 1 after the screen kernel, 2 end); prof_mark_sub(c) records the
+// end of the first of the screen's two kernels (split bounded screen).
 bool prof_step_begin(Ctx& c);
 void prof_mark(Ctx& c, int i);
+void prof_mark_sub(Ctx& c);
 
 // The step's fallback total from the screens' per-wave counts fbc[0, nwaves)
 // (the DELTA screens write per-wave counts only: thousands of same-address

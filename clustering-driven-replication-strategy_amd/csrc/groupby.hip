@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(kGbBThreads) void gb_bucket_big(
 // forget the profile triple of a step that returns before its last event
 void prof_drop(Ctx& c) {
   if (c.prof_cur >= 0) {
-    c.prof_used -= 3;
+    c.prof_used -= 4;
     c.prof_cur = -1;
   }
 }

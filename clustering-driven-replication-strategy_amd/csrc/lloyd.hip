@@ -1063,19 +1063,27 @@ bool prof_step_begin(Ctx& c) {
   c.prof_cur = -1;
   if (!c.prof_on) return false;
   if (c.prof_seen++ % c.prof_period != 0) return false;
-  if (c.prof_used + 3 > (size_t)(3 << 16)) return false;  // session cap: 65536 steps
-  while (c.prof_pool.size() < c.prof_used + 3) {
+  if (c.prof_used + 4 > (size_t)(4 << 16)) return false;  // session cap: 65536 steps
+  while (c.prof_pool.size() < c.prof_used + 4) {
     hipEvent_t e = nullptr;
     HIP_CHECK(hipEventCreate(&e));
     c.prof_pool.push_back(e);
   }
   c.prof_cur = (int64_t)c.prof_used;
-  c.prof_used += 3;
+  c.prof_used += 4;
+  c.prof_sub.resize(c.prof_used / 4);
+  c.prof_sub[c.prof_used / 4 - 1] = 0;
   return true;
 }
 
 void prof_mark(Ctx& c, int i) {
   if (c.prof_cur >= 0) HIP_CHECK(hipEventRecord(c.prof_pool[(size_t)c.prof_cur + i], c.stream));
+}
+
+void prof_mark_sub(Ctx& c) {
+  if (c.prof_cur < 0) return;
+  HIP_CHECK(hipEventRecord(c.prof_pool[(size_t)c.prof_cur + 3], c.stream));
+  c.prof_sub[(size_t)c.prof_cur / 4] = 1;
 }
 
 // End of a profiled screened step whose fallback total sits in fb_count
@@ -1093,14 +1101,20 @@ void prof_end_screened(Ctx& c) {
 // for the last one).
 void prof_collect(Ctx& c) {
   if (c.prof_used == 0) return;
-  HIP_CHECK(hipEventSynchronize(c.prof_pool[c.prof_used - 1]));
-  for (size_t t = 0; t + 3 <= c.prof_used; t += 3) {
+  HIP_CHECK(hipEventSynchronize(c.prof_pool[c.prof_used - 2]));  // (the last step's end)
+  for (size_t t = 0; t + 4 <= c.prof_used; t += 4) {
     float a = 0.f, b = 0.f;
     HIP_CHECK(hipEventElapsedTime(&a, c.prof_pool[t], c.prof_pool[t + 1]));
     HIP_CHECK(hipEventElapsedTime(&b, c.prof_pool[t], c.prof_pool[t + 2]));
     c.prof_screen_ms += a;
     c.prof_step_ms += b;
     c.prof_launches += 1;
+    if (c.prof_sub[t / 4]) {
+      float s = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&s, c.prof_pool[t], c.prof_pool[t + 3]));
+      c.prof_sub_ms += s;
+      c.prof_sub_launches += 1;
+    }
   }
   c.prof_used = 0;
   c.prof_cur = -1;
@@ -1624,6 +1638,8 @@ int cdr_profile_reset(cdr_ctx* h, int32_t enable) {
   c.prof_seen = 0;
   c.prof_screen_ms = c.prof_step_ms = c.prof_fb_points = 0.0;
   c.prof_launches = 0;
+  c.prof_sub_ms = 0.0;
+  c.prof_sub_launches = 0;
   c.fb_accum.ensure(2 * sizeof(long long));
   HIP_CHECK(hipMemsetAsync(c.fb_accum.p, 0, 2 * sizeof(long long), c.stream));
   if (c.q_acc.p) HIP_CHECK(hipMemsetAsync(c.q_acc.p, 0, c.q_acc.bytes, c.stream));
@@ -1658,6 +1674,17 @@ int cdr_profile_read(cdr_ctx* h, double* out) {
   out[3] = c.prof_fb_points + (double)fb[0];
   out[4] = (double)fb[1];
   out[5] = (double)tight;
+  CDR_CATCH
+}
+
+int cdr_profile_read_sub(cdr_ctx* h, double* out) {
+  CDR_TRY
+  if (!h || !out) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  prof_collect(c);
+  out[0] = c.prof_sub_ms;
+  out[1] = (double)c.prof_sub_launches;
   CDR_CATCH
 }
 

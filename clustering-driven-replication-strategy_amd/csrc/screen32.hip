@@ -1779,6 +1779,9 @@ __global__ __launch_bounds__(256, 5) void screen32p(S32PArgs a) {
 #ifndef CDR_S32BS_LAZY
 #define CDR_S32BS_LAZY 1  // screen32bs: phase 2 interleaved with the stream (0: in bursts)
 #endif
+#ifndef CDR_S32BS_DEFER
+#define CDR_S32BS_DEFER 0  // screen32bs: near ties listed and resolved after the last batch (1)
+#endif
 constexpr int kBChunk = 256;  // points per wave-chunk of the bound stream (4 per lane)
 constexpr int kBList = 512;   // per-wave LDS list of the points whose bound failed
 constexpr int kBPD = 4;       // chunks in flight per wave (phase 1)
@@ -1798,7 +1801,64 @@ struct S32BArgs {
   // strided split over all waves
   int slot_wg;
   int wsl[4];
+  // split form (screen32bz streams the words, screen32bs<Q, MT, true> decides):
+  // per-wave lists of the failed points in screen32bz's entry format, their
+  // lengths, and the entries each list has room for
+  uint32_t* zl;
+  int32_t* zn;
+  int64_t zcap;
 };
+
+// The chunks wave `wv` of this workgroup streams: wbase + i * wstride below
+// wend.  With slot_wg > 0 the workgroups of one CU slot (launch generation)
+// share a region in proportion to its weight: the later generations on a CU
+// get fewer issue slots (oldest-first) and otherwise finish last.
+__device__ __forceinline__ void bs_range(const S32BArgs& B, int wv, int64_t& wbase, int& wstride,
+                                         int64_t& wend) {
+  const int64_t nchunks = B.nchunks;
+  wbase = (int64_t)blockIdx.x * 4 + wv;
+  wend = nchunks;
+  wstride = (int)gridDim.x * 4;
+  if (B.slot_wg < 0) {
+    // contiguous ranges: wave w streams chunks [w cpw, (w + 1) cpw), so the
+    // rows its failed points gather lie in one ~cpw * 16 KiB stretch of the
+    // row-major copy (a few pages: the gathers stay TLB-resident) instead of
+    // spread over the whole copy
+    const int64_t nw = (int64_t)gridDim.x * 4, cpw = (nchunks + nw - 1) / nw;
+    wbase = wbase * cpw;
+    wend = wbase + cpw < nchunks ? wbase + cpw : nchunks;
+    wstride = 1;
+  } else if (B.slot_wg > 0) {
+    const int ns = (int)gridDim.x / B.slot_wg;
+    const int sl = (int)blockIdx.x / B.slot_wg;
+    int wsum = 0, wpre = 0;
+    for (int q = 0; q < ns; ++q) {
+      wsum += B.wsl[q];
+      if (q < sl) wpre += B.wsl[q];
+    }
+    const int64_t R0 = nchunks * wpre / wsum, R1 = nchunks * (wpre + B.wsl[sl]) / wsum;
+    wstride = B.slot_wg * 4;
+    wbase = R0 + (int64_t)((int)blockIdx.x - sl * B.slot_wg) * 4 + wv;
+    wend = R1;
+  }
+  wbase = __builtin_amdgcn_readfirstlane((int)wbase);
+}
+
+// Host mirror of bs_range: the most chunks any wave of the grid streams.
+static int64_t bs_max_chunks(const S32BArgs& B, int nwg) {
+  const int64_t nchunks = B.nchunks;
+  if (B.slot_wg <= 0) return ceil_div(nchunks, (int64_t)nwg * 4);  // (strided or contiguous)
+  const int ns = nwg / B.slot_wg;
+  int wsum = 0;
+  for (int q = 0; q < ns; ++q) wsum += B.wsl[q];
+  int64_t mx = 0, wpre = 0;
+  for (int q = 0; q < ns; ++q) {
+    const int64_t R0 = nchunks * wpre / wsum, R1 = nchunks * (wpre + B.wsl[q]) / wsum;
+    mx = std::max<int64_t>(mx, ceil_div(R1 - R0, (int64_t)B.slot_wg * 4));
+    wpre += B.wsl[q];
+  }
+  return mx;
+}
 
 // The stored word of bounds (l0, u0) and W_a rounded down (see above):
 // Z = l0 (1 - 2^-20) - u0 + w minus 2^-21 (|l0| + u0 + w), which covers the
@@ -2176,6 +2236,87 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
 }
 
 // ---------------------------------------------------------------------------
+// screen32bz: phase 1 of the bounded screen as its own launch (the split form,
+// the default; CDR_S32BS_FUSED=1 runs the fused kernel).  Streams every
+// point's bound word (4 per lane per 1 KiB chunk, KPD chunks in flight per
+// wave) and lists the points whose bound fails in the
+// wave's region of B.zl, in screen32bs's entry format (chunk iteration << 14 |
+// offset << 6 | label); screen32bs<Q, MT, true> then decides the lists with
+// every wave of the chip on the gathers and the MFMA screen.  In the fused
+// form a wave stops streaming while it decides a batch, so the stream and the
+// decisions add up; split, the stream is a plain HBM-bound pass (no plan, no
+// LDS beyond the list staging, low register count) and the decisions run at
+// full occupancy.  Entries are staged in LDS and written 64 at a time (one
+// 256-byte store), so stores rarely sit between a chunk load and its use.
+// ---------------------------------------------------------------------------
+template <int KPD>
+__global__ __launch_bounds__(256) void screen32bz(S32BArgs B) {
+  const S32PArgs& a = B.p;
+  if (a.gate && a.gate[0] == 0) return;
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  constexpr int kZList = KPD * kBChunk + 64;
+  __shared__ unsigned flist[4][kZList];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = t >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
+  const int64_t nchunks = B.nchunks;
+  int64_t wbase, wend;
+  int wstride;
+  bs_range(B, wv, wbase, wstride, wend);
+  auto zload = [&](u4v& z, int64_t ci) __attribute__((always_inline)) {
+    const int64_t cc = ci < nchunks ? ci : nchunks - 1;
+    z = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(B.zb + cc * kBChunk) + lane);
+  };
+  u4v zc[KPD];
+#pragma unroll
+  for (int i = 0; i < KPD - 1; ++i) zload(zc[i], wbase + (int64_t)i * wstride);
+  const float wup_l = B.wup[lane];  // lane j: W_j rounded up (k <= 64)
+  unsigned* const fl = flist[wv];
+  uint32_t* const out = B.zl + (size_t)wave * B.zcap;
+  int cnt = 0, total = 0;
+  int it = 0;
+  for (int64_t C0 = wbase; C0 < wend; C0 += (int64_t)KPD * wstride) {
+#pragma unroll
+    for (int i = 0; i < KPD; ++i, ++it) {
+      const int64_t Ci = C0 + (int64_t)i * wstride;
+      if (Ci >= wend) break;
+      zload(zc[(i + KPD - 1) % KPD], Ci + (int64_t)(KPD - 1) * wstride);
+      const u4v z = zc[i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const unsigned w = z[u];
+        const unsigned lab = w & 63u;
+        const bool fail = !(__uint_as_float(w & ~63u) > __shfl(wup_l, (int)lab)) || (B.dbg & 1);
+        const unsigned long long m = __ballot(fail);
+        if (m) {
+          if (fail) {
+            const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            fl[cnt + r] = (unsigned)it << 14 | (unsigned)(4 * lane + u) << 6 | lab;
+          }
+          cnt += __popcll(m);
+        }
+      }
+    }
+    if (cnt >= 64) {  // whole 64-entry rows out, the rest to the front
+      const int full = cnt & ~63;
+      __builtin_amdgcn_wave_barrier();
+      for (int o = 0; o < full; o += 64) out[total + o + lane] = fl[o + lane];
+      const int rem = cnt - full;
+      const unsigned v = lane < rem ? fl[full + lane] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < rem) fl[lane] = v;
+      total += full;
+      cnt = rem;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < cnt) out[total + lane] = fl[lane];
+  if (lane == 0) B.zn[wave] = total + cnt;
+}
+
+// ---------------------------------------------------------------------------
 // screen32bs: the bounded screen deciding in registers (device loop; d <= 16,
 // k <= 64).  Phase 1 is screen32b's.  Phase 2 gathers the listed points' fp32
 // rows (XA: one 64-byte line per point at d = 16, the same memory
@@ -2200,8 +2341,12 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
 // layout) flushed into one run_sums slice at the end when the workgroup moved
 // anything.  The split screen is ~2^8 tighter than the hi-only one, so almost
 // no point needs the exact fp64 pass.
+// SPLIT: phase 1 ran in screen32bz (same grid, so wave w decides the list of
+// screen32bz's wave w and decodes its entries with the same chunk range); the
+// batches come from that list, entries two batches ahead and rows one batch
+// ahead of the decision.
 // ---------------------------------------------------------------------------
-template <int Q, int MT>
+template <int Q, int MT, bool SPLIT = false>
 __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   const S32PArgs& a = B.p;
   const FixArgs& F = a.fx;
@@ -2223,7 +2368,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   // kBPD chunks streamed between two phase-2 passes, so phase 2 has one call
   // site (code size: the decision is inlined once)
   constexpr int kSList = kBPD * kBChunk + 256;
-  __shared__ unsigned flist[4][kSList];
+  __shared__ unsigned flist[4][SPLIT ? 1 : kSList];
   __shared__ unsigned long long mtab[64 * 17];  // this workgroup's moves, [k][d + 1]
   __shared__ float msl[16];                     // -mu_f 2^sigma
   const int t = threadIdx.x;
@@ -2231,7 +2376,6 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   const int wv = t >> 6;
   const int h = lane >> 5, p = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);
-  const int nwaves = gridDim.x * 4;
   const int64_t nchunks = B.nchunks;
   const int k = a.k, d = a.d, d1 = d + 1;
 
@@ -2241,28 +2385,14 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     z = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(B.zb + cc * kBChunk) + lane);
   };
   // this wave's chunks: wbase + i wstride below wend
-  int64_t wbase = wave, wend = nchunks;
-  int wstride = nwaves;
-  if (B.slot_wg > 0) {
-    // Workgroups of one CU slot (launch generation) share a region in
-    // proportion to its weight: the later generations on a CU get fewer
-    // issue slots (oldest-first) and otherwise finish last.
-    const int ns = (int)gridDim.x / B.slot_wg;
-    const int sl = (int)blockIdx.x / B.slot_wg;
-    int wsum = 0, wpre = 0;
-    for (int q = 0; q < ns; ++q) {
-      wsum += B.wsl[q];
-      if (q < sl) wpre += B.wsl[q];
-    }
-    const int64_t R0 = nchunks * wpre / wsum, R1 = nchunks * (wpre + B.wsl[sl]) / wsum;
-    wstride = B.slot_wg * 4;
-    wbase = R0 + (int64_t)((int)blockIdx.x - sl * B.slot_wg) * 4 + wv;
-    wend = R1;
-  }
-  wbase = __builtin_amdgcn_readfirstlane((int)wbase);
+  int64_t wbase, wend;
+  int wstride;
+  bs_range(B, wv, wbase, wstride, wend);
   u4v zc[kBPD];
+  if constexpr (!SPLIT) {
 #pragma unroll
-  for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], wbase + (int64_t)i * wstride);
+    for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], wbase + (int64_t)i * wstride);
+  }
 
   // ---- the plan ----
   __shared__ h8 sA[MT * 2 * 64];
@@ -2445,6 +2575,116 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     mv_used += __popcll(mm);
   };
   int2* fb_region = a.fb_list + (size_t)wave * a.cap;
+  // A point the split screen could not certify (a near tie; best key bkey):
+  // every centroid whose key is within the threshold of the best is a
+  // candidate (|S_j - T_j| <= E: the reference's argmin is among them); the
+  // candidates' direct fp32 distances from the LDS c32 copy decide with
+  // rigorous intervals, and only an interval overlap falls to the exact fp64
+  // NumPy-order evaluation (np.argmin of the reference's norms,
+  // src/kmeans_plusplus.py:33-34).  Every lane of the wave calls it (the
+  // screen values come from MFMAs over the wave's 64 points); lanes with
+  // live = false return ao.  c2: decided by the direct distances, with the
+  // bounds (u0, l0) of its new bound word; otherwise the point keeps "no
+  // bound".
+  auto near_tie = [&](bool live, int ao, unsigned bkey, const float (&xh)[DM],
+                      const u4v (&T0)[QH], const u4v (&T1)[QH], const f4 (&xr)[Q], float xx,
+                      bool& c2, float& u0, float& l0) __attribute__((always_inline)) -> int {
+    const double* cs = F.cent;
+    const float tau = fmaf(__uint_as_float(bkey & ~63u), thr_rel, thr0);
+    // tile tt's column p is the point of lane 32 tt + p, which holds its tau
+    unsigned mine[2], other[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const float tau_t = __shfl(tau, 32 * tt + p);
+      const unsigned r = cmask(tt == 0 ? T0 : T1, tau_t);
+      mine[tt] = r;
+      other[tt] = (unsigned)__shfl_xor((int)r, 32);
+    }
+    int lab = ao;
+    c2 = false;
+    u0 = l0 = 0.0f;
+    if (live) {
+      unsigned long long cand = 0;
+      const unsigned mh0 = h == 0 ? mine[0] : other[1], mh1 = h == 0 ? other[0] : mine[1];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        unsigned mmk = hh ? mh1 : mh0;  // rows of half hh of this lane's tile
+        while (mmk) {
+          const int bb = __builtin_ctz(mmk);
+          mmk &= mmk - 1;
+          const int m = bb >> 4, i = bb & 15;
+          cand |= 1ull << (32 * m + 8 * (i >> 2) + 4 * hh + (i & 3));
+        }
+      }
+      if (k < 64) cand &= (1ull << k) - 1;
+      // the candidates' direct fp32 distances (c32 in LDS): t_j = ||xhat -
+      // chat_j|| lies within sqrt(q_j) (1 -+ 2^-19) -+ (dn32 + ec_j), where
+      // dn32 >= ||xhat32 - xhat|| and ec_j >= ||c32_j - chat_j||: c32 is
+      // the fp32 rounding of chat_j in fp64, so ec_j <= (2^-24 + 2^-51)
+      // ||chat_j|| <= 2^-24 (1 + 2^-18) ||c32_j||
+      const float xu = fmaf(xx, 1.0f + 0x1p-19f, 0x1p-120f);
+      const float xl = xx * (1.0f - 0x1p-19f);
+      const float dn32 = fmaf(0x1p-24f * (1.0f + 0x1p-20f), __builtin_amdgcn_sqrtf(xu), 0x1p-120f);
+      float ub = INFINITY, lo_other = INFINITY, lb_best = INFINITY, rbest = INFINITY;
+      int jb = 0;
+      bool bad = false;  // a NaN distance: the exact pass decides
+      unsigned long long cm2 = cand;
+      while (cm2) {  // increasing j
+        const int j = __builtin_ctzll(cm2);
+        cm2 &= cm2 - 1;
+        float nc;
+        {
+          const float zr[DM] = {};
+          nc = q32(zr, j);  // ||c32_j||^2 (the same rounding bound)
+        }
+        const float ec = fmaf(0x1p-24f * (1.0f + 0x1p-18f),
+                              __builtin_amdgcn_sqrtf(nc * (1.0f + 0x1p-19f)), 0x1p-120f);
+        const float e2 = (dn32 + ec) * (1.0f + 0x1p-20f);
+        const float r = __builtin_amdgcn_sqrtf(q32(xh, j));
+        const float U = fmaf(r, 1.0f + 0x1p-19f, e2), L = fmaf(r, 1.0f - 0x1p-19f, -e2);
+        bad = bad || !(U == U) || !(L == L);
+        if (r < rbest) {
+          lo_other = fminf(lo_other, lb_best);
+          rbest = r;
+          ub = U;
+          lb_best = L;
+          jb = j;
+        } else {
+          lo_other = fminf(lo_other, L);
+        }
+      }
+      // every other centroid's key is above tau: its distance is at least
+      const float gs = tau - ((thr0 + Dhi) - xl);
+      const float lnc = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gs, 0.0f)), 1.0f - 0x1p-19f, -dn32);
+      c2 = !bad && rbest < INFINITY && lo_other > ub * (1.0f + 0x1p-20f);
+      if (c2) {
+        lab = jb;
+        u0 = ub;
+        l0 = fminf(lo_other, lnc);
+      } else {
+        float x[16];  // fp32 data, converted exactly where used
+#pragma unroll
+        for (int f = 0; f < 16; ++f) x[f] = f < DM ? xr[f >> 2][f & 3] : 0.0f;
+        double sb = INFINITY, rb = INFINITY;
+        int jmin = 0x7fffffff;
+        while (cand) {  // increasing j
+          const int j = __builtin_ctzll(cand);
+          cand &= cand - 1;
+          const double sq = np_sqdist16(x, cs + j * d, d);
+          if (sq < sb) {  // sqrt is monotone: only a smaller square gives a smaller root
+            const double rt = sqrt(sq);
+            sb = sq;
+            if (rt < rb) {
+              rb = rt;
+              jmin = j;
+            }
+          }
+        }
+        lab = jmin >= k ? 0 : jmin;  // every root NaN: np.argmin of all-NaN is 0
+      }
+    }
+    return lab;
+  };
   // one gathered batch: lane l decides point l
   auto decide = [&](const GB& g) __attribute__((always_inline)) {
     const bool valid = g.valid;
@@ -2497,9 +2737,10 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       const float l0 = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gs, 0.0f)), 1.0f - 0x1p-19f, -dn32);
       B.zb[pt] = zb_pack(l0, u0, w_lab, (unsigned)label);
     }
+    const unsigned long long um = __ballot(unc);
+#if CDR_S32BS_DEFER
     // uncertified (near ties): the wave's list {point, best key}, resolved
     // after the workgroup's last batch
-    const unsigned long long um = __ballot(unc);
     if (um) {
       if (unc) {
         const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(um >> 32),
@@ -2509,6 +2750,31 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       fb_used += __popcll(um);
     }
     move(need && cert, pt, ao, label, nullptr);
+#else
+    // uncertified (near ties, ~1 in 5 re-read points at config 3) resolved
+    // now, while the row, the split operands and the best key are in
+    // registers: no list, no dependent re-gather of the row and label
+    int labf = label;
+    if (um) {
+#ifdef CDR_EXPERIMENTS
+      if (!(B.dbg & 2)) {  // (timing: no near-tie pass)
+#endif
+      bool c2;
+      float u0, l0;
+      const int lab = near_tie(unc, ao, bA, xh, T0, T1, g.x, xx, c2, u0, l0);
+      if (unc) {
+        labf = lab;
+        B.zb[pt] = c2 ? zb_pack(l0, u0, __shfl(wdn_l, lab), (unsigned)lab) : (kZbStale | (unsigned)lab);
+      }
+#ifdef CDR_EXPERIMENTS
+      } else if (unc) {
+        labf = ao;
+      }
+#endif
+      fb_used += __popcll(um);
+    }
+    move(need, pt, ao, labf, g.x);
+#endif
   };
 
   // ---- phase 2: the listed points, 64 per batch, two batches in flight ----
@@ -2567,6 +2833,45 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     cnt = rem;
   };
 
+  if constexpr (SPLIT) {
+    // ---- the list screen32bz's wave `wave` wrote: 64 entries per batch ----
+    const uint32_t* const L = B.zl + (size_t)wave * B.zcap;
+    const int total = B.zn[wave];
+    const int nb = (total + 63) >> 6;
+    ttot = total;
+    if (nb > 0) {
+      auto eload = [&](int b) __attribute__((always_inline)) -> unsigned {
+        const int e = 64 * b + lane;
+        return L[e < total ? e : 64 * b];  // (entry 64 b exists: b < nb)
+      };
+      auto fill = [&](GB& g, unsigned ent, int b) __attribute__((always_inline)) {
+        g.valid = 64 * b + lane < total;
+        const int64_t ci = wbase + (int64_t)(ent >> 14) * wstride;
+        const int64_t pt = ci * kBChunk + ((ent >> 6) & 255);
+        g.pt = (int)pt;
+        g.ao = (int)(ent & 63);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) g.x[q] = __builtin_nontemporal_load(XA4 + pt * Q + q);
+      };
+      GB cur, nxt;
+      unsigned en = eload(0);
+      fill(cur, en, 0);
+      en = eload(nb > 1 ? 1 : 0);
+#pragma nounroll
+      for (int b = 0; b < nb; ++b) {
+        // the next batch's rows and the one after's entries load while this
+        // batch is decided (past the end: the last batch again, not decided)
+        const int b1 = b + 1 < nb ? b + 1 : nb - 1;
+        fill(nxt, en, b1);
+        en = eload(b + 2 < nb ? b + 2 : nb - 1);
+#ifdef CDR_EXPERIMENTS
+        if (!(B.dbg & 4))  // (timing: the listed points are gathered, not decided)
+#endif
+        decide(cur);
+        cur = nxt;
+      }
+    }
+  } else {
 #if CDR_S32BS_LAZY
   // Phase 2 interleaved with the stream: after every kBPD chunks the batch
   // whose rows were gathered one group of chunks earlier is decided and the
@@ -2659,6 +2964,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #endif
     if (!more) break;
   }
+  }  // (!SPLIT)
   // ---- the uncertified points: the same split screen again (the same values),
   // every centroid whose key is within the threshold of the best is a
   // candidate (|S_j - T_j| <= E: the reference's argmin is among them), and
@@ -2668,139 +2974,39 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #ifdef CDR_EXPERIMENTS
   if (B.dbg & 2) fb_used = 0;  // (timing: no exact pass)
 #endif
-  {
-    const double* cs = F.cent;
-    for (int e0 = 0; e0 < fb_used; e0 += 64) {
-      const int e = e0 + lane;
-      const bool live = e < fb_used;
-      const int2 rec = fb_region[live ? e : e0];
-      const int pt = rec.x;
-      const int ao = a.lab8[pt];  // (unchanged until this pass decides the point)
-      f4 xr[Q];
+#if CDR_S32BS_DEFER
+  for (int e0 = 0; e0 < fb_used; e0 += 64) {
+    const int e = e0 + lane;
+    const bool live = e < fb_used;
+    const int2 rec = fb_region[live ? e : e0];
+    const int pt = rec.x;
+    const int ao = a.lab8[pt];  // (unchanged until this pass decides the point)
+    f4 xr[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) xr[q] = XA4[(int64_t)pt * Q + q];
-      float xh[DM];
-      rowhat(xr, xh);
-      u4v T0[QH], T1[QH];
-      split_tiles(xh, T0, T1);
-      const float tau = fmaf(__uint_as_float((unsigned)rec.y & ~63u), thr_rel, thr0);
-      // tile tt's column p is the point of lane 32 tt + p, which holds its tau
-      unsigned mine[2], other[2];
+    for (int q = 0; q < Q; ++q) xr[q] = XA4[(int64_t)pt * Q + q];
+    float xh[DM];
+    rowhat(xr, xh);
+    u4v T0[QH], T1[QH];
+    split_tiles(xh, T0, T1);
+    float xx;
+    {
+      f2 acc = {0.0f, 0.0f};
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const float tau_t = __shfl(tau, 32 * tt + p);
-        const unsigned r = cmask(tt == 0 ? T0 : T1, tau_t);
-        mine[tt] = r;
-        other[tt] = (unsigned)__shfl_xor((int)r, 32);
+      for (int f = 0; f < DM; f += 2) {
+        const f2 v = {xh[f], xh[f + 1]};
+        acc = __builtin_elementwise_fma(v, v, acc);
       }
-      int lab = ao;
-      bool c2 = false;  // decided by the direct fp32 distances
-      float u0 = 0.0f, l0 = 0.0f;
-      if (live) {
-        unsigned long long cand = 0;
-        const unsigned mh0 = h == 0 ? mine[0] : other[1], mh1 = h == 0 ? other[0] : mine[1];
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          unsigned mmk = hh ? mh1 : mh0;  // rows of half hh of this lane's tile
-          while (mmk) {
-            const int bb = __builtin_ctz(mmk);
-            mmk &= mmk - 1;
-            const int m = bb >> 4, i = bb & 15;
-            cand |= 1ull << (32 * m + 8 * (i >> 2) + 4 * hh + (i & 3));
-          }
-        }
-        if (k < 64) cand &= (1ull << k) - 1;
-        // the candidates' direct fp32 distances (c32 in LDS): t_j = ||xhat -
-        // chat_j|| lies within sqrt(q_j) (1 -+ 2^-19) -+ (dn32 + ec_j), where
-        // dn32 >= ||xhat32 - xhat|| and ec_j >= ||c32_j - chat_j||: c32 is
-        // the fp32 rounding of chat_j in fp64, so ec_j <= (2^-24 + 2^-51)
-        // ||chat_j|| <= 2^-24 (1 + 2^-18) ||c32_j||
-        float xx;
-        {
-          f2 acc = {0.0f, 0.0f};
-#pragma unroll
-          for (int f = 0; f < DM; f += 2) {
-            const f2 v = {xh[f], xh[f + 1]};
-            acc = __builtin_elementwise_fma(v, v, acc);
-          }
-          xx = acc.x + acc.y;
-        }
-        const float xu = fmaf(xx, 1.0f + 0x1p-19f, 0x1p-120f);
-        const float xl = xx * (1.0f - 0x1p-19f);
-        const float dn32 = fmaf(0x1p-24f * (1.0f + 0x1p-20f), __builtin_amdgcn_sqrtf(xu), 0x1p-120f);
-        float ub = INFINITY, lo_other = INFINITY, lb_best = INFINITY, rbest = INFINITY;
-        int jb = 0;
-        bool bad = false;  // a NaN distance: the exact pass decides
-        unsigned long long cm2 = cand;
-        while (cm2) {  // increasing j
-          const int j = __builtin_ctzll(cm2);
-          cm2 &= cm2 - 1;
-          float nc;
-          {
-            const float zr[DM] = {};
-            nc = q32(zr, j);  // ||c32_j||^2 (the same rounding bound)
-          }
-          const float ec = fmaf(0x1p-24f * (1.0f + 0x1p-18f),
-                                __builtin_amdgcn_sqrtf(nc * (1.0f + 0x1p-19f)), 0x1p-120f);
-          const float e2 = (dn32 + ec) * (1.0f + 0x1p-20f);
-          const float r = __builtin_amdgcn_sqrtf(q32(xh, j));
-          const float U = fmaf(r, 1.0f + 0x1p-19f, e2), L = fmaf(r, 1.0f - 0x1p-19f, -e2);
-          bad = bad || !(U == U) || !(L == L);
-          if (r < rbest) {
-            lo_other = fminf(lo_other, lb_best);
-            rbest = r;
-            ub = U;
-            lb_best = L;
-            jb = j;
-          } else {
-            lo_other = fminf(lo_other, L);
-          }
-        }
-        // every other centroid's key is above tau: its distance is at least
-        const float gs = tau - ((thr0 + Dhi) - xl);
-        const float lnc = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gs, 0.0f)), 1.0f - 0x1p-19f, -dn32);
-        c2 = !bad && rbest < INFINITY && lo_other > ub * (1.0f + 0x1p-20f);
-        if (c2) {
-          lab = jb;
-          u0 = ub;
-          l0 = fminf(lo_other, lnc);
-        } else {
-        float x[16];  // fp32 data, converted exactly where used
-#pragma unroll
-        for (int f = 0; f < 16; ++f) x[f] = f < DM ? xr[f >> 2][f & 3] : 0.0f;
-        double sb = INFINITY, rb = INFINITY;
-        int jmin = 0x7fffffff;
-        while (cand) {  // increasing j
-          const int j = __builtin_ctzll(cand);
-          cand &= cand - 1;
-          const double sq = np_sqdist16(x, cs + j * d, d);
-          if (sq < sb) {  // sqrt is monotone: only a smaller square gives a smaller root
-            const double rt = sqrt(sq);
-            sb = sq;
-            if (rt < rb) {
-              rb = rt;
-              jmin = j;
-            }
-          }
-        }
-        lab = jmin >= k ? 0 : jmin;  // every root NaN: np.argmin of all-NaN is 0
-        }
-      }
-      const float w_lab = __shfl(wdn_l, lab);
-      if (live)  // the direct bounds, or none (decided again next step)
-        B.zb[pt] = c2 ? zb_pack(l0, u0, w_lab, (unsigned)lab) : (kZbStale | (unsigned)lab);
-#ifdef CDR_EXPERIMENTS
-      if (B.dbg & 64) continue;  // (timing: no moves from this pass)
-      const unsigned long long tm0 = __builtin_amdgcn_s_memrealtime();
-      tp[6] += 1;
-      tp[7] += __popcll(__ballot(live && lab != ao));
-#endif
-      move(live, pt, ao, lab, xr);
-#ifdef CDR_EXPERIMENTS
-      tp[5] += __builtin_amdgcn_s_memrealtime() - tm0;
-#endif
+      xx = acc.x + acc.y;
     }
+    bool c2;
+    float u0, l0;
+    const int lab = near_tie(live, ao, (unsigned)rec.y, xh, T0, T1, xr, xx, c2, u0, l0);
+    const float w_lab = __shfl(wdn_l, lab);
+    if (live)  // the direct bounds, or none (decided again next step)
+      B.zb[pt] = c2 ? zb_pack(l0, u0, w_lab, (unsigned)lab) : (kZbStale | (unsigned)lab);
+    move(live, pt, ao, lab, xr);
   }
+#endif
   CDR_TP(3);
   if (lane == 0) {
     a.fb_count[wave] = fb_used;
@@ -3158,11 +3364,23 @@ static int screen32bs_blocks_per_cu(int Q, int MT) {
   return nb;
 }
 
-static void screen32bs_launch(int Q, int MT, dim3 grid, hipStream_t s, const S32BArgs& p) {
-#define CDR_S32BS_GO(Q_, M_) \
-  if (Q == Q_ && MT == M_) hipLaunchKernelGGL((screen32bs<Q_, M_>), grid, dim3(256), 0, s, p);
+static void screen32bs_launch(int Q, int MT, dim3 grid, hipStream_t s, const S32BArgs& p,
+                              bool split) {
+#define CDR_S32BS_GO(Q_, M_)                                                                  \
+  if (Q == Q_ && MT == M_) {                                                                  \
+    if (split) hipLaunchKernelGGL((screen32bs<Q_, M_, true>), grid, dim3(256), 0, s, p);      \
+    else hipLaunchKernelGGL((screen32bs<Q_, M_>), grid, dim3(256), 0, s, p);                  \
+  }
   CDR_S32B_ALL(CDR_S32BS_GO)
 #undef CDR_S32BS_GO
+}
+
+// chunks in flight per wave of screen32bz (CDR_S32BZ_PD = 4 | 8 | 12)
+static void screen32bz_launch(dim3 grid, hipStream_t s, const S32BArgs& p) {
+  static const int pd = std::getenv("CDR_S32BZ_PD") ? std::atoi(std::getenv("CDR_S32BZ_PD")) : 8;
+  if (pd == 4) hipLaunchKernelGGL(screen32bz<4>, grid, dim3(256), 0, s, p);
+  else if (pd == 12) hipLaunchKernelGGL(screen32bz<12>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(screen32bz<8>, grid, dim3(256), 0, s, p);
 }
 
 // Prefetch depth of screen32d: CDR_S32D_PD=2|3|4 (comparisons), else the
@@ -3414,6 +3632,9 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
           b.slot_wg = cus;
           for (int q = 0; q < 4; ++q) b.wsl[q] = wenv[q];
         }
+        // contiguous chunk ranges per wave (CDR_S32BS_CONTIG=1)
+        if (std::getenv("CDR_S32BS_CONTIG") && std::atoi(std::getenv("CDR_S32BS_CONTIG")))
+          b.slot_wg = -1;
       }
 #ifdef CDR_EXPERIMENTS
       static unsigned long long* tprof_buf = nullptr;
@@ -3424,9 +3645,28 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       }
 #endif
       if (BS) {
-        snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32bs<%d,%d>", PQ, MT);
+        // split form (CDR_S32BS_FUSED=1: the fused kernel): screen32bz streams
+        // the words and lists the failed points, screen32bs decides the lists
+        const bool split_env =
+            !std::getenv("CDR_S32BS_FUSED") || !std::atoi(std::getenv("CDR_S32BS_FUSED"));
+        b.zl = nullptr;
+        b.zn = nullptr;
+        b.zcap = 0;
+        if (split_env) {
+          b.zcap = ceil_div(bs_max_chunks(b, nwg) * kBChunk, 64) * 64;
+          c.zl.ensure(sizeof(uint32_t) * (size_t)nwaves * (size_t)b.zcap);
+          c.zn.ensure(sizeof(int32_t) * (size_t)nwaves);
+          b.zl = c.zl.as<uint32_t>();
+          b.zn = c.zn.as<int32_t>();
+        }
+        snprintf(c.prof_kernel, sizeof(c.prof_kernel), split_env ? "screen32bs<%d,%d>split" : "screen32bs<%d,%d>",
+                 PQ, MT);
         if (prof) prof_mark(c, 0);
-        screen32bs_launch(PQ, MT, grid, c.stream, b);
+        if (split_env) {
+          screen32bz_launch(grid, c.stream, b);
+          if (prof) prof_mark_sub(c);
+        }
+        screen32bs_launch(PQ, MT, grid, c.stream, b, split_env);
 #ifdef CDR_EXPERIMENTS
         if (tprof_on) {  // per-wave phase times (100 MHz counter), to stderr
           std::vector<unsigned long long> h((size_t)nwaves * 8);

@@ -178,7 +178,7 @@ def sharded_compute_features(manifest: str, access_log: str, ctx, comm: Comm):
     ne_local = int(ctx._ev[0])
     send, handle = comm.exchange_buffer(ne_local * XREC)
     _, counts, mx = ctx.features_exchange_pack(bounds, handle)
-    recv, rhandle, recv_bytes = comm.all_to_all_bytes(send, counts * XREC)
+    recv, rhandle, recv_bytes = comm.fenced(ctx, comm.all_to_all_bytes, send, counts * XREC)
     n_recv = int(recv_bytes.sum()) // XREC
     ctx.features_exchange_unpack(rhandle, n_recv, lo, hi)
     # 3) the owned rows' counters

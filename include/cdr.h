@@ -221,6 +221,10 @@ int cdr_lloyd_stats(cdr_ctx* ctx, int64_t* n_fallback);
  * re-decided from their coordinates (sum)}.                                  */
 int cdr_profile_reset(cdr_ctx* ctx, int32_t enable);
 int cdr_profile_read(cdr_ctx* ctx, double* out);
+/* The same session's steps whose screen ran as two kernels (the split bounded
+ * screen: screen32bz, then screen32bs): out[2] = {ms from the step start to
+ * the end of the first kernel (sum), such steps}.                            */
+int cdr_profile_read_sub(cdr_ctx* ctx, double* out);
 
 /* ---- device-resident Lloyd loop: src/kmeans_plusplus.py:31-48 ----------- */
 /* The same iterations as cdr_lloyd_step + the host's means / reseed / shift,

@@ -214,6 +214,7 @@ class DeviceSeedShard(OracleShard):
     def __init__(self, X, fail_at=None):
         super().__init__(X)
         self.fail_at = fail_at
+        self.phases = 0
 
     def _red(self, red, hit, fail, nan):
         r = red.view(np.float64)
@@ -238,6 +239,11 @@ class DeviceSeedShard(OracleShard):
     def seed_shard_begin(self, row_begin, n_total, nranks, rank, first, k, u, red):
         self.rb, self.W, self.r, self.k, self.u = row_begin, nranks, rank, k, np.asarray(u)
         self.nbmax = -(-(-(-n_total // 8192)) // nranks)
+        # the kernel's layout checks (csrc/seed.hip seed_shard_begin)
+        if row_begin % 8192 != 0 and self.X.shape[0] > 0:
+            raise ValueError("shards must start on an 8192-row block")
+        if -(-self.X.shape[0] // 8192) > self.nbmax:
+            raise ValueError("shard larger than n_total / nranks blocks")
         self.step, self.fail, self.nan, self.nohit = 1, False, False, False
         self.picks = np.zeros(k, dtype=np.int64)
         self.cents = []
@@ -304,19 +310,28 @@ class DeviceSeedShard(OracleShard):
         return self.picks, np.array(self.cents), status
 
 
-def _seed_worker(rank, world, port, out_dir, fail_at):
+def _seed_worker(rank, world, port, out_dir, fail_at, starts=None, device=True):
     import torch.distributed as dist
 
     from cdr_dist import Comm, seed_sharded, shard_rows
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    begin, n_local = shard_rows(N_TOTAL, world, rank)
+    if starts is None:
+        begin, n_local = shard_rows(N_TOTAL, world, rank)
+    else:  # a whole-block layout of the caller's choosing
+        begin = starts[rank]
+        n_local = (starts[rank + 1] if rank + 1 < world else N_TOTAL) - begin
     shard = DeviceSeedShard(synth.generate(N_TOTAL, begin, n_local, D, K, 9),
                             fail_at if rank == world - 1 else None)
     comm = Comm(dist, None)
     C = seed_sharded(shard, comm, begin, N_TOTAL, K, random_state=42)
-    assert shard.phases == 3 * (K - 1)  # every step ran the three device phases
+    if device:
+        assert shard.phases == 3 * (K - 1)  # every step ran the three device phases
+    else:  # the layout does not fit the device protocol: every rank took the host one
+        assert shard.phases == 0
+        if rank > 0:
+            assert shard.begun == shard.ended == K - 1
     assert getattr(comm, "seed_fallbacks", 0) == (1 if fail_at else 0)
     if fail_at and rank > 0:  # the host protocol redid the seeding through the programs
         assert shard.begun == shard.ended == K - 1
@@ -341,6 +356,39 @@ def test_device_seeding_protocol_matches_reference(tmp_path, world, fail_at):
     C0 = ko.kmeans_plusplus_init(X, K, random_state=42)
     for r in range(world):
         np.testing.assert_array_equal(np.load(tmp_path / f"C{r}.npy"), C0)
+
+
+@pytest.mark.parametrize("starts,device", [((0, 8192), False), ((0, 3 * 8192), False),
+                                           ((0, 8192, 2 * 8192), True)],
+                         ids=["1+3blocks", "3+1blocks", "world3-1+1+2blocks"])
+def test_seeding_unbalanced_whole_block_layout(tmp_path, starts, device):
+    """a whole-block layout other than shard_rows' (a
+    shard over ceil(blocks / world) blocks) used to pass the device
+    protocol's check on some ranks and raise on others (a hang in the
+    collective); seed_sharded now decides from the all-gathered offsets on
+    every rank and runs the host protocol everywhere, with the reference's
+    centres.  A layout other than shard_rows' that fits (world 3: 1 + 1 + 2
+    blocks of 4, at most ceil(4 / 3) = 2 each) keeps the device protocol."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    world = len(starts)
+    mp.spawn(_seed_worker, args=(world, _free_port(), str(tmp_path), None, list(starts), device),
+             nprocs=world, join=True)
+    X = synth.generate(N_TOTAL, 0, N_TOTAL, D, K, 9)
+    C0 = ko.kmeans_plusplus_init(X, K, random_state=42)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"C{r}.npy"), C0)
+
+
+def test_device_seed_layout_ok():
+    from cdr_dist import device_seed_layout_ok, shard_rows
+
+    for n in (8192, 5 * 8192 + 7, 100_000_000, 12_500_000 * 8):
+        for w in (1, 2, 3, 8):
+            assert device_seed_layout_ok([shard_rows(n, w, r)[0] for r in range(w)], n, w)
+    assert not device_seed_layout_ok([0, 8192], 4 * 8192, 2)       # 1 + 3 blocks
+    assert not device_seed_layout_ok([0, 100], 4 * 8192, 2)        # not block-aligned
+    assert not device_seed_layout_ok([8192, 0], 4 * 8192, 2)       # not in rank order
+    assert device_seed_layout_ok([0, 2 * 8192], 3 * 8192 + 5, 2)   # 2 + 2 (partial) blocks
 
 
 class StatsShard:

@@ -181,24 +181,33 @@ def _every_label_exact(ctx, monkeypatch, n, d, k, steps):
 
 
 def test_config3_every_label_exact(ctx, monkeypatch):
-    """all 100M labels of the last of 6 device-loop steps (the
-    bounded DELTA screen screen32b, the bench's timed kernel, after a full
-    step and the bound rebuild) equal the exact fp64 NumPy-order assignment of
-    the same centroids (assign_exact_all on every point, CDR_EXACT_ASSIGN),
-    and so do the int64 sums; a host-plan DELTA step (pruned screen32p +
-    queued k-way MFMA screen + fixup32) on the same centroids agrees."""
+    """all 100M labels of the last of 25 device-loop steps
+    (the bounded DELTA screen, the bench's timed kernel, after a full step,
+    the bound rebuild and 22 more bounded steps: the driver's last timed step
+    at --warmup 5 --steps 20, where the drift bounds have accumulated longest)
+    equal the exact fp64 NumPy-order assignment of the same centroids
+    (assign_exact_all on every point, CDR_EXACT_ASSIGN), and so do the int64
+    sums; a host-plan DELTA step (pruned screen32p + queued k-way MFMA screen
+    + fixup32) on the same centroids agrees."""
     n, d, k = 100_000_000, 16, 64
-    C_prev, lab = _every_label_exact(ctx, monkeypatch, n, d, k, 6)
+    C_prev, lab = _every_label_exact(ctx, monkeypatch, n, d, k, 25)
     ctx.lloyd_step(C_prev)
     np.testing.assert_array_equal(ctx.labels(), lab)
 
 
+def test_config3_every_label_exact_fused_kernel(ctx, monkeypatch):
+    """The same at 12 steps with the fused bounded screen (one kernel streams
+    the bound words and decides the failed points, CDR_S32BS_FUSED=1)."""
+    monkeypatch.setenv("CDR_S32BS_FUSED", "1")
+    _every_label_exact(ctx, monkeypatch, 100_000_000, 16, 64, 12)
+
+
 def test_config2_every_label_exact(ctx, monkeypatch):
-    """BASELINE config 2 (10M x 8, k = 16) at full size,
-    8 device-loop steps (full screen, bound rebuild, 6 bounded DELTA steps:
-    the bench's timed kernel, d <= 8 form): every label and the int64 sums
-    equal the exact fp64 NumPy-order assignment."""
-    _every_label_exact(ctx, monkeypatch, 10_000_000, 8, 16, 8)
+    """BASELINE config 2 (10M x 8, k = 16) at full
+    size, 20 device-loop steps (full screen, bound rebuild, 18 bounded DELTA
+    steps: the bench's timed kernel, d <= 8 form): every label and the int64
+    sums equal the exact fp64 NumPy-order assignment."""
+    _every_label_exact(ctx, monkeypatch, 10_000_000, 8, 16, 20)
 
 
 def test_config5_full_size_and_scoring(ctx):
@@ -430,7 +439,9 @@ def _mirrored(n, d, k, seed):
                                         (120_000, 13, 50, "blobs"), (90_000, 3, 7, "uniform"),
                                         (160_000, 16, 64, "mirror"), (100_000, 8, 32, "mirror"),
                                         (160_000, 16, 64, "mirror-queue"),
-                                        (150_000, 8, 16, "uniform-queue")])
+                                        (150_000, 8, 16, "uniform-queue"),
+                                        (160_000, 16, 64, "mirror-fused"),
+                                        (150_000, 8, 16, "uniform-fused")])
 def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     """screen32b: after the bound rebuild a point keeps its
     label without its coordinates being read when its stored drift bound
@@ -438,11 +449,14 @@ def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     data (every step moves points across slowly moving boundaries) and on
     mirrored data with exact and near ties: labels and centroids equal the
     oracle's every time, and the bounded steps re-read fewer points than
-    they kept.  The default kernel decides in registers (screen32bs); the
-    "-queue" cases run screen32b (LDS queue + fused fixup, CDR_S32B_SPLIT=0)."""
+    they kept.  The default kernels decide in registers (screen32bz lists the
+    failed points, screen32bs decides them); the "-fused" cases run the one
+    fused screen32bs kernel (CDR_S32BS_FUSED=1), the "-queue" cases screen32b
+    (LDS queue + fused fixup, CDR_S32B_SPLIT=0)."""
     monkeypatch.setenv("CDR_BOUNDS", "1")
     queue = kind.endswith("-queue")
-    kind = kind.replace("-queue", "")
+    monkeypatch.setenv("CDR_S32BS_FUSED", "1" if kind.endswith("-fused") else "0")
+    kind = kind.replace("-queue", "").replace("-fused", "")
     monkeypatch.setenv("CDR_S32B_SPLIT", "0" if queue else "1")
     if kind == "blobs":
         X = synth.generate(n, 0, n, d, k, 17 * n + d)
