@@ -1779,9 +1779,6 @@ __global__ __launch_bounds__(256, 5) void screen32p(S32PArgs a) {
 #ifndef CDR_S32BS_LAZY
 #define CDR_S32BS_LAZY 1  // screen32bs: phase 2 interleaved with the stream (0: in bursts)
 #endif
-#ifndef CDR_S32BS_DEFER
-#define CDR_S32BS_DEFER 0  // screen32bs: near ties listed and resolved after the last batch (1)
-#endif
 constexpr int kBChunk = 256;  // points per wave-chunk of the bound stream (4 per lane)
 constexpr int kBList = 512;   // per-wave LDS list of the points whose bound failed
 constexpr int kBPD = 4;       // chunks in flight per wave (phase 1)
@@ -2237,7 +2234,7 @@ __global__ __launch_bounds__(256, 4) void screen32b(S32BArgs B) {
 
 // ---------------------------------------------------------------------------
 // screen32bz: phase 1 of the bounded screen as its own launch (the split form,
-// the default; CDR_S32BS_FUSED=1 runs the fused kernel).  Streams every
+// CDR_S32BS_SPLIT=1; the fused kernel is the default).  Streams every
 // point's bound word (4 per lane per 1 KiB chunk, KPD chunks in flight per
 // wave) and lists the points whose bound fails in the
 // wave's region of B.zl, in screen32bs's entry format (chunk iteration << 14 |
@@ -2358,6 +2355,10 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #endif
   constexpr int QH = FixDims<Q>::QH;
   constexpr int DM = FixDims<Q>::DM;
+  // near ties: the fused kernel lists them and resolves them after its last
+  // batch (inlined in the streaming loop, the resolver costs registers and
+  // code the stream needs); the split decide kernel resolves them at once
+  constexpr bool DEFER = !SPLIT;
   if (a.gate && a.gate[0] == 0) return;
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -2738,7 +2739,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       B.zb[pt] = zb_pack(l0, u0, w_lab, (unsigned)label);
     }
     const unsigned long long um = __ballot(unc);
-#if CDR_S32BS_DEFER
+    if constexpr (DEFER) {
     // uncertified (near ties): the wave's list {point, best key}, resolved
     // after the workgroup's last batch
     if (um) {
@@ -2750,7 +2751,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       fb_used += __popcll(um);
     }
     move(need && cert, pt, ao, label, nullptr);
-#else
+    } else {
     // uncertified (near ties, ~1 in 5 re-read points at config 3) resolved
     // now, while the row, the split operands and the best key are in
     // registers: no list, no dependent re-gather of the row and label
@@ -2774,7 +2775,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       fb_used += __popcll(um);
     }
     move(need, pt, ao, labf, g.x);
-#endif
+    }
   };
 
   // ---- phase 2: the listed points, 64 per batch, two batches in flight ----
@@ -2974,7 +2975,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #ifdef CDR_EXPERIMENTS
   if (B.dbg & 2) fb_used = 0;  // (timing: no exact pass)
 #endif
-#if CDR_S32BS_DEFER
+  if constexpr (DEFER) {
   for (int e0 = 0; e0 < fb_used; e0 += 64) {
     const int e = e0 + lane;
     const bool live = e < fb_used;
@@ -3006,7 +3007,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       B.zb[pt] = c2 ? zb_pack(l0, u0, w_lab, (unsigned)lab) : (kZbStale | (unsigned)lab);
     move(live, pt, ao, lab, xr);
   }
-#endif
+  }  // DEFER
   CDR_TP(3);
   if (lane == 0) {
     a.fb_count[wave] = fb_used;
@@ -3645,10 +3646,13 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       }
 #endif
       if (BS) {
-        // split form (CDR_S32BS_FUSED=1: the fused kernel): screen32bz streams
-        // the words and lists the failed points, screen32bs decides the lists
+        // split form (CDR_S32BS_SPLIT=1; default: the fused kernel): screen32bz
+        // streams the words and lists the failed points, screen32bs<.., true>
+        // decides the lists.  Measured at config 3 (profiles/r05_split_ab.txt):
+        // the stream alone takes ~80 us and the decisions ~100-130 us as their
+        // own launch, so the fused kernel (~165-180 us) stays the default
         const bool split_env =
-            !std::getenv("CDR_S32BS_FUSED") || !std::atoi(std::getenv("CDR_S32BS_FUSED"));
+            std::getenv("CDR_S32BS_SPLIT") && std::atoi(std::getenv("CDR_S32BS_SPLIT"));
         b.zl = nullptr;
         b.zn = nullptr;
         b.zcap = 0;

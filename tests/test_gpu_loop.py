@@ -195,10 +195,11 @@ def test_config3_every_label_exact(ctx, monkeypatch):
     np.testing.assert_array_equal(ctx.labels(), lab)
 
 
-def test_config3_every_label_exact_fused_kernel(ctx, monkeypatch):
-    """The same at 12 steps with the fused bounded screen (one kernel streams
-    the bound words and decides the failed points, CDR_S32BS_FUSED=1)."""
-    monkeypatch.setenv("CDR_S32BS_FUSED", "1")
+def test_config3_every_label_exact_split_kernels(ctx, monkeypatch):
+    """The same at 12 steps with the split bounded screen (screen32bz streams
+    the bound words and lists the failed points, screen32bs decides the
+    lists and resolves near ties at once, CDR_S32BS_SPLIT=1)."""
+    monkeypatch.setenv("CDR_S32BS_SPLIT", "1")
     _every_label_exact(ctx, monkeypatch, 100_000_000, 16, 64, 12)
 
 
@@ -440,8 +441,8 @@ def _mirrored(n, d, k, seed):
                                         (160_000, 16, 64, "mirror"), (100_000, 8, 32, "mirror"),
                                         (160_000, 16, 64, "mirror-queue"),
                                         (150_000, 8, 16, "uniform-queue"),
-                                        (160_000, 16, 64, "mirror-fused"),
-                                        (150_000, 8, 16, "uniform-fused")])
+                                        (160_000, 16, 64, "mirror-split"),
+                                        (150_000, 8, 16, "uniform-split")])
 def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     """screen32b: after the bound rebuild a point keeps its
     label without its coordinates being read when its stored drift bound
@@ -449,14 +450,14 @@ def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     data (every step moves points across slowly moving boundaries) and on
     mirrored data with exact and near ties: labels and centroids equal the
     oracle's every time, and the bounded steps re-read fewer points than
-    they kept.  The default kernels decide in registers (screen32bz lists the
-    failed points, screen32bs decides them); the "-fused" cases run the one
-    fused screen32bs kernel (CDR_S32BS_FUSED=1), the "-queue" cases screen32b
-    (LDS queue + fused fixup, CDR_S32B_SPLIT=0)."""
+    they kept.  The default kernel decides in registers (screen32bs); the
+    "-split" cases run it as two launches (screen32bz lists the failed
+    points, screen32bs decides the lists, CDR_S32BS_SPLIT=1), the "-queue"
+    cases screen32b (LDS queue + fused fixup, CDR_S32B_SPLIT=0)."""
     monkeypatch.setenv("CDR_BOUNDS", "1")
     queue = kind.endswith("-queue")
-    monkeypatch.setenv("CDR_S32BS_FUSED", "1" if kind.endswith("-fused") else "0")
-    kind = kind.replace("-queue", "").replace("-fused", "")
+    monkeypatch.setenv("CDR_S32BS_SPLIT", "1" if kind.endswith("-split") else "0")
+    kind = kind.replace("-queue", "").replace("-split", "")
     monkeypatch.setenv("CDR_S32B_SPLIT", "0" if queue else "1")
     if kind == "blobs":
         X = synth.generate(n, 0, n, d, k, 17 * n + d)
