@@ -419,11 +419,15 @@ def f64_bench(args, world: int, rank: int, json_fd: int) -> None:
     ctx.close()
 
 
-def pmc_traffic(config: str, n_local: int, kname: str | None = None):
+def pmc_traffic(config: str, n_local: int, kname: str | None = None, steps=None):
     """HBM bytes per launch of the config's dominant kernel from the committed
     PMC passes (profiles/pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, the
     MI355X_MICROARCH.md gfx950 correction), when they were taken on this size
-    and, if given, this kernel."""
+    and, if given, this kernel.  Records with one row per device-loop step
+    (per_step_read / per_step_write from first_step on: the bounded screen
+    re-reads fewer points as the run converges) are averaged over exactly the
+    steps `steps` whose kernel times the run measured; a step outside the
+    table gives None (no extrapolation)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
@@ -432,8 +436,16 @@ def pmc_traffic(config: str, n_local: int, kname: str | None = None):
     r = rec.get(config)
     if not r or int(r.get("n_local", -1)) != n_local:
         return None
-    if kname is not None and not str(r.get("kernel", "")).startswith(kname.split("<")[0] + "<"):
+    if kname is not None and not kname.startswith(str(r.get("kernel", "")).split("+")[0].split("<")[0]):
         return None
+    if "per_step_read" in r:
+        if not steps:
+            return None
+        first, rd, wr = int(r["first_step"]), r["per_step_read"], r["per_step_write"]
+        vals = [rd[s - first] + wr[s - first] for s in steps if 0 <= s - first < min(len(rd), len(wr))]
+        if len(vals) != len(steps):
+            return None
+        return float(sum(vals) / len(vals))
     return float(r["hbm_bytes_per_launch"])
 
 
@@ -623,7 +635,10 @@ def main() -> None:
     screen_ms = prof["screen_ms"] / max(prof["steps"], 1)
     step_kernel_ms = prof["step_ms"] / max(prof["steps"], 1)
     alg_bytes = n_local * (4 * d + 4)
-    traffic = pmc_traffic(args.config, n_local, kname)
+    # the loop steps whose kernels the HIP events timed: every 4th of the
+    # timed region, from the first (loop step warmup + 1)
+    prof_steps = list(range(args.warmup + 1, args.warmup + args.steps + 1, 4))[:prof["steps"]]
+    traffic = pmc_traffic(args.config, n_local, kname, prof_steps)
     value = n_total * args.steps / elapsed
     if kname.startswith("screen_big"):
         # large-k regime: the L1 screen is the dense contraction 2 n k d on
@@ -652,6 +667,7 @@ def main() -> None:
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                     "bytes_basis": "pmc" if traffic else "kernel_bytes_per_launch",
                     "kernel": kname, "kernel_ms": screen_ms, "kernel_bytes_per_launch": kb,
+                    "timed_steps": prof_steps,
                     "alg_bytes_per_launch": alg_bytes, "effective_achieved": eff,
                     "effective_frac": eff / HBM_PEAK_GBPS}
     # (the fallback counter accumulates over every profiled-session step)

@@ -85,6 +85,10 @@ SIGNATURES = {
     "cdr_profile_reset": ([_P, _I32], None),
     "cdr_profile_read": ([_P, _P], None),
     "cdr_profile_read_sub": ([_P, _P], None),
+    "cdr_f64s_begin": ([_P, _P, _I32, _I32, _I32, _P, _P], None),
+    "cdr_f64s_build": ([_P, _P, _P], None),
+    "cdr_f64s_finish": ([_P, _P, _P, _P, _P, _P], None),
+    "cdr_f64s_chain": ([_P, _P], None),
     "cdr_profile_kernel": ([_P, _P, _I32], None),
     "cdr_points_sqdev": ([_P, _P, _PF64], None),
     "cdr_lloyd_begin": ([_P, _P, _I32, _F64, _I32, _P, _F64], None),
@@ -459,6 +463,33 @@ class Context:
         counts = np.empty(k, dtype=np.int64)
         _check(self._lib.cdr_lloyd_step_f64(self._h, _ptr(C), k, _ptr(sums), _ptr(counts)))
         return sums, counts
+
+    # -- sharded F64 sums (include/cdr.h cdr_f64s_*; cdr_dist.f64_sharded_sums) --
+    def f64s_begin(self, C: np.ndarray, nranks: int, rank: int, tot_buf: int) -> np.ndarray:
+        """Assignment of this shard + its approximate totals into its slot of
+        the device buffer tot_buf; returns (tot slot bytes, program slot bytes)."""
+        C = np.ascontiguousarray(C, dtype=np.float64)
+        self._f64s_kd = C.shape
+        sizes = np.zeros(2, dtype=np.int64)
+        _check(self._lib.cdr_f64s_begin(self._h, _ptr(C), C.shape[0], int(nranks), int(rank),
+                                        _P(tot_buf), _ptr(sizes)))
+        return sizes
+
+    def f64s_build(self, tot_buf: int, prog_buf: int) -> None:
+        _check(self._lib.cdr_f64s_build(self._h, _P(tot_buf), _P(prog_buf)))
+
+    def f64s_finish(self, tot_buf: int, prog_buf: int):
+        """(sums (k, d), counts (k,), status: 0 exact, 1 run the rank chain)."""
+        k, d = self._f64s_kd
+        sums = np.empty((k, d), dtype=np.float64)
+        counts = np.empty(k, dtype=np.int64)
+        st = ctypes.c_int32(0)
+        _check(self._lib.cdr_f64s_finish(self._h, _P(tot_buf), _P(prog_buf), _ptr(sums),
+                                         _ptr(counts), ctypes.byref(st)))
+        return sums, counts, int(st.value)
+
+    def f64s_chain(self, chain_buf: int) -> None:
+        _check(self._lib.cdr_f64s_chain(self._h, _P(chain_buf)))
 
     def lloyd_step_f32r(self, C: np.ndarray):
         """The reference's float32 step: (sequential fp32 sums as float64

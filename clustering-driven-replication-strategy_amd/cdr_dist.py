@@ -266,6 +266,16 @@ class Comm:
         t = buf if self.device is not None else torch.from_numpy(buf)
         self.dist.all_reduce(t.view(torch.float64))
 
+    def bcast_buffer(self, buf, src: int) -> None:
+        """In-place broadcast of a byte buffer (device tensor or host array)
+        from rank src."""
+        if not self.dist:
+            return
+        import torch
+
+        t = buf if self.device is not None else torch.from_numpy(buf)
+        self.dist.broadcast(t, src)
+
     def bcast(self, arr: np.ndarray, src: int) -> np.ndarray:
         if not self.dist:
             return arr
@@ -598,17 +608,59 @@ def device_lloyd(ctx, C, max_iter: int, tol: float, reseed_row, n_total: int,
     return run.finish()
 
 
+def f64_sharded_sums(ctx, comm: Comm, C: np.ndarray):
+    """The exact sequential cluster sums of an F64 Lloyd step over rows sharded
+    in rank order (src/kmeans_plusplus.py:33-41: labels from C, then
+    X[labels == j] summed row after row, as NumPy's mean does), every rank
+    getting (sums (k, d), counts (k,)).  Two all-gathers per step: the
+    shards' approximate totals, then their programs (include/cdr.h
+    cdr_f64s_*), composed in rank order on every rank; when a program's
+    guess does not hold (every rank sees it), the exact rank chain: each
+    shard walks from the exact entry in turn, broadcasting its exit."""
+    k, d = C.shape
+    kd = k * d
+    tot, htot = comm.buffer(comm.world * 8 * (kd + k))
+    sizes = ctx.f64s_begin(C, comm.world, comm.rank, htot)
+    comm.fenced(ctx, comm.allgather_slots, tot, int(sizes[0]))
+    prog, hprog = comm.buffer(comm.world * int(sizes[1]))
+    ctx.f64s_build(htot, hprog)
+    comm.fenced(ctx, comm.allgather_slots, prog, int(sizes[1]))
+    sums, counts, status = ctx.f64s_finish(htot, hprog)
+    if status:
+        comm.f64_chains = getattr(comm, "f64_chains", 0) + 1
+        chain, hchain = comm.buffer(16 * kd)
+        if comm.device is not None:
+            chain.zero_()
+        else:
+            chain[:] = 0
+        for r in range(comm.world):
+            if comm.rank == r:
+                ctx.f64s_chain(hchain)
+            comm.fenced(ctx, comm.bcast_buffer, chain, r)
+        if comm.device is not None:
+            import torch
+
+            sums = chain.view(torch.float64)[:kd].cpu().numpy().reshape(k, d)
+        else:
+            sums = chain.view(np.float64)[:kd].copy().reshape(k, d)
+    return sums, counts
+
+
 class ShardedLloyd:
-    """Lloyd iterations over sharded F32X points with one all-reduce per step."""
+    """Lloyd iterations over sharded points: F32X (grid) points with one
+    int64 all-reduce per step (or the device-resident loop); F64 points with
+    the exact sharded sequential sums (f64_sharded_sums) and the host
+    forming the means, as src/kmeans_plusplus.py:37-48 does."""
 
     def __init__(self, ctx, comm: Comm, n_total: int, row_begin: int):
         ensure_unified(ctx, comm, n_total)
         info = ctx.info()
-        if info["mode"] != 1:
-            raise NotImplementedError("sharded Lloyd needs F32X (grid) points")
+        if info["mode"] not in (1, 2):
+            raise NotImplementedError("sharded Lloyd needs loaded points")
         self.ctx, self.comm = ctx, comm
         self.n_total, self.row_begin = n_total, row_begin
         self.d, self.S = info["d"], info["scale_bits"]
+        self.f64 = info["mode"] == 2
         self._dev_buf = None
 
     def partials(self, C: np.ndarray) -> np.ndarray:
@@ -627,9 +679,12 @@ class ShardedLloyd:
     def step(self, C: np.ndarray, reseed_row) -> tuple[np.ndarray, float]:
         """One iteration; returns (new centroids, shift)."""
         k, d = C.shape
-        acc = self.partials(C)
-        counts = acc[:, d]
-        sums = np.ldexp(acc[:, :d].astype(np.float64), -self.S)
+        if self.f64:
+            sums, counts = f64_sharded_sums(self.ctx, self.comm, np.asarray(C, dtype=np.float64))
+        else:
+            acc = self.partials(C)
+            counts = acc[:, d]
+            sums = np.ldexp(acc[:, :d].astype(np.float64), -self.S)
         with np.errstate(invalid="ignore", divide="ignore"):
             new = sums / counts[:, None].astype(np.float64)
         for j in np.flatnonzero(counts == 0):  # j order, as the reference draws
@@ -643,7 +698,10 @@ class ShardedLloyd:
         return _fetch_row(self.ctx, self.comm, owner, gidx - int(offs[owner]), self.d)
 
     def run(self, C: np.ndarray, max_iter: int, tol: float = 1e-4):
-        """max_iter Lloyd steps (fewer on convergence) on the device loop."""
+        """max_iter Lloyd steps (fewer on convergence): the device loop for
+        F32X points, the host-driven sharded F64 steps otherwise."""
+        if self.f64:
+            return self.run_host(C, max_iter, tol)
         C, self.last_status = device_lloyd(self.ctx, C, max_iter, tol, self.row, self.n_total,
                                            self.comm)
         return C

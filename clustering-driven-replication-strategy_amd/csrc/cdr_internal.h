@@ -154,6 +154,8 @@ struct Ctx {
   // the one the current transfers use, the next step's), valid for (k, blocks)
   DevBuf f64x_E2;
   DevBuf f64x_ord;  // f64_step_fused: each block's rows in cluster order (uint8 offsets)
+  DevBuf f64s_off;  // sharded F64 sums: earlier shards' approximate totals, end binades
+  int32_t f64s_k = 0, f64s_nranks = 0, f64s_rank = 0;  // cdr_f64s_begin's step
   bool f64x_e_ok = false;
   int f64x_e_cur = 0, f64x_e_k = 0;
   int64_t f64x_e_nb = 0;
@@ -349,6 +351,13 @@ bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max
 // exact sequential-order F64 centroid sums in parallel (f64sum.hip); false =
 // shape not covered (d < 2 or k > 64)
 bool f64_sums_parallel(Ctx& c, int k, double* d_sums, bool pre = false);
+// sharded F64 sums (f64sum.hip; include/cdr.h cdr_f64s_*)
+int f64s_cap();
+bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot);
+void f64s_build(Ctx& c, int k, int nranks, int rank, const double* tot_all, void* prog_all);
+void f64s_compose_all(Ctx& c, int k, int nranks, const double* tot_all, const void* prog_all,
+                      double* d_sums, long long* d_counts, int* d_status);
+void f64s_chain_walk(Ctx& c, int k, double* chain);
 bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
                     unsigned long long* d_counts, bool prof);
 void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,

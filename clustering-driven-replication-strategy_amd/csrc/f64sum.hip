@@ -179,12 +179,13 @@ __global__ __launch_bounds__(256) void f64_predict_a(const double* __restrict__ 
   if (lane == 0) GS[w] = v;
 }
 __global__ __launch_bounds__(256) void f64_predict_b(double* __restrict__ GS, int kd,
-                                                     int64_t ng) {
+                                                     int64_t ng, const double* __restrict__ off) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= kd) return;
   double* gs = GS + (int64_t)t * ng;
-  double carry = 0.0;
+  // a shard of sharded rows starts from the earlier shards' approximate sum
+  double carry = off ? off[t] : 0.0;
   for (int64_t g0 = 0; g0 < ng; g0 += 64) {
     const int64_t g = g0 + lane;
     const double v = g < ng ? gs[g] : 0.0;
@@ -348,7 +349,8 @@ struct GXfer {
 __global__ __launch_bounds__(256) void f64_group(const unsigned* __restrict__ cnt,
                                                  const int* __restrict__ E,
                                                  const Xfer* __restrict__ T, int64_t nb, int d,
-                                                 int k, int64_t ng, GXfer* __restrict__ G) {
+                                                 int k, int64_t ng, GXfer* __restrict__ G,
+                                                 const int* __restrict__ Eend) {
   const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int kd = k * d;
@@ -364,7 +366,11 @@ __global__ __launch_bounds__(256) void f64_group(const unsigned* __restrict__ cn
   const unsigned long long live = __ballot(c != 0);
   int e0 = kENone;
   if (live) e0 = __shfl(el, __ffsll((long long)live) - 1);
-  const bool ok = c == 0 || (e0 != kENone && el == e0 && !(xl.flags & 4));
+  // Eend (sharded programs, f64s_program): a block is usable only when the
+  // predicted binade at its end (the next block's start; Eend[t] after the
+  // last block) is its start binade too, so no crossing falls inside it
+  const int eafter = !Eend ? e0 : (bl + 1 < nb ? E[(int64_t)t * nb + bl + 1] : Eend[t]);
+  const bool ok = c == 0 || (e0 != kENone && el == e0 && !(xl.flags & 4) && eafter == e0);
   const bool usable = live && __ballot(!ok) == 0ull;
   XferC x;
   const bool on = c != 0;
@@ -403,15 +409,18 @@ __global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t
                                                 const GXfer* __restrict__ G, int64_t ng,
                                                 double* __restrict__ sums,
                                                 long long* __restrict__ walked,
-                                                long long* __restrict__ prof) {
+                                                long long* __restrict__ prof,
+                                                const double* __restrict__ entry) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= k * d) return;
   const int j = t / d, f = t % d;
   constexpr int MB = SumTraits<TA>::MB, kMinE = SumTraits<TA>::kMinE;
   constexpr long long kTop = 1ll << (MB + 1);
-  double s = 0.0;  // (a T value)
-  bool any = false;  // NumPy's reduce starts from the first selected row
+  // (entry: a shard of sharded rows continues the earlier shards' exact
+  // running values {s [k d], any [k d]}; else the sequence starts here)
+  double s = entry ? entry[t] : 0.0;  // (a T value)
+  bool any = entry ? entry[k * d + t] != 0.0 : false;  // NumPy's reduce starts from the first selected row
   long long nwalk = 0;
   long long pc_el = 0, pc_slow = 0, n_slow = 0;  // CDR_F64_PROF: cycles
   const long long pc0 = prof ? (long long)clock64() : 0;
@@ -613,6 +622,7 @@ __global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t
   if (lane == 0) {
     sums[(int64_t)j * d + f] = s;
     walked[t] = nwalk;
+    if (entry) sums[k * d + t] = any ? 1.0 : 0.0;  // (the exit state for the next shard)
   }
 }
 
@@ -871,9 +881,20 @@ __global__ __launch_bounds__(256) void count_total_kernel(const unsigned* __rest
 // sums (k, d) on the device, exact sequential row-order fp64 sums; returns
 // false when the shape is not covered (d < 2, k > 64): the caller runs the
 // serial kernel.
+// Sharded F64 sums (f64s_*): the earlier shards' approximate sums (off, k d),
+// the predicted binade at this shard's end (Eend, k d), and either the walk
+// from the exact entry state `entry` (rank 0: zeros) or no walk (the other
+// ranks build programs from the transfers and group compositions instead).
+struct F64Shard {
+  const double* off = nullptr;
+  const int* Eend = nullptr;
+  const double* entry = nullptr;
+  bool walk = true;
+};
 template <typename TA, typename S>
 static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
-                             const int* Ewalk, bool have_T, const unsigned char* ordr = nullptr);
+                             const int* Ewalk, bool have_T, const unsigned char* ordr = nullptr,
+                             const F64Shard& sh = F64Shard());
 
 // TA: the summed (arithmetic) type; S: the storage type of X.  pre: the
 // block sums and counts (f64x_A, f64x_cnt) were already written by the
@@ -903,7 +924,8 @@ static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums, bool pre = 
 // group compositions and the walk under Ewalk.
 template <typename TA, typename S>
 static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
-                             const int* Ewalk, bool have_T, const unsigned char* ordr) {
+                             const int* Ewalk, bool have_T, const unsigned char* ordr,
+                             const F64Shard& sh) {
   const int d = c.d;
   const int64_t n = c.n, nb = ceil_div(n, kFB);
   const size_t kd = (size_t)k * d;
@@ -913,7 +935,7 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
   hipLaunchKernelGGL(f64_predict_a, gwaves, dim3(256), 0, c.stream, c.f64x_A.as<double>(),
                      c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>());
   hipLaunchKernelGGL(f64_predict_b, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
-                     c.f64x_GS.as<double>(), (int)kd, ng);
+                     c.f64x_GS.as<double>(), (int)kd, ng, sh.off);
   hipLaunchKernelGGL(f64_predict_c, gwaves, dim3(256), 0, c.stream, c.f64x_A.as<double>(),
                      c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>(), Enew);
   HIP_CHECK(hipGetLastError());
@@ -945,13 +967,14 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
   if (prof_on) c.f64x_prof.ensure(sizeof(long long) * 4 * kd);
   hipLaunchKernelGGL(f64_group, dim3(ceil_div((int64_t)kd * ng, (int64_t)4)), dim3(256), 0,
                      c.stream, c.f64x_cnt.as<unsigned>(), Ewalk,
-                     c.f64x_T.as<Xfer>(), nb, d, k, ng, c.f64x_G.as<GXfer>());
+                     c.f64x_T.as<Xfer>(), nb, d, k, ng, c.f64x_G.as<GXfer>(), sh.Eend);
   HIP_CHECK(hipGetLastError());
+  if (!sh.walk) return true;
   hipLaunchKernelGGL((f64_walk<TA, S>), dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
                      X, n, c.n_pad, d, k, nb, c.labels.as<int32_t>(),
                      c.f64x_cnt.as<unsigned>(), Ewalk, c.f64x_T.as<Xfer>(),
                      c.f64x_G.as<GXfer>(), ng, d_sums, c.f64x_walk.as<long long>(),
-                     prof_on ? c.f64x_prof.as<long long>() : nullptr);
+                     prof_on ? c.f64x_prof.as<long long>() : nullptr, sh.entry);
   HIP_CHECK(hipGetLastError());
   if (prof_on) {
     std::vector<long long> h(4 * kd);
@@ -1065,6 +1088,364 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   c.f64x_e_nb = nb;
   return true;
 }
+// ---------------------------------------------------------------------------
+// Sharded F64 sums (include/cdr.h cdr_f64s_*).  Rows are sharded in rank
+// order, so sums[j][f] is the sequential sum over shard 0's members, then
+// shard 1's, ...: every shard but the first needs the exact running value the
+// earlier shards leave, which is not known until they are done.  Instead of a
+// rank chain, every shard describes its part of each sequence as a PROGRAM
+// built from approximate quantities only, and every rank runs all programs in
+// rank order from the exact start:
+//   * each rank all-gathers its approximate per-sequence totals (any order)
+//     and member counts; a shard's blocks get their binade predictions from
+//     the earlier shards' approximate total + its own approximate prefix
+//     (f64_predict_*, offset), and their transfers under them (f64_transfer);
+//   * rank 0 starts from the exact start (nothing), so it walks (f64_walk)
+//     and publishes the exact result: CONST {s, any};
+//   * rank r > 0 publishes, per sequence, RUN {e, D0, D1} for every maximal
+//     run of member blocks predicted in one binade e with no crossing inside
+//     (the start and end predictions agree) and usable transfers, composed
+//     (xc_compose; whole groups from f64_group with the end condition), and
+//     ELEM {x} for every member of any other block (a binade crossing, a
+//     flagged transfer, the sequence's first member, a negative addend);
+//   * composing (f64s_compose): a RUN applies only when the exact running
+//     value is in its binade and stays there (the transfer test: exact, as
+//     in f64_walk); ELEM adds x in real fp64 (NumPy's first row starts the
+//     reduce).  Every rank composes the same all-gathered programs, so the
+//     sums and the verdict are the same on every rank; a failed test (a
+//     prediction off by a binade) or an overfull program makes every rank
+//     take the exact rank chain instead (f64s_chain: each shard walks from
+//     the exact entry in turn).
+// ---------------------------------------------------------------------------
+namespace {
+
+struct F64Item {
+  long long a, b;  // RUN: D0, D1; ELEM / CONST: the value's bits
+  int e, kind;     // RUN: binade; CONST: any
+};
+static_assert(sizeof(F64Item) == 24, "item layout (include/cdr.h)");
+constexpr int kF64Run = 1, kF64Elem = 2, kF64Const = 3;
+
+// per-sequence approximate totals [k d] then member counts [k] (as doubles,
+// exact below 2^53): one wave per row
+__global__ __launch_bounds__(256) void f64s_totals(const double* __restrict__ A,
+                                                   const unsigned* __restrict__ cnt, int64_t nb,
+                                                   int kd, int k, double* __restrict__ out) {
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (r >= kd + k) return;
+  double v = 0.0;
+  if (r < kd) {
+    for (int64_t b = lane; b < nb; b += 64) v += A[(int64_t)r * nb + b];
+  } else {
+    unsigned long long c = 0;
+    for (int64_t b = lane; b < nb; b += 64) c += cnt[(int64_t)(r - kd) * nb + b];
+    v = (double)c;
+  }
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (lane == 0) out[r] = v;
+}
+
+// this rank's offsets (the earlier shards' approximate totals, added left to
+// right) and the predicted binade at its end
+__global__ __launch_bounds__(256) void f64s_offsets(const double* __restrict__ tot, int nranks,
+                                                    int rank, int kd, int k,
+                                                    double* __restrict__ off,
+                                                    int* __restrict__ Eend) {
+  const int stride = kd + k;
+  for (int t = threadIdx.x; t < kd; t += blockDim.x) {
+    double o = 0.0;
+    for (int r = 0; r < rank; ++r) o += tot[(int64_t)r * stride + t];
+    off[t] = o;
+    Eend[t] = binade_e(o + tot[(int64_t)rank * stride + t]);
+  }
+}
+
+// rank 0: the walk's exact result as one CONST item per sequence
+__global__ __launch_bounds__(256) void f64s_const(const double* __restrict__ sums,
+                                                  const double* __restrict__ tot, int kd, int d,
+                                                  int k, int cap, F64Item* __restrict__ slot) {
+  for (int t = threadIdx.x; t < kd; t += blockDim.x) {
+    F64Item* it = slot + (int64_t)t * (cap + 1);
+    const bool any = tot[kd + t / d] > 0.0;
+    it[0] = F64Item{1, 0, 0, 0};
+    it[1] = F64Item{__double_as_longlong(sums[t]), 0, any ? 1 : 0, kF64Const};
+  }
+}
+
+// rank r > 0: one wave per (cluster, feature) sequence builds its program
+// (header item: count, or -1 when it would exceed cap items)
+template <typename TA>
+__global__ __launch_bounds__(256) void f64s_program(const double* __restrict__ X, int64_t n,
+                                                    int64_t n_pad, int d, int k, int64_t nb,
+                                                    const int32_t* __restrict__ labels,
+                                                    const unsigned* __restrict__ cnt,
+                                                    const int* __restrict__ E,
+                                                    const int* __restrict__ Eend,
+                                                    const Xfer* __restrict__ T,
+                                                    const GXfer* __restrict__ G, int64_t ng,
+                                                    int cap, F64Item* __restrict__ slot) {
+  const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= k * d) return;
+  const int j = t / d, f = t % d;
+  F64Item* out = slot + (int64_t)t * (cap + 1);
+  int nit = 0;  // items so far (wave-uniform)
+  auto emit = [&](long long a, long long b, int e, int kind) {
+    if (nit < cap && lane == 0) out[1 + nit] = F64Item{a, b, e, kind};
+    ++nit;
+  };
+  bool run_on = false;
+  int run_e = kENone;
+  XferC run{0, 0, 2};
+  auto add_run = [&](int e, long long d0, long long d1, int p) {
+    const XferC x{d0, d1, p};
+    if (run_on && run_e == e) {
+      run = xc_compose(run, x);
+    } else {
+      if (run_on) emit(run.d0, run.d1, run_e, kF64Run);
+      run = x;
+      run_e = e;
+      run_on = true;
+    }
+  };
+  auto rd64 = [&](long long v, int l) {
+    return (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(v >> 32), l)
+                        << 32) |
+                       (unsigned)__builtin_amdgcn_readlane((int)v, l));
+  };
+  const GXfer* Gt = G + (int64_t)t * ng;
+  for (int64_t g0 = 0; g0 < ng; g0 += 64) {
+    const GXfer gl = g0 + lane < ng ? Gt[g0 + lane] : GXfer{0, 0, kENone, 0};
+    unsigned long long todo = __ballot((gl.p & 8) != 0);
+    while (todo) {
+      const int gi = __builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
+      todo &= todo - 1;
+      const int gp = __builtin_amdgcn_readlane(gl.p, gi);
+      if (gp & 4) {  // every member usable, one binade, no crossing inside
+        add_run(__builtin_amdgcn_readlane(gl.e, gi), rd64(gl.d0, gi), rd64(gl.d1, gi), gp & 3);
+        continue;
+      }
+      const int64_t b0 = (g0 + gi) * 64;
+      const int64_t bl = b0 + lane;
+      const bool in = bl < nb;
+      const unsigned c = in ? cnt[(int64_t)j * nb + bl] : 0u;
+      const int el = in ? E[(int64_t)t * nb + bl] : kENone;
+      const int ea = in ? (bl + 1 < nb ? E[(int64_t)t * nb + bl + 1] : Eend[t]) : kENone;
+      const Xfer xl = in ? T[(int64_t)t * nb + bl] : Xfer{0, 0, 4};
+      const bool safe = c != 0 && !(xl.flags & 4) && el != kENone && ea == el;
+      unsigned long long mem = __ballot(c != 0);
+      const unsigned long long sm = __ballot(safe);
+      while (mem) {
+        const int i = __builtin_amdgcn_readfirstlane(__ffsll((long long)mem) - 1);
+        mem &= mem - 1;
+        if ((sm >> i) & 1ull) {
+          const long long d0 = rd64(xl.d0, i);
+          const int dd = __builtin_amdgcn_readlane(xl.dd, i);
+          add_run(__builtin_amdgcn_readlane(el, i), d0, d0 + dd,
+                  __builtin_amdgcn_readlane(xl.flags, i) & 3);
+          continue;
+        }
+        // the block's members one by one (row order)
+        if (run_on) emit(run.d0, run.d1, run_e, kF64Run);
+        run_on = false;
+        const int64_t r0 = (b0 + i) * kFB;
+        int lj[4];
+        double lx[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t row = r0 + 64 * q + lane;
+          lj[q] = row < n ? labels[row] : -1;
+          lx[q] = row < n ? (double)X[xidx(f, row, n_pad)] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          unsigned long long mk = __ballot(lj[q] == j);
+          while (mk) {
+            const int l = __builtin_amdgcn_readfirstlane(__ffsll((long long)mk) - 1);
+            mk &= mk - 1;
+            emit(rd64(__double_as_longlong(lx[q]), l), 0, 0, kF64Elem);
+          }
+        }
+      }
+    }
+  }
+  if (run_on) emit(run.d0, run.d1, run_e, kF64Run);
+  if (lane == 0) out[0] = F64Item{nit <= cap ? nit : -1, 0, 0, 0};
+}
+
+// every rank: the programs of ranks 0 .. nranks-1 in order, one thread per
+// sequence; sums[t], counts[j] (exact, from the gathered totals), and
+// status |= 1 when a RUN's transfer test failed or a program overflowed
+template <typename TA>
+__global__ __launch_bounds__(256) void f64s_compose(const F64Item* __restrict__ progs,
+                                                    int64_t slot_items, const double* __restrict__ tot,
+                                                    int nranks, int kd, int k, int cap,
+                                                    double* __restrict__ sums,
+                                                    long long* __restrict__ counts,
+                                                    int* __restrict__ status) {
+  constexpr int MB = SumTraits<TA>::MB, kMinE = SumTraits<TA>::kMinE;
+  constexpr long long kTop = 1ll << (MB + 1);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < k) {
+    double c = 0.0;
+    for (int r = 0; r < nranks; ++r) c += tot[(int64_t)r * (kd + k) + kd + t];
+    counts[t] = (long long)c;
+  }
+  if (t >= kd) return;
+  double s = 0.0;
+  bool any = false, ok = true;
+  for (int r = 0; r < nranks && ok; ++r) {
+    const F64Item* it = progs + (int64_t)r * slot_items + (int64_t)t * (cap + 1);
+    const long long m = it[0].a;
+    if (m < 0 || m > cap) {
+      ok = false;
+      break;
+    }
+    for (long long i = 1; i <= m; ++i) {
+      const F64Item x = it[i];
+      if (x.kind == kF64Run) {
+        ok = false;
+        if (any && s > 0.0) {
+          int ex;
+          frexp(s, &ex);
+          if (ex - 1 == x.e && x.e >= kMinE) {
+            const long long g = (long long)ldexp(s, MB - x.e);  // exact: s is on the grid
+            const long long g2 = g + ((g & 1) ? x.b : x.a);
+            if (g2 < kTop) {
+              s = ldexp((double)g2, x.e - MB);
+              ok = true;
+            }
+          }
+        }
+        if (!ok) break;
+      } else if (x.kind == kF64Elem) {
+        const double v = __longlong_as_double(x.a);
+        s = any ? (double)((TA)s + (TA)v) : v;  // NumPy's reduce: the first row starts it
+        any = true;
+      } else if (x.kind == kF64Const) {
+        s = __longlong_as_double(x.a);
+        any = x.e != 0;
+      }
+    }
+  }
+  sums[t] = s;
+  if (!ok) atomicOr(status, 1);
+}
+
+}  // namespace
+
+int f64s_cap() {
+  static const int cap = std::getenv("CDR_F64S_CAP") ? std::max(1, std::atoi(std::getenv("CDR_F64S_CAP"))) : 127;
+  return cap;
+}
+
+// The step's assignment (labels, block sums and counts) and this shard's
+// totals into tot_slot (k d + k doubles).  false: shape not covered.
+bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot) {
+  const int d = c.d;
+  if (d < 2 || d > 16 || k < 1 || k > kFMaxK) return false;
+  const int64_t n = c.n, nb = ceil_div(std::max<int64_t>(n, 1), kFB);
+  const size_t kd = (size_t)k * d;
+  c.f64x_A.ensure(sizeof(double) * nb * kd);
+  c.f64x_cnt.ensure(sizeof(unsigned) * nb * k);
+  c.f64x_E.ensure(sizeof(int) * nb * kd);
+  c.f64x_T.ensure(sizeof(Xfer) * nb * kd);
+  c.f64x_walk.ensure(sizeof(long long) * kd);
+  c.f64x_e_ok = false;  // (the fused step's carried predictions belong to other rows)
+  if (n > 0) {
+    typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
+                       unsigned*, const int*, Xfer*, unsigned char*);
+    static const Fn fns[17] = {nullptr, f64_assign_block<1, false>, f64_assign_block<2, false>,
+                               f64_assign_block<3, false>, f64_assign_block<4, false>,
+                               f64_assign_block<5, false>, f64_assign_block<6, false>,
+                               f64_assign_block<7, false>, f64_assign_block<8, false>,
+                               f64_assign_block<9, false>, f64_assign_block<10, false>,
+                               f64_assign_block<11, false>, f64_assign_block<12, false>,
+                               f64_assign_block<13, false>, f64_assign_block<14, false>,
+                               f64_assign_block<15, false>, f64_assign_block<16, false>};
+    hipLaunchKernelGGL(fns[d], dim3((unsigned)nb), dim3(kFB), 0, c.stream, c.x64.as<double>(), n,
+                       c.n_pad, dC, k, c.labels.as<int32_t>(), c.f64x_A.as<double>(),
+                       c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(),
+                       nullptr);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(f64s_totals, dim3((unsigned)ceil_div((int64_t)kd + k, 4)), dim3(256), 0,
+                       c.stream, c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), nb, (int)kd, k,
+                       tot_slot);
+  } else {
+    HIP_CHECK(hipMemsetAsync(tot_slot, 0, sizeof(double) * (kd + k), c.stream));
+  }
+  HIP_CHECK(hipGetLastError());
+  return true;
+}
+
+// This shard's program into its slot of prog_all ([nranks][k d][cap + 1]
+// items) from the gathered totals tot_all ([nranks][k d + k]).
+void f64s_build(Ctx& c, int k, int nranks, int rank, const double* tot_all, void* prog_all) {
+  const int d = c.d, cap = f64s_cap();
+  const int64_t n = c.n, nb = ceil_div(std::max<int64_t>(n, 1), kFB);
+  const int kd = k * d;
+  const int64_t slot_items = (int64_t)kd * (cap + 1);
+  F64Item* slot = static_cast<F64Item*>(prog_all) + (size_t)rank * slot_items;
+  c.f64s_off.ensure(sizeof(double) * kd + sizeof(int) * kd);
+  double* off = c.f64s_off.as<double>();
+  int* Eend = reinterpret_cast<int*>(off + kd);
+  hipLaunchKernelGGL(f64s_offsets, dim3(1), dim3(256), 0, c.stream, tot_all, nranks, rank, kd, k,
+                     off, Eend);
+  HIP_CHECK(hipGetLastError());
+  c.f64_sums.ensure(sizeof(double) * 2 * kd);
+  if (n > 0) {
+    F64Shard sh;
+    sh.off = off;
+    sh.Eend = rank > 0 ? Eend : nullptr;  // (rank 0 walks: no crossing condition needed)
+    sh.walk = rank == 0;
+    sums_after_block<double, double>(c, c.x64.as<double>(), k, c.f64_sums.as<double>(),
+                                     c.f64x_E.as<int>(), c.f64x_E.as<int>(), false, nullptr, sh);
+  }
+  if (rank == 0) {
+    if (n == 0) HIP_CHECK(hipMemsetAsync(c.f64_sums.p, 0, sizeof(double) * kd, c.stream));
+    hipLaunchKernelGGL(f64s_const, dim3(1), dim3(256), 0, c.stream, c.f64_sums.as<double>(),
+                       tot_all, kd, d, k, cap, slot);
+  } else if (n > 0) {
+    const int64_t ng = ceil_div(nb, (int64_t)64);
+    hipLaunchKernelGGL(f64s_program<double>, dim3((unsigned)ceil_div((int64_t)kd, 4)), dim3(256), 0,
+                       c.stream, c.x64.as<double>(), n, c.n_pad, d, k, nb,
+                       c.labels.as<int32_t>(), c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(),
+                       Eend, c.f64x_T.as<Xfer>(), c.f64x_G.as<GXfer>(), ng, cap, slot);
+  } else {  // an empty shard: the identity (no items)
+    std::vector<F64Item> z((size_t)slot_items, F64Item{0, 0, 0, 0});
+    HIP_CHECK(hipMemcpyAsync(slot, z.data(), sizeof(F64Item) * z.size(), hipMemcpyHostToDevice,
+                             c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+void f64s_compose_all(Ctx& c, int k, int nranks, const double* tot_all, const void* prog_all,
+                      double* d_sums, long long* d_counts, int* d_status) {
+  const int kd = k * c.d, cap = f64s_cap();
+  const int64_t slot_items = (int64_t)kd * (cap + 1);
+  HIP_CHECK(hipMemsetAsync(d_status, 0, sizeof(int), c.stream));
+  hipLaunchKernelGGL(f64s_compose<double>, dim3((unsigned)ceil_div(std::max(kd, k), 256)),
+                     dim3(256), 0, c.stream, static_cast<const F64Item*>(prog_all), slot_items,
+                     tot_all, nranks, kd, k, cap, d_sums, d_counts, d_status);
+  HIP_CHECK(hipGetLastError());
+}
+
+// The exact rank chain (fallback): this shard walks from the exact entry
+// chain[0, 2 k d) = {s, any} and leaves its exit there.
+void f64s_chain_walk(Ctx& c, int k, double* chain) {
+  const int kd = k * c.d;
+  if (c.n == 0) return;  // nothing added: the entry is the exit
+  F64Shard sh;
+  sh.off = chain;  // the exact entry predicts every binade
+  sh.entry = chain;
+  sh.walk = true;
+  c.f64s_off.ensure(sizeof(double) * kd + sizeof(int) * kd);
+  sums_after_block<double, double>(c, c.x64.as<double>(), k, chain, c.f64x_E.as<int>(),
+                                   c.f64x_E.as<int>(), false, nullptr, sh);
+}
+
 // The reference's float32 runs: sequential fp32 sums of fp32 points (X:
 // F32X storage, or F64 storage holding fp32 values), returned as doubles.
 bool f32_sums_parallel(Ctx& c, int k, double* d_sums) {

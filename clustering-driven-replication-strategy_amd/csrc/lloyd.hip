@@ -1564,6 +1564,85 @@ int cdr_lloyd_step_f64(cdr_ctx* h, const double* C, int32_t k, double* sums,
   CDR_CATCH
 }
 
+// ---- sharded F64 sums (f64sum.hip, include/cdr.h cdr_f64s_*) ----
+int cdr_f64s_begin(cdr_ctx* h, const double* C, int32_t k, int32_t nranks, int32_t rank,
+                   void* tot_buf, int64_t* sizes) {
+  CDR_TRY
+  if (!h || !C || !tot_buf || !sizes) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  check_k(c, k);
+  if (c.mode != CDR_MODE_F64) CDR_FAIL(CDR_ERR_STATE, "cdr_f64s_begin: points are not F64");
+  if (nranks < 1 || rank < 0 || rank >= nranks) CDR_FAIL(CDR_ERR_ARG, "bad ranks");
+  if (c.d < 2 || c.d > 16 || k > 64)
+    CDR_FAIL(CDR_ERR_UNSUPPORTED, "sharded F64 sums need 2 <= d <= 16 and k <= 64");
+  c.run_valid = false;
+  c.lab8_valid = false;
+  c.zb_valid = false;
+  c.big_valid = false;
+  upload_centroids(c, C, k);
+  const int kd = k * c.d;
+  double* slot = static_cast<double*>(tot_buf) + (size_t)rank * (kd + k);
+  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "f64_assign_block<%d>", c.d);
+  if (!f64s_assign_totals(c, k, c.cent64.as<double>(), slot))
+    CDR_FAIL(CDR_ERR_UNSUPPORTED, "sharded F64 sums: shape not covered");
+  c.f64s_k = k;
+  c.f64s_nranks = nranks;
+  c.f64s_rank = rank;
+  sizes[0] = (int64_t)sizeof(double) * (kd + k);
+  sizes[1] = (int64_t)24 * kd * (f64s_cap() + 1);
+  c.last_k = k;
+  c.have_labels = true;
+  CDR_CATCH
+}
+
+int cdr_f64s_build(cdr_ctx* h, const void* tot_buf, void* prog_buf) {
+  CDR_TRY
+  if (!h || !tot_buf || !prog_buf) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  if (c.f64s_k < 1) CDR_FAIL(CDR_ERR_STATE, "cdr_f64s_begin first");
+  f64s_build(c, c.f64s_k, c.f64s_nranks, c.f64s_rank, static_cast<const double*>(tot_buf),
+             prog_buf);
+  CDR_CATCH
+}
+
+int cdr_f64s_finish(cdr_ctx* h, const void* tot_buf, const void* prog_buf, double* sums,
+                    int64_t* counts, int32_t* status) {
+  CDR_TRY
+  if (!h || !tot_buf || !prog_buf || !sums || !counts || !status)
+    CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  const int k = c.f64s_k, kd = k * c.d;
+  if (k < 1) CDR_FAIL(CDR_ERR_STATE, "cdr_f64s_begin first");
+  c.f64_sums.ensure(sizeof(double) * 2 * kd);
+  c.f64_counts.ensure(sizeof(long long) * k * 2 + sizeof(int));
+  int* dst = reinterpret_cast<int*>(c.f64_counts.as<long long>() + 2 * k);
+  f64s_compose_all(c, k, c.f64s_nranks, static_cast<const double*>(tot_buf), prog_buf,
+                   c.f64_sums.as<double>(), c.f64_counts.as<long long>(), dst);
+  HIP_CHECK(hipMemcpyAsync(sums, c.f64_sums.p, sizeof(double) * kd, hipMemcpyDeviceToHost,
+                           c.stream));
+  HIP_CHECK(hipMemcpyAsync(counts, c.f64_counts.p, sizeof(long long) * k, hipMemcpyDeviceToHost,
+                           c.stream));
+  HIP_CHECK(hipMemcpyAsync(status, dst, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  const bool force = getenv("CDR_F64S_FORCE_CHAIN") && atoi(getenv("CDR_F64S_FORCE_CHAIN"));
+  if (force) *status |= 1;  // (tests: the exact rank chain on every rank)
+  CDR_CATCH
+}
+
+int cdr_f64s_chain(cdr_ctx* h, void* chain_buf) {
+  CDR_TRY
+  if (!h || !chain_buf) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  Ctx& c = h->c;
+  HIP_CHECK(hipSetDevice(c.device));
+  if (c.f64s_k < 1) CDR_FAIL(CDR_ERR_STATE, "cdr_f64s_begin first");
+  f64s_chain_walk(c, c.f64s_k, static_cast<double*>(chain_buf));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  CDR_CATCH
+}
+
 int cdr_lloyd_step_f32r(cdr_ctx* h, const float* C, int32_t k, double* sums, int64_t* counts) {
   CDR_TRY
   if (!h || !C || !sums || !counts) CDR_FAIL(CDR_ERR_ARG, "null argument");

@@ -207,6 +207,33 @@ int cdr_lloyd_step_f32r(cdr_ctx* ctx, const float* C, int32_t k, double* sums,
  * (cluster, feature) sequences re-added element by element in the last step,
  * or -1 when the step used the serial kernel.                               */
 int cdr_lloyd_f64_walked(cdr_ctx* ctx, int64_t* walked);
+/* Sharded F64 sums (src/kmeans_plusplus.py:33-41 on rows sharded in rank
+ * order, float64 data off any grid: src/main.py:81).  Per Lloyd step, with
+ * one collective between the calls (buffers are device memory: all ranks'
+ * slots, rank r's at offset r x its slot size):
+ *   cdr_f64s_begin   assignment (labels) + this shard's approximate
+ *                    per-(cluster, feature) totals and member counts into
+ *                    its slot of tot_buf; sizes = {tot slot bytes, program
+ *                    slot bytes}                       -> all-gather tot_buf
+ *   cdr_f64s_build   this shard's program (rank 0: its exact walked sums;
+ *                    rank > 0: transfer runs and element lists built from
+ *                    the gathered approximate totals) -> all-gather prog_buf
+ *   cdr_f64s_finish  every rank composes all programs in rank order: the
+ *                    exact sequential sums (k x d) and counts (k); *status
+ *                    1 when a program's guess did not hold, the same on
+ *                    every rank: then run the rank chain, cdr_f64s_chain on
+ *                    rank r (walks its shard from the exact entry
+ *                    chain_buf[0, 2 k d) = {sums, any}, leaving its exit
+ *                    there) followed by a broadcast of chain_buf from rank r,
+ *                    for r = 0 .. nranks - 1 (chain_buf zeroed first).
+ * Replaces the sequential NumPy mean (kmeans_plusplus.py:41) over the whole
+ * array; 2 <= d <= 16, k <= 64.                                            */
+int cdr_f64s_begin(cdr_ctx* ctx, const double* C, int32_t k, int32_t nranks, int32_t rank,
+                   void* tot_buf, int64_t* sizes);
+int cdr_f64s_build(cdr_ctx* ctx, const void* tot_buf, void* prog_buf);
+int cdr_f64s_finish(cdr_ctx* ctx, const void* tot_buf, const void* prog_buf, double* sums,
+                    int64_t* counts, int32_t* status);
+int cdr_f64s_chain(cdr_ctx* ctx, void* chain_buf);
 /* Labels of the last assignment as int64 (np.argmin dtype, :34).           */
 int cdr_lloyd_labels(cdr_ctx* ctx, int64_t* labels);
 /* Diagnostics of the last step: points the fast screen could not certify

@@ -1,0 +1,86 @@
+"""Per-step numbers of one kernel from rocprofv3 output (dev/profiling tool).
+
+    python tools/window_stats.py trace  RUN_kernel_trace.csv KERNEL FIRST_STEP [STEPS...]
+        per-step durations of KERNEL's dispatches (the i-th dispatch = loop
+        step FIRST_STEP + i) and their mean over STEPS (e.g. bench.py's
+        profiled window)
+    python tools/window_stats.py pmc FETCH_DIR WRITE_DIR KERNEL FIRST_STEP CONFIG N_LOCAL
+        per-step HBM bytes from a FETCH_SIZE pass and a WRITE_SIZE pass
+        (FETCH_SIZE KiB x 1024 x 2: the gfx950 half-count of MI355X_MICROARCH.md;
+        WRITE_SIZE KiB x 1024) written into profiles/pmc_traffic.json[CONFIG]
+
+KERNEL is a substring of the kernel name; several kernels of one step can be
+given as "a+b" (their per-step values are summed, dispatches paired in order).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _dispatches(rows, kern):
+    parts = kern.split("+")
+    per = {p: [r for r in rows if p in r["Kernel_Name"]] for p in parts}
+    n = min(len(v) for v in per.values())
+    return per, n
+
+
+def trace(path, kern, first, window):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    per, n = _dispatches(rows, kern)
+    dur = []
+    for i in range(n):
+        dur.append(sum((int(per[p][i]["End_Timestamp"]) - int(per[p][i]["Start_Timestamp"])) / 1e3
+                       for p in per))
+    for i, v in enumerate(dur):
+        print(f"step {first + i:3d} {v:9.1f} us")
+    if window:
+        w = [dur[s - first] for s in window if 0 <= s - first < n]
+        print(f"mean over steps {window}: {sum(w) / len(w):.1f} us ({len(w)} dispatches)")
+
+
+def _counter(dirpath, name, kern):
+    files = glob.glob(os.path.join(dirpath, "**", "*_counter_collection.csv"), recursive=True)
+    rows = [r for f in files for r in csv.DictReader(open(f)) if r["Counter_Name"] == name]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    # one row per dispatch (the counter summed over its instances)
+    agg, order, names = {}, [], {}
+    for r in rows:
+        d = int(r["Dispatch_Id"])
+        if d not in agg:
+            agg[d] = 0.0
+            order.append(d)
+            names[d] = r["Kernel_Name"]
+        agg[d] += float(r["Counter_Value"])
+    out = [{"Kernel_Name": names[d], "v": agg[d]} for d in order]
+    per, n = _dispatches(out, kern)
+    return [sum(per[p][i]["v"] for p in per) for i in range(n)]
+
+
+def pmc(fdir, wdir, kern, first, config, n_local):
+    rd = [v * 1024 * 2 for v in _counter(fdir, "FETCH_SIZE", kern)]
+    wr = [v * 1024 for v in _counter(wdir, "WRITE_SIZE", kern)]
+    n = min(len(rd), len(wr))
+    for i in range(n):
+        print(f"step {first + i:3d}: read {rd[i] / 1e6:10.1f} MB  write {wr[i] / 1e6:8.1f} MB")
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    rec = json.load(open(path)) if os.path.exists(path) else {}
+    rec[config] = {"n_local": n_local, "kernel": kern, "first_step": first,
+                   "per_step_read": rd[:n], "per_step_write": wr[:n],
+                   "source": f"rocprofv3 --pmc FETCH_SIZE ({fdir}) and --pmc WRITE_SIZE ({wdir}), "
+                             "one row per device-loop step",
+                   "note": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count of wide streaming "
+                           "reads, MI355X_MICROARCH.md) + WRITE_SIZE KiB x 1024; bench.py "
+                           "averages the rows of the steps it times"}
+    json.dump(rec, open(path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "trace":
+        trace(sys.argv[2], sys.argv[3], int(sys.argv[4]), [int(s) for s in sys.argv[5:]])
+    else:
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6], int(sys.argv[7]))
