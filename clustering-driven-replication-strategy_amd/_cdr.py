@@ -79,6 +79,7 @@ SIGNATURES = {
     "cdr_lloyd_step_f64": ([_P, _P, _I32, _P, _P], None),
     "cdr_lloyd_step_f32r": ([_P, _P, _I32, _P, _P], None),
     "cdr_f32r_seed_update": ([_P, _P, _I32, _P], None),
+    "cdr_f32r_seed_run": ([_P, _I64, _I32, _P, _P], None),
     "cdr_lloyd_labels": ([_P, _P], None),
     "cdr_lloyd_stats": ([_P, _PI64], None),
     "cdr_debug_screen": ([_P, _P, _I32, _P, _P], None),
@@ -202,6 +203,9 @@ def _check(rc: int) -> None:
         return
     msg = load_library().cdr_last_error().decode(errors="replace")
     if rc == CDR_ERR_NAN:
+        if "do not sum to 1" in msg:  # Generator.choice on all-zero probabilities
+            raise ValueError("Probabilities do not sum to 1. See Notes section of docstring "
+                             "for more information.")
         raise NanProbabilities("Probabilities contain NaN")
     if rc == CDR_ERR_ARG:
         raise ValueError(msg)
@@ -512,6 +516,16 @@ class Context:
             raise NanProbabilities("Probabilities contain NaN")
         _check(code)
         return float(np.float32(tot.value))
+
+    def f32r_seed_run(self, first: int, k: int, u) -> np.ndarray:
+        """The reference's float32 seeding with every step on the device
+        (cdr_f32r_seed_run): u = the k - 1 rng.random() draws; returns the
+        k picked rows."""
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        picks = np.zeros(k, dtype=np.int64)
+        _check(self._lib.cdr_f32r_seed_run(self._h, int(first), int(k),
+                                           _ptr(u) if u.size else None, _ptr(picks)))
+        return picks
 
     def f64_walked(self) -> int:
         """Blocks the last F64 step re-added element-wise (-1: serial kernel)."""

@@ -2459,8 +2459,10 @@ template <typename S, int D>
 __global__ __launch_bounds__(256) void f32r_min_kernel(const S* __restrict__ X, int64_t n,
                                                        int64_t n_pad, int d,
                                                        const float* __restrict__ cen,
-                                                       float* __restrict__ dmin32) {
+                                                       float* __restrict__ dmin32,
+                                                       int* __restrict__ infflag) {
   const int dd = D ? D : d;
+  bool inf = false;
   for (int64_t pt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pt < n;
        pt += (int64_t)gridDim.x * blockDim.x) {
     auto xv = [&](int f) { return (float)X[xidx(f, pt, n_pad)]; };  // exact: fp32 values
@@ -2469,7 +2471,13 @@ __global__ __launch_bounds__(256) void f32r_min_kernel(const S* __restrict__ X, 
     const float t = (float)sqrt((double)R);  // = the correctly rounded fp32 sqrt
     const float t2 = t * t;
     const float m = dmin32[pt];
-    dmin32[pt] = (m != m || t2 != t2) ? NAN : (t2 < m ? t2 : m);
+    const float v = (m != m || t2 != t2) ? NAN : (t2 < m ? t2 : m);
+    dmin32[pt] = v;
+    inf = inf || isinf(v);
+  }
+  // (device-resident run: an infinite dist_sq makes probs inf / inf = NaN)
+  if (infflag && __ballot(inf)) {
+    if ((threadIdx.x & 63) == __ffsll((long long)__ballot(inf)) - 1) atomicOr(infflag, 1);
   }
 }
 __global__ void f32r_fill_kernel(float* __restrict__ p, int64_t n_pad, int64_t n) {
@@ -2503,11 +2511,13 @@ __global__ __launch_bounds__(64) void f32r_block_kernel(const float* __restrict_
 // p = fl32(dist_sq / total) as doubles (the scan's dmin, rows >= n zero) and
 // each chunk's sum in any order (the scan's binade guesses only)
 __global__ __launch_bounds__(256) void f32r_prob_kernel(const float* __restrict__ dmin32,
-                                                        int64_t n, float total,
+                                                        int64_t n, float total_v,
                                                         double* __restrict__ dmin,
-                                                        double* __restrict__ bs) {
+                                                        double* __restrict__ bs,
+                                                        const float* __restrict__ dtotal) {
   __shared__ double red[4];
   const int64_t b = blockIdx.x;
+  const float total = dtotal ? dtotal[0] : total_v;
   double acc = 0.0;
   for (int i = threadIdx.x; i < kSeedBlock; i += 256) {
     const int64_t pt = b * kSeedBlock + i;
@@ -2539,13 +2549,14 @@ void f32r_seed_update(Ctx& c, const float* cen, int reset, float* total_out) {
   HIP_CHECK(hipMemcpyAsync(dcen, cen, sizeof(float) * c.d, hipMemcpyHostToDevice, c.stream));
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(c.n, 256), 4096)));
   const int d = c.d;
+#define INF_ ((int*)nullptr)
 #define CDR_F32R_MIN(S_, X_)                                                                \
   switch (d) {                                                                             \
-    case 2: hipLaunchKernelGGL((f32r_min_kernel<S_, 2>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); break; \
-    case 5: hipLaunchKernelGGL((f32r_min_kernel<S_, 5>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); break; \
-    case 8: hipLaunchKernelGGL((f32r_min_kernel<S_, 8>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); break; \
-    case 16: hipLaunchKernelGGL((f32r_min_kernel<S_, 16>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); break; \
-    default: hipLaunchKernelGGL((f32r_min_kernel<S_, 0>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>()); \
+    case 2: hipLaunchKernelGGL((f32r_min_kernel<S_, 2>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), INF_); break; \
+    case 5: hipLaunchKernelGGL((f32r_min_kernel<S_, 5>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), INF_); break; \
+    case 8: hipLaunchKernelGGL((f32r_min_kernel<S_, 8>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), INF_); break; \
+    case 16: hipLaunchKernelGGL((f32r_min_kernel<S_, 16>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), INF_); break; \
+    default: hipLaunchKernelGGL((f32r_min_kernel<S_, 0>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), INF_); \
   }
   if (c.mode == CDR_MODE_F32X) {
     CDR_F32R_MIN(float, c.x32.as<float>())
@@ -2553,6 +2564,7 @@ void f32r_seed_update(Ctx& c, const float* cen, int reset, float* total_out) {
     CDR_F32R_MIN(double, c.x64.as<double>())
   }
 #undef CDR_F32R_MIN
+#undef INF_
   HIP_CHECK(hipGetLastError());
   float total = 0.0f;
   if (nb > 0) {
@@ -2570,16 +2582,141 @@ void f32r_seed_update(Ctx& c, const float* cen, int reset, float* total_out) {
   if (nb > 0) {
     hipLaunchKernelGGL(f32r_prob_kernel, dim3((unsigned)nb), dim3(256), 0, c.stream,
                        c.dmin32.as<float>(), c.n, total, c.dmin.as<double>(),
-                       c.blocksums.as<double>());
+                       c.blocksums.as<double>(), nullptr);
     HIP_CHECK(hipGetLastError());
   }
   c.seed_scanned = false;
   c.seed_prog_ready = false;
 }
 
+// ---- the reference's float32 seeding, every step on the device ----------
+// The pick's row as the fp32 centre.
+__global__ __launch_bounds__(64) void f32r_gather_kernel(const float* __restrict__ x32,
+                                                         const double* __restrict__ x64,
+                                                         const int64_t* __restrict__ pick, int d,
+                                                         int64_t n_pad, float* __restrict__ cen) {
+  const int64_t p = pick[0];
+  for (int f = threadIdx.x; f < d; f += 64)
+    cen[f] = x32 ? x32[xidx(f, p, n_pad)] : (float)x64[xidx(f, p, n_pad)];
+}
+// dist_sq.sum() in fp32: the chunk sums from 0, left to right (one lane:
+// the additions are sequential), and the step's verdict as Generator.choice
+// gives it: a NaN, zero or infinite total with an infinite dist_sq
+// (probs inf / inf) or a NaN is "Probabilities contain NaN" (code 1); an
+// infinite total from finite dist_sq (overflow: probs all 0) is
+// "probabilities do not sum to 1" (code 2).  The first bad step's code is
+// kept; later steps run on total 1 (their picks are never used).
+__global__ __launch_bounds__(64) void f32r_total_kernel(const float* __restrict__ bs32,
+                                                        int64_t nb, int* __restrict__ infflag,
+                                                        float* __restrict__ dtotal,
+                                                        double* __restrict__ dbad) {
+  if (threadIdx.x != 0) return;
+  float total = 0.0f;
+  for (int64_t b = 0; b < nb; ++b) total = total + bs32[b];
+  if (!(total > 0.0f) || isinf(total)) {
+    const double code = (isinf(total) && total > 0.0f && infflag[0] == 0) ? 2.0 : 1.0;
+    if (dbad[0] == 0.0) dbad[0] = code;
+    total = 1.0f;
+  }
+  infflag[0] = 0;
+  dtotal[0] = total;
+}
+
+void f32r_seed_run(Ctx& c, int64_t first, int k, const double* u, int64_t* picks) {
+  check_points(c);
+  if (k < 1) CDR_FAIL(CDR_ERR_ARG, "k >= 1");
+  if (first < 0 || first >= c.n) CDR_FAIL(CDR_ERR_ARG, "first row out of range");
+  picks[0] = first;
+  if (k == 1) return;
+  const int64_t nb = c.nblocks();
+  const int d = c.d;
+  // [u: k-1][picks: k][bad x2][total f32 | inf flag][centre f32 x d]
+  const size_t words = (size_t)(k - 1) + (size_t)k + 3 + (size_t)(d + 1) / 2 + 1;
+  c.seed_run_buf.ensure(sizeof(double) * words);
+  double* du = c.seed_run_buf.as<double>();
+  int64_t* dpick = reinterpret_cast<int64_t*>(du + (k - 1));
+  double* dbad = du + (k - 1) + k;
+  float* dtotal = reinterpret_cast<float*>(dbad + 2);
+  int* dinf = reinterpret_cast<int*>(dtotal + 1);
+  float* dcen = reinterpret_cast<float*>(dbad + 3);
+  HIP_CHECK(hipMemcpyAsync(du, u, sizeof(double) * (k - 1), hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(dpick, &first, sizeof(int64_t), hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemsetAsync(dbad, 0, sizeof(double) * 3, c.stream));
+  c.dmin32.ensure(sizeof(float) * (size_t)(c.n_pad > 0 ? c.n_pad : 1));
+  c.dmin.ensure(sizeof(double) * (size_t)(c.n_pad > 0 ? c.n_pad : 1));
+  c.blocksums.ensure(sizeof(double) * (nb > 0 ? nb : 1));
+  c.bs32.ensure(sizeof(float) * (nb > 0 ? nb : 1));
+  c.cend.ensure(sizeof(double) * nb * 2);
+  c.seg_meta.ensure(sizeof(long long) * 8);
+  hipLaunchKernelGGL(f32r_fill_kernel, dim3(2048), dim3(256), 0, c.stream, c.dmin32.as<float>(),
+                     c.n_pad, c.n);
+  HIP_CHECK(hipGetLastError());
+  const float* x32 = c.mode == CDR_MODE_F32X ? c.x32.as<float>() : nullptr;
+  const double* x64 = c.mode == CDR_MODE_F64 ? c.x64.as<double>() : nullptr;
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(c.n, 256), 4096)));
+  for (int i = 1; i < k; ++i) {
+    hipLaunchKernelGGL(f32r_gather_kernel, dim3(1), dim3(64), 0, c.stream, x32, x64,
+                       dpick + (i - 1), d, c.n_pad, dcen);
+#define CDR_F32R_MIN(S_, X_)                                                                  \
+    switch (d) {                                                                             \
+      case 2: hipLaunchKernelGGL((f32r_min_kernel<S_, 2>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), dinf); break; \
+      case 5: hipLaunchKernelGGL((f32r_min_kernel<S_, 5>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), dinf); break; \
+      case 8: hipLaunchKernelGGL((f32r_min_kernel<S_, 8>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), dinf); break; \
+      case 16: hipLaunchKernelGGL((f32r_min_kernel<S_, 16>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), dinf); break; \
+      default: hipLaunchKernelGGL((f32r_min_kernel<S_, 0>), grid, dim3(256), 0, c.stream, X_, c.n, c.n_pad, d, dcen, c.dmin32.as<float>(), dinf); \
+    }
+    if (x32) {
+      CDR_F32R_MIN(float, x32)
+    } else {
+      CDR_F32R_MIN(double, x64)
+    }
+#undef CDR_F32R_MIN
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(f32r_block_kernel, dim3((unsigned)std::max<int64_t>(nb, 1)), dim3(64), 0,
+                       c.stream, c.dmin32.as<float>(), c.n, c.bs32.as<float>());
+    hipLaunchKernelGGL(f32r_total_kernel, dim3(1), dim3(64), 0, c.stream, c.bs32.as<float>(), nb,
+                       dinf, dtotal, dbad);
+    hipLaunchKernelGGL(f32r_prob_kernel, dim3((unsigned)std::max<int64_t>(nb, 1)), dim3(256), 0,
+                       c.stream, c.dmin32.as<float>(), c.n, 1.0f, c.dmin.as<double>(),
+                       c.blocksums.as<double>(), dtotal);
+    HIP_CHECK(hipGetLastError());
+    // Generator.choice on the float64 probabilities: the exact cumsum scan
+    // (program, then the gated block walk) and the search, S = 1
+    double* res = seed_res(c);
+    SeedDev dv;
+    seed_scan_program(c, 1.0, 0.0, dv);
+    seed_scan_finish(c, 0.0, nullptr, dv);
+    dv.gate = res + 1;  // the fallback runs only when the program failed
+    seed_scan_walk(c, 1.0, 0.0, nullptr, dv, res);
+    SeedDev ds;
+    ds.c_last = res;
+    ds.u = du + (i - 1);
+    hipLaunchKernelGGL(search_kernel, dim3(1), dim3(64), 0, c.stream, c.dmin.as<double>(), c.n,
+                       1.0, c.cend.as<double>(), nb, 0.0, 1.0, 0.5, dpick + i, ds);
+    HIP_CHECK(hipGetLastError());
+  }
+  double bad[2];
+  HIP_CHECK(hipMemcpyAsync(picks, dpick, sizeof(int64_t) * k, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(bad, dbad, sizeof(bad), hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.seed_scanned = false;
+  c.seed_prog_ready = false;
+  if (bad[0] == 2.0) CDR_FAIL(CDR_ERR_NAN, "probabilities do not sum to 1");
+  if (bad[0] != 0.0) CDR_FAIL(CDR_ERR_NAN, "Probabilities contain NaN");
+  if (bad[1] != 0.0) CDR_FAIL(CDR_ERR_STATE, "k-means++ sampler found no index");
+}
+
 }  // namespace cdr
 
 extern "C" {
+
+int cdr_f32r_seed_run(cdr_ctx* h, int64_t first, int32_t k, const double* u, int64_t* picks) {
+  CDR_TRY
+  if (!h || !picks || (k > 1 && !u)) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  f32r_seed_run(h->c, first, (int)k, u, picks);
+  CDR_CATCH
+}
 
 int cdr_seed_reset(cdr_ctx* h) {
   CDR_TRY

@@ -31,6 +31,7 @@ default; pass ``max_iter=`` to run large inputs.
 """
 from __future__ import annotations
 
+import os
 import warnings
 
 import numpy as np
@@ -82,14 +83,25 @@ def _seed_on_device(ctx: Context, X: np.ndarray, k: int, random_state) -> np.nda
 
 def _seed_f32r(ctx: Context, X: np.ndarray, k: int, random_state) -> np.ndarray:
     """The reference's seeding on a float32 X (:6, 14-19 in float32): the
-    device forms fp32 dist_sq, its fp32 total and fp32 probabilities
-    (cdr_f32r_seed_update), then the exact float64 cumsum scan and search of
-    Generator.choice run as in the float64 case with S = 1."""
+    device forms fp32 dist_sq, its fp32 total and fp32 probabilities, then
+    the exact float64 cumsum scan and search of Generator.choice as in the
+    float64 case with S = 1.  Every step runs on the device
+    (cdr_f32r_seed_run): Generator.choice draws exactly one rng.random() per
+    step (:19), so the k - 1 draws are taken up front and one readback
+    returns the picks.  CDR_F32R_STEPS=1: the per-step host loop instead."""
     rng = np.random.default_rng(random_state)
     n_samples, n_features = X.shape
     centroids = np.empty((k, n_features), dtype=X.dtype)
     first_idx = rng.integers(0, n_samples)
     centroids[0] = X[first_idx]
+    if k > 1 and hasattr(ctx, "f32r_seed_run") and not os.environ.get("CDR_F32R_STEPS"):
+        u = rng.random(k - 1)
+        try:
+            picks = ctx.f32r_seed_run(int(first_idx), k, u)
+        except NanProbabilities:
+            _nan_probabilities()
+        centroids[:] = X[picks]
+        return centroids
     for i in range(1, k):
         try:
             ctx.f32r_seed_update(centroids[i - 1], reset=(i == 1))
