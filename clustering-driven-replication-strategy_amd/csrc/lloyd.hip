@@ -1584,8 +1584,11 @@ int cdr_f64s_begin(cdr_ctx* h, const double* C, int32_t k, int32_t nranks, int32
   const int kd = k * c.d;
   double* slot = static_cast<double*>(tot_buf) + (size_t)rank * (kd + k);
   snprintf(c.prof_kernel, sizeof(c.prof_kernel), "f64_assign_block<%d>", c.d);
+  const bool prof = prof_step_begin(c);
+  if (prof) prof_mark(c, 0);
   if (!f64s_assign_totals(c, k, c.cent64.as<double>(), slot))
     CDR_FAIL(CDR_ERR_UNSUPPORTED, "sharded F64 sums: shape not covered");
+  if (prof) prof_mark(c, 1);
   c.f64s_k = k;
   c.f64s_nranks = nranks;
   c.f64s_rank = rank;
@@ -1621,6 +1624,7 @@ int cdr_f64s_finish(cdr_ctx* h, const void* tot_buf, const void* prog_buf, doubl
   int* dst = reinterpret_cast<int*>(c.f64_counts.as<long long>() + 2 * k);
   f64s_compose_all(c, k, c.f64s_nranks, static_cast<const double*>(tot_buf), prog_buf,
                    c.f64_sums.as<double>(), c.f64_counts.as<long long>(), dst);
+  if (c.prof_cur >= 0) prof_mark(c, 2);  // (the step's kernels end here)
   HIP_CHECK(hipMemcpyAsync(sums, c.f64_sums.p, sizeof(double) * kd, hipMemcpyDeviceToHost,
                            c.stream));
   HIP_CHECK(hipMemcpyAsync(counts, c.f64_counts.p, sizeof(long long) * k, hipMemcpyDeviceToHost,

@@ -34,6 +34,8 @@
 
 namespace cdr {
 
+void ensure_rowmajor(Ctx& c);  // screen32.hip: the row-major copy xa32
+
 struct Xfer {
   long long d0, d1;
   int e;      // binade exponent the transfer was computed for
@@ -463,6 +465,141 @@ __global__ __launch_bounds__(256) void seed_update16_kernel(
     }
   }
   if (!TAIL && threadIdx.x == 0) blocksums[b] = halves[0] + halves[1];
+}
+
+// The same update with the block's pairwise tree kept in registers (the
+// default for d = 8 and 16; CDR_SEED16_LDS=1: seed_update16_kernel).  One
+// 512-thread workgroup per 8192-row block; thread (half h, leaf L, j) owns
+// NumPy's accumulator j of the 128-element leaf L of half h, i.e. the rows
+// 128 L + j + 8 i (i = 0 .. 15), and adds its 16 updated minima in NumPy's
+// order (r = v_0, then r += v_i) as it produces them: no LDS staging of the
+// half's 4096 values (34 KB per workgroup capped seed_update16_kernel at 4
+// workgroups per CU) and no transposed re-read.  Accumulators combine by
+// shuffles ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) and the leaves
+// and waves by the same perfect tree, exactly seed_update16_kernel's sums.
+// A wave's load instruction reads 8 runs of 8 consecutive rows (64 B of
+// dmin, 128 B of each copy group).  Rows are taken 4 per batch, the batch's
+// loads issued together; the fp32 row is read only where the fp16
+// certificate cannot prove the minimum unchanged.
+template <int D>
+__global__ __launch_bounds__(512) void seed_update16r_kernel(
+    const float* __restrict__ X, const uint4* __restrict__ x16, const float* __restrict__ e16,
+    int64_t n, int64_t n_pad, const double* __restrict__ cen, const float* __restrict__ ch,
+    const float* __restrict__ Ecp, double rscale, double* __restrict__ dmin,
+    double* __restrict__ blocksums, int32_t* __restrict__ near, int cidx,
+    const float* __restrict__ XA) {
+  constexpr int G = (D + 7) / 8;
+  constexpr int Q = (D + 3) / 4;
+  constexpr int kB = D <= 8 ? 4 : 2;  // rows per batch (registers: 4 at d = 16 left 3 waves / SIMD)
+  constexpr float kRel = 1.0f - (float)(D + 8) * 0x1p-23f;
+  __shared__ double swave[8];
+  const float Ec = Ecp[0];
+  const int64_t b = blockIdx.x;
+  const int64_t base = b * kSeedBlock;
+  const int m = (n - base) < kSeedBlock ? (int)(n - base) : kSeedBlock;
+  const int t = threadIdx.x;
+  const int h = t >> 8, L = (t >> 3) & 31, j = t & 7;
+  const int r0 = h * 4096 + 128 * L + j;  // row of i = 0 (row of i: r0 + 8 i)
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* X4 = reinterpret_cast<const f4v*>(X);
+  float chv[D];
+#pragma unroll
+  for (int f = 0; f < D; ++f) chv[f] = ch[f];
+  double acc = 0.0;
+  // batch bi's streamed words (dmin, the fp16 copy, its error), two batches
+  // in flight: the next batch's loads are issued before this batch's
+  // certificate and exact-path gather, so the dependent gather's latency
+  // overlaps them
+  struct SB {
+    double old[kB];
+    uint4 hv[kB][G];
+    float ev[kB];
+  };
+  auto sload = [&](SB& sb, int i0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int r = r0 + 8 * (i0 + u);
+      const int64_t i = base + (r < m ? r : 0);
+      sb.old[u] = dmin[i];
+#pragma unroll
+      for (int g = 0; g < G; ++g) sb.hv[u][g] = x16[(int64_t)g * n_pad + i];
+      sb.ev[u] = e16[i];
+    }
+  };
+  SB sbuf[2];
+  sload(sbuf[0], 0);
+#pragma unroll
+  for (int bi = 0; bi < 16 / kB; ++bi) {
+    const int i0 = bi * kB;
+    if (bi + 1 < 16 / kB) sload(sbuf[(bi + 1) & 1], i0 + kB);
+    const SB& sb = sbuf[bi & 1];
+    bool in[kB], need[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      in[u] = r0 + 8 * (i0 + u) < m;
+      need[u] = in[u];
+      if (in[u] && cidx > 0) {
+        float sacc = 0.0f;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const unsigned w[4] = {sb.hv[u][g].x, sb.hv[u][g].y, sb.hv[u][g].z, sb.hv[u][g].w};
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if (8 * g + q < D) {
+              const float xv = __half2float(
+                  __ushort_as_half((unsigned short)(w[q >> 1] >> (16 * (q & 1)))));
+              const float dd = xv - chv[8 * g + q];
+              sacc = fmaf(dd, dd, sacc);
+            }
+          }
+        }
+        const float lo = sqrtf(sacc) * kRel - sb.ev[u] - Ec;
+        if (lo > 0.0f) {
+          const double rr = (double)lo * rscale;
+          need[u] = !(rr * rr >= sb.old[u] * (1.0 + 0x1p-30));
+        }
+      }
+    }
+    // the exact path for the rows left: the fp32 row from the row-major copy
+    // (one 64-byte line at d = 16; XA null: the quad planes, Q lines)
+    f4v xv[kB][Q];
+    const f4v* XA4 = reinterpret_cast<const f4v*>(XA);
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int64_t i = base + r0 + 8 * (i0 + u);
+      if (need[u]) {
+#pragma unroll
+        for (int qq = 0; qq < Q; ++qq)
+          xv[u][qq] = XA4 ? XA4[i * Q + qq] : X4[(int64_t)qq * n_pad + i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      double v = in[u] ? sb.old[u] : 0.0;
+      if (need[u]) {
+        auto xf = [&](int f) { return (double)xv[u][f >> 2][f & 3]; };
+        auto cf = [&](int f) { return cen[f]; };
+        const double R = np_sqdist(xf, cf, D);
+        const double rt = sqrt(R);
+        const double tt = rt * rt;
+        if (tt < sb.old[u]) {
+          v = tt;
+          const int64_t i = base + r0 + 8 * (i0 + u);
+          dmin[i] = tt;
+          near[i] = cidx;
+        }
+      }
+      acc = (i0 + u == 0) ? v : acc + v;  // NumPy: r[j] = a[j], then r[j] += a[j + 8 i]
+    }
+  }
+  if (m < kSeedBlock) return;  // the partial last block: seed_tail_sum_kernel sums it
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) acc = acc + __shfl_xor(acc, o);
+  if ((t & 63) == 0) swave[t >> 6] = acc;
+  __syncthreads();
+  if (t == 0)
+    blocksums[b] = ((swave[0] + swave[1]) + (swave[2] + swave[3])) +
+                   ((swave[4] + swave[5]) + (swave[6] + swave[7]));
 }
 
 // The partial last block's pairwise sum (m < 8192 elements at base): its
@@ -1743,6 +1880,32 @@ void seed_update(Ctx& c, const double* cen) {
                             double*, int32_t*, const double*, int);
       static const int u16 = std::getenv("CDR_SEED16_U") ? std::atoi(std::getenv("CDR_SEED16_U")) : 0;
       static const bool pr16 = std::getenv("CDR_SEED16_PR") != nullptr;  // A/B: prune at d <= 16
+      // the pairwise tree in registers (d = 8, 16; CDR_SEED16_LDS=1: staged in LDS)
+      const bool lds16 = std::getenv("CDR_SEED16_LDS") && std::atoi(std::getenv("CDR_SEED16_LDS"));
+      if ((d == 8 || d == 16) && !lds16 && !pr16 && !u16) {
+        // the exact path's rows from the row-major copy (built once per point
+        // set; the bounded Lloyd screen gathers from it too); CDR_SEED_XA=0:
+        // from the quad planes
+        const bool xa = !std::getenv("CDR_SEED_XA") || std::atoi(std::getenv("CDR_SEED_XA"));
+        if (xa) ensure_rowmajor(c);
+        hipLaunchKernelGGL(d == 8 ? seed_update16r_kernel<8> : seed_update16r_kernel<16>,
+                           dim3(nb), dim3(512), 0, c.stream, c.x32.as<float>(),
+                           c.seed_x16.as<uint4>(), c.seed_e16.as<float>(), c.n, c.n_pad,
+                           c.seed_scalar.as<double>(), dch, dEc, std::ldexp(1.0, -tau),
+                           c.dmin.as<double>(), c.blocksums.as<double>(), near, cidx,
+                           xa ? c.xa32.as<float>() : nullptr);
+        HIP_CHECK(hipGetLastError());
+        if (nb > nfull) {
+          seed_tail_plan(c, c.n - nfull * kSeedBlock);
+          hipLaunchKernelGGL(seed_tail_sum_kernel, dim3(1), dim3(256), 0, c.stream,
+                             c.dmin.as<double>(), nfull, c.seed_tail_plan.as<int>(),
+                             c.seed_tail_nleaves, c.seed_tail_nheights, c.blocksums.as<double>());
+          HIP_CHECK(hipGetLastError());
+        }
+        c.seed_count += 1;
+        c.seed_scanned = false;
+        return;
+      }
       const S16Fn f16 = d == 8    ? (pr16 ? seed_update16_kernel<8, 0, true> : seed_update16_kernel<8>)
                         : d == 16 ? (pr16       ? seed_update16_kernel<16, 0, true>
                                      : u16 == 1 ? seed_update16_kernel<16, 1>
