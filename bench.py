@@ -340,12 +340,15 @@ def f64_data(n: int, d: int, k: int, seed: int):
     return (X - mn) / (mx - mn)
 
 
-def f64_bench(args, world: int, rank: int, json_fd: int) -> None:
+def f64_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
     """F64 mode (`main.py`'s real data path): exact fp64
-    NumPy-order assignment of every point (assign_exact_all) + exact
-    sequential-order cluster sums (csrc/f64sum.hip), one host round trip per
-    step (cdr_lloyd_step_f64), centroids = sums / counts on the host as
-    src/kmeans_plusplus.py:41 does.  Single GPU (replicas at N > 1)."""
+    NumPy-order assignment of every point + exact sequential-order cluster
+    sums (csrc/f64sum.hip), centroids = sums / counts on the host as
+    src/kmeans_plusplus.py:41 does.  One GPU: cdr_lloyd_step_f64.  N GPUs:
+    the rows sharded in rank order (strong: the config's n in total; weak: n
+    per GPU), each step's exact sequential sums composed from the shards'
+    programs after two all-gathers (cdr_dist.f64_sharded_sums, DESIGN.md
+    4.5b)."""
     import numpy as np
 
     import _cdr
@@ -354,15 +357,31 @@ def f64_bench(args, world: int, rank: int, json_fd: int) -> None:
     if args.n_total:
         n = args.n_total
     k = args.k or 16
-    X = f64_data(n, d, k, args.seed)
+    n_total = n * world if args.scaling == "weak" else n
+    X = f64_data(n_total, d, k, args.seed)
     ctx = _cdr.Context(int(os.environ.get("LOCAL_RANK", "0")))
-    ctx.load_points(X)
+    comm = None
+    if dist is not None and world > 1:
+        import torch
+
+        from cdr_dist import Comm, f64_sharded_sums, shard_rows
+
+        comm = Comm(dist, device)
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        begin, n_local = shard_rows(n_total, world, rank)
+        ctx.load_points(X[begin:begin + n_local])
+    else:
+        ctx.load_points(X)
     if ctx.info()["mode"] != _cdr.MODE_F64:
         raise RuntimeError("F64 leg: the points did not load in F64 mode")
-    C = X[np.sort(np.random.default_rng(42).choice(n, k, replace=False))].copy()
+    C = X[np.sort(np.random.default_rng(42).choice(n_total, k, replace=False))].copy()
+    del X
 
     def step(C):
-        sums, counts = ctx.lloyd_step_f64(C)
+        if comm is not None:
+            sums, counts = f64_sharded_sums(ctx, comm, C)
+        else:
+            sums, counts = ctx.lloyd_step_f64(C)
         nz = counts > 0
         C = C.copy()
         C[nz] = sums[nz] / counts[nz, None]
@@ -371,25 +390,39 @@ def f64_bench(args, world: int, rank: int, json_fd: int) -> None:
     for _ in range(args.warmup):
         C = step(C)
     ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
     ctx.profile_reset(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         C = step(C)
+    ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     prof = ctx.profile_read()
     ctx.profile_reset(False)
     assign_ms = prof["screen_ms"] / max(prof["steps"], 1)
     kern_ms = prof["step_ms"] / max(prof["steps"], 1)
-    alg = n * (8 * d + 4)  # read the fp64 point, write its int32 label
+    n_local = ctx.info()["n"]
+    alg = n_local * (8 * d + 4)  # read the fp64 point, write its int32 label
     achieved = alg / (assign_ms / 1e3) / 1e9
     out = {
         "metric": "Lloyd point-iters/sec, F64 mode (exact fp64 assignment + exact sequential sums)",
-        "value": world * n * args.steps / elapsed, "unit": "point-iters/s", "n_gpus": world,
+        "value": n_total * args.steps / elapsed, "unit": "point-iters/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
         "data": "synthetic blobs, min-max normalised on the host (non-grid fp64)",
-        "config": {"workload": desc.format(k=k), "n_files": n, "d": d, "k": k,
-                   "parallelism": "one GPU (independent replicas at N > 1)"},
+        "config": {"workload": desc.format(k=k), "n_files": n_total, "d": d, "k": k,
+                   "parallelism": "one GPU" if comm is None else
+                   f"rows sharded over {world} GPUs; exact sequential sums composed from the "
+                   "shards' programs after two all-gathers per step"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                      "kernel": ctx.profile_kernel(), "alg_bytes_per_launch": alg,
@@ -546,7 +579,7 @@ def main() -> None:
         ingest_bench(args, world, rank, dist, device, json_fd)
         return
     if args.config == "f64":
-        f64_bench(args, world, rank, json_fd)
+        f64_bench(args, world, rank, dist, device, json_fd)
         if dist is not None:
             dist.destroy_process_group()
         return

@@ -207,6 +207,7 @@ struct Ctx {
   // step gathers from, and the cumulative drifts bnd = int64 W[64] (2^-40
   // units) | float W up [64] | float W down [64]
   DevBuf zb, xh16, bnd, t_acc;
+  DevBuf rs_hist;  // radix.hip: per-tile digit counts and digit bases of the fallback sort
   DevBuf zl, zn;  // split bounded screen: per-wave lists of failed points (screen32bz), lengths
   bool zb_valid = false, xh_valid = false, bnd_ok = false;
   int32_t run_k = 0;
@@ -351,6 +352,10 @@ bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max
 // exact sequential-order F64 centroid sums in parallel (f64sum.hip); false =
 // shape not covered (d < 2 or k > 64)
 bool f64_sums_parallel(Ctx& c, int k, double* d_sums, bool pre = false);
+// stable LSD radix sort of (key, value) pairs over key bits [0, end_bit)
+// (radix.hip); true when the sorted pairs are in (k1, v1)
+template <typename K, typename V>
+bool radix_sort_pairs(Ctx& c, K* k0, K* k1, V* v0, V* v1, int64_t n, int end_bit);
 // sharded F64 sums (f64sum.hip; include/cdr.h cdr_f64s_*)
 int f64s_cap();
 bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot);

@@ -7,9 +7,10 @@
 //   total_accesses = count(events)                    :42
 //   max_concurrency = max over sec of count(file, sec), sec = floor(ts_epoch) :44-46
 //   max_ts = max(ts_epoch) over the whole log         :48
-// Events are keyed (file << 32 | sec - sec_min), radix-sorted (skipped when the
-// input is already grouped by file and ordered by second, which is what the
-// per-file Poisson generator produces), then each file's run is reduced.
+// Events are keyed (file << 32 | sec - sec_min), radix-sorted (radix.hip, a
+// hand-written stable LSD sort; skipped when the input is already grouped by
+// file and ordered by second, which is what the per-file Poisson generator
+// produces), then each file's run is reduced.
 // Integer counts are exact by construction.
 //
 // K6 finalize (:53-94): age = observation_end - creation_ts_epoch (0 when the
@@ -17,7 +18,6 @@
 // (mean 0 -> 1.0), locality = local / total (total 0 -> 1.0), then min-max
 // normalisation of the five columns (max == min -> 0.0).  Long columns are
 // normalised as double(v - min) / double(max - min), as Spark's `/` does.
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -442,15 +442,11 @@ void features_aggregate_resident(Ctx& c, int64_t ne, int64_t n_files, int64_t* o
     HIP_CHECK(hipStreamSynchronize(c.stream));
     unsigned* keys = k0;
     unsigned long long* vals = v0;
-    if (hunsorted) {
-      size_t tmp_bytes = 0;
-      HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, v0, v1, (int)ne,
-                                                   0, fb32, c.stream));
-      c.ev_scratch2.ensure(tmp_bytes + 256);
-      HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c.ev_scratch2.p, tmp_bytes, k0, k1, v0, v1,
-                                                   (int)ne, 0, fb32, c.stream));
-      keys = k1;
-      vals = v1;
+    if (hunsorted) {  // stable: a file's events keep their time order (radix.hip)
+      if (radix_sort_pairs(c, k0, k1, v0, v1, ne, fb32)) {
+        keys = k1;
+        vals = v1;
+      }
     }
     HIP_CHECK(hipMemsetAsync(start, 0xFF, 8 * nf1, c.stream));  // -1
     HIP_CHECK(hipMemsetAsync(end, 0, 8 * nf1, c.stream));
@@ -493,14 +489,10 @@ void features_aggregate_resident(Ctx& c, int64_t ne, int64_t n_files, int64_t* o
   unsigned long long* keys = k0;
   uint8_t* flags = f0;
   if (hunsorted && ne > 1) {
-    size_t tmp_bytes = 0;
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, k0, k1, f0, f1, (int)ne, 0,
-                                                 end_bit, c.stream));
-    c.ev_scratch2.ensure(tmp_bytes + 256);
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(c.ev_scratch2.p, tmp_bytes, k0, k1, f0, f1,
-                                                 (int)ne, 0, end_bit, c.stream));
-    keys = k1;
-    flags = f1;
+    if (radix_sort_pairs(c, k0, k1, f0, f1, ne, end_bit)) {
+      keys = k1;
+      flags = f1;
+    }
   }
   // runs per file
   HIP_CHECK(hipMemsetAsync(start, 0xFF, 8 * nf1, c.stream));  // -1

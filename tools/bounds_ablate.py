@@ -26,6 +26,7 @@ np.random.seed(0)
 run = DeviceLloyd(ctx, C, -1.0, lambda g: ctx.get_rows([g])[0], n)
 run.advance(6)
 res = {m: [] for m in masks}
+first = {}
 for rnd in range(3):
     for m in masks:
         fix = m.startswith("F")
@@ -34,7 +35,9 @@ for rnd in range(3):
         ctx.profile_reset(True)
         run.advance(4, chunk=4, chunk_max=4)
         p = ctx.profile_read()
+        q = ctx.profile_read_sub()
         res[m].append(p["screen_ms"] / max(p["steps"], 1))
+        first.setdefault(m, []).append(q["first_ms"] / max(q["steps"], 1))
         if not m.startswith("F") and int(m) & 128:  # candidates of the exact pass (high word)
             print(f"mask {m}: steps {p['steps']} tight {p['tight_points'] & 0xFFFFFFFF} "
                   f"candidates {p['tight_points'] >> 32} profile {p}")
@@ -42,5 +45,6 @@ for rnd in range(3):
 os.environ["CDR_BOUNDS_DBG"] = "0"
 os.environ["CDR_FIX_ABL"] = "0"
 for m in masks:
-    print(f"mask {m:>4}: screen32b {np.median(res[m]) * 1e3:8.1f} us  (rounds {[round(x * 1e3, 1) for x in res[m]]})")
+    print(f"mask {m:>4}: screen32b {np.median(res[m]) * 1e3:8.1f} us  first kernel "
+          f"{np.median(first[m]) * 1e3:6.1f} us (rounds {[round(x * 1e3, 1) for x in res[m]]})")
 run.finish()
