@@ -466,7 +466,7 @@ def pmc_traffic(config: str, n_local: int, kname: str | None = None, steps=None)
         return None
     with open(path) as fh:
         rec = json.load(fh)
-    r = rec.get(config)
+    r = rec.get(f"{config}@{n_local}") or rec.get(config)
     if not r or int(r.get("n_local", -1)) != n_local:
         return None
     if kname is not None and not kname.startswith(str(r.get("kernel", "")).split("+")[0].split("<")[0]):
