@@ -488,6 +488,10 @@ def kernel_bytes(kname: str, n_local: int, prof: dict, steps: int) -> int:
     bounded screen32b the 4-byte bound word of every point, plus, for each
     point whose bound failed (profile counter, per step), its hi row and its
     new bound word."""
+    if kname.startswith("screen32bs16<"):  # 2-byte words (DESIGN.md 4.3g)
+        q = int(kname[len("screen32bs16<"):].split(",")[0])
+        tight = prof.get("tight_points", 0) / max(steps, 1)
+        return int(n_local * 2 + tight * (16 * q + 2))
     if kname.startswith("screen32bs<"):  # the fp32 row (16 Q bytes) of each re-read point
         q = int(kname[len("screen32bs<"):].split(",")[0])
         tight = prof.get("tight_points", 0) / max(steps, 1)

@@ -270,6 +270,14 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
   const double mu0 = v0 ? a.ref[d + f0] : 0.0, mu1 = v1 ? a.ref[d + f0 + 1] : 0.0;
   const bool whead = a.bnd && row && (t & 7) == 0;
   const long long w_old = whead ? a.bnd[j] : 0;
+  // the 2-byte words' base and header (plan32.h kBnd*)
+  unsigned char* const bb = reinterpret_cast<unsigned char*>(a.bnd);
+  const long long g_old = whead ? reinterpret_cast<const long long*>(bb + kBndG)[j] : 0;
+  int hdr0 = 0, e0c = 0;
+  if (a.bnd) {
+    hdr0 = reinterpret_cast<const int*>(bb + kBndHdr)[0];
+    e0c = reinterpret_cast<const int*>(bb + kBndHdr)[2];
+  }
   const long long st0 = state[0];
   if (st0 == 0) return;  // uniform: the loop has stopped
   if (a.abl & 1) {
@@ -421,6 +429,61 @@ __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
     float* wf = reinterpret_cast<float*>(a.bnd + 64);
     wf[j] = wn < (1LL << 52) ? f32_up(wvv) : INFINITY;
     wf[64 + j] = f32_dn(wvv);
+  }
+  if (a.bnd) {  // (uniform) the 2-byte words' tables
+    // A_j = W_j - G_j: what the current base has accumulated.  Rebase (G_j =
+    // W_j, every kept word re-encoded by the next screen) when the base was
+    // never set, when the code's 2^-6 truncation of A reaches half the
+    // step's drift budget (A > 32 M), when the drift has fallen to twice the
+    // code floor 2^E0 (margins near M would not be representable), or when
+    // A nears the code range (2^(E0 + 16)).  The floor follows the drift,
+    // E0 = floor(log2(M / 64)) (a margin below M is spent within a step;
+    // the range reaches ~1000 M), so a decaying drift rebases rarely
+    long long wn = 0;
+    double Aj = 0.0;
+    if (whead) {
+      wn = a.bnd[j];  // (this thread's own store above)
+      Aj = ldexp((double)(wn - g_old), -40);
+    }
+    __shared__ double r_A[8];
+    double am = Aj;
+#pragma unroll
+    for (int o = 32; o >= 8; o >>= 1) am = fmax(am, __shfl_xor(am, o));
+    if (lane == 0) r_A[wv] = am;
+    __syncthreads();
+    double Amax = 0.0, M = 0.0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      Amax = fmax(Amax, r_A[w]);
+      M = fmax(M, r_dm[w]);
+    }
+    const bool rebase = hdr0 == 0 ||
+                        (M > 0.0 && (Amax > 32.0 * M || ldexp(1.0, e0c + 1) > M)) ||
+                        Amax > ldexp(1.0, e0c + 14);
+    int e0n = e0c;
+    if (rebase) {
+      if (M > 0.0) e0n = ilogb(M * 0x1p-6);
+      else if (hdr0 == 0) e0n = -20;
+      e0n = e0n < -120 ? -120 : (e0n > 100 ? 100 : e0n);
+    }
+    if (whead) {
+      const bool exact = wn < (1LL << 52);  // (saturated W: every test fails)
+      const long long g_new = rebase ? wn : g_old;
+      reinterpret_cast<long long*>(bb + kBndG)[j] = g_new;
+      reinterpret_cast<unsigned*>(bb + kBndT)[j] =
+          exact ? zb16_thr(f32_up(ldexp((double)(wn - g_old), -40)), e0c) : 1022u;
+      reinterpret_cast<float*>(bb + kBndWdg)[j] =
+          exact ? f32_dn(ldexp((double)(wn - g_new), -40)) : -1.0f;
+      reinterpret_cast<float*>(bb + kBndDG)[j] =
+          rebase ? f32_up(ldexp((double)(g_new - g_old), -40)) : 0.0f;
+    }
+    if (t == 0) {
+      int* hd = reinterpret_cast<int*>(bb + kBndHdr);
+      hd[0] = 1;
+      hd[1] = e0c;
+      hd[2] = e0n;
+      hd[3] = rebase ? 1 : 0;
+    }
   }
   if (!a.plan || reason != kLLRun || (a.abl & 2)) return;
   // ---- the next step's plan (plan32_build, per element) ----
@@ -696,7 +759,7 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   // screen32b's drift bounds (kept by ll_finalize32 only)
   const bool fin_old = std::getenv("CDR_FIN_OLD") && std::atoi(std::getenv("CDR_FIN_OLD"));
   c.bnd_ok = c.ll_devplan && !fin_old;
-  c.bnd.ensure(sizeof(long long) * 64 + 2 * sizeof(float) * 64);
+  c.bnd.ensure(kBndBytes);
   HIP_CHECK(hipMemsetAsync(c.bnd.p, 0, c.bnd.bytes, c.stream));
   std::vector<double> rm(2 * d);
   for (int f = 0; f < d; ++f) {

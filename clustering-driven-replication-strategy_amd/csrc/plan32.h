@@ -30,6 +30,37 @@ __host__ __device__ inline Plan32Layout plan32_layout(int MT, int k, int d) {
   return L;
 }
 
+// Drift-bound buffer (Ctx::bnd, kept by ll_finalize32):
+//   W [64] int64 (2^-40 units) | wup [64] f32 | wdn [64] f32   (4-byte words)
+//   G [64] int64 (the 2-byte words' per-centroid base: W_j at the last rebase)
+//   T [64] u32   this step's code thresholds (base G, exponent E0 old)
+//   wdg [64] f32 W_j - G_j (new base) rounded down, for the words written now
+//   dG [64] f32  G_j(new) - G_j(old) rounded up (0 unless this step rebases)
+//   hdr [4] int32: base set, E0 old, E0 new, rebase
+constexpr size_t kBndWup = 512, kBndWdn = 768, kBndG = 1024, kBndT = 1536, kBndWdg = 1792,
+                 kBndDG = 2048, kBndHdr = 2304, kBndBytes = 2320;
+
+// 2-byte bound words (screen32bs): code << 6 | label.  The
+// code is a truncated 10-bit float (4 exponent bits from 2^E0, 6 mantissa
+// bits) of v = Z - G_label, Z the 4-byte word's value; truncation rounds
+// down, so G + dec(code) <= Z.  Code 0: no bound (always fails); 1023: a
+// padding row (always kept); real points are clamped to 1022.
+constexpr unsigned kZ16Pad = 1023u << 6;
+__host__ __device__ inline int zb16_code(float v, int e0) {  // -1: v <= 0 (or NaN)
+  if (!(v > 0.0f)) return -1;
+  return (int)(__builtin_bit_cast(unsigned, v) >> 17) - ((127 + e0) << 6);
+}
+__host__ __device__ inline float zb16_dec(int code, int e0) {  // 1 <= code <= 1022
+  return __builtin_bit_cast(float, (unsigned)(code + ((127 + e0) << 6)) << 17);
+}
+// the test threshold of a centroid: a word passes iff code > T, i.e. when
+// dec(code) > v >= W_j(t) - G_j (v rounded up)
+__host__ __device__ inline unsigned zb16_thr(float v, int e0) {
+  if (v != v) return 1022u;
+  const int c = zb16_code(v, e0);
+  return (unsigned)(c < 0 ? 0 : (c > 1022 ? 1022 : c));
+}
+
 // Bound on ||fp16(xhat32) - xhat|| over the point set (screen32p): xhat32 =
 // fma(x, 2^sigma, -mu 2^sigma) errs by <= 2^-24 |xhat| (0 when exact) and the
 // fp16 rounding by <= 2^-11 |xhat32| + 2^-25 per feature; with dev_f >=

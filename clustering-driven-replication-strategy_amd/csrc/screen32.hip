@@ -1804,7 +1804,12 @@ struct S32BArgs {
   uint32_t* zl;
   int32_t* zn;
   int64_t zcap;
+  // the fused screen32bs: 2-byte words and their tables in
+  // Ctx::bnd (plan32.h kBnd*)
+  uint16_t* zh;
+  const unsigned char* bt;
 };
+constexpr int kZ16Chunk = 512;  // points per wave-chunk of the 2-byte word stream (8 per lane)
 
 // The chunks wave `wv` of this workgroup streams: wbase + i * wstride below
 // wend.  With slot_wg > 0 the workgroups of one CU slot (launch generation)
@@ -1867,6 +1872,30 @@ __device__ __forceinline__ unsigned zb_pack(float l0, float u0, float w, unsigne
   const float m = 0x1p-21f * ((l0 + u0) + w);
   const float z = s - m;
   return (z > 0.0f ? (__float_as_uint(z) & ~63u) : 0xBF800000u) | label;
+}
+
+// The 2-byte word of a decided point: zb_pack's Z relative to the point's
+// base (w = W_a - G_a rounded down), truncated to its code (plan32.h); no
+// bound (code 0) when Z <= G_a + 2^E0.
+__device__ __forceinline__ unsigned short zb16_pack(float l0, float u0, float w, int e0,
+                                                    unsigned label) {
+  if (!(l0 > 0.0f) || !(u0 >= 0.0f) || !(w >= 0.0f)) return (unsigned short)label;
+  l0 = fminf(l0, 0x1p60f) * (1.0f - 0x1p-20f);
+  const float s = (l0 - u0) + w;
+  const float m = 0x1p-21f * ((l0 + u0) + w);
+  int c = zb16_code(s - m, e0);
+  c = c < 0 ? 0 : (c > 1022 ? 1022 : c);
+  return (unsigned short)((unsigned)c << 6 | label);
+}
+// A kept word carried to a new base (G_a grows by dg >= the exact step) and
+// exponent: dec(code) - dg rounded down, then truncated; codes 0 and 1023 stay
+__device__ __forceinline__ unsigned zb16_rebase(unsigned w, float dg, int e0o, int e0n) {
+  const unsigned c = w >> 6;
+  if (c == 0u || c == 1023u) return w;
+  const float t = zb16_dec((int)c, e0o) - dg;  // |error| <= 2^-24 |t|
+  int cn = t > 0.0f ? zb16_code(t * (1.0f - 0x1p-22f), e0n) : -1;
+  cn = cn < 0 ? 0 : (cn > 1022 ? 1022 : cn);
+  return (unsigned)cn << 6 | (w & 63u);
 }
 
 template <int Q, int MT>
@@ -2372,6 +2401,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   __shared__ unsigned flist[4][SPLIT ? 1 : kSList];
   __shared__ unsigned long long mtab[64 * 17];  // this workgroup's moves, [k][d + 1]
   __shared__ float msl[16];                     // -mu_f 2^sigma
+  __shared__ float dgs[64];                     // 2-byte words: this step's base moves (rebase)
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wv = t >> 6;
@@ -2380,10 +2410,14 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   const int64_t nchunks = B.nchunks;
   const int k = a.k, d = a.d, d1 = d + 1;
 
-  // ---- phase 1 loads (screen32b's) ----
+  // ---- phase 1 loads: 2-byte words, 8 per lane per 1 KiB chunk (the split
+  // form: screen32bz streamed 4-byte words) ----
+  // points per chunk and the entry format's chunk-iteration shift
+  constexpr int CH = SPLIT ? kBChunk : kZ16Chunk;
+  constexpr int SH = SPLIT ? 14 : 15;
   auto zload = [&](u4v& z, int64_t ci) __attribute__((always_inline)) {
     const int64_t cc = ci < nchunks ? ci : nchunks - 1;
-    z = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(B.zb + cc * kBChunk) + lane);
+    z = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(B.zh + cc * kZ16Chunk) + lane);
   };
   // this wave's chunks: wbase + i wstride below wend
   int64_t wbase, wend;
@@ -2408,7 +2442,29 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   float cv = 0.0f;
   const int cm = t >> 5, ci4 = (t >> 3) & 3, chh = (t >> 2) & 1, cc = t & 3;
   if (t < MT * 32) cv = a.cinit[(cm * 16 + ci4 * 4 + cc) * 64 + chh * 32];
-  const float wup_l = B.wup[lane], wdn_l = B.wdn[lane];  // lane j: W_j (k <= 64)
+  // lane j: W_j (4-byte words: wup for the test, wdn for new words); 2-byte
+  // words: the code threshold T_j, W_j - G_j for new words, the rebase step
+  float wup_l = 0.0f, wnew_l;
+  unsigned thr_l = 0u;
+  int e0o = 0, e0n = 0, rebase = 0;
+  if constexpr (SPLIT) {
+    wup_l = B.wup[lane];
+    wnew_l = B.wdn[lane];
+  } else {
+    // (CDR_BOUNDS_DBG=1, tests: every real point's bound fails)
+    thr_l = (B.dbg & 1) ? 1022u : reinterpret_cast<const unsigned*>(B.bt + kBndT)[lane];
+    wnew_l = reinterpret_cast<const float*>(B.bt + kBndWdg)[lane];
+    const int* hd = reinterpret_cast<const int*>(B.bt + kBndHdr);
+    e0o = hd[1];
+    e0n = hd[2];
+    rebase = hd[3];
+  }
+  // a decided point's word (ok: bounds (l0, u0); w = __shfl(wnew_l, lab),
+  // taken by every lane) or "no bound"
+  auto zput = [&](int pt, bool ok, float l0, float u0, float w, unsigned lab) __attribute__((always_inline)) {
+    if constexpr (SPLIT) B.zb[pt] = ok ? zb_pack(l0, u0, w, lab) : (kZbStale | lab);
+    else B.zh[pt] = ok ? zb16_pack(l0, u0, w, e0n, lab) : (unsigned short)lab;
+  };
   const float msv = lane < d ? F.ms[lane] : 0.0f;        // lane f: -mu_f 2^sigma
   const float thr0 = a.thr_dev ? a.thr_dev[0] : a.thr0, thr_rel = a.thr_rel;
   const float Dv = a.thr_dev ? a.thr_dev[1] : a.Dv;
@@ -2420,6 +2476,8 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   if (t < MT * 32) sC[t] = cv;
   for (int e = t; e < 64 * 17; e += 256) mtab[e] = 0ull;
   if (t < 16) msl[t] = msv;
+  if constexpr (!SPLIT)  // (LDS: a vector load here would wait behind the stream's)
+    if (t < 64) dgs[t] = reinterpret_cast<const float*>(B.bt + kBndDG)[t];
   __syncthreads();
   CDR_TP(1);
 
@@ -2697,8 +2755,8 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     const float uba = fmaf(__builtin_amdgcn_sqrtf(qa), 1.0f + 0x1p-18f, eb[ao]);
     const float l0P = fmaf(hc[ao], 1.0f - 0x1p-22f, -uba);
     const bool keep = l0P > uba * (1.0f + 0x1p-20f);
-    const float w_ao = __shfl(wdn_l, ao);
-    if (valid && keep) B.zb[pt] = zb_pack(l0P, uba, w_ao, (unsigned)ao);
+    const float w_ao = __shfl(wnew_l, ao);
+    if (valid && keep) zput(pt, true, l0P, uba, w_ao, (unsigned)ao);
     const bool need = valid && !keep;
     const unsigned long long nm = __ballot(need);
     if (!nm) return;
@@ -2726,7 +2784,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     const float vs = __uint_as_float(sA_ & ~63u);
     const bool cert = vs > fmaf(vb, thr_rel, thr0);  // NaN: never certified
     const bool unc = need && !cert;
-    const float w_lab = __shfl(wdn_l, label);
+    const float w_lab = __shfl(wnew_l, label);
     // K-case: the point's bound word from its split keys
     if (need && cert) {
       const float xu = fmaf(xx, 1.0f + 0x1p-19f, 0x1p-120f);  // >= ||xhat32||^2
@@ -2736,7 +2794,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       const float gs = vs - ((thr0 + Dhi) - xl);
       const float u0 = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gb, 0.0f)), 1.0f + 0x1p-19f, dn32);
       const float l0 = fmaf(__builtin_amdgcn_sqrtf(fmaxf(gs, 0.0f)), 1.0f - 0x1p-19f, -dn32);
-      B.zb[pt] = zb_pack(l0, u0, w_lab, (unsigned)label);
+      zput(pt, true, l0, u0, w_lab, (unsigned)label);
     }
     const unsigned long long um = __ballot(unc);
     if constexpr (DEFER) {
@@ -2763,9 +2821,10 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       bool c2;
       float u0, l0;
       const int lab = near_tie(unc, ao, bA, xh, T0, T1, g.x, xx, c2, u0, l0);
+      const float wl = __shfl(wnew_l, lab);
       if (unc) {
         labf = lab;
-        B.zb[pt] = c2 ? zb_pack(l0, u0, __shfl(wdn_l, lab), (unsigned)lab) : (kZbStale | (unsigned)lab);
+        zput(pt, c2, l0, u0, wl, (unsigned)lab);
       }
 #ifdef CDR_EXPERIMENTS
       } else if (unc) {
@@ -2784,8 +2843,8 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     const int e = 64 * b + lane;
     g.valid = e < cnt;
     const unsigned ent = fl[g.valid ? e : 64 * b];  // (entry 64 b exists)
-    const int64_t ci = wbase + (int64_t)(ent >> 14) * wstride;
-    const int64_t pt = ci * kBChunk + ((ent >> 6) & 255);
+    const int64_t ci = wbase + (int64_t)(ent >> SH) * wstride;
+    const int64_t pt = ci * CH + ((ent >> 6) & (CH - 1));
     g.pt = (int)pt;
     g.ao = (int)(ent & 63);
 #pragma unroll
@@ -2883,8 +2942,10 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   GB cur;
   bool pend = false;
   int head = 0;  // listed entries before head are gathered (wave-uniform)
+  // (returns with room for one more chunk's entries: the stream breaks its
+  // group early when a chunk would not fit, which only dense failures do)
   auto step2 = [&](int& cnt, bool last) __attribute__((always_inline)) {
-    constexpr int kRoom = kBPD * kBChunk;
+    constexpr int kRoom = CH;
     for (;;) {
       if (pend) {
         decide(cur);
@@ -2895,8 +2956,8 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
         const int e = head + lane;
         cur.valid = e < cnt;
         const unsigned ent = fl[cur.valid ? e : head];
-        const int64_t ci = wbase + (int64_t)(ent >> 14) * wstride;
-        const int64_t pt = ci * kBChunk + ((ent >> 6) & 255);
+        const int64_t ci = wbase + (int64_t)(ent >> SH) * wstride;
+        const int64_t pt = ci * CH + ((ent >> 6) & (CH - 1));
         cur.pt = (int)pt;
         cur.ao = (int)(ent & 63);
 #pragma unroll
@@ -2922,48 +2983,91 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       if (!again) break;
     }
   };
+#else
+  constexpr int head = 0;  // (phase 2 in bursts compacts the list itself)
 #endif
 
-  // ---- phase 1: the bound words, 4 points per lane per chunk ----
+  // ---- phase 1: the bound words, 8 points per lane per chunk ----
+  // Groups of kBPD chunks, kBPD in flight; phase 2 between groups.  A chunk
+  // whose entries would not fit the list ends its group early: phase 2
+  // drains, and the stream resumes at that chunk (loads issued again).
+  // Rebase steps carry every kept word to the new base as it streams past
+  // (a failed point's word is written by its decision instead).
   int cnt = 0;
-  int64_t it = 0;
-  for (int64_t C0 = wbase;; C0 += (int64_t)kBPD * wstride) {
+  int it = 0;  // chunk ordinal within this wave's range (the entries' high bits)
+  for (int64_t C0 = wbase;;) {
     const bool more = C0 < wend;  // (wave-uniform)
+    int64_t next = C0 + (int64_t)kBPD * wstride;
     if (more) {
 #pragma unroll
-    for (int i = 0; i < kBPD; ++i, ++it) {
-      const int64_t Ci = C0 + (int64_t)i * wstride;
-      if (Ci >= wend) break;
-      zload(zc[(i + kBPD - 1) % kBPD], Ci + (int64_t)(kBPD - 1) * wstride);
-      const u4v z = zc[i];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const unsigned w = z[u];
-        const unsigned lab = w & 63u;
-#ifdef CDR_EXPERIMENTS
-        const bool fail = (!(__uint_as_float(w & ~63u) > __shfl(wup_l, (int)lab)) || (B.dbg & 1)) &&
-                          !(B.dbg & 16);  // (timing: the stream alone)
-#else
-        const bool fail = !(__uint_as_float(w & ~63u) > __shfl(wup_l, (int)lab)) || (B.dbg & 1);
-#endif
-        const unsigned long long m = __ballot(fail);
-        if (m) {
-          if (fail) {
-            const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            fl[cnt + r] = (unsigned)it << 14 | (unsigned)(4 * lane + u) << 6 | lab;
-          }
-          cnt += __popcll(m);
+      for (int i = 0; i < kBPD; ++i) {
+        const int64_t Ci = C0 + (int64_t)i * wstride;
+        if (Ci >= wend) break;
+        if (cnt - head + CH > kSList) {  // (dense failures only)
+          next = Ci;
+          break;
         }
+        zload(zc[(i + kBPD - 1) % kBPD], Ci + (int64_t)(kBPD - 1) * wstride);
+        const u4v z = zc[i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const unsigned w = (z[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+          const unsigned lab = w & 63u;
+#ifdef CDR_EXPERIMENTS
+          const bool fail = !((w >> 6) > __shfl(thr_l, (int)lab)) && !(B.dbg & 16);  // (16: the stream alone)
+#else
+          const bool fail = !((w >> 6) > __shfl(thr_l, (int)lab));
+#endif
+          const unsigned long long m = __ballot(fail);
+          if (m) {
+            if (fail) {
+              const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+              fl[cnt + r] = (unsigned)it << 15 | (unsigned)(8 * lane + u) << 6 | lab;
+            }
+            cnt += __popcll(m);
+          }
+        }
+        if (rebase) {  // (uniform) the kept words to the new base
+          uint16_t* zp = B.zh + Ci * kZ16Chunk + 8 * lane;
+          u4v nz;
+          bool all = true;  // every point of the lane kept: one 16-byte store
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            unsigned o = 0;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const unsigned w = (z[q] >> (16 * hh)) & 0xFFFFu;
+              all = all && (w >> 6) > __shfl(thr_l, (int)(w & 63u));  // (the test again)
+              o |= zb16_rebase(w, dgs[w & 63u], e0o, e0n) << (16 * hh);
+            }
+            nz[q] = o;
+          }
+          if (all) {
+            *reinterpret_cast<u4v*>(zp) = nz;
+          } else {  // (a failed point's word is its decision's)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const unsigned w = (z[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+              if ((w >> 6) > __shfl(thr_l, (int)(w & 63u)))
+                zp[u] = (uint16_t)(nz[u >> 1] >> (16 * (u & 1)));
+            }
+          }
+        }
+        ++it;
       }
-    }
     }
 #if CDR_S32BS_LAZY
     step2(cnt, !more);
 #else
-    if (!more || cnt > kSList - kBPD * kBChunk) phase2(cnt, !more);
+    if (!more || cnt - head + CH > kSList - (kBPD - 1) * CH) phase2(cnt, !more);
 #endif
     if (!more) break;
+    if (next != C0 + (int64_t)kBPD * wstride) {  // resumed mid-group: load the ring again
+#pragma unroll
+      for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], next + (int64_t)i * wstride);
+    }
+    C0 = next;
   }
   }  // (!SPLIT)
   // ---- the uncertified points: the same split screen again (the same values),
@@ -3002,9 +3106,8 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     bool c2;
     float u0, l0;
     const int lab = near_tie(live, ao, (unsigned)rec.y, xh, T0, T1, xr, xx, c2, u0, l0);
-    const float w_lab = __shfl(wdn_l, lab);
-    if (live)  // the direct bounds, or none (decided again next step)
-      B.zb[pt] = c2 ? zb_pack(l0, u0, w_lab, (unsigned)lab) : (kZbStale | (unsigned)lab);
+    const float w_lab = __shfl(wnew_l, lab);
+    if (live) zput(pt, c2, l0, u0, w_lab, (unsigned)lab);  // the direct bounds, or none
     move(live, pt, ao, lab, xr);
   }
   }  // DEFER
@@ -3040,6 +3143,16 @@ __global__ void zb_reset_kernel(const uint8_t* __restrict__ lab8, uint32_t* __re
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad;
        i += (int64_t)gridDim.x * blockDim.x)
     zb[i] = i < n ? (kZbStale | lab8[i]) : 0x7F000000u;  // (2^127: above any W)
+}
+
+// 2-byte words before the first bounded step: every real point "no bound"
+// (code 0) with its current label, padding rows "always keep" (code 1023).
+__global__ void zh_reset_kernel(const uint8_t* __restrict__ lab8, uint16_t* __restrict__ zh,
+                                int64_t n, int64_t n_pad, const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad;
+       i += (int64_t)gridDim.x * blockDim.x)
+    zh[i] = i < n ? (uint16_t)lab8[i] : (uint16_t)kZ16Pad;
 }
 
 // The hi-only screen copy row by row (XH: screen32b's gathers read one line
@@ -3575,10 +3688,22 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     if (BND) {
       // bound words: reset (every point "no bound", labels from lab8) at the
       // first bounded step of a run; the row-major hi copy once per point set
+      // the fused screen32bs keeps 2-byte words; the split
+      // form (CDR_S32BS_SPLIT=1) and screen32b 4-byte ones
+      const bool split_env =
+          BS && std::getenv("CDR_S32BS_SPLIT") && std::atoi(std::getenv("CDR_S32BS_SPLIT"));
+      const bool z16 = BS && !split_env;
+      const int zfmt = z16 ? 16 : 32;
+      if (c.zb_fmt != zfmt) c.zb_valid = false;
+      c.zb_fmt = zfmt;
       c.zb.ensure(sizeof(uint32_t) * (size_t)c.n_pad);
       if (!c.zb_valid) {
-        hipLaunchKernelGGL(zb_reset_kernel, dim3(2048), dim3(256), 0, c.stream,
-                           c.lab8.as<uint8_t>(), c.zb.as<uint32_t>(), c.n, c.n_pad, gate);
+        if (z16)
+          hipLaunchKernelGGL(zh_reset_kernel, dim3(2048), dim3(256), 0, c.stream,
+                             c.lab8.as<uint8_t>(), c.zb.as<uint16_t>(), c.n, c.n_pad, gate);
+        else
+          hipLaunchKernelGGL(zb_reset_kernel, dim3(2048), dim3(256), 0, c.stream,
+                             c.lab8.as<uint8_t>(), c.zb.as<uint32_t>(), c.n, c.n_pad, gate);
         HIP_CHECK(hipGetLastError());
       }
       if (!BS && !c.xh_valid) {
@@ -3604,7 +3729,9 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       b.zb = c.zb.as<uint32_t>();
       b.wup = reinterpret_cast<const float*>(c.bnd.as<long long>() + 64);
       b.wdn = b.wup + 64;
-      b.nchunks = c.n_pad / kBChunk;
+      b.nchunks = c.n_pad / (z16 ? kZ16Chunk : kBChunk);
+      b.zh = z16 ? c.zb.as<uint16_t>() : nullptr;
+      b.bt = reinterpret_cast<const unsigned char*>(c.bnd.p);
       b.t_acc = c.prof_on ? c.t_acc.as<long long>() : nullptr;
       b.dbg = std::getenv("CDR_BOUNDS_DBG") ? std::atoi(std::getenv("CDR_BOUNDS_DBG")) : 0;
 #ifndef CDR_EXPERIMENTS
@@ -3651,8 +3778,13 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
         // decides the lists.  Measured at config 3 (profiles/r05_split_ab.txt):
         // the stream alone takes ~80 us and the decisions ~100-130 us as their
         // own launch, so the fused kernel (~165-180 us) stays the default
-        const bool split_env =
-            std::getenv("CDR_S32BS_SPLIT") && std::atoi(std::getenv("CDR_S32BS_SPLIT"));
+        // the near-tie list holds at most the points of a wave's chunks
+        const int64_t need = bs_max_chunks(b, nwg) * (z16 ? kZ16Chunk : kBChunk);
+        if (need > b.p.cap) {
+          c.fb_list.ensure(sizeof(int2) * (size_t)nwaves * (size_t)need);
+          b.p.fb_list = c.fb_list.as<int2>();
+          b.p.cap = (int)need;
+        }
         b.zl = nullptr;
         b.zn = nullptr;
         b.zcap = 0;
@@ -3663,8 +3795,8 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
           b.zl = c.zl.as<uint32_t>();
           b.zn = c.zn.as<int32_t>();
         }
-        snprintf(c.prof_kernel, sizeof(c.prof_kernel), split_env ? "screen32bs<%d,%d>split" : "screen32bs<%d,%d>",
-                 PQ, MT);
+        snprintf(c.prof_kernel, sizeof(c.prof_kernel),
+                 split_env ? "screen32bs<%d,%d>split" : "screen32bs16<%d,%d>", PQ, MT);
         if (prof) prof_mark(c, 0);
         if (split_env) {
           screen32bz_launch(grid, c.stream, b);

@@ -1656,6 +1656,49 @@ __global__ __launch_bounds__(256) void seg_fill_kernel(const SegScan* __restrict
 
 // ---- device-resident seeding (seed_run) -----------------------------------
 
+// The left-to-right sum of v[0 .. n) in one wave (the value in every lane):
+// windows of 64 W values held one per lane per register (value 64 j + l in
+// lane l of register j), the next window's loads in flight, and the chain of
+// adds reading each value through v_readlane (an SGPR operand), so the only
+// serial latency is the adds' own.  Padding past n adds +0.0, which leaves a
+// sum of non-negative terms unchanged.
+template <typename T>
+__device__ __forceinline__ T rl_lane(T v, int l) {
+  if constexpr (sizeof(T) == 8) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+    return __builtin_bit_cast(T, (unsigned long long)hi << 32 | lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  }
+}
+template <typename T>
+__device__ __forceinline__ T wave_seq_sum(const T* __restrict__ v, int64_t n) {
+  constexpr int W = 8;
+  const int lane = threadIdx.x & 63;
+  T cur[W], nxt[W];
+  auto load = [&](T (&r)[W], int64_t w0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const int64_t i = w0 + 64 * j + lane;
+      r[j] = i < n ? v[i] : T(0);
+    }
+  };
+  load(cur, 0);
+  T s = T(0);
+  for (int64_t w0 = 0; w0 < n; w0 += 64 * W) {
+    load(nxt, w0 + 64 * W);
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+#pragma unroll
+      for (int l = 0; l < 64; ++l) s = s + rl_lane(cur[j], l);
+#pragma unroll
+    for (int j = 0; j < W; ++j) cur[j] = nxt[j];
+  }
+  return s;
+}
+
 // total = dist_sq.sum() (:18): the block sums added left to right, as the host
 // does (cdr_host_seq_sum).  A total that is not finite and positive raises
 // "Probabilities contain NaN" on the host at the end; S = 1 keeps the rest of
@@ -1663,35 +1706,8 @@ __global__ __launch_bounds__(256) void seg_fill_kernel(const SegScan* __restrict
 __global__ __launch_bounds__(64) void seed_total_kernel(const double* __restrict__ bs,
                                                         int64_t nb, double* __restrict__ S,
                                                         double* __restrict__ bad) {
-  // windows of the block sums staged in LDS by the whole wave (coalesced),
-  // then added by one lane from LDS (reads run ahead of the add chain)
-  constexpr int kWin = 4096;
-  __shared__ double2 sv[kWin / 2];
-  const int lane = threadIdx.x;
-  double s = 0.0;
-  for (int64_t w0 = 0; w0 < nb; w0 += kWin) {
-    const int m = (int)((nb - w0) < kWin ? (nb - w0) : kWin);
-    __syncthreads();
-    double* svd = reinterpret_cast<double*>(sv);
-    for (int i = lane; i < m; i += 64) svd[i] = bs[w0 + i];
-    __syncthreads();
-    if (lane == 0) {
-      int i = 0;
-      for (; i + 8 <= m; i += 8) {
-        const double2 a = sv[i / 2], b = sv[i / 2 + 1], c = sv[i / 2 + 2], d = sv[i / 2 + 3];
-        s = s + a.x;
-        s = s + a.y;
-        s = s + b.x;
-        s = s + b.y;
-        s = s + c.x;
-        s = s + c.y;
-        s = s + d.x;
-        s = s + d.y;
-      }
-      for (; i < m; ++i) s = s + svd[i];
-    }
-  }
-  if (lane == 0) {
+  const double s = wave_seq_sum(bs, nb);
+  if (threadIdx.x == 0) {
     const bool ok = s > 0.0 && !isinf(s);
     S[0] = ok ? s : 1.0;
     if (!ok) bad[0] = 1.0;
@@ -2773,9 +2789,8 @@ __global__ __launch_bounds__(64) void f32r_total_kernel(const float* __restrict_
                                                         int64_t nb, int* __restrict__ infflag,
                                                         float* __restrict__ dtotal,
                                                         double* __restrict__ dbad) {
+  float total = wave_seq_sum(bs32, nb);
   if (threadIdx.x != 0) return;
-  float total = 0.0f;
-  for (int64_t b = 0; b < nb; ++b) total = total + bs32[b];
   if (!(total > 0.0f) || isinf(total)) {
     const double code = (isinf(total) && total > 0.0f && infflag[0] == 0) ? 2.0 : 1.0;
     if (dbad[0] == 0.0) dbad[0] = code;

@@ -456,7 +456,8 @@ def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     cases screen32b (LDS queue + fused fixup, CDR_S32B_SPLIT=0)."""
     monkeypatch.setenv("CDR_BOUNDS", "1")
     queue = kind.endswith("-queue")
-    monkeypatch.setenv("CDR_S32BS_SPLIT", "1" if kind.endswith("-split") else "0")
+    split = kind.endswith("-split")
+    monkeypatch.setenv("CDR_S32BS_SPLIT", "1" if split else "0")
     kind = kind.replace("-queue", "").replace("-split", "")
     monkeypatch.setenv("CDR_S32B_SPLIT", "0" if queue else "1")
     if kind == "blobs":
@@ -478,8 +479,9 @@ def test_bounded_screen_many_steps_vs_oracle(ctx, n, d, k, kind, monkeypatch):
     C, st = _loop(ctx, C0, steps, -1.0, X)
     prof = ctx.profile_read()
     ctx.profile_reset(False)
-    assert ctx.profile_kernel().startswith("screen32b<" if queue else "screen32bs<"), \
-        ctx.profile_kernel()
+    # (the fused default keeps 2-byte words)
+    want = "screen32b<" if queue else ("screen32bs<" if split else "screen32bs16<")
+    assert ctx.profile_kernel().startswith(want), ctx.profile_kernel()
     np.random.seed(3)
     C_ref, lab_ref, _, _ = ko.lloyd(X, C0, steps, -1.0)
     np.testing.assert_array_equal(ctx.labels(), lab_ref)
