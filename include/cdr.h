@@ -147,6 +147,13 @@ int cdr_seed_stats(cdr_ctx* ctx, int64_t* out);
  * picks[0..k) = the chosen rows.  CDR_ERR_NAN when a total is not finite and
  * positive ("Probabilities contain NaN").                                   */
 int cdr_seed_run(cdr_ctx* ctx, int64_t first, int32_t k, const double* u, int64_t* picks);
+/* The reference's float32 seeding (src/kmeans_plusplus.py:3-22 on a float32
+ * X, the semantics of cdr_f32r_seed_update) as one device-resident run, like
+ * cdr_seed_run: fp32 dist_sq, totals and probabilities, rng.choice's pick per
+ * step on the device.  CDR_ERR_NAN as cdr_f32r_seed_update, with the message
+ * "probabilities do not sum to 1" (Generator.choice's) when a total overflows
+ * to +inf while every dist_sq is finite.                                    */
+int cdr_f32r_seed_run(cdr_ctx* ctx, int64_t first, int32_t k, const double* u, int64_t* picks);
 /* The same over rows sharded across nranks ranks (whole 8192-row blocks per
  * shard, this context holding rows [row_begin, row_begin + n) of n_total),
  * device-resident: per step three phases, each followed by one collective the
