@@ -29,11 +29,11 @@
 #include <cstring>
 
 #include "cdr_internal.h"
+#include "fin32.h"
 #include "plan32.h"
 
 namespace cdr {
 
-enum : long long { kLLRun = 0, kLLConverged = 1, kLLEmpty = 2, kLLHostPlan = 3, kLLAmbiguous = 4 };
 constexpr int kLLState = 8;  // int64 words of ll_state
 
 bool screen32_supported(const Ctx& c, int k);
@@ -41,43 +41,6 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
                    float* dbg, float* thr_out, long long* gate);
 void plan32_point_side(const Ctx& c, double& xxmax, double& l1x);
 void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_dev);
-
-struct FinArgs {
-  const long long* sums;  // nslices x (k, d+1) int64 fixed-point sums | counts
-  int nslices;
-  int k, d, sbits, round32;
-  double tol, margin, x2;
-  const double* ref;  // inertia reference row (d), then mu (d)
-  double* C;          // current centroids (k x d)
-  double* Cnew;       // k x d means, then k counts (int64)
-  long long* state;
-  // screen32's fallback counter (device plan steps): fbc[nwaves] -> [nwaves+1]
-  int* fbc;
-  int nwaves;
-  long long* fb_acc;
-  // device plan of the next step (null: host plan)
-  unsigned char* plan;
-  int QH, MT;
-  double sc, xxmax, l1x;
-  // screen32b's drift bounds (Ctx::bnd; null: not kept): when the centroids
-  // move, W_j += M + delta_j (int64, 2^-40 units, rounded up), with
-  // delta_j >= ||chat_j(new) - chat_j(old)|| and M = max_j delta_j; then W_j
-  // rounded up and down to fp32 for the next screen
-  long long* bnd;
-  int abl;  // timing experiments only (0 in the product build)
-};
-
-// fp64 -> fp32 rounded up / down (W_j for screen32b)
-__device__ inline float f32_up(double v) {
-  float f = (float)v;
-  if ((double)f < v) f = nextafterf(f, INFINITY);
-  return f;
-}
-__device__ inline float f32_dn(double v) {
-  float f = (float)v;
-  if ((double)f > v) f = nextafterf(f, -INFINITY);
-  return f;
-}
 
 constexpr int kFinThreads = 512;
 constexpr int kFinLds = 64 * 17;  // (k, d+1) cells staged in LDS (screen32 shapes)
@@ -232,401 +195,11 @@ __global__ __launch_bounds__(kFinThreads) void ll_finalize(FinArgs a) {
 }
 
 // ll_finalize for the screen32 device plan (k <= 64, d <= 16), written for
-// latency: it is a single workgroup between two full-GPU launches, so its
-// time is its chain of dependent phases.  Thread t owns row j = t / 8 and the
-// feature pair 2 (t % 8), 2 (t % 8) + 1 of it, from the loads of the sums to
-// the plan entries of those two elements:
-//   loads (every slice of its cells, its centroid values: one round trip)
-//   -> means, shift / inertia terms -> wave sums -> [sync] -> the decision
-//   (every thread, from the 8 wave partials) -> fp16 halves, fp32 centroid,
-//   row values staged -> [sync] -> row sums (one thread per row, the host's
-//   order), nearest-centroid distances (8 lanes per row) -> maxima -> [sync]
-//   -> bounds (every thread) -> fragments, C operand, prune block.
-// Same results as ll_finalize + plan32_build (same fp64 operations per value;
-// the row sums in the same sequential order).
+// latency: a single workgroup between two full-GPU launches (fin32.h).  The
+// fused screen32bs runs the same body in its last workgroup instead.
 __global__ __launch_bounds__(512) void ll_finalize32(FinArgs a) {
-  long long* __restrict__ state = a.state;
-  if (a.abl & 8) {  // (the step still counts, so the host's polling goes on)
-    if (threadIdx.x == 0) state[1] += 1;
-    return;
-  }
-  const int k = a.k, d = a.d, d1 = d + 1, cells = k * d1;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int j = t >> 3, f0 = 2 * (t & 7);
-  const bool row = j < k;
-  const bool v0 = row && f0 < d, v1 = row && f0 + 1 < d;
-  // ---- loads ----
-  long long s0[kRunSlices], s1[kRunSlices], sn[kRunSlices];
-#pragma unroll
-  for (int sl = 0; sl < kRunSlices; ++sl) {
-    const bool on = sl < a.nslices;
-    const long long* base = a.sums + (size_t)sl * cells + (size_t)j * d1;
-    s0[sl] = on && v0 ? base[f0] : 0;
-    s1[sl] = on && v1 ? base[f0 + 1] : 0;
-    sn[sl] = on && row ? base[d] : 0;
-  }
-  const double c0 = v0 ? a.C[j * d + f0] : 0.0, c1 = v1 ? a.C[j * d + f0 + 1] : 0.0;
-  const double r0 = v0 ? a.ref[f0] : 0.0, r1 = v1 ? a.ref[f0 + 1] : 0.0;
-  const double mu0 = v0 ? a.ref[d + f0] : 0.0, mu1 = v1 ? a.ref[d + f0 + 1] : 0.0;
-  const bool whead = a.bnd && row && (t & 7) == 0;
-  const long long w_old = whead ? a.bnd[j] : 0;
-  // the 2-byte words' base and header (plan32.h kBnd*)
-  unsigned char* const bb = reinterpret_cast<unsigned char*>(a.bnd);
-  const long long g_old = whead ? reinterpret_cast<const long long*>(bb + kBndG)[j] : 0;
-  int hdr0 = 0, e0c = 0;
-  if (a.bnd) {
-    hdr0 = reinterpret_cast<const int*>(bb + kBndHdr)[0];
-    e0c = reinterpret_cast<const int*>(bb + kBndHdr)[2];
-  }
-  const long long st0 = state[0];
-  if (st0 == 0) return;  // uniform: the loop has stopped
-  if (a.abl & 1) {
-    long long z = 0;
-#pragma unroll
-    for (int sl = 0; sl < kRunSlices; ++sl) z += s0[sl] + s1[sl] + sn[sl];
-    if (z == 0x7fffffffffffffffll) state[7] = z + (long long)(c0 + c1 + r0 + r1 + mu0 + mu1);
-    if (threadIdx.x == 0) state[1] += 1;
-    return;
-  }
-  // ---- means, shift / inertia terms ----
-  long long S0 = 0, S1 = 0, cnt = 0;
-#pragma unroll
-  for (int sl = 0; sl < kRunSlices; ++sl) {
-    S0 += s0[sl];
-    S1 += s1[sl];
-    cnt += sn[sl];
-  }
-  double* __restrict__ Cnew = a.Cnew;
-  long long* cnt_out = reinterpret_cast<long long*>(Cnew + (size_t)k * d);
-  if (row && (t & 7) == 0) cnt_out[j] = cnt;
-  // the per-wave fallback counts (the step's total: the decision sync below)
-  // (eight loads in flight per thread: a rolled loop waited for each one)
-  int fbv = 0;
-  if (a.fbc) {
-    int acc[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = t + u * (int)blockDim.x;
-      acc[u] = i < a.nwaves ? a.fbc[i] : 0;
-    }
-    for (int i = t + 8 * (int)blockDim.x; i < a.nwaves; i += blockDim.x) acc[0] += a.fbc[i];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) fbv += acc[u];
-  }
-  // the host's np.ldexp(acc.astype(float64), -S) / counts (kmeans_plusplus.py)
-  const double sj0 = ldexp((double)S0, -a.sbits), sj1 = ldexp((double)S1, -a.sbits);
-  double m0 = sj0 / (double)cnt, m1 = sj1 / (double)cnt;
-  if (a.round32) {
-    m0 = (double)(float)m0;
-    m1 = (double)(float)m1;
-  }
-  if (v0) Cnew[j * d + f0] = m0;
-  if (v1) Cnew[j * d + f0 + 1] = m1;
-  double ss = 0.0, cross = 0.0, quad = 0.0;
-  int empty = row && cnt == 0;
-  if (row && cnt != 0) {
-    if (v0) {
-      const double df = m0 - c0, ct = c0 - r0;
-      ss += df * df;
-      cross += ct * (sj0 - (double)cnt * r0);
-      quad += (double)cnt * (ct * ct);
-    }
-    if (v1) {
-      const double df = m1 - c1, ct = c1 - r1;
-      ss += df * df;
-      cross += ct * (sj1 - (double)cnt * r1);
-      quad += (double)cnt * (ct * ct);
-    }
-  }
-  // how far centroid j moves (its 8 threads' features; screen32b's drift):
-  // fp64 errs by < 20 2^-53 relative here, sc is a power of two
-  double dq = 0.0;
-  if (v0) dq += (m0 - c0) * (m0 - c0);
-  if (v1) dq += (m1 - c1) * (m1 - c1);
-  dq += __shfl_xor(dq, 1);
-  dq += __shfl_xor(dq, 2);
-  dq += __shfl_xor(dq, 4);
-  const double dlt = sqrt(dq) * a.sc * (1.0 + 0x1p-45);
-  double dmx = row ? dlt : 0.0;
-#pragma unroll
-  for (int o = 32; o >= 8; o >>= 1) dmx = fmax(dmx, __shfl_xor(dmx, o));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {  // fixed pattern: deterministic
-    ss += __shfl_xor(ss, o);
-    cross += __shfl_xor(cross, o);
-    quad += __shfl_xor(quad, o);
-    empty |= __shfl_xor(empty, o);
-    fbv += __shfl_xor(fbv, o);
-  }
-  __shared__ double r_ss[8], r_cross[8], r_quad[8], r_dm[8];
-  __shared__ int r_empty[8], r_fb[8];
-  if (lane == 0) {
-    r_dm[wv] = dmx;
-    r_ss[wv] = ss;
-    r_cross[wv] = cross;
-    r_quad[wv] = quad;
-    r_empty[wv] = empty;
-    r_fb[wv] = fbv;
-  }
-  __syncthreads();
-  if (t == 0 && a.fbc) {
-    int fb = 0;
-    for (int w = 0; w < 8; ++w) fb += r_fb[w];
-    a.fbc[a.nwaves] = 0;
-    a.fbc[a.nwaves + 1] = fb;
-    if (a.fb_acc) a.fb_acc[0] += fb;
-  }
-  // ---- the decision (every thread, the same fixed order) ----
-  double sst = 0.0, crs = 0.0, qd = 0.0;
-  int emp = 0;
-#pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    sst += r_ss[w];
-    crs += r_cross[w];
-    qd += r_quad[w];
-    emp |= r_empty[w];
-  }
-  long long reason = kLLRun;
-  int mv = 0;
-  if (emp) {
-    reason = kLLEmpty;
-  } else {
-    const double sh = sqrt(sst);
-    mv = 1;
-    if (a.tol > 0.0 && !(sh > a.tol * (1.0 + a.margin))) {
-      if (sh < a.tol * (1.0 - a.margin)) {
-        reason = kLLConverged;  // shift < tol: the reference breaks after moving
-      } else {
-        reason = kLLAmbiguous;  // too close to call in fp64: the host decides
-        mv = 0;
-      }
-    }
-  }
-  if (t == 0) {
-    if (mv) state[1] += 1;
-    if (reason != kLLRun) {
-      state[0] = 0;
-      state[2] = reason;
-    }
-    state[3] = __double_as_longlong(sst);
-    state[4] = __double_as_longlong(a.x2 - 2.0 * crs + qd);
-  }
-  if (!mv) return;
-  if (v0) a.C[j * d + f0] = m0;
-  if (v1) a.C[j * d + f0 + 1] = m1;
-  if (whead) {  // screen32b's drift bounds of this move
-    double M = 0.0;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) M = fmax(M, r_dm[w]);
-    double inc = (M + dlt) * (1.0 + 0x1p-50);
-    if (!(inc < 0x1p10)) inc = 0x1p10;  // (NaN too)
-    // saturating: past 2^52 units the fp64 value is no longer exact and every
-    // bound test fails from then on (W up = inf)
-    const long long wn =
-        w_old >= (1LL << 60) ? w_old : w_old + (long long)ceil(ldexp(inc, 40));
-    a.bnd[j] = wn;
-    const double wvv = ldexp((double)wn, -40);
-    float* wf = reinterpret_cast<float*>(a.bnd + 64);
-    wf[j] = wn < (1LL << 52) ? f32_up(wvv) : INFINITY;
-    wf[64 + j] = f32_dn(wvv);
-  }
-  if (a.bnd) {  // (uniform) the 2-byte words' tables
-    // A_j = W_j - G_j: what the current base has accumulated.  Rebase (G_j =
-    // W_j, every kept word re-encoded by the next screen) when the base was
-    // never set, when the code's 2^-6 truncation of A reaches half the
-    // step's drift budget (A > 32 M), when the drift has fallen to twice the
-    // code floor 2^E0 (margins near M would not be representable), or when
-    // A nears the code range (2^(E0 + 16)).  The floor follows the drift,
-    // E0 = floor(log2(M / 64)) (a margin below M is spent within a step;
-    // the range reaches ~1000 M), so a decaying drift rebases rarely
-    long long wn = 0;
-    double Aj = 0.0;
-    if (whead) {
-      wn = a.bnd[j];  // (this thread's own store above)
-      Aj = ldexp((double)(wn - g_old), -40);
-    }
-    __shared__ double r_A[8];
-    double am = Aj;
-#pragma unroll
-    for (int o = 32; o >= 8; o >>= 1) am = fmax(am, __shfl_xor(am, o));
-    if (lane == 0) r_A[wv] = am;
-    __syncthreads();
-    double Amax = 0.0, M = 0.0;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      Amax = fmax(Amax, r_A[w]);
-      M = fmax(M, r_dm[w]);
-    }
-    const bool rebase = hdr0 == 0 ||
-                        (M > 0.0 && (Amax > 32.0 * M || ldexp(1.0, e0c + 1) > M)) ||
-                        Amax > ldexp(1.0, e0c + 14);
-    int e0n = e0c;
-    if (rebase) {
-      if (M > 0.0) e0n = ilogb(M * 0x1p-6);
-      else if (hdr0 == 0) e0n = -20;
-      e0n = e0n < -120 ? -120 : (e0n > 100 ? 100 : e0n);
-    }
-    if (whead) {
-      const bool exact = wn < (1LL << 52);  // (saturated W: every test fails)
-      const long long g_new = rebase ? wn : g_old;
-      reinterpret_cast<long long*>(bb + kBndG)[j] = g_new;
-      reinterpret_cast<unsigned*>(bb + kBndT)[j] =
-          exact ? zb16_thr(f32_up(ldexp((double)(wn - g_old), -40)), e0c) : 1022u;
-      reinterpret_cast<float*>(bb + kBndWdg)[j] =
-          exact ? f32_dn(ldexp((double)(wn - g_new), -40)) : -1.0f;
-      reinterpret_cast<float*>(bb + kBndDG)[j] =
-          rebase ? f32_up(ldexp((double)(g_new - g_old), -40)) : 0.0f;
-    }
-    if (t == 0) {
-      int* hd = reinterpret_cast<int*>(bb + kBndHdr);
-      hd[0] = 1;
-      hd[1] = e0c;
-      hd[2] = e0n;
-      hd[3] = rebase ? 1 : 0;
-    }
-  }
-  if (!a.plan || reason != kLLRun || (a.abl & 2)) return;
-  // ---- the next step's plan (plan32_build, per element) ----
-  unsigned char* __restrict__ plan = a.plan;
-  const int QH = a.QH, MT = a.MT;
-  const Plan32Layout L = plan32_layout(MT, k, d);
-  plan_h8* frag = reinterpret_cast<plan_h8*>(plan);
-  float* cinit = reinterpret_cast<float*>(plan + L.cinit);
-  double* cent = reinterpret_cast<double*>(plan + L.cent);
-  float* pc = reinterpret_cast<float*>(plan + L.prune);
-  float* pE = pc + 64 * kPrStr;
-  float* ph = pE + 64;
-  __shared__ _Float16 m2h[64 * 16], m2l[64 * 16];
-  __shared__ double vrow[64 * 16];
-  __shared__ float c32[64 * 16];
-  __shared__ double cc[64];
-  const double vv[2] = {v0 ? (m0 - mu0) * a.sc : 0.0, v1 ? (m1 - mu1) * a.sc : 0.0};
-  const double mm[2] = {m0, m1};
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int f = f0 + u;
-    const double v = vv[u];
-    const _Float16 hi = f64_to_f16(v);
-    const _Float16 lo = f64_to_f16(v - (double)hi);
-    m2h[j * 16 + f] = f64_to_f16(-2.0 * (double)hi);
-    m2l[j * 16 + f] = f64_to_f16(-2.0 * (double)lo);
-    vrow[j * 16 + f] = v;
-    const float cf = (float)v;
-    c32[j * 16 + f] = cf;
-    pc[j * kPrStr + f] = cf;
-    if (row && f < d) cent[j * d + f] = mm[u];
-  }
-  if ((t & 7) < 2) pc[j * kPrStr + 16 + 2 * (t & 7)] = 0.0f, pc[j * kPrStr + 17 + 2 * (t & 7)] = 0.0f;
-  __syncthreads();
-  // ---- row sums (host order), nearest-centroid distances, maxima ----
-  double s = 0.0, l1 = 0.0, ca = 0.0, e2 = 0.0;
-  if ((t & 7) == 0 && row) {
-    for (int f = 0; f < d; ++f) {
-      const double v = vrow[j * 16 + f];
-      s += v * v;
-      l1 += fabs(v);
-      ca = fmax(ca, fabs(v));
-      const double r = (double)c32[j * 16 + f] - v;  // exact
-      e2 += r * r;
-    }
-    cc[j] = s;
-  }
-  const double ec = plan32_prune_ec(e2, s);
-  double sm = INFINITY;  // smallest squared distance of c32_j to another c32
-  if (row && !(a.abl & 4)) {
-    // own row in registers, four partial sums per pair (a short dependency
-    // chain; every term >= 0 and at most 6 roundings on any path, within
-    // plan32_prune_h's 2^-44 margin)
-    float cj[16];
-#pragma unroll
-    for (int f = 0; f < 16; ++f) cj[f] = c32[j * 16 + f];
-    for (int jj = t & 7; jj < k; jj += 8) {
-      if (jj == j) continue;
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int f = 0; f < 16; ++f) {
-        const double df = (double)cj[f] - (double)c32[jj * 16 + f];  // exact
-        acc[f & 3] += df * df;
-      }
-      sm = fmin(sm, (acc[0] + acc[1]) + (acc[2] + acc[3]));
-    }
-  }
-  sm = fmin(sm, __shfl_xor(sm, 1));
-  sm = fmin(sm, __shfl_xor(sm, 2));
-  sm = fmin(sm, __shfl_xor(sm, 4));
-  const bool head = (t & 7) == 0 && row;
-  double ccmax = head ? s : 0.0, l1c = head ? l1 : 0.0, cabs = head ? ca : 0.0,
-         ecmax = head ? ec : 0.0;
-#pragma unroll
-  for (int o = 32; o >= 8; o >>= 1) {  // max is exact: any order
-    ccmax = fmax(ccmax, __shfl_xor(ccmax, o));
-    l1c = fmax(l1c, __shfl_xor(l1c, o));
-    cabs = fmax(cabs, __shfl_xor(cabs, o));
-    ecmax = fmax(ecmax, __shfl_xor(ecmax, o));
-  }
-  __shared__ double x_cc[8], x_l1[8], x_ca[8], x_ec[8];
-  if (lane == 0) {
-    x_cc[wv] = ccmax;
-    x_l1[wv] = l1c;
-    x_ca[wv] = cabs;
-    x_ec[wv] = ecmax;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    ccmax = fmax(ccmax, x_cc[w]);
-    l1c = fmax(l1c, x_l1[w]);
-    cabs = fmax(cabs, x_ca[w]);
-    ecmax = fmax(ecmax, x_ec[w]);
-  }
-  if (!(cabs <= 1024.0)) {  // fp16 split range (and NaN) guard: the host plans this step
-    if (t == 0) {
-      state[0] = 0;
-      state[2] = kLLHostPlan;
-    }
-    return;
-  }
-  double D;
-  float thr0;
-  plan32_bounds(ccmax, l1c, a.xxmax, a.l1x, QH, D, thr0);
-  if (t == 0) {
-    reinterpret_cast<float*>(plan + L.thr)[0] = thr0;
-    reinterpret_cast<float*>(plan + L.thr)[1] = (float)D;
-  }
-  if ((t & 7) == 0) {
-    pE[j] = plan32_prune_E(plan32_prune_dn(a.xxmax), row ? ec : 0.0);
-    ph[j] = row ? plan32_prune_h(sm, ec, ecmax) : INFINITY;
-  }
-  for (int idx = t; idx < MT * 64; idx += blockDim.x) {  // the layout of plan32_lane
-    const int m = idx >> 6, ln = idx & 63;
-    const int h = ln >> 5, jr = 32 * m + (ln & 31);
-    plan_h8 A1, A3;
-    for (int i = 0; i < 8; ++i) {
-      A1[i] = (_Float16)0.0f;
-      A3[i] = (_Float16)0.0f;
-    }
-    for (int uq = 0; uq < QH; ++uq)
-      for (int i = 0; i < 4; ++i) {
-        const int f = 4 * (QH * h + uq) + i;
-        if (jr >= k || f >= d) continue;
-        const _Float16 x = m2h[jr * 16 + f], y = m2l[jr * 16 + f];
-        if (QH == 1) {
-          A1[i] = x;
-          A1[4 + i] = x;
-          A3[i] = y;
-        } else {
-          A1[4 * uq + i] = x;
-          A3[4 * uq + i] = y;
-        }
-      }
-    frag[(m * 2 + 0) * 64 + ln] = A1;
-    frag[(m * 2 + 1) * 64 + ln] = A3;
-  }
-  for (int idx = t; idx < MT * 16 * 64; idx += blockDim.x) {
-    const int ln = idx & 63, mi = idx >> 6, m = mi >> 4, i = mi & 15;
-    const int rw = 32 * m + 8 * (i >> 2) + 4 * (ln >> 5) + (i & 3);
-    cinit[idx] = rw < k ? (float)(cc[rw] + D) : 1.0e30f;
-  }
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kFin32Lds];
+  fin32_body<512>(a, lds);
 }
 
 // Per-block partial sums of ||x_i - r||^2 (features in order, fp64).
@@ -798,6 +371,7 @@ static void ll_enqueue_assign(Ctx& c, int64_t* dsums) {
     // single process: no published copy, ll_finalize reads the running sums
     screen32_step(c, nullptr, c.ll_k, dsums ? dout : nullptr, nullptr, prof, nullptr, nullptr,
                   state);
+    // (after the step: it may allocate run_sums)
     c.ll_fin_sums = dsums ? dout : c.run_sums.as<long long>();
     c.ll_fin_slices = dsums ? 1 : kRunSlices;
     c.ll_fin_devstep = true;
@@ -837,9 +411,8 @@ static void ll_enqueue_assign(Ctx& c, int64_t* dsums) {
   c.ll_enqueued += 1;
 }
 
-static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
-  if (dsums && reinterpret_cast<const long long*>(dsums) != c.ll_fin_sums)
-    CDR_FAIL(CDR_ERR_ARG, "lloyd finalize: pass the buffer given to the assign");
+// The finalize's arguments for the step just assigned.
+FinArgs ll_fin_args(Ctx& c) {
   const int kd = c.ll_k * c.d;
   const bool r32 = (c.ll_flags & 1) != 0;
   FinArgs a;
@@ -873,6 +446,13 @@ static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
   if (const char* e = std::getenv("CDR_FIN_ABL")) a.abl = std::atoi(e);
   if (std::getenv("CDR_FIN_NOPLAN")) a.plan = nullptr;  // timing experiments only
 #endif
+  return a;
+}
+
+static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
+  if (dsums && reinterpret_cast<const long long*>(dsums) != c.ll_fin_sums)
+    CDR_FAIL(CDR_ERR_ARG, "lloyd finalize: pass the buffer given to the assign");
+  const FinArgs a = ll_fin_args(c);
   // screen32 device plan: the latency-oriented finalize (CDR_FIN_OLD=1: the
   // generic one, for comparisons)
   static const bool fin_old = std::getenv("CDR_FIN_OLD") && std::atoi(std::getenv("CDR_FIN_OLD"));

@@ -2398,7 +2398,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   // kBPD chunks streamed between two phase-2 passes, so phase 2 has one call
   // site (code size: the decision is inlined once)
   constexpr int kSList = kBPD * kBChunk + 256;
-  __shared__ unsigned flist[4][SPLIT ? 1 : kSList];
+  __shared__ __attribute__((aligned(16))) unsigned flist[4][SPLIT ? 1 : kSList];
   __shared__ unsigned long long mtab[64 * 17];  // this workgroup's moves, [k][d + 1]
   __shared__ float msl[16];                     // -mu_f 2^sigma
   __shared__ float dgs[64];                     // 2-byte words: this step's base moves (rebase)
