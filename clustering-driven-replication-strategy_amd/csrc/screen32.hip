@@ -2387,7 +2387,10 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   // near ties: the fused kernel lists them and resolves them after its last
   // batch (inlined in the streaming loop, the resolver costs registers and
   // code the stream needs); the split decide kernel resolves them at once
-  constexpr bool DEFER = !SPLIT;
+#ifndef CDR_S32BS_DEFER
+#define CDR_S32BS_DEFER 1
+#endif
+  constexpr bool DEFER = !SPLIT && CDR_S32BS_DEFER;
   if (a.gate && a.gate[0] == 0) return;
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -2402,6 +2405,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   __shared__ unsigned long long mtab[64 * 17];  // this workgroup's moves, [k][d + 1]
   __shared__ float msl[16];                     // -mu_f 2^sigma
   __shared__ float dgs[64];                     // 2-byte words: this step's base moves (rebase)
+  __shared__ unsigned tls[64];                  // 2-byte words: this step's code thresholds
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wv = t >> 6;
@@ -2445,14 +2449,11 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   // lane j: W_j (4-byte words: wup for the test, wdn for new words); 2-byte
   // words: the code threshold T_j, W_j - G_j for new words, the rebase step
   float wup_l = 0.0f, wnew_l;
-  unsigned thr_l = 0u;
   int e0o = 0, e0n = 0, rebase = 0;
   if constexpr (SPLIT) {
     wup_l = B.wup[lane];
     wnew_l = B.wdn[lane];
   } else {
-    // (CDR_BOUNDS_DBG=1, tests: every real point's bound fails)
-    thr_l = (B.dbg & 1) ? 1022u : reinterpret_cast<const unsigned*>(B.bt + kBndT)[lane];
     wnew_l = reinterpret_cast<const float*>(B.bt + kBndWdg)[lane];
     const int* hd = reinterpret_cast<const int*>(B.bt + kBndHdr);
     e0o = hd[1];
@@ -2476,8 +2477,11 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   if (t < MT * 32) sC[t] = cv;
   for (int e = t; e < 64 * 17; e += 256) mtab[e] = 0ull;
   if (t < 16) msl[t] = msv;
-  if constexpr (!SPLIT)  // (LDS: a vector load here would wait behind the stream's)
+  if constexpr (!SPLIT) {  // (LDS: a vector load here would wait behind the stream's)
     if (t < 64) dgs[t] = reinterpret_cast<const float*>(B.bt + kBndDG)[t];
+    // (CDR_BOUNDS_DBG=1, tests: every real point's bound fails)
+    if (t < 64) tls[t] = (B.dbg & 1) ? 1022u : reinterpret_cast<const unsigned*>(B.bt + kBndT)[t];
+  }
   __syncthreads();
   CDR_TP(1);
 
@@ -3009,23 +3013,32 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
         }
         zload(zc[(i + kBPD - 1) % kBPD], Ci + (int64_t)(kBPD - 1) * wstride);
         const u4v z = zc[i];
+        // the 8 thresholds first (independent LDS permutes, one wait), then
+        // the tests; entries only from chunks with a failed point
+        // (the thresholds from LDS: 8 independent reads, one wait)
+        unsigned fm = 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const unsigned w = (z[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-          const unsigned lab = w & 63u;
+          fm |= (unsigned)((w >> 6) <= tls[w & 63u]) << u;
+        }
 #ifdef CDR_EXPERIMENTS
-          const bool fail = !((w >> 6) > __shfl(thr_l, (int)lab)) && !(B.dbg & 16);  // (16: the stream alone)
-#else
-          const bool fail = !((w >> 6) > __shfl(thr_l, (int)lab));
+        if (B.dbg & 16) fm = 0;  // (timing: the stream alone)
 #endif
-          const unsigned long long m = __ballot(fail);
-          if (m) {
-            if (fail) {
-              const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-              fl[cnt + r] = (unsigned)it << 15 | (unsigned)(8 * lane + u) << 6 | lab;
+        if (__ballot(fm != 0u)) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const bool fail = (fm >> u) & 1u;
+            const unsigned long long m = __ballot(fail);
+            if (m) {
+              if (fail) {
+                const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                fl[cnt + r] = (unsigned)it << 15 | (unsigned)(8 * lane + u) << 6 |
+                              ((z[u >> 1] >> (16 * (u & 1))) & 63u);
+              }
+              cnt += __popcll(m);
             }
-            cnt += __popcll(m);
           }
         }
         if (rebase) {  // (uniform) the kept words to the new base
@@ -3038,7 +3051,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
               const unsigned w = (z[q] >> (16 * hh)) & 0xFFFFu;
-              all = all && (w >> 6) > __shfl(thr_l, (int)(w & 63u));  // (the test again)
+              all = all && (w >> 6) > tls[w & 63u];  // (the test again)
               o |= zb16_rebase(w, dgs[w & 63u], e0o, e0n) << (16 * hh);
             }
             nz[q] = o;
@@ -3049,7 +3062,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
               const unsigned w = (z[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-              if ((w >> 6) > __shfl(thr_l, (int)(w & 63u)))
+              if ((w >> 6) > tls[w & 63u])
                 zp[u] = (uint16_t)(nz[u >> 1] >> (16 * (u & 1)));
             }
           }
