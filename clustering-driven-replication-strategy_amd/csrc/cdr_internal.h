@@ -211,6 +211,7 @@ struct Ctx {
   DevBuf zl, zn;  // split bounded screen: per-wave lists of failed points (screen32bz), lengths
   bool zb_valid = false, xh_valid = false, bnd_ok = false;
   int zb_fmt = 0;  // bound words in zb: 16 (2-byte, screen32bs) or 32 bits
+  int64_t ll_fin_count = 0;  // finalizes since lloyd_begin (2-byte rebase schedule)
   int32_t run_k = 0;
   bool last_delta = false;
 #ifdef CDR_EXPERIMENTS

@@ -52,6 +52,9 @@ struct FinArgs {
   // rounded up and down to fp32 for the next screen, and the 2-byte words'
   // tables (plan32.h kBnd*)
   long long* bnd;
+  // a rebase of the 2-byte words may be decided at this step (the host then
+  // runs zh_rebase_kernel before the next screen; screen32.hip)
+  int rebase_ok;
   int abl;  // timing experiments only (0 in the product build)
 };
 
@@ -329,9 +332,10 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
     double Amax = 0.0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) Amax = fmax(Amax, r_A[q]);
-    const bool rebase = hdr0 == 0 ||
-                        (M > 0.0 && (Amax > 32.0 * M || ldexp(1.0, e0c + 1) > M)) ||
-                        Amax > ldexp(1.0, e0c + 14);
+    // (only at the steps the host follows with zh_rebase_kernel)
+    const bool rebase = a.rebase_ok &&
+                        (hdr0 == 0 || (M > 0.0 && (Amax > 32.0 * M || ldexp(1.0, e0c + 1) > M)) ||
+                         Amax > ldexp(1.0, e0c + 14));
     int e0n = e0c;
     if (rebase) {
       if (M > 0.0) e0n = ilogb(M * 0x1p-6);
@@ -345,8 +349,9 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
       const bool exact = wn[v] < (1LL << 52);  // (saturated W: every test fails)
       const long long g_new = rebase ? wn[v] : g_old[v];
       reinterpret_cast<long long*>(bb + kBndG)[jj] = g_new;
+      // (the words are in the new base when the next screen tests them)
       reinterpret_cast<unsigned*>(bb + kBndT)[jj] =
-          exact ? zb16_thr(f32_up(ldexp((double)(wn[v] - g_old[v]), -40)), e0c) : 1022u;
+          exact ? zb16_thr(f32_up(ldexp((double)(wn[v] - g_new), -40)), e0n) : 1022u;
       reinterpret_cast<float*>(bb + kBndWdg)[jj] =
           exact ? f32_dn(ldexp((double)(wn[v] - g_new), -40)) : -1.0f;
       reinterpret_cast<float*>(bb + kBndDG)[jj] =

@@ -41,6 +41,8 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
                    float* dbg, float* thr_out, long long* gate);
 void plan32_point_side(const Ctx& c, double& xxmax, double& l1x);
 void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_dev);
+void zh_rebase(Ctx& c, const long long* gate);  // screen32.hip
+constexpr int kRebaseEvery = 4;  // finalizes between 2-byte rebase opportunities
 
 constexpr int kFinThreads = 512;
 constexpr int kFinLds = 64 * 17;  // (k, d+1) cells staged in LDS (screen32 shapes)
@@ -348,6 +350,7 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   HIP_CHECK(hipStreamSynchronize(c.stream));  // rm and st0 live on this stack
   c.ll_on = true;
   c.ll_enqueued = 0;
+  c.ll_fin_count = 0;
   c.ll_hostplan_once = false;
   // the first step recomputes the running sums from scratch (see resume)
   c.run_valid = false;
@@ -441,6 +444,9 @@ FinArgs ll_fin_args(Ctx& c) {
   a.xxmax = c.ll_xxmax;
   a.l1x = c.ll_l1x;
   a.bnd = c.bnd_ok ? c.bnd.as<long long>() : nullptr;
+  // 2-byte words: a rebase may be decided every kRebaseEvery-th finalize
+  // (the first one sets the base), each followed by zh_rebase_kernel
+  a.rebase_ok = c.ll_fin_count % kRebaseEvery == 0 ? 1 : 0;
   a.abl = 0;
 #ifdef CDR_EXPERIMENTS
   if (const char* e = std::getenv("CDR_FIN_ABL")) a.abl = std::atoi(e);
@@ -456,11 +462,15 @@ static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
   // screen32 device plan: the latency-oriented finalize (CDR_FIN_OLD=1: the
   // generic one, for comparisons)
   static const bool fin_old = std::getenv("CDR_FIN_OLD") && std::atoi(std::getenv("CDR_FIN_OLD"));
-  if (a.plan && c.ll_k <= 64 && c.d <= 16 && a.nslices <= kRunSlices && !fin_old)
+  if (a.plan && c.ll_k <= 64 && c.d <= 16 && a.nslices <= kRunSlices && !fin_old) {
     hipLaunchKernelGGL(ll_finalize32, dim3(1), dim3(512), 0, c.stream, a);
-  else
+    HIP_CHECK(hipGetLastError());
+    if (a.rebase_ok && a.bnd) zh_rebase(c, c.ll_state.as<long long>());  // (gated on the device)
+  } else {
     hipLaunchKernelGGL(ll_finalize, dim3(1), dim3(kFinThreads), 0, c.stream, a);
+  }
   HIP_CHECK(hipGetLastError());
+  c.ll_fin_count += 1;
   if (c.ll_devbig) ll_plan_big(c);  // the next step's plan (skipped once the loop stopped)
   if (c.ll_fin_devstep && c.prof_cur >= 0) prof_mark(c, 2);
 }

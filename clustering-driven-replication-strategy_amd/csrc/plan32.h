@@ -33,10 +33,10 @@ __host__ __device__ inline Plan32Layout plan32_layout(int MT, int k, int d) {
 // Drift-bound buffer (Ctx::bnd, kept by ll_finalize32):
 //   W [64] int64 (2^-40 units) | wup [64] f32 | wdn [64] f32   (4-byte words)
 //   G [64] int64 (the 2-byte words' per-centroid base: W_j at the last rebase)
-//   T [64] u32   this step's code thresholds (base G, exponent E0 old)
+//   T [64] u32   the next screen's code thresholds (base G, exponent E0 new)
 //   wdg [64] f32 W_j - G_j (new base) rounded down, for the words written now
 //   dG [64] f32  G_j(new) - G_j(old) rounded up (0 unless this step rebases)
-//   hdr [4] int32: base set, E0 old, E0 new, rebase
+//   hdr [4] int32: base set, E0 old, E0 new, rebase (zh_rebase_kernel: old -> new)
 constexpr size_t kBndWup = 512, kBndWdn = 768, kBndG = 1024, kBndT = 1536, kBndWdg = 1792,
                  kBndDG = 2048, kBndHdr = 2304, kBndBytes = 2320;
 

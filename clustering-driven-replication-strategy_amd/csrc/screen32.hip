@@ -2404,7 +2404,6 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   __shared__ __attribute__((aligned(16))) unsigned flist[4][SPLIT ? 1 : kSList];
   __shared__ unsigned long long mtab[64 * 17];  // this workgroup's moves, [k][d + 1]
   __shared__ float msl[16];                     // -mu_f 2^sigma
-  __shared__ float dgs[64];                     // 2-byte words: this step's base moves (rebase)
   __shared__ unsigned tls[64];                  // 2-byte words: this step's code thresholds
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -2428,10 +2427,6 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   int wstride;
   bs_range(B, wv, wbase, wstride, wend);
   u4v zc[kBPD];
-  if constexpr (!SPLIT) {
-#pragma unroll
-    for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], wbase + (int64_t)i * wstride);
-  }
 
   // ---- the plan ----
   __shared__ h8 sA[MT * 2 * 64];
@@ -2447,18 +2442,16 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   const int cm = t >> 5, ci4 = (t >> 3) & 3, chh = (t >> 2) & 1, cc = t & 3;
   if (t < MT * 32) cv = a.cinit[(cm * 16 + ci4 * 4 + cc) * 64 + chh * 32];
   // lane j: W_j (4-byte words: wup for the test, wdn for new words); 2-byte
-  // words: the code threshold T_j, W_j - G_j for new words, the rebase step
+  // words: W_j - G_j for new words (the thresholds T_j: LDS, below) and the
+  // codes' exponent
   float wup_l = 0.0f, wnew_l;
-  int e0o = 0, e0n = 0, rebase = 0;
+  int e0n = 0;
   if constexpr (SPLIT) {
     wup_l = B.wup[lane];
     wnew_l = B.wdn[lane];
   } else {
     wnew_l = reinterpret_cast<const float*>(B.bt + kBndWdg)[lane];
-    const int* hd = reinterpret_cast<const int*>(B.bt + kBndHdr);
-    e0o = hd[1];
-    e0n = hd[2];
-    rebase = hd[3];
+    e0n = reinterpret_cast<const int*>(B.bt + kBndHdr)[2];
   }
   // a decided point's word (ok: bounds (l0, u0); w = __shfl(wnew_l, lab),
   // taken by every lane) or "no bound"
@@ -2477,8 +2470,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   if (t < MT * 32) sC[t] = cv;
   for (int e = t; e < 64 * 17; e += 256) mtab[e] = 0ull;
   if (t < 16) msl[t] = msv;
-  if constexpr (!SPLIT) {  // (LDS: a vector load here would wait behind the stream's)
-    if (t < 64) dgs[t] = reinterpret_cast<const float*>(B.bt + kBndDG)[t];
+  if constexpr (!SPLIT) {
     // (CDR_BOUNDS_DBG=1, tests: every real point's bound fails)
     if (t < 64) tls[t] = (B.dbg & 1) ? 1022u : reinterpret_cast<const unsigned*>(B.bt + kBndT)[t];
   }
@@ -2952,8 +2944,19 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     constexpr int kRoom = CH;
     for (;;) {
       if (pend) {
+#ifdef CDR_EXPERIMENTS
+        const unsigned long long td0 = __builtin_amdgcn_s_memrealtime();
+        if (!SPLIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // (timing: the gathered rows' arrival)
+        const unsigned long long td1 = __builtin_amdgcn_s_memrealtime();
+#endif
         decide(cur);
         pend = false;
+#ifdef CDR_EXPERIMENTS
+        const unsigned long long td2 = __builtin_amdgcn_s_memrealtime();
+        tp[5] += td2 - td1;  // decide
+        tp[6] += 1;          // batches
+        tp[7] += td1 - td0;  // waiting for the rows (and the stream's loads)
+#endif
       }
       const int avail = cnt - head;
       if (avail >= 64 || (last && avail > 0)) {
@@ -2967,7 +2970,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) cur.x[q] = __builtin_nontemporal_load(XA4 + pt * Q + q);
         const int take = avail < 64 ? avail : 64;
-        head += take;
+        head = __builtin_amdgcn_readfirstlane(head + take);
         ttot += take;
         pend = true;
       }
@@ -2992,95 +2995,92 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #endif
 
   // ---- phase 1: the bound words, 8 points per lane per chunk ----
-  // Groups of kBPD chunks, kBPD in flight; phase 2 between groups.  A chunk
-  // whose entries would not fit the list ends its group early: phase 2
-  // drains, and the stream resumes at that chunk (loads issued again).
-  // Rebase steps carry every kept word to the new base as it streams past
-  // (a failed point's word is written by its decision instead).
+  // Groups of kBPD chunks issued together, phase 2 between groups.  The waits
+  // must stay exact: vmcnt counts stores too and is in order, so a store or a
+  // reload between a chunk's load and its use made the compiler wait for
+  // every load in flight (a rebase is zh_rebase_kernel's).  A chunk whose
+  // entries would not fit the list (dense failures: the first bounded step)
+  // hands the rest of the wave's range to a plain loop, one chunk at a time,
+  // phase 2 draining the list whenever it must.
   int cnt = 0;
   int it = 0;  // chunk ordinal within this wave's range (the entries' high bits)
-  for (int64_t C0 = wbase;;) {
-    const bool more = C0 < wend;  // (wave-uniform)
-    int64_t next = C0 + (int64_t)kBPD * wstride;
-    if (more) {
+  auto insert = [&](const u4v& z) __attribute__((always_inline)) {
+    // the 8 thresholds from LDS (independent reads, one wait), then the
+    // tests; entries only from chunks with a failed point
+    unsigned fm = 0;
 #pragma unroll
-      for (int i = 0; i < kBPD; ++i) {
-        const int64_t Ci = C0 + (int64_t)i * wstride;
-        if (Ci >= wend) break;
-        if (cnt - head + CH > kSList) {  // (dense failures only)
-          next = Ci;
-          break;
-        }
-        zload(zc[(i + kBPD - 1) % kBPD], Ci + (int64_t)(kBPD - 1) * wstride);
-        const u4v z = zc[i];
-        // the 8 thresholds first (independent LDS permutes, one wait), then
-        // the tests; entries only from chunks with a failed point
-        // (the thresholds from LDS: 8 independent reads, one wait)
-        unsigned fm = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const unsigned w = (z[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-          fm |= (unsigned)((w >> 6) <= tls[w & 63u]) << u;
-        }
+    for (int u = 0; u < 8; ++u) {
+      const unsigned w = (z[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+      fm |= (unsigned)((w >> 6) <= tls[w & 63u]) << u;
+    }
 #ifdef CDR_EXPERIMENTS
-        if (B.dbg & 16) fm = 0;  // (timing: the stream alone)
+    if (B.dbg & 16) fm = 0;  // (timing: the stream alone)
 #endif
-        if (__ballot(fm != 0u)) {
+    if (__ballot(fm != 0u)) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const bool fail = (fm >> u) & 1u;
-            const unsigned long long m = __ballot(fail);
-            if (m) {
-              if (fail) {
-                const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                fl[cnt + r] = (unsigned)it << 15 | (unsigned)(8 * lane + u) << 6 |
-                              ((z[u >> 1] >> (16 * (u & 1))) & 63u);
-              }
-              cnt += __popcll(m);
-            }
+      for (int u = 0; u < 8; ++u) {
+        const bool fail = (fm >> u) & 1u;
+        const unsigned long long m = __ballot(fail);
+        if (m) {
+          if (fail) {
+            const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            fl[cnt + r] = (unsigned)it << 15 | (unsigned)(8 * lane + u) << 6 |
+                          ((z[u >> 1] >> (16 * (u & 1))) & 63u);
           }
+          // (readfirstlane: uniform to the compiler, so the loops branch on
+          // scalars and the waits stay exact)
+          cnt = __builtin_amdgcn_readfirstlane(cnt + __popcll(m));
         }
-        if (rebase) {  // (uniform) the kept words to the new base
-          uint16_t* zp = B.zh + Ci * kZ16Chunk + 8 * lane;
-          u4v nz;
-          bool all = true;  // every point of the lane kept: one 16-byte store
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            unsigned o = 0;
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-              const unsigned w = (z[q] >> (16 * hh)) & 0xFFFFu;
-              all = all && (w >> 6) > tls[w & 63u];  // (the test again)
-              o |= zb16_rebase(w, dgs[w & 63u], e0o, e0n) << (16 * hh);
-            }
-            nz[q] = o;
-          }
-          if (all) {
-            *reinterpret_cast<u4v*>(zp) = nz;
-          } else {  // (a failed point's word is its decision's)
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const unsigned w = (z[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-              if ((w >> 6) > tls[w & 63u])
-                zp[u] = (uint16_t)(nz[u >> 1] >> (16 * (u & 1)));
-            }
-          }
-        }
-        ++it;
       }
     }
+    ++it;
+  };
+  int64_t C0 = wbase;
+  bool dense = false;  // (wave-uniform) the plain loop takes over at chunk C0
+  for (bool first = true;; first = false) {
+    const bool more = C0 < wend;  // (wave-uniform)
+    // phase 2 first: the rows it gathers load under this group's stream, and
+    // this group's loads are the youngest, so each chunk waits for itself
+    // only (vmcnt(kBPD - 1 - i)) whatever phase 2 issued
 #if CDR_S32BS_LAZY
-    step2(cnt, !more);
+    if (!first) step2(cnt, !more);
 #else
-    if (!more || cnt - head + CH > kSList - (kBPD - 1) * CH) phase2(cnt, !more);
+    if (!first && (!more || cnt - head + CH > kSList - (kBPD - 1) * CH)) phase2(cnt, !more);
 #endif
     if (!more) break;
-    if (next != C0 + (int64_t)kBPD * wstride) {  // resumed mid-group: load the ring again
 #pragma unroll
-      for (int i = 0; i < kBPD - 1; ++i) zload(zc[i], next + (int64_t)i * wstride);
+    for (int i = 0; i < kBPD; ++i) {
+      zload(zc[i], C0 + (int64_t)i * wstride);
+      __builtin_amdgcn_sched_barrier(0);  // (issued in chunk order)
     }
-    C0 = next;
+#pragma unroll
+    for (int i = 0; i < kBPD; ++i) {
+      const int64_t Ci = C0 + (int64_t)i * wstride;
+      if (Ci >= wend) break;
+      if (cnt - head + CH > kSList) {  // (dense failures only)
+        dense = true;
+        C0 = Ci;
+        break;
+      }
+      insert(zc[i]);
+    }
+    if (dense) break;
+    C0 += (int64_t)kBPD * wstride;
+  }
+  if (dense) {
+    for (int64_t Ci = C0;; Ci += wstride) {
+      const bool more = Ci < wend;
+#if CDR_S32BS_LAZY
+      if (!more || cnt - head + CH > kSList) step2(cnt, !more);  // (returns with room)
+#else
+      if (!more || cnt - head + CH > kSList) phase2(cnt, !more);
+#endif
+      if (!more) break;
+      u4v z;
+      zload(z, Ci);
+      insert(z);
+    }
   }
   }  // (!SPLIT)
   // ---- the uncertified points: the same split screen again (the same values),
@@ -3166,6 +3166,41 @@ __global__ void zh_reset_kernel(const uint8_t* __restrict__ lab8, uint16_t* __re
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad;
        i += (int64_t)gridDim.x * blockDim.x)
     zh[i] = i < n ? (uint16_t)lab8[i] : (uint16_t)kZ16Pad;
+}
+
+// A rebase of the 2-byte words (plan32.h; decided by ll_finalize32, run
+// before the next screen at the steps the host allows, gated on the device):
+// every kept word to the new base and exponent, 8 words per thread
+// (dec(code) - dG rounded down, truncated; codes 0 and 1023 stay).
+__global__ __launch_bounds__(256) void zh_rebase_kernel(uint16_t* __restrict__ zh, int64_t n_pad,
+                                                        const unsigned char* __restrict__ bt,
+                                                        const long long* __restrict__ gate) {
+  if (gate && gate[0] == 0) return;
+  const int* hd = reinterpret_cast<const int*>(bt + kBndHdr);
+  if (hd[3] == 0) return;
+  __shared__ float dgs[64];
+  if (threadIdx.x < 64) dgs[threadIdx.x] = reinterpret_cast<const float*>(bt + kBndDG)[threadIdx.x];
+  __syncthreads();
+  const int e0o = hd[1], e0n = hd[2];
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  u4v* z4 = reinterpret_cast<u4v*>(zh);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad / 8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    u4v z = __builtin_nontemporal_load(z4 + i);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned lo = z[q] & 0xFFFFu, hi = z[q] >> 16;
+      z[q] = zb16_rebase(lo, dgs[lo & 63u], e0o, e0n) | zb16_rebase(hi, dgs[hi & 63u], e0o, e0n) << 16;
+    }
+    __builtin_nontemporal_store(z, z4 + i);
+  }
+}
+
+void zh_rebase(Ctx& c, const long long* gate) {
+  if (!c.zb_valid || c.zb_fmt != 16 || !c.bnd_ok) return;  // (no words to carry)
+  hipLaunchKernelGGL(zh_rebase_kernel, dim3(2048), dim3(256), 0, c.stream, c.zb.as<uint16_t>(),
+                     c.n_pad, reinterpret_cast<const unsigned char*>(c.bnd.p), gate);
+  HIP_CHECK(hipGetLastError());
 }
 
 // The hi-only screen copy row by row (XH: screen32b's gathers read one line
@@ -3849,11 +3884,12 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
           std::fprintf(stderr,
                        "TPROF waves %d span %.1f us | avg/max us: start %.1f/%.1f prologue %.1f/%.1f "
                        "phases %.1f/%.1f tail %.1f/%.1f flush %.1f/%.1f idle-end %.1f/%.1f | "
-                       "tail batches/wave %.2f tail moves/wave %.1f tail move us/wave %.2f\n",
+                       "| (split form: tail batches/wave, moves/wave, move us/wave; fused: batches/wave, "
+                       "row-wait us/wave, decide us/wave) %.2f %.1f %.2f\n",
                        nwaves, (t4 - t0) / 100.0, sum[0] / nwaves / 100, mx[0] / 100,
                        sum[1] / nwaves / 100, mx[1] / 100, sum[2] / nwaves / 100, mx[2] / 100,
                        sum[3] / nwaves / 100, mx[3] / 100, sum[4] / nwaves / 100, mx[4] / 100,
-                       sum[5] / nwaves / 100, mx[5] / 100, nb / nwaves, mv / nwaves,
+                       sum[5] / nwaves / 100, mx[5] / 100, nb / nwaves, split_env ? mv / nwaves : mv / nwaves / 100,
                        mvt / nwaves / 100);
         }
 #endif
