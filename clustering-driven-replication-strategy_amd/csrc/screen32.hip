@@ -2800,7 +2800,9 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
       if (unc) {
         const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(um >> 32),
                                                 __builtin_amdgcn_mbcnt_lo((unsigned)um, 0u));
-        fb_region[fb_used + r] = int2{pt, (int)bA};
+        // (the best key's label bits carry the old label: near_tie reads
+        // the key's value only, and the tail needs no lab8 load)
+        fb_region[fb_used + r] = int2{pt, (int)((bA & ~63u) | (unsigned)ao)};
       }
       fb_used += __popcll(um);
     }
@@ -3093,15 +3095,26 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   if (B.dbg & 2) fb_used = 0;  // (timing: no exact pass)
 #endif
   if constexpr (DEFER) {
+  // the next batch's records and rows load while one is decided
+  auto tload = [&](int e0, int2& rec, f4 (&xr)[Q]) __attribute__((always_inline)) {
+    const int e = e0 + lane;
+    rec = fb_region[e < fb_used ? e : e0];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) xr[q] = XA4[(int64_t)rec.x * Q + q];
+  };
+  int2 rec_n = {0, 0};
+  f4 xr_n[Q];
+  if (fb_used > 0) tload(0, rec_n, xr_n);
   for (int e0 = 0; e0 < fb_used; e0 += 64) {
     const int e = e0 + lane;
     const bool live = e < fb_used;
-    const int2 rec = fb_region[live ? e : e0];
-    const int pt = rec.x;
-    const int ao = a.lab8[pt];  // (unchanged until this pass decides the point)
+    const int2 rec = rec_n;
     f4 xr[Q];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) xr[q] = XA4[(int64_t)pt * Q + q];
+    for (int q = 0; q < Q; ++q) xr[q] = xr_n[q];
+    if (e0 + 64 < fb_used) tload(e0 + 64, rec_n, xr_n);
+    const int pt = rec.x;
+    const int ao = rec.y & 63;  // (the record's: unchanged until this pass decides the point)
     float xh[DM];
     rowhat(xr, xh);
     u4v T0[QH], T1[QH];
@@ -3789,13 +3802,16 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       b.tprof = nullptr;
       b.slot_wg = 0;
       // chunk shares of screen32bs's 4 launch generations (workgroups per CU):
-      // one region per generation, equal by default (A/B at 100M: 180 -> 166
-      // us against one strided split; speed-proportional weights 100,82,68,61
-      // 166 us); CDR_S32BS_W="w0,w1,w2,w3" sets them, CDR_S32BS_W=0 the split
+      // one region per generation (4-byte words, A/B at 100M: 180 -> 166 us
+      // against one strided split; speed-proportional weights 100,82,68,61
+      // 166 us); 2-byte words: 115,105,95,85 (0.161-0.163 ms per step against
+      // 0.168-0.178 equal, profiles/r05_generation_weights.txt);
+      // CDR_S32BS_W="w0,w1,w2,w3" sets them, CDR_S32BS_W=0 the split
       if (BS) {
         static int wenv[4] = {-1, 0, 0, 0};
         if (wenv[0] < 0) {
-          for (int q = 0; q < 4; ++q) wenv[q] = 100;
+          const int wdef[4] = {115, 105, 95, 85};
+          for (int q = 0; q < 4; ++q) wenv[q] = split_env ? 100 : wdef[q];
           if (const char* e = std::getenv("CDR_S32BS_W")) {
             wenv[0] = 0;
             int v[4] = {0, 0, 0, 0};
