@@ -3602,6 +3602,9 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   const int PD = PR ? PPD : LRn ? LRn : s32d_depth(QH);
   if (BS) {
     bpc = screen32bs_blocks_per_cu(PQ, MT);
+    // (experiments: fewer workgroups per CU, CDR_S32BS_BPC=1..3)
+    static const int bsb_env = std::getenv("CDR_S32BS_BPC") ? std::atoi(std::getenv("CDR_S32BS_BPC")) : 0;
+    if (bsb_env >= 1 && bsb_env < bpc) bpc = bsb_env;
   } else if (BND) {
     bpc = screen32b_blocks_per_cu(PQ, MT);
   } else if (PR) {
