@@ -2774,7 +2774,11 @@ __global__ __launch_bounds__(64) void f32r_gather_kernel(const float* __restrict
                                                          const double* __restrict__ x64,
                                                          const int64_t* __restrict__ pick, int d,
                                                          int64_t n_pad, float* __restrict__ cen) {
-  const int64_t p = pick[0];
+  // (a step after a bad total searches probabilities that may all be 0 and
+  // find no row, -1: its pick is never used, the run raises; row 0 keeps the
+  // gather in bounds)
+  int64_t p = pick[0];
+  if (p < 0 || p >= n_pad) p = 0;
   for (int f = threadIdx.x; f < d; f += 64)
     cen[f] = x32 ? x32[xidx(f, p, n_pad)] : (float)x64[xidx(f, p, n_pad)];
 }
