@@ -375,6 +375,8 @@ def f64_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
     if ctx.info()["mode"] != _cdr.MODE_F64:
         raise RuntimeError("F64 leg: the points did not load in F64 mode")
     C = X[np.sort(np.random.default_rng(42).choice(n_total, k, replace=False))].copy()
+    # (the CPU baseline's sample: the first rows of the same data)
+    cpu_rows = X[:1_000_000].copy() if rank == 0 and world == 1 and not args.no_cpu_baseline else None
     del X
 
     def step(C):
@@ -433,8 +435,9 @@ def f64_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import kmeans_oracle
 
-        rows, iters = 1_000_000, 2
-        Xs = X[:rows]
+        iters = 2
+        Xs = cpu_rows
+        rows = Xs.shape[0]
         Cs = Xs[:k].copy()
         c0 = time.perf_counter()
         for _ in range(iters):
