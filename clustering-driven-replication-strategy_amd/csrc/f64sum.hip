@@ -515,6 +515,45 @@ __global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t
     const unsigned long long gl_live = __ballot((gl.p & 8) != 0);
     unsigned long long todo = gl_live;
     while (todo) {
+      // a run of whole groups in the running value's binade, composed in one
+      // step: the ordered prefix of their transfers (a 6-level shuffle
+      // tree), then the longest prefix that stays in the binade (the values
+      // only grow, so staying there at the end means staying throughout).
+      // Stepping them one at a time cost ~430 cycles per group
+      if (sE != kENone) {
+        const int i0 = __builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
+        const bool lv = (gl.p & 8) != 0;
+        const bool okg = !lv || ((gl.p & 4) && gl.e == sE);
+        const unsigned long long brk = ~__ballot(okg) & (~0ull << i0);
+        const int r = __builtin_amdgcn_readfirstlane(brk ? __ffsll((long long)brk) - 1 : 64);
+        if (r > i0 + 1) {
+          const bool on = lane >= i0 && lane < r && lv;
+          XferC x;
+          x.d0 = on ? gl.d0 : 0;
+          x.d1 = on ? gl.d1 : 0;
+          x.p = on ? (gl.p & 3) : 2;  // identity: P0 = 0, P1 = 1
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            XferC y;
+            y.d0 = __shfl_up(x.d0, o);
+            y.d1 = __shfl_up(x.d1, o);
+            y.p = __shfl_up(x.p, o);
+            if (lane >= o) x = xc_compose(y, x);
+          }
+          const long long mq = sN + ((sN & 1) ? x.d1 : x.d0);
+          const bool inrun = lane >= i0 && lane < r;
+          const unsigned long long bad = __ballot(inrun && !(mq < kTop));
+          const int L = __builtin_amdgcn_readfirstlane(bad ? __ffsll((long long)bad) - 1 : r);
+          if (L > i0) {  // groups i0 .. L-1 at once
+            sN = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
+                                  (int)(mq >> 32), L - 1)
+                              << 32) |
+                             (unsigned)__builtin_amdgcn_readlane((int)mq, L - 1));
+            todo &= L >= 64 ? 0ull : (~0ull << L);
+            continue;
+          }
+        }
+      }
       const int gi = __builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
       todo &= todo - 1;
       const int gp = __builtin_amdgcn_readlane(gl.p, gi);
