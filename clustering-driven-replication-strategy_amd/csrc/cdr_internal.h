@@ -208,6 +208,8 @@ struct Ctx {
   // units) | float W up [64] | float W down [64]
   DevBuf zb, xh16, bnd, t_acc;
   DevBuf rs_hist;  // radix.hip: per-tile digit counts and digit bases of the fallback sort
+  DevBuf s32_dyn;  // screen32bs16's dynamic-tail counters (2 parities x 4 regions x 8 XCDs)
+  int s32_dyn_par = 0;  // the parity the next launch claims from
   DevBuf zl, zn;  // split bounded screen: per-wave lists of failed points (screen32bz), lengths
   bool zb_valid = false, xh_valid = false, bnd_ok = false;
   int zb_fmt = 0;  // bound words in zb: 16 (2-byte, screen32bs) or 32 bits

@@ -1808,15 +1808,26 @@ struct S32BArgs {
   // Ctx::bnd (plan32.h kBnd*)
   uint16_t* zh;
   const unsigned char* bt;
+  // the 2-byte screen's dynamic tail (slot_wg > 0; null: off): each
+  // generation region streams its first dyn_pct % statically (strided over
+  // its waves) and hands the rest out kBPD chunks at a time from a counter
+  // (dyn[((par * 4 + region) * 8 + xcd) * 32]: per XCD, a 128-byte line
+  // each; the launch zeroes the other parity's counters for the next one)
+  unsigned* dyn;
+  int dyn_par, dyn_pct;
 };
 constexpr int kZ16Chunk = 512;  // points per wave-chunk of the 2-byte word stream (8 per lane)
+// the dynamic tail's static percent (100: off; 90: 3-5 us less per config-3
+// step than 100, profiles/r05_dynamic_tail_ab.txt)
+constexpr int kS32DynPct = 90;
 
 // The chunks wave `wv` of this workgroup streams: wbase + i * wstride below
 // wend.  With slot_wg > 0 the workgroups of one CU slot (launch generation)
 // share a region in proportion to its weight: the later generations on a CU
 // get fewer issue slots (oldest-first) and otherwise finish last.
 __device__ __forceinline__ void bs_range(const S32BArgs& B, int wv, int64_t& wbase, int& wstride,
-                                         int64_t& wend) {
+                                         int64_t& wend, int64_t* rr0 = nullptr,
+                                         int* rsl = nullptr) {
   const int64_t nchunks = B.nchunks;
   wbase = (int64_t)blockIdx.x * 4 + wv;
   wend = nchunks;
@@ -1842,11 +1853,26 @@ __device__ __forceinline__ void bs_range(const S32BArgs& B, int wv, int64_t& wba
     wstride = B.slot_wg * 4;
     wbase = R0 + (int64_t)((int)blockIdx.x - sl * B.slot_wg) * 4 + wv;
     wend = R1;
+    if (rr0) *rr0 = R0;
+    if (rsl) *rsl = sl;
   }
   wbase = __builtin_amdgcn_readfirstlane((int)wbase);
 }
 
 // Host mirror of bs_range: the most chunks any wave of the grid streams.
+// the largest generation region (chunks; slot_wg > 0)
+static int64_t bs_max_region(const S32BArgs& B, int nwg) {
+  const int ns = nwg / B.slot_wg;
+  int wsum = 0;
+  for (int q = 0; q < ns; ++q) wsum += B.wsl[q];
+  int64_t mx = 0, wpre = 0;
+  for (int q = 0; q < ns; ++q) {
+    mx = std::max<int64_t>(mx, B.nchunks * (wpre + B.wsl[q]) / wsum - B.nchunks * wpre / wsum);
+    wpre += B.wsl[q];
+  }
+  return mx;
+}
+
 static int64_t bs_max_chunks(const S32BArgs& B, int nwg) {
   const int64_t nchunks = B.nchunks;
   if (B.slot_wg <= 0) return ceil_div(nchunks, (int64_t)nwg * 4);  // (strided or contiguous)
@@ -2391,6 +2417,10 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #define CDR_S32BS_DEFER 1
 #endif
   constexpr bool DEFER = !SPLIT && CDR_S32BS_DEFER;
+  // the dynamic tail's counters for the next launch (the other parity; before
+  // the gate, so a skipped launch leaves them zeroed too)
+  if (!SPLIT && B.dyn && blockIdx.x == 0 && threadIdx.x < 32)
+    B.dyn[((B.dyn_par ^ 1) * 32 + threadIdx.x) * 32] = 0u;
   if (a.gate && a.gate[0] == 0) return;
   typedef unsigned u4v __attribute__((ext_vector_type(4)));
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -2425,7 +2455,28 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   // this wave's chunks: wbase + i wstride below wend
   int64_t wbase, wend;
   int wstride;
-  bs_range(B, wv, wbase, wstride, wend);
+  int64_t rR0 = 0;
+  int rsl = 0;
+  bs_range(B, wv, wbase, wstride, wend, &rR0, &rsl);
+  // the dynamic tail (B.dyn): this wave's static chunks end at swend, the
+  // region's pool [P0, wend) goes out kBPD chunks at a time from dctr
+  // (chunk indices: int, below 2^31 - the host's n_pad)
+  const bool dyn = !SPLIT && B.dyn != nullptr && B.slot_wg > 0;
+  // The pool is split over the 8 XCDs (workgroup b runs on XCD b % 8), one
+  // counter each in its own 128-byte line: claims on one address serialise
+  // (~10 ns apart, measured), so one counter per region holds the waves up
+  int swend = (int)wend, P0 = (int)wend, P1 = (int)wend;
+  if (dyn) {
+    const int spw = (int)((wend - rR0) * B.dyn_pct / 100 / wstride);  // static chunks per wave
+    swend = (int)rR0 + spw * wstride;
+    const int xcd = blockIdx.x & 7;
+    P0 = swend + (int)((wend - swend) * xcd / 8);
+    P1 = swend + (int)((wend - swend) * (xcd + 1) / 8);
+  }
+  // the entries' chunk field: region-relative chunk (dynamic tail) or the
+  // chunk ordinal in this wave's range
+  const int ebase = dyn ? (int)rR0 : (int)wbase;
+  const int estride = dyn ? 1 : wstride;
   u4v zc[kBPD];
 
   // ---- the plan ----
@@ -2841,7 +2892,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     const int e = 64 * b + lane;
     g.valid = e < cnt;
     const unsigned ent = fl[g.valid ? e : 64 * b];  // (entry 64 b exists)
-    const int64_t ci = wbase + (int64_t)(ent >> SH) * wstride;
+    const int64_t ci = ebase + (int64_t)(ent >> SH) * estride;
     const int64_t pt = ci * CH + ((ent >> 6) & (CH - 1));
     g.pt = (int)pt;
     g.ao = (int)(ent & 63);
@@ -2965,7 +3016,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
         const int e = head + lane;
         cur.valid = e < cnt;
         const unsigned ent = fl[cur.valid ? e : head];
-        const int64_t ci = wbase + (int64_t)(ent >> SH) * wstride;
+        const int64_t ci = ebase + (int64_t)(ent >> SH) * estride;
         const int64_t pt = ci * CH + ((ent >> 6) & (CH - 1));
         cur.pt = (int)pt;
         cur.ao = (int)(ent & 63);
@@ -3006,7 +3057,8 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
   // phase 2 draining the list whenever it must.
   int cnt = 0;
   int it = 0;  // chunk ordinal within this wave's range (the entries' high bits)
-  auto insert = [&](const u4v& z) __attribute__((always_inline)) {
+  auto insert = [&](const u4v& z, int ci) __attribute__((always_inline)) {
+    const unsigned enc = dyn ? (unsigned)(ci - ebase) : (unsigned)it;
     // the 8 thresholds from LDS (independent reads, one wait), then the
     // tests; entries only from chunks with a failed point
     unsigned fm = 0;
@@ -3027,7 +3079,7 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
           if (fail) {
             const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            fl[cnt + r] = (unsigned)it << 15 | (unsigned)(8 * lane + u) << 6 |
+            fl[cnt + r] = enc << 15 | (unsigned)(8 * lane + u) << 6 |
                           ((z[u >> 1] >> (16 * (u & 1))) & 63u);
           }
           // (readfirstlane: uniform to the compiler, so the loops branch on
@@ -3038,10 +3090,40 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     }
     ++it;
   };
-  int64_t C0 = wbase;
+  // the group walk: chunks gC + i gS below gEnd (static: this wave's range;
+  // then, with the dynamic tail, groups claimed from the region's pool)
+  int gC = (int)wbase, gEnd = swend;
+  bool dynph = false;
+#define gS (dynph ? 1 : wstride)
+  int ncl = -1;  // a claim made ahead: its pool offset (-1: none)
+  // a wave claims while its near-tie region (a.cap points) holds the chunks
+  // it may yet stream: the one in hand and the one claimed (the host sizes
+  // the regions so the waves' budgets cover the pool)
+#define budget (a.cap / CH - 2 * kBPD)
+  auto claim = [&]() __attribute__((always_inline)) -> unsigned {
+    unsigned v = 0;
+    if (lane == 0)
+      v = atomicAdd(B.dyn + ((B.dyn_par * 4 + rsl) * 8 + (blockIdx.x & 7)) * 32, (unsigned)kBPD);
+    return v;
+  };
+  // the next group when the current phase is spent (uniform)
+  auto next_group = [&]() __attribute__((always_inline)) -> bool {
+    if (gC < gEnd) return true;
+    if (!dyn) return false;
+    dynph = true;
+    if (ncl < 0) {
+      if (it > budget) return false;
+      ncl = (int)__builtin_amdgcn_readfirstlane(claim());
+    }
+    gC = P0 + ncl;
+    ncl = -1;
+    gEnd = gC + kBPD < P1 ? gC + kBPD : P1;
+    return gC < gEnd;
+  };
+  int C0 = gC;
   bool dense = false;  // (wave-uniform) the plain loop takes over at chunk C0
   for (bool first = true;; first = false) {
-    const bool more = C0 < wend;  // (wave-uniform)
+    const bool more = next_group();  // (wave-uniform)
     // phase 2 first: the rows it gathers load under this group's stream, and
     // this group's loads are the youngest, so each chunk waits for itself
     // only (vmcnt(kBPD - 1 - i)) whatever phase 2 issued
@@ -3053,26 +3135,35 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     if (!more) break;
 #pragma unroll
     for (int i = 0; i < kBPD; ++i) {
-      zload(zc[i], C0 + (int64_t)i * wstride);
+      zload(zc[i], gC + i * gS);
       __builtin_amdgcn_sched_barrier(0);  // (issued in chunk order)
     }
+    // the next dynamic group's claim, ahead of its use (returned under this
+    // group's tests)
+    const bool ahead = dyn && it <= budget && (dynph || gC + kBPD * gS >= gEnd);
+    unsigned clv = 0;
+    if (ahead) clv = claim();
 #pragma unroll
     for (int i = 0; i < kBPD; ++i) {
-      const int64_t Ci = C0 + (int64_t)i * wstride;
-      if (Ci >= wend) break;
+      const int Ci = gC + i * gS;
+      if (Ci >= gEnd) break;
       if (cnt - head + CH > kSList) {  // (dense failures only)
         dense = true;
         C0 = Ci;
         break;
       }
-      insert(zc[i]);
+      insert(zc[i], Ci);
     }
+    if (ahead) ncl = (int)__builtin_amdgcn_readfirstlane(clv);
     if (dense) break;
-    C0 += (int64_t)kBPD * wstride;
+    gC = dynph ? gEnd : gC + kBPD * gS;
   }
   if (dense) {
-    for (int64_t Ci = C0;; Ci += wstride) {
-      const bool more = Ci < wend;
+    // the rest of the current group / phase one chunk at a time, then (the
+    // dynamic tail) further claimed groups
+    gC = C0;
+    for (;;) {
+      const bool more = next_group();
 #if CDR_S32BS_LAZY
       if (!more || cnt - head + CH > kSList) step2(cnt, !more);  // (returns with room)
 #else
@@ -3080,10 +3171,13 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #endif
       if (!more) break;
       u4v z;
-      zload(z, Ci);
-      insert(z);
+      zload(z, gC);
+      insert(z, gC);
+      gC += gS;
     }
   }
+#undef gS
+#undef budget
   }  // (!SPLIT)
   // ---- the uncertified points: the same split screen again (the same values),
   // every centroid whose key is within the threshold of the best is a
@@ -3096,11 +3190,13 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
 #endif
   if constexpr (DEFER) {
   // the next batch's records and rows load while one is decided
+  // (Q = 4: the records only - the rows ahead too spill registers)
+  constexpr int QA = Q < 4 ? Q : 0;
   auto tload = [&](int e0, int2& rec, f4 (&xr)[Q]) __attribute__((always_inline)) {
     const int e = e0 + lane;
     rec = fb_region[e < fb_used ? e : e0];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) xr[q] = XA4[(int64_t)rec.x * Q + q];
+    for (int q = 0; q < QA; ++q) xr[q] = XA4[(int64_t)rec.x * Q + q];
   };
   int2 rec_n = {0, 0};
   f4 xr_n[Q];
@@ -3111,7 +3207,9 @@ __global__ __launch_bounds__(256, 4) void screen32bs(S32BArgs B) {
     const int2 rec = rec_n;
     f4 xr[Q];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) xr[q] = xr_n[q];
+    for (int q = 0; q < QA; ++q) xr[q] = xr_n[q];
+#pragma unroll
+    for (int q = QA; q < Q; ++q) xr[q] = XA4[(int64_t)rec.x * Q + q];
     if (e0 + 64 < fb_used) tload(e0 + 64, rec_n, xr_n);
     const int pt = rec.x;
     const int ao = rec.y & 63;  // (the record's: unchanged until this pass decides the point)
@@ -3831,6 +3929,29 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
         if (std::getenv("CDR_S32BS_CONTIG") && std::atoi(std::getenv("CDR_S32BS_CONTIG")))
           b.slot_wg = -1;
       }
+      // the dynamic tail (2-byte words in generation regions): CDR_S32BS_DYN
+      // = the statically streamed percent (100: off)
+      b.dyn = nullptr;
+      b.dyn_par = 0;
+      b.dyn_pct = 100;
+      if (BS && z16 && !split_env && b.slot_wg > 0) {
+        static int dyn_env = -1;
+        if (dyn_env < 0) {
+          dyn_env = kS32DynPct;
+          if (const char* e = std::getenv("CDR_S32BS_DYN")) dyn_env = std::atoi(e);
+          dyn_env = std::min(std::max(dyn_env, 0), 100);
+        }
+        if (dyn_env < 100 && bs_max_region(b, nwg) < (1 << 17) && b.slot_wg % 8 == 0) {
+          if (c.s32_dyn.bytes < sizeof(unsigned) * 2 * 32 * 32) {
+            c.s32_dyn.ensure(sizeof(unsigned) * 2 * 32 * 32);
+            HIP_CHECK(hipMemsetAsync(c.s32_dyn.p, 0, c.s32_dyn.bytes, c.stream));
+          }
+          b.dyn = c.s32_dyn.as<unsigned>();
+          b.dyn_par = c.s32_dyn_par;
+          b.dyn_pct = dyn_env;
+          c.s32_dyn_par ^= 1;
+        }
+      }
 #ifdef CDR_EXPERIMENTS
       static unsigned long long* tprof_buf = nullptr;
       const bool tprof_on = BS && std::getenv("CDR_S32BS_TPROF");
@@ -3846,7 +3967,11 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
         // the stream alone takes ~80 us and the decisions ~100-130 us as their
         // own launch, so the fused kernel (~165-180 us) stays the default
         // the near-tie list holds at most the points of a wave's chunks
-        const int64_t need = bs_max_chunks(b, nwg) * (z16 ? kZ16Chunk : kBChunk);
+        // (the dynamic tail: twice the static share plus the two groups a
+        // claiming wave may hold, so the waves' budgets cover the pool)
+        const int64_t need =
+            (b.dyn ? 2 * bs_max_chunks(b, nwg) + 2 * kBPD + 1 : bs_max_chunks(b, nwg)) *
+            (z16 ? kZ16Chunk : kBChunk);
         if (need > b.p.cap) {
           c.fb_list.ensure(sizeof(int2) * (size_t)nwaves * (size_t)need);
           b.p.fb_list = c.fb_list.as<int2>();
