@@ -1820,6 +1820,11 @@ constexpr int kZ16Chunk = 512;  // points per wave-chunk of the 2-byte word stre
 // the dynamic tail's static percent (100: off; 90: 3-5 us less per config-3
 // step than 100, profiles/r05_dynamic_tail_ab.txt)
 constexpr int kS32DynPct = 90;
+// ... from this many chunks per wave: a wave's last claim (the one that finds
+// the pool empty) is an exposed atomic round trip, and with a few chunks per
+// wave the tail costs more than it balances (12.5M x 16: 0.050 ms per step
+// without, 0.055 with; 10M x 8: 0.036 / 0.040)
+constexpr int kS32DynMinChunks = 24;
 
 // The chunks wave `wv` of this workgroup streams: wbase + i * wstride below
 // wend.  With slot_wg > 0 the workgroups of one CU slot (launch generation)
@@ -3941,7 +3946,8 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
           if (const char* e = std::getenv("CDR_S32BS_DYN")) dyn_env = std::atoi(e);
           dyn_env = std::min(std::max(dyn_env, 0), 100);
         }
-        if (dyn_env < 100 && bs_max_region(b, nwg) < (1 << 17) && b.slot_wg % 8 == 0) {
+        if (dyn_env < 100 && bs_max_region(b, nwg) < (1 << 17) && b.slot_wg % 8 == 0 &&
+            bs_max_chunks(b, nwg) >= kS32DynMinChunks) {
           if (c.s32_dyn.bytes < sizeof(unsigned) * 2 * 32 * 32) {
             c.s32_dyn.ensure(sizeof(unsigned) * 2 * 32 * 32);
             HIP_CHECK(hipMemsetAsync(c.s32_dyn.p, 0, c.s32_dyn.bytes, c.stream));
