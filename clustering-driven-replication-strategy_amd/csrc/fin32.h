@@ -56,6 +56,7 @@ struct FinArgs {
   // runs zh_rebase_kernel before the next screen; screen32.hip)
   int rebase_ok;
   int abl;  // timing experiments only (0 in the product build)
+  unsigned long long* tprof;  // (experiments build: phase timestamps, thread 0)
 };
 
 // fp64 -> fp32 rounded up / down (W_j for screen32b)
@@ -83,6 +84,13 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
   constexpr int V = 512 / NT;
   long long* __restrict__ state = a.state;
   const int t = threadIdx.x;
+#ifdef CDR_EXPERIMENTS
+#define FIN_TP(i) \
+  if (a.tprof && t == 0) a.tprof[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define FIN_TP(i)
+#endif
+  FIN_TP(0);
   if (a.abl & 8) {  // (the step still counts, so the host's polling goes on)
     if (t == 0) state[1] += 1;
     return;
@@ -246,7 +254,9 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
     }
     if constexpr (V > 1) asm volatile("" ::: "memory");  // (one virtual thread's loads at a time)
   }
+  FIN_TP(1);
   __syncthreads();
+  FIN_TP(2);
   if (t == 0 && a.fbc) {
     int fb = 0;
     for (int q = 0; q < 8; ++q) fb += r_fb[q];
@@ -365,6 +375,7 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
       hd[3] = rebase ? 1 : 0;
     }
   }
+  FIN_TP(3);
   if (!a.plan || reason != kLLRun || (a.abl & 2)) return;
   // ---- the next step's plan (plan32_build, per element) ----
   unsigned char* __restrict__ plan = a.plan;
@@ -399,7 +410,9 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
     const int p = vt[v] & 7;
     if (p < 2) pc[jj * kPrStr + 16 + 2 * p] = 0.0f, pc[jj * kPrStr + 17 + 2 * p] = 0.0f;
   }
+  FIN_TP(4);
   __syncthreads();
+  FIN_TP(5);
   // ---- row sums (host order), nearest-centroid distances, maxima ----
   double ec[V], sm[V];
 #pragma unroll
@@ -438,6 +451,7 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
         smv = fmin(smv, (acc[0] + acc[1]) + (acc[2] + acc[3]));
       }
     }
+    if (v == 0) FIN_TP(6);
     smv = fmin(smv, __shfl_xor(smv, 1));
     smv = fmin(smv, __shfl_xor(smv, 2));
     smv = fmin(smv, __shfl_xor(smv, 4));
@@ -458,7 +472,9 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
       x_ec[vw[v]] = ecmax;
     }
   }
+  FIN_TP(7);
   __syncthreads();
+  FIN_TP(8);
   double ccmax = 0.0, l1c = 0.0, cabs = 0.0, ecmax = 0.0;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -518,6 +534,8 @@ __device__ __forceinline__ void fin32_body(const FinArgs& a, unsigned char* __re
     const int rw = 32 * m + 8 * (i >> 2) + 4 * (ln >> 5) + (i & 3);
     cinit[idx] = rw < k ? (float)(cc[rw] + D) : 1.0e30f;
   }
+  FIN_TP(9);
+#undef FIN_TP
 }
 
 }  // namespace cdr

@@ -26,6 +26,7 @@
 // pass over the points per run (cdr_points_sqdev; all-reduced once when the
 // points are sharded).
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 
 #include "cdr_internal.h"
@@ -448,8 +449,15 @@ FinArgs ll_fin_args(Ctx& c) {
   // (the first one sets the base), each followed by zh_rebase_kernel
   a.rebase_ok = c.ll_fin_count % kRebaseEvery == 0 ? 1 : 0;
   a.abl = 0;
+  a.tprof = nullptr;
 #ifdef CDR_EXPERIMENTS
   if (const char* e = std::getenv("CDR_FIN_ABL")) a.abl = std::atoi(e);
+  static unsigned long long* fin_tp = nullptr;
+  if (std::getenv("CDR_FIN_TPROF")) {
+    if (!fin_tp) HIP_CHECK(hipMalloc(&fin_tp, sizeof(unsigned long long) * 16));
+    HIP_CHECK(hipMemsetAsync(fin_tp, 0, sizeof(unsigned long long) * 16, c.stream));
+    a.tprof = fin_tp;
+  }
   if (std::getenv("CDR_FIN_NOPLAN")) a.plan = nullptr;  // timing experiments only
 #endif
   return a;
@@ -465,6 +473,17 @@ static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
   if (a.plan && c.ll_k <= 64 && c.d <= 16 && a.nslices <= kRunSlices && !fin_old) {
     hipLaunchKernelGGL(ll_finalize32, dim3(1), dim3(512), 0, c.stream, a);
     HIP_CHECK(hipGetLastError());
+#ifdef CDR_EXPERIMENTS
+    if (a.tprof) {  // phase times (us from the start; 100 MHz counter), to stderr
+      unsigned long long h[16];
+      HIP_CHECK(hipMemcpyAsync(h, a.tprof, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+      HIP_CHECK(hipStreamSynchronize(c.stream));
+      fprintf(stderr, "FINTP");
+      for (int i = 1; i < 10; ++i)
+        fprintf(stderr, " %d:%.2f", i, h[i] ? (double)(h[i] - h[0]) * 0.01 : -1.0);
+      fprintf(stderr, "\n");
+    }
+#endif
     if (a.rebase_ok && a.bnd) zh_rebase(c, c.ll_state.as<long long>());  // (gated on the device)
   } else {
     hipLaunchKernelGGL(ll_finalize, dim3(1), dim3(kFinThreads), 0, c.stream, a);

@@ -7,7 +7,9 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(REPO, "clustering-driven-replication-strategy_amd"), REPO]
+# CDR_PKG: another build of the package (A/B of two library versions on one box)
+PKG = os.environ.get("CDR_PKG") or os.path.join(REPO, "clustering-driven-replication-strategy_amd")
+sys.path[:0] = [PKG, REPO]
 import _cdr  # noqa: E402
 from cdr_dist import Comm, DeviceLloyd, seed_sharded  # noqa: E402
 
