@@ -389,15 +389,28 @@ def f64_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
         C[nz] = sums[nz] / counts[nz, None]
         return C
 
-    for _ in range(args.warmup):
-        C = step(C)
+    # one GPU: the steps resident on the device (cdr_lloyd_f64_run: means and
+    # shift on the device too, one synchronisation per call; tol -1 = no
+    # convergence test, every step applied)
+    resident = comm is None and hasattr(ctx, "lloyd_f64_run")
+
+    def run(C, steps):
+        if resident:
+            C, applied, _, _, _ = ctx.lloyd_f64_run(C, steps, -1.0)
+            if applied != steps:
+                raise RuntimeError("F64 leg: the device run stopped early (empty cluster)")
+            return C
+        for _ in range(steps):
+            C = step(C)
+        return C
+
+    C = run(C, args.warmup)
     ctx.synchronize()
     if dist is not None:
         dist.barrier()
     ctx.profile_reset(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        C = step(C)
+    C = run(C, args.steps)
     ctx.synchronize()
     if dist is not None:
         dist.barrier()

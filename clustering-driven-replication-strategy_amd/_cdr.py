@@ -77,6 +77,7 @@ SIGNATURES = {
     "cdr_seed_run_sharded": ([_P, _I64, _I64, _I64, _I32, _P, _P, _P, _P], None),
     "cdr_lloyd_step": ([_P, _P, _I32, _P, _I32], None),
     "cdr_lloyd_step_f64": ([_P, _P, _I32, _P, _P], None),
+    "cdr_lloyd_f64_run": ([_P, _P, _I32, _I32, _F64, _P, _P, _P, _P], None),
     "cdr_lloyd_step_f32r": ([_P, _P, _I32, _P, _P], None),
     "cdr_f32r_seed_update": ([_P, _P, _I32, _P], None),
     "cdr_f32r_seed_run": ([_P, _I64, _I32, _P, _P], None),
@@ -467,6 +468,24 @@ class Context:
         counts = np.empty(k, dtype=np.int64)
         _check(self._lib.cdr_lloyd_step_f64(self._h, _ptr(C), k, _ptr(sums), _ptr(counts)))
         return sums, counts
+
+    F64_RUN_ALL, F64_RUN_CONVERGED, F64_RUN_HOST = 0, 1, 2
+
+    def lloyd_f64_run(self, C: np.ndarray, max_steps: int, tol: float):
+        """F64: up to max_steps Lloyd steps resident on the device
+        (cdr_lloyd_f64_run).  Returns (C after the applied steps, steps
+        applied, reason, means, counts): reason F64_RUN_HOST = the next step
+        stopped for the host (empty cluster / shift near tol) with its means
+        and counts; F64_RUN_CONVERGED = the last applied step had shift < tol."""
+        C = np.ascontiguousarray(C, dtype=np.float64)
+        k, d = C.shape
+        C_out = np.empty((k, d), dtype=np.float64)
+        means = np.empty((k, d), dtype=np.float64)
+        counts = np.empty(k, dtype=np.int64)
+        info = np.zeros(2, dtype=np.int32)
+        _check(self._lib.cdr_lloyd_f64_run(self._h, _ptr(C), k, int(max_steps), float(tol),
+                                           _ptr(C_out), _ptr(means), _ptr(counts), _ptr(info)))
+        return C_out, int(info[0]), int(info[1]), means, counts
 
     # -- sharded F64 sums (include/cdr.h cdr_f64s_*; cdr_dist.f64_sharded_sums) --
     def f64s_begin(self, C: np.ndarray, nranks: int, rank: int, tot_buf: int) -> np.ndarray:

@@ -148,6 +148,9 @@ struct Ctx {
   int fb_regions = 0;
   DevBuf f64_sums;  // double k*d
   DevBuf f64_counts;  // int64 k
+  // the device-resident F64 run (cdr_lloyd_f64_run): state {running, steps,
+  // reason, shift^2 bits}, the last step's means (k*d) and counts (k)
+  DevBuf f64r_state, f64r_keep;
   // f64sum.hip: block sums, counts, predicted binades, transfers, walk counts
   DevBuf f64x_A, f64x_cnt, f64x_E, f64x_T, f64x_walk, f64x_G, f64x_GS, f64x_prof;
   // f64_step_fused: the binade predictions of the last F64 step (two buffers:
@@ -368,7 +371,7 @@ void f64s_compose_all(Ctx& c, int k, int nranks, const double* tot_all, const vo
                       double* d_sums, long long* d_counts, int* d_status);
 void f64s_chain_walk(Ctx& c, int k, double* chain);
 bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
-                    unsigned long long* d_counts, bool prof);
+                    unsigned long long* d_counts, bool prof, const long long* gate = nullptr);
 void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
                        const double* creation_s, double observation_end,
                        double* out);

@@ -682,7 +682,11 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
                                                         unsigned* __restrict__ cnt,
                                                         const int* __restrict__ Eprev,
                                                         Xfer* __restrict__ T,
-                                                        unsigned char* __restrict__ ordr) {
+                                                        unsigned char* __restrict__ ordr,
+                                                        const long long* __restrict__ gate) {
+  // (the device-resident F64 run: a stopped run keeps the labels of the
+  // assignment that stopped it)
+  if (gate && gate[0] == 0) return;
   __shared__ double tab[kFMaxK * D];
   __shared__ unsigned cc[kFMaxK];
   __shared__ int coff[kFMaxK];
@@ -1039,7 +1043,7 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums, bool pre) {
 // predictions, the transfers otherwise, groups and walk.  false: shape not
 // covered (d > 16, d < 2, k > 64), nothing launched.
 bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
-                    unsigned long long* d_counts, bool prof) {
+                    unsigned long long* d_counts, bool prof, const long long* gate) {
   const int d = c.d;
   if (d < 2 || d > 16 || k < 1 || k > kFMaxK || c.n < 1) return false;
   const int64_t n = c.n, nb = ceil_div(n, kFB);
@@ -1067,7 +1071,7 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
     ordr = c.f64x_ord.as<unsigned char>();
   }
   typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
-                     unsigned*, const int*, Xfer*, unsigned char*);
+                     unsigned*, const int*, Xfer*, unsigned char*, const long long*);
 #define CDR_FAB(D_) f64_assign_block<D_, false>, f64_assign_block<D_, true>
   static const Fn fns[17][2] = {{nullptr, nullptr}, {CDR_FAB(1)},  {CDR_FAB(2)},  {CDR_FAB(3)},
                                 {CDR_FAB(4)},       {CDR_FAB(5)},  {CDR_FAB(6)},  {CDR_FAB(7)},
@@ -1078,7 +1082,7 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   hipLaunchKernelGGL(fns[d][xf ? 1 : 0], dim3((unsigned)nb), dim3(kFB), 0, c.stream,
                      c.x64.as<double>(), n, c.n_pad, dC, k, c.labels.as<int32_t>(),
                      c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), Ecur, c.f64x_T.as<Xfer>(),
-                     ordr);
+                     ordr, gate);
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
   HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(unsigned long long) * k, c.stream));
@@ -1394,7 +1398,7 @@ bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot) {
   c.f64x_e_ok = false;  // (the fused step's carried predictions belong to other rows)
   if (n > 0) {
     typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
-                       unsigned*, const int*, Xfer*, unsigned char*);
+                       unsigned*, const int*, Xfer*, unsigned char*, const long long*);
     static const Fn fns[17] = {nullptr, f64_assign_block<1, false>, f64_assign_block<2, false>,
                                f64_assign_block<3, false>, f64_assign_block<4, false>,
                                f64_assign_block<5, false>, f64_assign_block<6, false>,
@@ -1406,7 +1410,7 @@ bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot) {
     hipLaunchKernelGGL(fns[d], dim3((unsigned)nb), dim3(kFB), 0, c.stream, c.x64.as<double>(), n,
                        c.n_pad, dC, k, c.labels.as<int32_t>(), c.f64x_A.as<double>(),
                        c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(),
-                       nullptr);
+                       nullptr, nullptr);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(f64s_totals, dim3((unsigned)ceil_div((int64_t)kd + k, 4)), dim3(256), 0,
                        c.stream, c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), nb, (int)kd, k,

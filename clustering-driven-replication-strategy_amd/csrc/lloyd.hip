@@ -1310,6 +1310,123 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
   }
 }
 
+// The device-resident F64 run's update (one workgroup, after each fused
+// step): means = sums / counts (np.mean's true division), shift =
+// ||means - C|| (src/kmeans_plusplus.py:37-48).  The step is applied on the
+// device when every cluster has members and the shift is clear of tol: C =
+// means, and the run stops once shift < tol.  An empty cluster (the reference
+// reseeds it from np.random) or a shift within 2^-36 of tol (the reference's
+// BLAS summation order is not ours) stops the run WITHOUT applying the step:
+// the host finishes that step from the kept means and counts.  The shift's
+// square is summed in a fixed tree: <= 1024 non-negative terms, within 2^-42
+// of any other order's, so the margin decides both sides rigorously.
+constexpr int kF64RunThreads = 1024;
+__global__ __launch_bounds__(kF64RunThreads) void f64_run_update(
+    const double* __restrict__ sums, const unsigned long long* __restrict__ counts,
+    double* __restrict__ C, double* __restrict__ keep, int k, int d, double tol,
+    long long* __restrict__ st) {
+  __shared__ double red[kF64RunThreads / 64];
+  __shared__ int empty_any;
+  if (st[0] == 0) return;  // (uniform) stopped: this step's kernels ran for nothing
+  const int t = threadIdx.x, kd = k * d;
+  if (t == 0) empty_any = 0;
+  __syncthreads();
+  double m = 0.0, sq = 0.0;
+  if (t < kd) {
+    const unsigned long long cnt = counts[t / d];
+    m = sums[t] / (double)cnt;
+    if (cnt == 0) {
+      empty_any = 1;
+    } else {
+      const double df = m - C[t];
+      sq = df * df;
+    }
+    keep[t] = m;
+    if (t % d == 0) reinterpret_cast<long long*>(keep + kd)[t / d] = (long long)cnt;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+  if ((t & 63) == 0) red[t >> 6] = sq;
+  __syncthreads();
+  double ss = 0.0;
+#pragma unroll
+  for (int w = 0; w < kF64RunThreads / 64; ++w) ss += red[w];
+  const double sh = sqrt(ss);
+  const double mg = 0x1p-36;
+  long long reason = 0;  // 0: applied, go on; 1: applied, converged; 2: the host's step
+  if (empty_any) reason = 2;
+  else if (tol > 0.0 && !(sh > tol * (1.0 + mg))) reason = sh < tol * (1.0 - mg) ? 1 : 2;
+  if (reason != 2 && t < kd) C[t] = m;
+  if (t == 0) {
+    if (reason != 2) st[1] += 1;
+    st[2] = reason;
+    st[3] = __double_as_longlong(ss);
+    if (reason != 0) st[0] = 0;
+  }
+}
+
+// cdr_lloyd_f64_run: up to max_steps fused F64 steps (f64sum.hip) with the
+// update above on the device; one synchronisation at the end.
+void lloyd_run_f64(Ctx& c, const double* C, int32_t k, int32_t max_steps, double tol,
+                   double* C_out, double* means_out, int64_t* counts_out, int32_t* info) {
+  check_k(c, k);
+  if (c.mode != CDR_MODE_F64) CDR_FAIL(CDR_ERR_STATE, "lloyd_run_f64: points are not F64");
+  const int d = c.d;
+  if (d < 2 || d > 16 || k > 64 || k * d > kF64RunThreads)
+    CDR_FAIL(CDR_ERR_UNSUPPORTED, "device F64 run: needs 2 <= d <= 16 and k <= 64");
+  if (max_steps < 0) CDR_FAIL(CDR_ERR_ARG, "max_steps < 0");
+  c.run_valid = false;
+  c.lab8_valid = false;
+  c.zb_valid = false;
+  c.big_valid = false;
+  upload_centroids(c, C, k);
+  const size_t kd = (size_t)k * d;
+  c.f64_sums.ensure(sizeof(double) * kd);
+  c.f64_counts.ensure(sizeof(long long) * k * 2);
+  c.f64r_state.ensure(sizeof(long long) * 4);
+  c.f64r_keep.ensure(sizeof(double) * kd + sizeof(long long) * k);
+  c.h_small.ensure(sizeof(long long) * 4);
+  long long* hst = c.h_small.as<long long>();
+  hst[0] = 1;
+  hst[1] = hst[2] = hst[3] = 0;
+  long long* st = c.f64r_state.as<long long>();
+  HIP_CHECK(hipMemcpyAsync(st, hst, sizeof(long long) * 4, hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemsetAsync(c.f64r_keep.p, 0, c.f64r_keep.bytes, c.stream));
+  snprintf(c.prof_kernel, sizeof(c.prof_kernel), "f64_assign_block<%d>", d);
+  for (int s = 0; s < max_steps; ++s) {
+    const bool prof = prof_step_begin(c);
+    if (prof) prof_mark(c, 0);
+    if (!f64_step_fused(c, k, c.cent64.as<double>(), c.f64_sums.as<double>(),
+                        reinterpret_cast<unsigned long long*>(c.f64_counts.as<long long>()), prof,
+                        st))
+      CDR_FAIL(CDR_ERR_UNSUPPORTED, "device F64 run: shape not covered");
+    hipLaunchKernelGGL(f64_run_update, dim3(1), dim3(kF64RunThreads), 0, c.stream,
+                       c.f64_sums.as<double>(),
+                       reinterpret_cast<const unsigned long long*>(c.f64_counts.as<long long>()),
+                       c.cent64.as<double>(), c.f64r_keep.as<double>(), k, d, tol, st);
+    HIP_CHECK(hipGetLastError());
+    if (prof) prof_mark(c, 2);
+  }
+  HIP_CHECK(hipMemcpyAsync(hst, st, sizeof(long long) * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipMemcpyAsync(C_out, c.cent64.p, sizeof(double) * kd, hipMemcpyDeviceToHost,
+                           c.stream));
+  HIP_CHECK(hipMemcpyAsync(means_out, c.f64r_keep.p, sizeof(double) * kd, hipMemcpyDeviceToHost,
+                           c.stream));
+  HIP_CHECK(hipMemcpyAsync(counts_out, c.f64r_keep.as<double>() + kd, sizeof(long long) * k,
+                           hipMemcpyDeviceToHost, c.stream));
+  std::vector<long long> w(kd);
+  HIP_CHECK(hipMemcpyAsync(w.data(), c.f64x_walk.p, sizeof(long long) * w.size(),
+                           hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.f64x_walked = 0;
+  for (long long v : w) c.f64x_walked += v;
+  info[0] = (int32_t)hst[1];
+  info[1] = max_steps == 0 ? 0 : (int32_t)hst[2];
+  c.last_k = k;
+  c.have_labels = max_steps > 0 || c.have_labels;
+  c.last_fallback = c.n;
+}
+
 void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* counts) {
   check_k(c, k);
   if (c.mode != CDR_MODE_F64) CDR_FAIL(CDR_ERR_STATE, "lloyd_step_f64: points are not F64");
@@ -1561,6 +1678,15 @@ int cdr_lloyd_step_f64(cdr_ctx* h, const double* C, int32_t k, double* sums,
   if (!h || !C || !sums || !counts) CDR_FAIL(CDR_ERR_ARG, "null argument");
   HIP_CHECK(hipSetDevice(h->c.device));
   lloyd_step_f64(h->c, C, k, sums, counts);
+  CDR_CATCH
+}
+
+int cdr_lloyd_f64_run(cdr_ctx* h, const double* C, int32_t k, int32_t max_steps, double tol,
+                      double* C_out, double* means_out, int64_t* counts_out, int32_t* info) {
+  CDR_TRY
+  if (!h || !C || !C_out || !means_out || !counts_out || !info) CDR_FAIL(CDR_ERR_ARG, "null argument");
+  HIP_CHECK(hipSetDevice(h->c.device));
+  lloyd_run_f64(h->c, C, k, max_steps, tol, C_out, means_out, counts_out, info);
   CDR_CATCH
 }
 

@@ -36,7 +36,7 @@ import warnings
 
 import numpy as np
 
-from _cdr import MODE_F32X, Context, NanProbabilities, default_context, host_seq_sum
+from _cdr import MODE_F32X, MODE_F64, Context, NanProbabilities, default_context, host_seq_sum
 
 __all__ = ["kmeans_plusplus_init", "kmeans"]
 
@@ -145,6 +145,31 @@ def _cluster_means(ctx: Context, C: np.ndarray, mode: int, scale_bits: int):
     return means, counts
 
 
+def _f64_device_loop(ctx: Context, X: np.ndarray, centroids: np.ndarray, max_iter: int,
+                     tol: float) -> np.ndarray:
+    """max_iter Lloyd steps (fewer on convergence) of F64 points on the
+    device; a step the device hands back (an empty cluster, or a shift too
+    close to tol) is finished here exactly as the reference does (:37-48)."""
+    n_samples = X.shape[0]
+    done = 0
+    while done < max_iter:
+        C, steps, reason, means, counts = ctx.lloyd_f64_run(centroids, max_iter - done, tol)
+        centroids, done = C, done + steps
+        if reason == ctx.F64_RUN_CONVERGED:
+            break
+        if reason != ctx.F64_RUN_HOST:
+            break  # every step applied
+        new_centroids = np.empty_like(centroids)
+        new_centroids[...] = means
+        for j in np.flatnonzero(counts == 0):  # j order, as the reference draws (:43)
+            new_centroids[j] = X[np.random.randint(0, n_samples)]
+        shift = np.linalg.norm(new_centroids - centroids)
+        centroids, done = new_centroids, done + 1
+        if shift < tol:
+            break
+    return centroids
+
+
 def kmeans(X, k, number_of_files=100, tol=1e-4, random_state=None, *,
            max_iter=None, context: Context | None = None):
     """Lloyd's k-means after k-means++ seeding (reference :24-50).
@@ -195,6 +220,13 @@ def kmeans(X, k, number_of_files=100, tol=1e-4, random_state=None, *,
                                      lambda g: X[g], n_samples, dtype=centroids.dtype)
         ctx.last_inertia = st["inertia"]
         return centroids, ctx.labels()
+
+    if (mode == MODE_F64 and centroids.dtype == np.float64 and len(iters) > 0
+            and 2 <= centroids.shape[1] <= 16 and k <= 64):
+        # F64: the steps resident on the device (exact assignment, exact
+        # sequential sums, means and shift), the host only for empty clusters
+        # and near-tol shifts (cdr_lloyd_f64_run)
+        return _f64_device_loop(ctx, X, centroids, len(iters), tol), ctx.labels()
 
     ran = False
     for _ in iters:

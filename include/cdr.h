@@ -201,6 +201,19 @@ int cdr_lloyd_step(cdr_ctx* ctx, const double* C, int32_t k, int64_t* out,
  * order exactly like X[labels == j].mean(axis=0)'s sum; counts (k).        */
 int cdr_lloyd_step_f64(cdr_ctx* ctx, const double* C, int32_t k, double* sums,
                        int64_t* counts);
+/* F64 mode, 2 <= d <= 16, k <= 64: up to max_steps Lloyd steps resident on
+ * the device (src/kmeans_plusplus.py:31-48; replaces a host loop of
+ * cdr_lloyd_step_f64 + means + shift): each step's exact assignment and
+ * sequential sums, then means = sums / counts and shift = ||means - C|| on
+ * the device.  info[0] = steps applied (C replaced by the means); info[1] =
+ * 0 all max_steps applied, 1 converged (the last applied step had shift <
+ * tol), 2 the next step needs the host (an empty cluster, or a shift too
+ * close to tol to decide): that step is NOT applied, C_out is the centroids
+ * it started from, means_out (k, d) / counts_out (k) are its means and
+ * counts, and the labels on the device are its assignment.  C_out (k, d):
+ * the centroids after the applied steps.  tol <= 0: never converges.      */
+int cdr_lloyd_f64_run(cdr_ctx* ctx, const double* C, int32_t k, int32_t max_steps, double tol,
+                      double* C_out, double* means_out, int64_t* counts_out, int32_t* info);
 /* The reference's float32 runs (X float32 keeps its dtype,
  * src/kmeans_plusplus.py:6, 33-34, 41): float32 norms in NumPy order, argmin
  * of the fp32 norms, sums (k, d) = the SEQUENTIAL float32 sums of each

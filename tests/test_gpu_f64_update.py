@@ -209,3 +209,77 @@ def test_sharded_f64_sums_contexts(ctx, monkeypatch, n, d, k, W, force):
     finally:
         for c in ctxs:
             c.close()
+
+
+def _host_steps(ctx, C, steps):
+    """The host loop of src/kmeans_plusplus.py:33-46 over cdr_lloyd_step_f64
+    (no empty clusters here): C <- sums / counts, `steps` times."""
+    for _ in range(steps):
+        sums, counts = ctx.lloyd_step_f64(C)
+        assert (counts > 0).all()
+        C = sums / counts[:, None].astype(np.float64)
+    return C
+
+
+def test_device_run_matches_host_steps(ctx):
+    """cdr_lloyd_f64_run (the steps resident on the device: means and shift
+    on the device) = the host loop of single steps, bit for bit, labels too;
+    tol <= 0 applies every step."""
+    rng = np.random.default_rng(21)
+    X = _minmax(rng, 300_001, 5)
+    ctx.load_points(X)
+    C0 = X[rng.choice(X.shape[0], 16, replace=False)].copy()
+    C_host = _host_steps(ctx, C0, 7)
+    lab_host = ctx.labels()
+    C_dev, applied, reason, means, counts = ctx.lloyd_f64_run(C0, 7, -1.0)
+    assert (applied, reason) == (7, ctx.F64_RUN_ALL)
+    np.testing.assert_array_equal(C_dev, C_host)
+    np.testing.assert_array_equal(ctx.labels(), lab_host)
+    # the last step's means and counts are kept: its means are the result
+    np.testing.assert_array_equal(means, C_dev)
+    np.testing.assert_array_equal(counts, np.bincount(lab_host, minlength=16))
+    # in two calls (the run resumes from the centroids it returned)
+    C_a, n_a, _, _, _ = ctx.lloyd_f64_run(C0, 3, -1.0)
+    C_b, n_b, _, _, _ = ctx.lloyd_f64_run(C_a, 4, -1.0)
+    assert (n_a, n_b) == (3, 4)
+    np.testing.assert_array_equal(C_b, C_host)
+
+
+def test_device_run_hands_back_empty_cluster(ctx):
+    """A cluster without members stops the run before that step is applied:
+    C_out = the centroids the step started from, means / counts = the step's
+    (counts 0 for the empty one), labels = its assignment (the oracle's)."""
+    rng = np.random.default_rng(22)
+    X = _minmax(rng, 120_000, 4)
+    ctx.load_points(X)
+    C0 = X[rng.choice(X.shape[0], 6, replace=False)].copy()
+    C0[2] = 40.0  # far from every point: no members
+    C_dev, applied, reason, means, counts = ctx.lloyd_f64_run(C0, 5, -1.0)
+    assert (applied, reason) == (0, ctx.F64_RUN_HOST)
+    np.testing.assert_array_equal(C_dev, C0)
+    lab = ko.assign(X, C0)
+    np.testing.assert_array_equal(ctx.labels(), lab)
+    np.testing.assert_array_equal(counts, np.bincount(lab, minlength=6))
+    assert counts[2] == 0
+    sums, _ = ctx.lloyd_step_f64(C0)
+    nz = counts > 0
+    np.testing.assert_array_equal(means[nz], sums[nz] / counts[nz, None])
+
+
+@pytest.mark.parametrize("n,d,k,seed", [(200_000, 5, 6, 31), (150_000, 3, 12, 32)])
+def test_kmeans_device_run_vs_oracle(ctx, n, d, k, seed):
+    """kmeans() on F64 points runs the device loop to convergence (tol 1e-4,
+    decided on the device, near-tol shifts by the host) and matches the
+    oracle's reference loop bit for bit: centroids, labels.  Three far points
+    give D^2 seeding a small cluster to pick."""
+    import kmeans_plusplus as kp
+
+    rng = np.random.default_rng(seed)
+    X = _minmax(rng, n, d)
+    X[:3] = 5.0  # three far points: their cluster empties after the first moves
+    np.random.seed(seed)
+    C, labels = kp.kmeans(X, k, random_state=seed, max_iter=40, context=ctx)
+    np.random.seed(seed)
+    C_ref, labels_ref = ko.kmeans(X, k, random_state=seed, max_iter=40)
+    np.testing.assert_array_equal(C, C_ref)
+    np.testing.assert_array_equal(labels, labels_ref)
