@@ -665,6 +665,81 @@ __global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t
   }
 }
 
+// The exact argmin (exact_argmin: the first index of the smallest correctly
+// rounded NumPy-order root) behind an fp32 screen, for k <= kF64ScrK.  With
+// every x_f and c_f zero or within [2^-60, 2^60] (normal fp32 squares), the
+// fp32 value S = fma-chain sum of fl32(fl32(x) - fl32(c))^2 is within
+//   (d + 5.01) 2^-24 sum_f (|x_f| + |c_f|)^2 <= (d + 5.01) 2^-23 (|x|^2 + |c|^2)
+// of the real squared distance (two conversions and a subtraction per term,
+// d fused steps of non-negative terms), plus 2^-126 per step for a result
+// flushed below the normal range.  E = (d + 12) 2^-23 (xx + cc) + d 2^-125
+// (xx, cc: the fp32 squared norms) covers that, the two roundings of S -+ E,
+// the fp64 NumPy sum's own error and a relative gap of 2^-48 beyond it.  So a
+// centroid with S - E > min_i (S_i + E_i) has an fp64 square at least 2^-48
+// above the winner's and a strictly larger rounded root: it can neither win
+// nor tie.  The rest (usually the winner alone) go through exact_argmin's
+// comparison in index order, which gives exact_argmin's answer.  fp64 VALU is
+// a quarter of the fp32 rate on gfx950 and the full pass was issue-bound
+// (PMC: 66 % of wave cycles stalled on issue).
+constexpr int kF64ScrK = 16;
+__device__ __forceinline__ bool f64_screen_ok(double v) {
+  const double a = fabs(v);
+  return v == 0.0 || (a >= 0x1p-60 && a <= 0x1p60);
+}
+template <int D>
+__device__ __forceinline__ int f64_screen_argmin(const double (&xr)[D], const double* cs64,
+                                                 const float* cs32, const float* cn32, int k) {
+  float xs[D];
+  float xx = 0.0f;
+  bool ok = true;
+#pragma unroll
+  for (int f = 0; f < D; ++f) {
+    ok &= f64_screen_ok(xr[f]);
+    xs[f] = (float)xr[f];
+    xx = fmaf(xs[f], xs[f], xx);
+  }
+  if (!ok) return exact_argmin([&](int f) { return xr[f]; }, cs64, k, D);
+  const float kE = (float)(D + 12) * 0x1p-23f, eabs = (float)D * 0x1p-125f;
+  float lo[kF64ScrK];
+  float best = INFINITY;
+#pragma unroll
+  for (int jj = 0; jj < kF64ScrK; ++jj) {
+    lo[jj] = INFINITY;
+    if (jj < k) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int f = 0; f < D; ++f) {
+        const float t = xs[f] - cs32[jj * D + f];
+        acc = fmaf(t, t, acc);
+      }
+      const float e = fmaf(kE, xx + cn32[jj], eabs);
+      lo[jj] = acc - e;
+      best = fminf(best, acc + e);
+    }
+  }
+  unsigned cand = 0;
+#pragma unroll
+  for (int jj = 0; jj < kF64ScrK; ++jj)
+    if (lo[jj] <= best) cand |= 1u << jj;
+  double Rb = INFINITY, rb = INFINITY;
+  int jb = 0;
+  while (cand) {
+    const int jj = __builtin_ctz(cand);
+    cand &= cand - 1u;
+    const double* cj = cs64 + jj * D;
+    const double R = np_sqdist([&](int f) { return xr[f]; }, [&](int f) { return cj[f]; }, D);
+    if (R < Rb) {
+      const double r = sqrt(R);
+      if (r < rb) {
+        rb = r;
+        Rb = R;
+        jb = jj;
+      }
+    }
+  }
+  return jb;
+}
+
 // F64 mode, the assignment fused with the block pass (one workgroup per
 // block of kFB rows): labels (exact_argmin, src/kmeans_plusplus.py:33-34),
 // the block's approximate sums and exact counts in f64_blocksum's layout,
@@ -705,11 +780,35 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
   if (threadIdx.x < kFMaxK) cc[threadIdx.x] = 0u;
   const int64_t row = b * kFB + threadIdx.x;
   double xr[D];
-  int j = -1;
   if (row < n) {
 #pragma unroll
     for (int f = 0; f < D; ++f) xr[f] = X[xidx(f, row, n_pad)];
-    j = exact_argmin([&](int f) { return xr[f]; }, C, k, D);
+  }
+  // the centroids in LDS: fp64 for the exact pass, fp32 and their fp32
+  // squared norms for the screen (k <= 16, every value 0 or within
+  // [2^-60, 2^60]: see f64_screen_argmin)
+  __shared__ double cs64[kF64ScrK * D];
+  __shared__ float cs32[kF64ScrK * D];
+  __shared__ float cn32[kF64ScrK];
+  bool cbad = k > kF64ScrK;
+  for (int i = threadIdx.x; i < k * D && !cbad; i += kFB) {
+    const double v = C[i];
+    cs64[i] = v;
+    cs32[i] = (float)v;
+    cbad |= !f64_screen_ok(v);
+  }
+  const bool scr = !__syncthreads_or(cbad);  // (block-uniform)
+  if (scr && threadIdx.x < k) {
+    float sq = 0.0f;
+#pragma unroll
+    for (int f = 0; f < D; ++f) sq = fmaf(cs32[threadIdx.x * D + f], cs32[threadIdx.x * D + f], sq);
+    cn32[threadIdx.x] = sq;
+  }
+  __syncthreads();
+  int j = -1;
+  if (row < n) {
+    j = scr ? f64_screen_argmin<D>(xr, cs64, cs32, cn32, k)
+            : exact_argmin([&](int f) { return xr[f]; }, C, k, D);
     labels[row] = j;
   }
   if constexpr (XF) {

@@ -283,3 +283,23 @@ def test_kmeans_device_run_vs_oracle(ctx, n, d, k, seed):
     C_ref, labels_ref = ko.kmeans(X, k, random_state=seed, max_iter=40)
     np.testing.assert_array_equal(C, C_ref)
     np.testing.assert_array_equal(labels, labels_ref)
+
+
+def test_assign_screen_ties_duplicates_and_ranges(ctx, monkeypatch):
+    """The fp32 screen in front of the exact argmin (k <= 16,
+    f64_screen_argmin): grid points exactly between two centroids (the first
+    index wins), a duplicated centroid (never chosen), points with a value
+    below 2^-60 or above 2^60 (the exact pass alone) - labels equal the
+    oracle's, sums NumPy's, and the same at k = 17 (no screen)."""
+    rng = np.random.default_rng(23)
+    X = _minmax(rng, 60_000, 4)
+    X[:2000] = np.round(X[:2000] * 4) / 4
+    X[2000:2100, 0] = 1e-30
+    X[2100:2200, 1] = 3e20
+    base = np.array([[0.25, 0.25, 0.25, 0.25], [0.75, 0.25, 0.25, 0.25], [0.25, 0.75, 0.25, 0.25],
+                     [0.25, 0.25, 0.25, 0.25], [0.5, 0.5, 0.5, 0.5], [0.25, 0.25, 0.75, 0.75]])
+    C = np.vstack([base, X[rng.choice(np.arange(2200, 60_000), 10, replace=False)]])
+    assert C.shape[0] == 16
+    _check_step(ctx, X, C, monkeypatch)
+    C17 = np.vstack([C, X[2200:2201]])
+    _check_step(ctx, X, C17, monkeypatch)
