@@ -682,13 +682,21 @@ __global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t
 // a quarter of the fp32 rate on gfx950 and the full pass was issue-bound
 // (PMC: 66 % of wave cycles stalled on issue).
 constexpr int kF64ScrK = 16;
+// a centroid's fp32 row in LDS: its d values, then its squared norm, padded
+// to whole 16-byte reads
+template <int D>
+struct F64ScrRow {
+  static constexpr int P = (D + 1 + 3) & ~3;
+};
 __device__ __forceinline__ bool f64_screen_ok(double v) {
   const double a = fabs(v);
   return v == 0.0 || (a >= 0x1p-60 && a <= 0x1p60);
 }
 template <int D>
 __device__ __forceinline__ int f64_screen_argmin(const double (&xr)[D], const double* cs64,
-                                                 const float* cs32, const float* cn32, int k) {
+                                                 const float* cs32, int k) {
+  constexpr int DP = F64ScrRow<D>::P;
+  typedef float f4v __attribute__((ext_vector_type(4)));
   float xs[D];
   float xx = 0.0f;
   bool ok = true;
@@ -706,13 +714,16 @@ __device__ __forceinline__ int f64_screen_argmin(const double (&xr)[D], const do
   for (int jj = 0; jj < kF64ScrK; ++jj) {
     lo[jj] = INFINITY;
     if (jj < k) {
+      f4v cr[DP / 4];
+#pragma unroll
+      for (int q = 0; q < DP / 4; ++q) cr[q] = reinterpret_cast<const f4v*>(cs32 + jj * DP)[q];
       float acc = 0.0f;
 #pragma unroll
       for (int f = 0; f < D; ++f) {
-        const float t = xs[f] - cs32[jj * D + f];
+        const float t = xs[f] - cr[f >> 2][f & 3];
         acc = fmaf(t, t, acc);
       }
-      const float e = fmaf(kE, xx + cn32[jj], eabs);
+      const float e = fmaf(kE, xx + cr[D >> 2][D & 3], eabs);
       lo[jj] = acc - e;
       best = fminf(best, acc + e);
     }
@@ -787,27 +798,27 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
   // the centroids in LDS: fp64 for the exact pass, fp32 and their fp32
   // squared norms for the screen (k <= 16, every value 0 or within
   // [2^-60, 2^60]: see f64_screen_argmin)
+  constexpr int DP = F64ScrRow<D>::P;
   __shared__ double cs64[kF64ScrK * D];
-  __shared__ float cs32[kF64ScrK * D];
-  __shared__ float cn32[kF64ScrK];
+  __shared__ __attribute__((aligned(16))) float cs32[kF64ScrK * DP];
   bool cbad = k > kF64ScrK;
   for (int i = threadIdx.x; i < k * D && !cbad; i += kFB) {
     const double v = C[i];
     cs64[i] = v;
-    cs32[i] = (float)v;
+    cs32[(i / D) * DP + i % D] = (float)v;
     cbad |= !f64_screen_ok(v);
   }
   const bool scr = !__syncthreads_or(cbad);  // (block-uniform)
   if (scr && threadIdx.x < k) {
     float sq = 0.0f;
 #pragma unroll
-    for (int f = 0; f < D; ++f) sq = fmaf(cs32[threadIdx.x * D + f], cs32[threadIdx.x * D + f], sq);
-    cn32[threadIdx.x] = sq;
+    for (int f = 0; f < D; ++f) sq = fmaf(cs32[threadIdx.x * DP + f], cs32[threadIdx.x * DP + f], sq);
+    cs32[threadIdx.x * DP + D] = sq;
   }
   __syncthreads();
   int j = -1;
   if (row < n) {
-    j = scr ? f64_screen_argmin<D>(xr, cs64, cs32, cn32, k)
+    j = scr ? f64_screen_argmin<D>(xr, cs64, cs32, k)
             : exact_argmin([&](int f) { return xr[f]; }, C, k, D);
     labels[row] = j;
   }
