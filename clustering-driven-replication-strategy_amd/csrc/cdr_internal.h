@@ -156,6 +156,7 @@ struct Ctx {
   // f64_step_fused: the binade predictions of the last F64 step (two buffers:
   // the one the current transfers use, the next step's), valid for (k, blocks)
   DevBuf f64x_E2;
+  DevBuf f64x_GC;  // f64_step_fused: per (cluster, group of 64 blocks) member counts
   DevBuf f64x_ord;  // f64_step_fused: each block's rows in cluster order (uint8 offsets)
   DevBuf f64s_off;  // sharded F64 sums: earlier shards' approximate totals, end binades
   int32_t f64s_k = 0, f64s_nranks = 0, f64s_rank = 0;  // cdr_f64s_begin's step

@@ -163,10 +163,13 @@ __device__ __forceinline__ int binade_e(double P) {
   frexp(P, &ex);  // P in [2^(ex-1), 2^ex)
   return ex - 1;
 }
+// (GC: the clusters' member counts per group as well, from the waves of
+// feature 0 - f64_predict_b adds them up; null: not wanted)
 __global__ __launch_bounds__(256) void f64_predict_a(const double* __restrict__ A,
                                                      const unsigned* __restrict__ cnt,
                                                      int64_t nb, int d, int k, int64_t ng,
-                                                     double* __restrict__ GS) {
+                                                     double* __restrict__ GS,
+                                                     unsigned long long* __restrict__ GC) {
   const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (w >= (int64_t)k * d * ng) return;
@@ -174,15 +177,33 @@ __global__ __launch_bounds__(256) void f64_predict_a(const double* __restrict__ 
   const int64_t g = w % ng;
   const int j = t / d;
   const int64_t b = g * 64 + lane;
-  double v = (b < nb && cnt[(int64_t)j * nb + b]) ? A[(int64_t)t * nb + b] : 0.0;
+  const unsigned cb = b < nb ? cnt[(int64_t)j * nb + b] : 0u;
+  double v = cb ? A[(int64_t)t * nb + b] : 0.0;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   if (lane == 0) GS[w] = v;
+  if (GC && t % d == 0) {  // (wave-uniform)
+    unsigned long long s = cb;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) GC[(int64_t)j * ng + g] = s;
+  }
 }
+// (GC non-null: the waves of feature 0 also write cluster t / d's member
+// count, the sum of its group counts - the fused step's counts)
 __global__ __launch_bounds__(256) void f64_predict_b(double* __restrict__ GS, int kd,
-                                                     int64_t ng, const double* __restrict__ off) {
+                                                     int64_t ng, const double* __restrict__ off,
+                                                     const unsigned long long* __restrict__ GC,
+                                                     int d,
+                                                     unsigned long long* __restrict__ counts) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= kd) return;
+  if (GC && t % d == 0) {  // (wave-uniform)
+    const unsigned long long* gc = GC + (int64_t)(t / d) * ng;
+    unsigned long long s = 0;
+    for (int64_t g = lane; g < ng; g += 64) s += gc[g];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) counts[t / d] = s;
+  }
   double* gs = GS + (int64_t)t * ng;
   // a shard of sharded rows starts from the earlier shards' approximate sum
   double carry = off ? off[t] : 0.0;
@@ -1010,25 +1031,6 @@ __global__ __launch_bounds__(256) void f64_transfer_sorted(const S* __restrict__
   }
 }
 
-// counts[j] += the sum over a slice of blocks of cnt[j][b] (grid (k,
-// slices); counts zeroed first)
-__global__ __launch_bounds__(256) void count_total_kernel(const unsigned* __restrict__ cnt,
-                                                          int64_t nb,
-                                                          unsigned long long* __restrict__ counts) {
-  __shared__ unsigned long long red[4];
-  const int j = blockIdx.x;
-  unsigned long long s = 0;
-  for (int64_t b = (int64_t)blockIdx.y * 256 + threadIdx.x; b < nb; b += (int64_t)gridDim.y * 256)
-    s += cnt[(int64_t)j * nb + b];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long v = (red[0] + red[1]) + (red[2] + red[3]);
-    if (v) atomicAdd(&counts[j], v);
-  }
-}
-
 }  // namespace
 
 // sums (k, d) on the device, exact sequential row-order fp64 sums; returns
@@ -1047,7 +1049,8 @@ struct F64Shard {
 template <typename TA, typename S>
 static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
                              const int* Ewalk, bool have_T, const unsigned char* ordr = nullptr,
-                             const F64Shard& sh = F64Shard());
+                             const F64Shard& sh = F64Shard(),
+                             unsigned long long* d_counts = nullptr);
 
 // TA: the summed (arithmetic) type; S: the storage type of X.  pre: the
 // block sums and counts (f64x_A, f64x_cnt) were already written by the
@@ -1078,17 +1081,22 @@ static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums, bool pre = 
 template <typename TA, typename S>
 static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
                              const int* Ewalk, bool have_T, const unsigned char* ordr,
-                             const F64Shard& sh) {
+                             const F64Shard& sh, unsigned long long* d_counts) {
   const int d = c.d;
   const int64_t n = c.n, nb = ceil_div(n, kFB);
   const size_t kd = (size_t)k * d;
   const int64_t ng = ceil_div(nb, (int64_t)64);
   c.f64x_GS.ensure(sizeof(double) * ng * kd);
   const dim3 gwaves((unsigned)ceil_div((int64_t)kd * ng, (int64_t)4));
+  unsigned long long* GC = nullptr;
+  if (d_counts) {
+    c.f64x_GC.ensure(sizeof(unsigned long long) * ng * k);
+    GC = c.f64x_GC.as<unsigned long long>();
+  }
   hipLaunchKernelGGL(f64_predict_a, gwaves, dim3(256), 0, c.stream, c.f64x_A.as<double>(),
-                     c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>());
+                     c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>(), GC);
   hipLaunchKernelGGL(f64_predict_b, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
-                     c.f64x_GS.as<double>(), (int)kd, ng, sh.off);
+                     c.f64x_GS.as<double>(), (int)kd, ng, sh.off, GC, d, d_counts);
   hipLaunchKernelGGL(f64_predict_c, gwaves, dim3(256), 0, c.stream, c.f64x_A.as<double>(),
                      c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>(), Enew);
   HIP_CHECK(hipGetLastError());
@@ -1195,16 +1203,12 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
                      ordr, gate);
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
-  HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(unsigned long long) * k, c.stream));
-  hipLaunchKernelGGL(count_total_kernel,
-                     dim3(k, (unsigned)std::min<int64_t>(64, ceil_div(nb, (int64_t)256))),
-                     dim3(256), 0, c.stream, c.f64x_cnt.as<unsigned>(), nb, d_counts);
-  HIP_CHECK(hipGetLastError());
+  // (the counts: written by f64_predict_b from f64_predict_a's group counts)
   // with transfers formed under Ecur: predict into the other buffer, walk
   // under Ecur; else predict into Ecur and form the transfers under it
   int* Enew = xf ? Eoth : Ecur;
   sums_after_block<double, double>(c, c.x64.as<double>(), k, d_sums, Enew, xf ? Ecur : Enew, xf,
-                                   ordr);
+                                   ordr, F64Shard(), d_counts);
   static const bool xcheck = std::getenv("CDR_F64_XCHECK") != nullptr;
   if (xcheck && xf) {  // (diagnostics) the fused transfers vs f64_transfer under the same E
     DevBuf t2;

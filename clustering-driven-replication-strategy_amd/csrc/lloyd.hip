@@ -1322,7 +1322,7 @@ void lloyd_step_f32x(Ctx& c, const double* C, int32_t k, int64_t* out, bool out_
 // of any other order's, so the margin decides both sides rigorously.
 constexpr int kF64RunThreads = 1024;
 __global__ __launch_bounds__(kF64RunThreads) void f64_run_update(
-    const double* __restrict__ sums, const unsigned long long* __restrict__ counts,
+    const double* __restrict__ sums, unsigned long long* __restrict__ counts,
     double* __restrict__ C, double* __restrict__ keep, int k, int d, double tol,
     long long* __restrict__ st) {
   __shared__ double red[kF64RunThreads / 64];
@@ -1344,6 +1344,7 @@ __global__ __launch_bounds__(kF64RunThreads) void f64_run_update(
     keep[t] = m;
     if (t % d == 0) reinterpret_cast<long long*>(keep + kd)[t / d] = (long long)cnt;
   }
+
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
   if ((t & 63) == 0) red[t >> 6] = sq;
@@ -1402,7 +1403,7 @@ void lloyd_run_f64(Ctx& c, const double* C, int32_t k, int32_t max_steps, double
       CDR_FAIL(CDR_ERR_UNSUPPORTED, "device F64 run: shape not covered");
     hipLaunchKernelGGL(f64_run_update, dim3(1), dim3(kF64RunThreads), 0, c.stream,
                        c.f64_sums.as<double>(),
-                       reinterpret_cast<const unsigned long long*>(c.f64_counts.as<long long>()),
+                       reinterpret_cast<unsigned long long*>(c.f64_counts.as<long long>()),
                        c.cent64.as<double>(), c.f64r_keep.as<double>(), k, d, tol, st);
     HIP_CHECK(hipGetLastError());
     if (prof) prof_mark(c, 2);
