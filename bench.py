@@ -26,7 +26,8 @@ timed region.  `frac` is an HBM fraction of the bytes that kernel moves: the
 PMC-measured HBM bytes per launch (`traffic`, profiles/pmc_traffic.json, when
 a rocprof pass of this kernel at this size is committed) or else the bytes it
 must move by construction (`kernel_bytes_per_launch`: the bounded screen's
-4-byte bound word per point + the hi row of each point whose bound failed),
+2-byte bound word per point (screen32bs16) + the fp32 row of each point whose
+bound failed),
 divided by its mean launch time and 8 TB/s.  The SURVEY.md 8(d) contract
 figure, n_local * (4*d + 4) bytes (read the fp32 point, write its int32 label),
 over the same time is `effective_achieved` / `effective_frac` — above 1,
@@ -91,7 +92,7 @@ def cpu_baseline(d: int, k: int, seed: int, rows: int = 1_000_000, iters: int = 
             "seconds": dt}
 
 
-def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
+def features_bench(args, world: int, rank: int, dist, device, json_fd) -> dict:
     """Config 4: the compute_features group-by (src/compute_features.py:31-54)
     over a device-resident, time-ordered log from the device access simulator
     (csrc/simulate.hip, the model of src/access_simulator.py).  A step = one
@@ -107,9 +108,9 @@ def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> N
         nf = max(1, int(args.n_total / EVENTS_PER_FILE))
     ctx = _cdr.Context(int(os.environ.get("LOCAL_RANK", "0")))
     if dist is not None:
-        import torch
+        from cdr_dist import bind_stream
 
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        bind_stream(ctx, device)
     ne = ctx.features_simulate(nf, duration, nclients, seed=args.seed, file_begin=rank * nf)
 
     def step():
@@ -180,11 +181,12 @@ def features_bench(args, world: int, rank: int, dist, device, json_fd: int) -> N
                                          "NumPy restatement of the group-by (oracle/"
                                          "features_oracle.counts_from_arrays), 1 thread",
                                "seconds": dt}
-    if rank == 0:
+    if rank == 0 and json_fd is not None:
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     ctx.close()
-    if dist is not None:
+    if dist is not None and json_fd is not None:
         dist.destroy_process_group()
+    return out
 
 
 INGEST_CFG = (20_000_000, 2_000_000,
@@ -340,7 +342,7 @@ def f64_data(n: int, d: int, k: int, seed: int):
     return (X - mn) / (mx - mn)
 
 
-def f64_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
+def f64_bench(args, world: int, rank: int, dist, device, json_fd) -> dict:
     """F64 mode (`main.py`'s real data path): exact fp64
     NumPy-order assignment of every point + exact sequential-order cluster
     sums (csrc/f64sum.hip), centroids = sums / counts on the host as
@@ -364,10 +366,10 @@ def f64_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
     if dist is not None and world > 1:
         import torch
 
-        from cdr_dist import Comm, f64_sharded_sums, shard_rows
+        from cdr_dist import Comm, bind_stream, f64_sharded_sums, shard_rows
 
         comm = Comm(dist, device)
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        bind_stream(ctx, device)
         begin, n_local = shard_rows(n_total, world, rank)
         ctx.load_points(X[begin:begin + n_local])
     else:
@@ -463,9 +465,10 @@ def f64_bench(args, world: int, rank: int, dist, device, json_fd: int) -> None:
                                          f"F64 data, d={d}, k={k}; NumPy oracle restatement of "
                                          "src/kmeans_plusplus.py:33-43, 1 thread",
                                "seconds": dt}
-    if rank == 0:
+    if rank == 0 and json_fd is not None:
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     ctx.close()
+    return out
 
 
 def pmc_traffic(config: str, n_local: int, kname: str | None = None, steps=None):
@@ -556,6 +559,8 @@ def main() -> None:
                     help="strong (default): the config's n points in total over the N GPUs; "
                          "weak: n points per GPU (N x n in total)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="config 3 at N = 1: skip the other configs' legs (secondary)")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
     ap.add_argument("--rccl", action="store_true",
                     help="use torch.distributed (RCCL) even at WORLD_SIZE=1 (path testing)")
@@ -587,11 +592,6 @@ def main() -> None:
         dist = tdist
         device = torch.device("cuda", local_rank)
 
-    import numpy as np
-
-    import _cdr
-    from cdr_dist import Comm, DeviceLloyd, row_fetcher, seed_sharded, shard_rows, unify_points
-
     if args.config == "4":
         features_bench(args, world, rank, dist, device, json_fd)
         return
@@ -603,6 +603,56 @@ def main() -> None:
         if dist is not None:
             dist.destroy_process_group()
         return
+    out = lloyd_bench(args, world, rank, local_rank, dist, device)
+    if world == 1 and args.config == "3" and not args.no_secondary and not args.n_total:
+        out["secondary"] = secondary_configs(args, rank, local_rank)
+    if rank == 0:
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def secondary_configs(args, rank: int, local_rank: int) -> dict:
+    """The other BASELINE configs, measured in the same default run (N = 1
+    only) after the headline's context is closed: config 2 (10M x 8, k = 16,
+    50 Lloyd iterations), config 4 (its whole 1B-event workload on this one
+    GPU), config 5 (50M x 64, k = 1024 + replica scoring) and the F64 leg
+    (src/main.py's min-max-normalised data).  Each entry is that leg's own
+    bench line (roofline included; no CPU baseline - the committed builder
+    lines under profiles/ carry those)."""
+    import argparse as _ap
+
+    legs = {}
+    plan = [("2", {"steps": 50, "warmup": 3}, None),
+            ("4", {"steps": 10, "warmup": 2, "n_total": 1_000_000_000}, features_bench),
+            ("5", {"steps": 10, "warmup": 2}, None),
+            ("f64", {"steps": 20, "warmup": 2}, f64_bench)]
+    for name, over, fn in plan:
+        a2 = _ap.Namespace(**vars(args))
+        a2.config, a2.n_total, a2.no_cpu_baseline = name, 0, True
+        for key, v in over.items():
+            setattr(a2, key, v)
+        t0 = time.perf_counter()
+        try:
+            if fn is None:
+                o = lloyd_bench(a2, 1, rank, local_rank, None, None)
+            else:
+                o = fn(a2, 1, rank, None, None, None)
+        except Exception as e:  # noqa: BLE001 - recorded, the headline line still prints
+            o = {"error": f"{type(e).__name__}: {e}"}
+        o["leg_wall_s"] = time.perf_counter() - t0
+        legs[name] = o
+    return legs
+
+
+def lloyd_bench(args, world: int, rank: int, local_rank: int, dist, device) -> dict:
+    """Lloyd leg (configs 2, 3, 5): generation, sharded seeding, warmup steps,
+    then exactly args.steps timed device-loop steps; returns the bench dict."""
+    import numpy as np
+
+    import _cdr
+    from cdr_dist import Comm, DeviceLloyd, row_fetcher, seed_sharded, shard_rows, unify_points
+
     n_cfg, d, k, desc = CONFIGS[args.config]
     if args.n_total:
         n_cfg = args.n_total
@@ -614,9 +664,9 @@ def main() -> None:
     comm = Comm(dist, device)
     ctx = _cdr.Context(local_rank)
     if dist is not None:
-        import torch
+        from cdr_dist import bind_stream
 
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        bind_stream(ctx, device)  # one stream: fenced collectives need no host sync
     g0 = time.perf_counter()
     ctx.generate_points(n_total, begin, n_local, d, k, args.seed)
     unify_points(ctx, comm, n_total)  # one scale / screen transform on every rank
@@ -748,8 +798,9 @@ def main() -> None:
                                   f"k x (d+1) int64 per step" + (
                                       " (ncclAllReduce enqueued from libcdr between the "
                                       "step's kernels)" if native else " (none at 1 GPU)"),
-                   "screen": "exact drift-bound pruning (Hamerly bounds: a 4-byte bound word per "
-                             "point, coordinates re-read only where the bound fails), labels "
+                   "screen": "exact drift-bound pruning (Hamerly bounds: a "
+                             + ("2-byte" if kname.startswith("screen32bs16") else "4-byte")
+                             + " bound word per point, coordinates re-read only where the bound fails), labels "
                              "bit-identical; re-read points decided by a certified fp16 hi/lo "
                              "split MFMA screen + exact fp64 fallback; int64 fixed-point sums "
                              "(results bit-identical to fp64 NumPy)" if kname.startswith("screen32b")
@@ -778,13 +829,10 @@ def main() -> None:
     }
     if scoring_ms is not None:
         out["replica_scoring_ms"] = scoring_ms
+    ctx.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(d, k, args.seed)
-    if rank == 0:
-        os.write(json_fd, (json.dumps(out) + "\n").encode())
-    ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":

@@ -47,6 +47,22 @@ def shard_rows(n_total: int, world: int, rank: int) -> tuple[int, int]:
     return begin, end - begin
 
 
+def bind_stream(ctx, device):
+    """Put ctx and torch on ONE HIP stream, so Comm.fenced needs no host
+    synchronisation around the collectives on the context's buffers.  The
+    legacy default stream's handle is 0, which cdr_set_stream reads as "the
+    context's own stream" (every fenced collective then paid two
+    host syncs); in that case a torch stream is created and made current."""
+    import torch
+
+    cur = torch.cuda.current_stream(device)
+    if not cur.cuda_stream:
+        cur = torch.cuda.Stream(device)
+        torch.cuda.set_stream(cur)
+    ctx.set_stream(cur.cuda_stream)
+    return cur
+
+
 class Comm:
     """Thin collective layer over torch.distributed (or a single process)."""
 
@@ -336,6 +352,11 @@ def row_fetcher(ctx, comm: Comm, row_begin: int, d: int):
     return row
 
 
+def _is_device_context(ctx) -> bool:
+    """ctx is libcdr's GPU context (not a host-side model of one)."""
+    return type(ctx).__module__ == "_cdr" and type(ctx).__name__ == "Context"
+
+
 def _owner_of(offsets: np.ndarray, gidx: int) -> int:
     return int(np.searchsorted(offsets, gidx, side="right") - 1)
 
@@ -438,11 +459,9 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
     if host_seq_sum is None:
         from _cdr import host_seq_sum
     ensure_unified(ctx, comm, n_total)
-    d = ctx.info()["d"]
     offsets = np.array([b for b in comm.allgather(np.array([row_begin], dtype=np.int64))],
                        dtype=np.int64).ravel()
     rng = np.random.default_rng(random_state)
-    C = np.empty((k, d), dtype=np.float64)
     first = int(rng.integers(0, n_total))
     # rng.choice draws one uniform per step (:19): all k - 1 taken up front
     u = rng.random(k - 1) if k > 1 else np.zeros(0)
@@ -461,6 +480,18 @@ def seed_sharded(ctx, comm: Comm, row_begin: int, n_total: int, k: int, random_s
         if status == 0:
             return cents
         comm.seed_fallbacks = getattr(comm, "seed_fallbacks", 0) + 1
+    return seed_host_protocol(ctx, comm, offsets, n_total, first, k, u, host_seq_sum)
+
+
+def seed_host_protocol(ctx, comm: Comm, offsets, n_total: int, first: int, k: int, u,
+                       host_seq_sum) -> np.ndarray:
+    """The sharded seeding steps (:13-20) with the host in every step: the
+    block sums all-gathered and added left to right, the cumsum programs
+    composed on every rank (shard_scan), the hits all-gathered, the picked row
+    broadcast by its owner.  Runs when the device protocol cannot (its layout,
+    or status 1 seen by every rank); collective."""
+    d = ctx.info()["d"]
+    C = np.empty((k, d), dtype=np.float64)
     owner = _owner_of(offsets, first)
     C[0] = _fetch_row(ctx, comm, owner, first - int(offsets[owner]), d)
     if k > 1:
@@ -630,7 +661,16 @@ def f64_sharded_sums(ctx, comm: Comm, C: np.ndarray):
         comm.f64_chains = getattr(comm, "f64_chains", 0) + 1
         chain, hchain = comm.buffer(16 * kd)
         if comm.device is not None:
+            import torch
+
             chain.zero_()
+            # the zeroing runs on torch's current stream; rank 0's f64s_chain
+            # reads chain[0, 2kd) as its exact entry on the context's stream
+            # (without this fence it could walk from the
+            # uninitialised buffer)
+            if getattr(ctx, "stream_handle", lambda: None)() != \
+                    torch.cuda.current_stream(comm.device).cuda_stream:
+                torch.cuda.current_stream(comm.device).synchronize()
         else:
             chain[:] = 0
         for r in range(comm.world):
@@ -662,6 +702,13 @@ class ShardedLloyd:
         self.d, self.S = info["d"], info["scale_bits"]
         self.f64 = info["mode"] == 2
         self._dev_buf = None
+        if self.f64 and comm.dist and comm.device is None and _is_device_context(ctx):
+            # the F64 programs are all-gathered in device buffers that the
+            # context's kernels read and write; gloo hands host arrays
+            # (this used to fail with an obscure ctypes TypeError)
+            raise NotImplementedError(
+                "sharded F64 Lloyd on a GPU context needs a device communicator "
+                "(torch.distributed with the nccl backend); gloo is not supported")
 
     def partials(self, C: np.ndarray) -> np.ndarray:
         k = C.shape[0]

@@ -481,14 +481,14 @@ def main(argv=None):
         import torch
         import torch.distributed as dist
 
-        from cdr_dist import Comm
+        from cdr_dist import Comm, bind_stream
         from features_dist import sharded_compute_features
 
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
         ctx = Context(local)
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        bind_stream(ctx, torch.device("cuda", local))
         paths, table = sharded_compute_features(args.manifest, args.access_log, ctx,
                                                 Comm(dist, torch.device("cuda", local)))
         if dist.get_rank() == 0:

@@ -308,7 +308,7 @@ struct Ctx {
   // ---- access-log ingest (ingest.hip) ----
   DevBuf ing_log;              // log bytes, zero-padded to a whole tile
   DevBuf ing_blk;              // int64 per tile: record counts, then offsets
-  DevBuf ing_tmp;              // hipcub scan scratch
+  DevBuf ing_tmp;              // int64 per scan part: the tile-count scan's partials (tile_scan_*)
   DevBuf ing_mask;             // uint16 per 16 log bytes: record-terminator mask
   DevBuf ing_ends;             // int64 per record: byte index of its terminator
   DevBuf ing_scalar;           // int64 scratch: totals, error rows, flags

@@ -266,6 +266,27 @@ def test_device_run_hands_back_empty_cluster(ctx):
     np.testing.assert_array_equal(means[nz], sums[nz] / counts[nz, None])
 
 
+def test_device_run_stops_queueing_after_it_stops(ctx):
+    """A run that converges early does not queue the rest of max_steps: the
+    steps go to the device in chunks (4, 8, 16) with the state read between
+    them, so at most one chunk (16 steps) runs after the stop (the
+    dead steps' kernels cost ~0.5 ms each).  Queued steps are counted by the
+    per-step profile."""
+    rng = np.random.default_rng(24)
+    X = _minmax(rng, 200_000, 5)
+    ctx.load_points(X)
+    C0 = X[rng.choice(X.shape[0], 8, replace=False)].copy()
+    ctx.profile_reset(True, every=1)
+    C_dev, applied, reason, _, _ = ctx.lloyd_f64_run(C0, 400, 1e-3)
+    queued = ctx.profile_read()["steps"]
+    ctx.profile_reset(False)
+    assert reason in (ctx.F64_RUN_CONVERGED, ctx.F64_RUN_HOST)
+    assert applied < 200
+    assert applied <= queued <= applied + 1 + 16, (applied, queued)
+    # the stopped run's result is the host loop's
+    np.testing.assert_array_equal(C_dev, _host_steps(ctx, C0, applied))
+
+
 @pytest.mark.parametrize("n,d,k,seed", [(200_000, 5, 6, 31), (150_000, 3, 12, 32)])
 def test_kmeans_device_run_vs_oracle(ctx, n, d, k, seed):
     """kmeans() on F64 points runs the device loop to convergence (tol 1e-4,
@@ -303,3 +324,41 @@ def test_assign_screen_ties_duplicates_and_ranges(ctx, monkeypatch):
     _check_step(ctx, X, C, monkeypatch)
     C17 = np.vstack([C, X[2200:2201]])
     _check_step(ctx, X, C17, monkeypatch)
+
+
+def _gloo_f64_worker(rank, world, port, out_dir):
+    import os
+
+    import torch.distributed as dist
+
+    from _cdr import Context
+    from cdr_dist import Comm, ShardedLloyd
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X = np.load(os.path.join(out_dir, "X.npy"))
+    ctx = Context(0)
+    ctx.load_points(X)
+    msg = "no error"
+    try:
+        ShardedLloyd(ctx, Comm(dist, None), X.shape[0], 0)
+    except NotImplementedError as e:
+        msg = "NotImplementedError: " + str(e)
+    with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as fh:
+        fh.write(msg)
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def test_sharded_f64_on_gloo_raises_clearly(tmp_path):
+    """F64 points on a real GPU context under gloo (host buffers): the
+    sharded F64 sums cannot run there, and ShardedLloyd says so up front
+    instead of failing inside ctypes."""
+    from test_features_dist import _free_port
+
+    mp = pytest.importorskip("torch.multiprocessing")
+    rng = np.random.default_rng(25)
+    np.save(tmp_path / "X.npy", _minmax(rng, 20_000, 4))
+    mp.spawn(_gloo_f64_worker, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    msg = (tmp_path / "r0.txt").read_text()
+    assert msg.startswith("NotImplementedError") and "nccl" in msg, msg

