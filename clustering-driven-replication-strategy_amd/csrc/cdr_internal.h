@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include <stdint.h>
 #include <string>
@@ -86,6 +87,21 @@ __host__ __device__ __forceinline__ int64_t xidx(int64_t f, int64_t i, int64_t n
 }
 __host__ __device__ __forceinline__ int d4_of(int d) { return (d + 3) & ~3; }
 constexpr int kPointGroup = 64;   // points per wave iteration in the screen
+
+// Ablation and A/B switches of the experiments build (-DCDR_EXPERIMENTS,
+// libcdr_exp.so): the product library ignores them and always takes the
+// default path.  The switches the tests use to reach a tested alternative
+// (CDR_BOUNDS, CDR_NO_DELTA, CDR_S32B_SPLIT, CDR_S32BS_SPLIT, CDR_EXACT_ASSIGN,
+// CDR_F64_SERIAL, CDR_F64S_FORCE_CHAIN, CDR_GROUPBY_SORT, CDR_GB_BLOCK,
+// CDR_GB_BALLOT, CDR_GB_PASS3) are read with getenv in both builds.
+inline const char* exp_env(const char* name) {
+#ifdef CDR_EXPERIMENTS
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 struct Ctx {
   int device = 0;
@@ -299,6 +315,7 @@ struct Ctx {
   // hand-written group-by (groupby.hip) scratch and what its last run did
   DevBuf gb_tilepref, gb_chunk, gb_rsum, gb_part, gb_small, gb_res, gb_bbase, gb_p1, gb_p2, gb_hist2,
       gb_list, gb_slots;
+  DevBuf gb_bbase3, gb_t3;  // a third partition pass (large file counts): bucket bases, tile starts
   DevBuf sim_cnt, sim_off, sim_tmp, sim_ms, sim_mbase;  // simulate.hip scratch
   DevBuf x_small, x_buf, x_prim;                        // exchange.hip scratch
   int gb_last_hand = 0, gb_last_L = 0, gb_last_passes = 0, gb_last_pbytes = 0, gb_last_big = 0,

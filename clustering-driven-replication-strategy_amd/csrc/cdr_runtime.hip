@@ -418,7 +418,7 @@ int cdr_create(int device, cdr_ctx** out) {
   }
   h->c.own_stream = true;
 #ifdef CDR_EXPERIMENTS
-  if (const char* ab = getenv("CDR_SCREEN_ABLATE")) h->c.screen_ablate = atoi(ab);
+  if (const char* ab = exp_env("CDR_SCREEN_ABLATE")) h->c.screen_ablate = atoi(ab);
 #endif
   *out = h;
   CDR_CATCH

@@ -1104,7 +1104,7 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
   const size_t lds = (size_t)nt * k * (8 + 4 + 4 + 4);
   // (CDR_F64_TBLOCK=1: the one-workgroup-per-block transfer; measured slower
   // at 10M x 5, k = 16: 0.25-0.30 ms against f64_transfer's 0.24 ms)
-  static const bool tb_env = std::getenv("CDR_F64_TBLOCK") && std::atoi(std::getenv("CDR_F64_TBLOCK"));
+  static const bool tb_env = exp_env("CDR_F64_TBLOCK") && std::atoi(exp_env("CDR_F64_TBLOCK"));
   if (!have_T && ordr) {
     hipLaunchKernelGGL((f64_transfer_sorted<TA, S>), dim3((unsigned)ceil_div(nb * d, (int64_t)256)),
                        dim3(256), 0, c.stream, X, n, c.n_pad, d, k, nb, c.f64x_cnt.as<unsigned>(),
@@ -1124,7 +1124,7 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
     HIP_CHECK(hipGetLastError());
   }
   c.f64x_G.ensure(sizeof(GXfer) * ng * kd);
-  static const bool prof_on = std::getenv("CDR_F64_PROF") != nullptr;
+  static const bool prof_on = exp_env("CDR_F64_PROF") != nullptr;
   if (prof_on) c.f64x_prof.ensure(sizeof(long long) * 4 * kd);
   hipLaunchKernelGGL(f64_group, dim3(ceil_div((int64_t)kd * ng, (int64_t)4)), dim3(256), 0,
                      c.stream, c.f64x_cnt.as<unsigned>(), Ewalk,
@@ -1175,14 +1175,14 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   // transfers under the previous step's predictions (CDR_F64_CARRY=1): right
   // only near convergence — between early steps 8-25 % of the blocks' binades
   // move and every such block is re-added element by element — so off by default
-  static const bool carry = std::getenv("CDR_F64_CARRY") && std::atoi(std::getenv("CDR_F64_CARRY"));
+  static const bool carry = exp_env("CDR_F64_CARRY") && std::atoi(exp_env("CDR_F64_CARRY"));
   const bool xf = carry && c.f64x_e_ok && c.f64x_e_k == k && c.f64x_e_nb == nb;
   int* Ecur = (c.f64x_e_cur ? c.f64x_E2 : c.f64x_E).as<int>();
   int* Eoth = (c.f64x_e_cur ? c.f64x_E : c.f64x_E2).as<int>();
   // the rows in cluster order per block and f64_transfer_sorted (CDR_F64_SORTED=1;
   // measured slower at 10M x 5, k = 16: 0.43 ms against f64_transfer's 0.24 ms,
   // the order itself +0.04 ms in the assignment)
-  static const bool sorted_env = std::getenv("CDR_F64_SORTED") && std::atoi(std::getenv("CDR_F64_SORTED"));
+  static const bool sorted_env = exp_env("CDR_F64_SORTED") && std::atoi(exp_env("CDR_F64_SORTED"));
   unsigned char* ordr = nullptr;
   if (sorted_env && !xf) {
     c.f64x_ord.ensure((size_t)nb * kFB);
@@ -1209,7 +1209,7 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   int* Enew = xf ? Eoth : Ecur;
   sums_after_block<double, double>(c, c.x64.as<double>(), k, d_sums, Enew, xf ? Ecur : Enew, xf,
                                    ordr, F64Shard(), d_counts);
-  static const bool xcheck = std::getenv("CDR_F64_XCHECK") != nullptr;
+  static const bool xcheck = exp_env("CDR_F64_XCHECK") != nullptr;
   if (xcheck && xf) {  // (diagnostics) the fused transfers vs f64_transfer under the same E
     DevBuf t2;
     t2.ensure(sizeof(Xfer) * nb * kd);
@@ -1493,7 +1493,7 @@ __global__ __launch_bounds__(256) void f64s_compose(const F64Item* __restrict__ 
 }  // namespace
 
 int f64s_cap() {
-  static const int cap = std::getenv("CDR_F64S_CAP") ? std::max(1, std::atoi(std::getenv("CDR_F64S_CAP"))) : 127;
+  static const int cap = exp_env("CDR_F64S_CAP") ? std::max(1, std::atoi(exp_env("CDR_F64S_CAP"))) : 127;
   return cap;
 }
 

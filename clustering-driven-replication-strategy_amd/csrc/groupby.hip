@@ -500,6 +500,77 @@ __global__ __launch_bounds__(kGbThreads) void gb_hist2(const T* __restrict__ in,
   if (threadIdx.x < R2) hist2[t2 * R2 + threadIdx.x] = h[threadIdx.x];
 }
 
+// Pass 3 (large file counts): the R regions of pass 2 (bases bbase[0..R])
+// become the regions pass 3 splits; tstart[r] = the 8192-event tiles before
+// region r (exclusive scan of ceil(size / tile)), tstart[R] and *tot the
+// total.  One workgroup of 1024 threads, each a contiguous run of regions.
+__global__ __launch_bounds__(1024) void gb_tilestart3(const unsigned* __restrict__ bbase, int R,
+                                                      int* __restrict__ tstart,
+                                                      long long* __restrict__ tot) {
+  __shared__ unsigned wsum[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int per = (R + 1023) / 1024, lo = t * per, hi = min(lo + per, R);
+  unsigned s = 0;
+  for (int r0 = lo; r0 < hi; r0 += 16) {  // 17 bases in flight per batch
+    unsigned v[17];
+#pragma unroll
+    for (int j = 0; j < 17; ++j) v[j] = r0 + j <= R ? bbase[r0 + j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (r0 + j < hi) s += (v[j + 1] - v[j] + kGbTile - 1) / kGbTile;
+  }
+  unsigned inc = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  unsigned run = inc - s;
+  for (int i = 0; i < w; ++i) run += wsum[i];
+  for (int r0 = lo; r0 < hi; r0 += 16) {
+    unsigned v[17];
+#pragma unroll
+    for (int j = 0; j < 17; ++j) v[j] = r0 + j <= R ? bbase[r0 + j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (r0 + j < hi) {
+        tstart[r0 + j] = (int)run;
+        run += (v[j + 1] - v[j] + kGbTile - 1) / kGbTile;
+      }
+    }
+  }
+  if (t == 1023) {
+    tstart[R] = (int)run;
+    *tot = run;
+  }
+}
+
+// Pass 3's scan with few bins (R3 <= 16): one thread per region sd (most
+// regions span one or two tiles): running offsets over its tiles per bin,
+// then its bucket bases bbase3[sd * R3 + r].
+constexpr int kGbScan3Max = 16;
+__global__ __launch_bounds__(256) void gb_scan3(unsigned* __restrict__ hist3,
+                                                const int* __restrict__ tstart,
+                                                const unsigned* __restrict__ bbase, int R12, int R3,
+                                                unsigned* __restrict__ bbase3) {
+  const int sd = blockIdx.x * 256 + threadIdx.x;
+  if (sd >= R12) return;
+  const int t0 = tstart[sd], t1 = tstart[sd + 1];
+  unsigned base = bbase[sd];
+  for (int r = 0; r < R3; ++r) {
+    unsigned run = 0;
+    for (int tb = t0; tb < t1; ++tb) {
+      const unsigned v = hist3[(int64_t)tb * R3 + r];
+      hist3[(int64_t)tb * R3 + r] = run;
+      run += v;
+    }
+    bbase3[(int64_t)sd * R3 + r] = base;
+    base += run;
+  }
+  if (sd == R12 - 1) bbase3[(int64_t)R12 * R3] = bbase[R12];
+}
+
 // One workgroup per pass-1 digit sd, thread r = pass-2 digit: running offsets
 // over the digit's tiles, then the bucket bases bbase[sd * R2 + r].
 __global__ __launch_bounds__(kGbMaxBins) void gb_scan2(unsigned* __restrict__ hist2,
@@ -1267,7 +1338,7 @@ int bitlen(unsigned long long v) {  // bits to hold v (0 -> 0)
 }
 
 template <typename T>
-void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, bool dense,
+void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, int B3, bool dense,
             GbPay p, int64_t T1, int64_t* out, const long long* res) {
   const int R1 = 1 << B1, R2 = 1 << B2;
   const int shift1 = fbits - B1;
@@ -1293,7 +1364,7 @@ void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, bo
     bbase = c.gb_bbase.as<unsigned>();
     c.gb_hist2.ensure(sizeof(unsigned) * (size_t)std::max<int64_t>(T2, 1) * R2);
     unsigned* hist2 = c.gb_hist2.as<unsigned>();
-    const int shift2 = p.fshift + L;
+    const int shift2 = p.fshift + L + B3;
     if (T2 > 0)
       hipLaunchKernelGGL(gb_hist2<T>, dim3(T2), dim3(kGbThreads), 0, c.stream, p1, binbase,
                          tile2start, R1, R2, shift2, hist2);
@@ -1308,6 +1379,42 @@ void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, bo
       HIP_CHECK(hipGetLastError());
     }
     pb = c.gb_p2.as<T>();
+  }
+  if (B3 > 0) {
+    // pass 3 within each of the R1 R2 pass-2 regions (the same kernels: its
+    // regions take the place of pass 1's digits); output into p1's buffer
+    const int R12 = R1 * R2, R3 = 1 << B3;
+    const int shift3 = p.fshift + L;
+    c.gb_t3.ensure(sizeof(int) * ((size_t)R12 + 1) + 64);
+    int* tstart3 = c.gb_t3.as<int>();
+    long long* tot3 = reinterpret_cast<long long*>(c.gb_res.as<long long>() + 6);
+    hipLaunchKernelGGL(gb_tilestart3, dim3(1), dim3(1024), 0, c.stream, bbase, R12, tstart3, tot3);
+    HIP_CHECK(hipGetLastError());
+    long long T3 = 0;
+    HIP_CHECK(hipMemcpyAsync(&T3, tot3, sizeof(T3), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    c.gb_hist2.ensure(sizeof(unsigned) * (size_t)std::max<long long>(T3, 1) * R3);
+    unsigned* hist3 = c.gb_hist2.as<unsigned>();
+    c.gb_bbase3.ensure(sizeof(unsigned) * ((size_t)R12 * R3 + 1) + 64);
+    unsigned* bbase3 = c.gb_bbase3.as<unsigned>();
+    if (T3 > 0)
+      hipLaunchKernelGGL(gb_hist2<T>, dim3((unsigned)T3), dim3(kGbThreads), 0, c.stream, pb, bbase,
+                         tstart3, R12, R3, shift3, hist3);
+    if (R3 <= kGbScan3Max)
+      hipLaunchKernelGGL(gb_scan3, dim3((R12 + 255) / 256), dim3(256), 0, c.stream, hist3, tstart3,
+                         bbase, R12, R3, bbase3);
+    else
+      hipLaunchKernelGGL(gb_scan2, dim3(R12), dim3(kGbMaxBins), 0, c.stream, hist3, tstart3, bbase,
+                         R12, R3, bbase3);
+    HIP_CHECK(hipGetLastError());
+    if (T3 > 0) {
+      const int64_t per3 = ceil_div((int64_t)T3, 8);
+      hipLaunchKernelGGL(gb_scatter2<T>, dim3(8 * per3), dim3(kGbThreads), 0, c.stream, pb, bbase,
+                         tstart3, R12, R3, shift3, (int64_t)T3, per3, hist3, bbase3, p1);
+      HIP_CHECK(hipGetLastError());
+    }
+    pb = p1;
+    bbase = bbase3;
   }
   prof_mark(c, 1);  // partition done
   GbKey k;
@@ -1425,7 +1532,7 @@ bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max
   c.gb_chunk.ensure(sizeof(unsigned) * (size_t)C * R1);
   c.gb_part.ensure(sizeof(long long) * 3 * (size_t)C + 64);
   c.gb_small.ensure(sizeof(int) * (3 * (kGbMaxBins + 1) + 8));
-  c.gb_res.ensure(sizeof(long long) * 8);
+  c.gb_res.ensure(sizeof(long long) * 8);  // (res[6]: pass 3's tile total)
   c.gb_bbase.ensure(sizeof(unsigned) * ((size_t)R1 << kGbMaxDigit) + 64);
   const size_t ne1 = ne > 0 ? (size_t)ne : 1;
   c.ev_out.ensure(8 * 6 * (size_t)nf + 64);
@@ -1433,7 +1540,7 @@ bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max
   prof_step_begin(c);
   prof_mark(c, 0);
   // the producer's timestamp range, when it computed one for these events
-  const bool tsr = c.ev_tsr_valid && c.ev_tsr_n == ne && !getenv("CDR_GB_TSRANGE");
+  const bool tsr = c.ev_tsr_valid && c.ev_tsr_n == ne && !exp_env("CDR_GB_TSRANGE");
   hipLaunchKernelGGL(tsr ? gb_hist1<false> : gb_hist1<true>, dim3(C), dim3(kGbThreads), 0,
                      c.stream, c.ev_file.as<int32_t>(), c.ev_ts.as<long long>(), ne, nf,
                      fbits - B1, R1, c.gb_tilepref.as<unsigned>(), c.gb_chunk.as<unsigned>(),
@@ -1468,20 +1575,41 @@ bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max
   }
   const int sbits = std::max(1, bitlen((unsigned long long)(sec_max - sec_min) + 1));
   const double a = (double)std::max<int64_t>(res[4], 1) / (double)nf;  // events per file
-  const bool dense = sbits + Lmin <= kGbDenseBits && !getenv("CDR_GB_HASH");
-  int L;
-  if (dense) {
-    const int Lt = (int)std::floor(std::log2(2048.0 / a));
-    L = std::max(Lmin, std::min({Lt, Lmax, kGbDenseBits - sbits}));
-  } else {
+  // the bucket shape from the smallest file-local width the passes allow
+  auto shape = [&](int lmin, bool& dn) -> int {
+    dn = sbits + lmin <= kGbDenseBits && !exp_env("CDR_GB_HASH");
+    if (dn) {
+      const int Lt = (int)std::floor(std::log2(2048.0 / a));
+      return std::max(lmin, std::min({Lt, Lmax, kGbDenseBits - sbits}));
+    }
     const int Lt = (int)std::floor(std::log2(1024.0 / a));
-    L = std::max(Lmin, std::min(Lt, Lmax));
-    if (L + sbits > 40) {  // hash key + count in 64 bits
-      prof_drop(c);
-      return false;
+    return std::max(lmin, std::min(Lt, Lmax));
+  };
+  bool dense;
+  int L = shape(Lmin, dense);
+  int B2 = rem - L, B3 = 0;
+  // Two passes leave buckets over the LDS tables (about 3 million files and
+  // more: the one-GPU 1B-event log's 5.95M files gave 32-file buckets of ~5400
+  // events, every one through the global-memory hash): a third pass
+  // (9 + 9 + B3 bits) brings the buckets back to the LDS shapes.
+  // (CDR_GB_PASS3=1, tests: the third pass whenever the file bits allow it)
+  const bool force3 = getenv("CDR_GB_PASS3") != nullptr;
+  if (rem > kGbMaxDigit && (a * std::ldexp(1.0, L) > 0.5 * kGbLdsCap || force3)) {
+    bool dn3;
+    const int lmin3 = std::max(0, rem - 2 * kGbMaxDigit);
+    int L3 = shape(lmin3, dn3);
+    if (force3) L3 = std::max(lmin3, std::min(L3, rem - kGbMaxDigit - 1));
+    if (rem - kGbMaxDigit - L3 >= 1 && L3 < L) {
+      L = L3;
+      dense = dn3;
+      B2 = kGbMaxDigit;
+      B3 = rem - kGbMaxDigit - L;
     }
   }
-  const int B2 = rem - L;
+  if (!dense && L + sbits > 40) {  // hash key + count in 64 bits
+    prof_drop(c);
+    return false;
+  }
   GbPay p;
   p.cbits = cbits;
   p.sshift = 2 + cbits;
@@ -1499,16 +1627,16 @@ bool groupby_resident(Ctx& c, int64_t ne, int64_t nf, int64_t* out, int64_t* max
   // pass-2 tiles per digit were counted by S1 for the same tile size
   c.gb_last_hand = 1;
   c.gb_last_L = L;
-  c.gb_last_passes = B2 > 0 ? 2 : 1;
+  c.gb_last_passes = B3 > 0 ? 3 : (B2 > 0 ? 2 : 1);
   c.gb_last_pbytes = pbits <= 32 ? 4 : 8;
   c.gb_last_dense = dense ? 1 : 0;
   const size_t pay = pbits <= 32 ? 4 : 8;
   c.gb_p1.ensure(pay * ne1);
   if (B2 > 0) c.gb_p2.ensure(pay * ne1);
   if (pbits <= 32)
-    gb_run<unsigned>(c, ne, nf, fbits, L, B1, B2, dense, p, T1, out, res);
+    gb_run<unsigned>(c, ne, nf, fbits, L, B1, B2, B3, dense, p, T1, out, res);
   else
-    gb_run<unsigned long long>(c, ne, nf, fbits, L, B1, B2, dense, p, T1, out, res);
+    gb_run<unsigned long long>(c, ne, nf, fbits, L, B1, B2, B3, dense, p, T1, out, res);
   return true;
 }
 

@@ -1458,7 +1458,7 @@ void lloyd_step_f64(Ctx& c, const double* C, int32_t k, double* sums, int64_t* c
   long long* cnt_pre = c.f64_counts.as<long long>() + k;
   // the fused pipeline (f64sum.hip: assignment + block pass, transfers from
   // the previous step's binade predictions; CDR_F64_FUSE=0: separate passes)
-  static const bool fuse_env = !getenv("CDR_F64_FUSE") || atoi(getenv("CDR_F64_FUSE"));
+  static const bool fuse_env = !exp_env("CDR_F64_FUSE") || atoi(exp_env("CDR_F64_FUSE"));
   if (fuse_env && !getenv("CDR_F64_SERIAL")) {
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "f64_assign_block<%d>", d);
     if (prof) prof_mark(c, 0);

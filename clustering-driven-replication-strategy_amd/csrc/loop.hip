@@ -324,8 +324,8 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   c.ll_flags = flags;
   c.ll_tol = tol;
   c.ll_x2 = std::isnan(x2_total) ? points_sqdev(c, ref) : x2_total;
-  c.ll_devplan = screen32_supported(c, k) && !std::getenv("CDR_NO_DEVPLAN");
-  c.ll_devbig = !c.ll_devplan && big_supported(c, k) && !std::getenv("CDR_NO_DEVPLAN");
+  c.ll_devplan = screen32_supported(c, k) && !exp_env("CDR_NO_DEVPLAN");
+  c.ll_devbig = !c.ll_devplan && big_supported(c, k) && !exp_env("CDR_NO_DEVPLAN");
   plan32_point_side(c, c.ll_xxmax, c.ll_l1x);
   c.ll_C.ensure(sizeof(double) * (size_t)k * d);
   c.ll_new.ensure(sizeof(double) * (size_t)k * (d + 1));
@@ -333,7 +333,7 @@ int cdr_lloyd_begin(cdr_ctx* h, const double* C, int32_t k, double tol, int32_t 
   c.ll_ref.ensure(sizeof(double) * 2 * d);
   c.ll_state.ensure(sizeof(long long) * kLLState);
   // screen32b's drift bounds (kept by ll_finalize32 only)
-  const bool fin_old = std::getenv("CDR_FIN_OLD") && std::atoi(std::getenv("CDR_FIN_OLD"));
+  const bool fin_old = exp_env("CDR_FIN_OLD") && std::atoi(exp_env("CDR_FIN_OLD"));
   c.bnd_ok = c.ll_devplan && !fin_old;
   c.bnd.ensure(kBndBytes);
   HIP_CHECK(hipMemsetAsync(c.bnd.p, 0, c.bnd.bytes, c.stream));
@@ -451,14 +451,14 @@ FinArgs ll_fin_args(Ctx& c) {
   a.abl = 0;
   a.tprof = nullptr;
 #ifdef CDR_EXPERIMENTS
-  if (const char* e = std::getenv("CDR_FIN_ABL")) a.abl = std::atoi(e);
+  if (const char* e = exp_env("CDR_FIN_ABL")) a.abl = std::atoi(e);
   static unsigned long long* fin_tp = nullptr;
-  if (std::getenv("CDR_FIN_TPROF")) {
+  if (exp_env("CDR_FIN_TPROF")) {
     if (!fin_tp) HIP_CHECK(hipMalloc(&fin_tp, sizeof(unsigned long long) * 16));
     HIP_CHECK(hipMemsetAsync(fin_tp, 0, sizeof(unsigned long long) * 16, c.stream));
     a.tprof = fin_tp;
   }
-  if (std::getenv("CDR_FIN_NOPLAN")) a.plan = nullptr;  // timing experiments only
+  if (exp_env("CDR_FIN_NOPLAN")) a.plan = nullptr;  // timing experiments only
 #endif
   return a;
 }
@@ -469,7 +469,7 @@ static void ll_enqueue_finalize(Ctx& c, const int64_t* dsums) {
   const FinArgs a = ll_fin_args(c);
   // screen32 device plan: the latency-oriented finalize (CDR_FIN_OLD=1: the
   // generic one, for comparisons)
-  static const bool fin_old = std::getenv("CDR_FIN_OLD") && std::atoi(std::getenv("CDR_FIN_OLD"));
+  static const bool fin_old = exp_env("CDR_FIN_OLD") && std::atoi(exp_env("CDR_FIN_OLD"));
   if (a.plan && c.ll_k <= 64 && c.d <= 16 && a.nslices <= kRunSlices && !fin_old) {
     hipLaunchKernelGGL(ll_finalize32, dim3(1), dim3(512), 0, c.stream, a);
     HIP_CHECK(hipGetLastError());

@@ -3361,7 +3361,7 @@ __global__ __launch_bounds__(256) void pull_host_kernel(const uint4* __restrict_
 // when that count is < 2^23.  nwg >= #CUs (screen32_step).
 bool screen32_supported(const Ctx& c, int k) {
   if (c.mode != CDR_MODE_F32X || c.d > 16 || k > 64 || k < 1) return false;
-  if (std::getenv("CDR_NO_SCREEN32")) return false;
+  if (exp_env("CDR_NO_SCREEN32")) return false;
   const int64_t groups = c.n_pad / 64;
   const int64_t per_wg = ceil_div(groups, lloyd_num_cus(c.device)) * 64;
   return per_wg < (int64_t(1) << 23);
@@ -3474,10 +3474,10 @@ __global__ __launch_bounds__(256) void plan32_kernel(const double* __restrict__ 
 static int s32_blocks_per_cu(int QH, int MT, size_t lds) {
   int nb = 0;
   hipError_t e = hipErrorInvalidValue;
-  if (QH == 1 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 1, true, true, false, true>, 256, lds);
-  if (QH == 1 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 2, true, true, false, true>, 256, lds);
-  if (QH == 2 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 1, true, true, false, true>, 256, lds);
-  if (QH == 2 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 2, true, true, false, true>, 256, lds);
+  if (QH == 1 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 1, true, false, false, true>, 256, lds);
+  if (QH == 1 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<1, 2, true, false, false, true>, 256, lds);
+  if (QH == 2 && MT == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 1, true, false, false, true>, 256, lds);
+  if (QH == 2 && MT == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, screen32<2, 2, true, false, false, true>, 256, lds);
   if (e != hipSuccess || nb < 1) nb = 2;
   return nb > 8 ? 8 : nb;
 }
@@ -3655,7 +3655,7 @@ static void screen32bs_launch(int Q, int MT, dim3 grid, hipStream_t s, const S32
 
 // chunks in flight per wave of screen32bz (CDR_S32BZ_PD = 4 | 8 | 12)
 static void screen32bz_launch(dim3 grid, hipStream_t s, const S32BArgs& p) {
-  static const int pd = std::getenv("CDR_S32BZ_PD") ? std::atoi(std::getenv("CDR_S32BZ_PD")) : 8;
+  static const int pd = exp_env("CDR_S32BZ_PD") ? std::atoi(exp_env("CDR_S32BZ_PD")) : 8;
   if (pd == 4) hipLaunchKernelGGL(screen32bz<4>, grid, dim3(256), 0, s, p);
   else if (pd == 12) hipLaunchKernelGGL(screen32bz<12>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(screen32bz<8>, grid, dim3(256), 0, s, p);
@@ -3664,7 +3664,7 @@ static void screen32bz_launch(dim3 grid, hipStream_t s, const S32BArgs& p) {
 // Prefetch depth of screen32d: CDR_S32D_PD=2|3|4 (comparisons), else the
 // measured default per shape.
 static int s32d_depth(int QH) {
-  static const int env = std::getenv("CDR_S32D_PD") ? std::atoi(std::getenv("CDR_S32D_PD")) : 0;
+  static const int env = exp_env("CDR_S32D_PD") ? std::atoi(exp_env("CDR_S32D_PD")) : 0;
   if (env >= 2 && env <= 4) return env;
   return QH == 1 ? 3 : 2;  // A/B at configs 2 and 3: 3 helps the d <= 8 screen (0.108 -> 0.102 ms), not d = 16
 }
@@ -3675,23 +3675,23 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
                            const float* dthr, long long* dout, long long* hout, bool prof,
                            long long* gate) {
   // d > 8: the hi-only screen (half the bytes; CDR_S32D_HO=0: the split copy)
-  static const bool ho_env = !std::getenv("CDR_S32D_HO") || std::atoi(std::getenv("CDR_S32D_HO"));
+  static const bool ho_env = !exp_env("CDR_S32D_HO") || std::atoi(exp_env("CDR_S32D_HO"));
   const bool HO = ho_env;
   // hi-only: LDS ring of CDR_S32H_LR slots per wave (2..4; 0: register prefetch);
   // A/B at config 3: 2 slots 0.90-0.91 ms, 3-4 slots 0.92-0.95, registers 0.93
-  static const int lr_env = std::getenv("CDR_S32H_LR") ? std::atoi(std::getenv("CDR_S32H_LR")) : 2;
+  static const int lr_env = exp_env("CDR_S32H_LR") ? std::atoi(exp_env("CDR_S32H_LR")) : 2;
   const int LRn = HO && QH == 2 && lr_env >= 2 && lr_env <= 4 ? lr_env : 0;
   ensure_split(c, HO ? (QH == 2 ? 3 : 4) : QH);
   const int64_t groups = c.n_pad / 64;
   const int cus = lloyd_num_cus(c.device);
   // pruned screen (screen32p) on the hi-only copy: CDR_PRUNE=0 turns it off
-  static const bool pr_env = !std::getenv("CDR_PRUNE") || std::atoi(std::getenv("CDR_PRUNE"));
+  static const bool pr_env = !exp_env("CDR_PRUNE") || std::atoi(exp_env("CDR_PRUNE"));
   const bool PR = pr_env && HO && c.prune_on;
   const int PPD = 3;
   const int PQ = d4_of(c.d) / 4;
   // the fixup fused into screen32p's tail (CDR_PRUNE_FUSE=0: a separate fixup32)
   static const bool fuse_env =
-      !std::getenv("CDR_PRUNE_FUSE") || std::atoi(std::getenv("CDR_PRUNE_FUSE"));
+      !exp_env("CDR_PRUNE_FUSE") || std::atoi(exp_env("CDR_PRUNE_FUSE"));
   // bounded screen (screen32b) in the device loop, where ll_finalize32 keeps
   // the drift bounds of every centroid move (CDR_BOUNDS=0 turns it off)
   const bool bnd_env = !std::getenv("CDR_BOUNDS") || std::atoi(std::getenv("CDR_BOUNDS"));
@@ -3706,14 +3706,20 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   if (BS) {
     bpc = screen32bs_blocks_per_cu(PQ, MT);
     // (experiments: fewer workgroups per CU, CDR_S32BS_BPC=1..3)
-    static const int bsb_env = std::getenv("CDR_S32BS_BPC") ? std::atoi(std::getenv("CDR_S32BS_BPC")) : 0;
+    static const int bsb_env = exp_env("CDR_S32BS_BPC") ? std::atoi(exp_env("CDR_S32BS_BPC")) : 0;
     if (bsb_env >= 1 && bsb_env < bpc) bpc = bsb_env;
   } else if (BND) {
     bpc = screen32b_blocks_per_cu(PQ, MT);
   } else if (PR) {
     bpc = screen32p_blocks_per_cu(PQ, MT, PPD);
-    static const int bpc_env = std::getenv("CDR_S32P_BPC") ? std::atoi(std::getenv("CDR_S32P_BPC")) : 0;
+    static const int bpc_env = exp_env("CDR_S32P_BPC") ? std::atoi(exp_env("CDR_S32P_BPC")) : 0;
     if (bpc_env >= 1 && bpc_env < bpc) bpc = bpc_env;
+#ifndef CDR_EXPERIMENTS
+  } else {
+    // (the unpruned DELTA screens: CDR_PRUNE=0 / CDR_S32D_HO=0, experiments build)
+    CDR_FAIL(CDR_ERR_STATE, "screen32d: the unpruned DELTA screens are in the experiments build");
+  }
+#else
   } else if (LRn) {
     if (PD == 2) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 2, true, true>() : s32d_blocks_per_cu<2, 2, 2, true, true>();
     else if (PD == 3) bpc = MT == 1 ? s32d_blocks_per_cu<2, 1, 3, true, true>() : s32d_blocks_per_cu<2, 2, 3, true, true>();
@@ -3742,6 +3748,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     else if (MT == 1) bpc = s32d_blocks_per_cu<2, 1, 2>();
     else bpc = s32d_blocks_per_cu<2, 2, 2>();
   }
+#endif
   // (screen32b: a wave's unit is a chunk of kBChunk points, not a 64-point group)
   const int64_t units = BND ? c.n_pad / kBChunk : groups;
   const int unit_pts = BND ? kBChunk : 64;
@@ -3813,7 +3820,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
   f.sig = (float)std::ldexp(1.0, c.sigma);
   f.zb = nullptr;
 #ifdef CDR_EXPERIMENTS
-  if (const char* e = std::getenv("CDR_FIX_ABL")) f.abl = std::atoi(e);
+  if (const char* e = exp_env("CDR_FIX_ABL")) f.abl = std::atoi(e);
 #endif
   const dim3 grid(nwg), blk(256);
   const bool fused = PR && fuse_env;
@@ -3847,7 +3854,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     p.q_acc = c.prof_on ? c.q_acc.as<long long>() : nullptr;
     p.abl = 0;
 #ifdef CDR_EXPERIMENTS
-    if (const char* e = std::getenv("CDR_S32P_ABL")) p.abl = std::atoi(e);
+    if (const char* e = exp_env("CDR_S32P_ABL")) p.abl = std::atoi(e);
 #endif
     p.fx = f;
     p.fx.fr = 4;
@@ -3900,7 +3907,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       b.zh = z16 ? c.zb.as<uint16_t>() : nullptr;
       b.bt = reinterpret_cast<const unsigned char*>(c.bnd.p);
       b.t_acc = c.prof_on ? c.t_acc.as<long long>() : nullptr;
-      b.dbg = std::getenv("CDR_BOUNDS_DBG") ? std::atoi(std::getenv("CDR_BOUNDS_DBG")) : 0;
+      b.dbg = exp_env("CDR_BOUNDS_DBG") ? std::atoi(exp_env("CDR_BOUNDS_DBG")) : 0;
 #ifndef CDR_EXPERIMENTS
       b.dbg &= 1;  // (the other bits are timing experiments: experiments build only)
 #endif
@@ -3918,7 +3925,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
         if (wenv[0] < 0) {
           const int wdef[4] = {115, 105, 95, 85};
           for (int q = 0; q < 4; ++q) wenv[q] = split_env ? 100 : wdef[q];
-          if (const char* e = std::getenv("CDR_S32BS_W")) {
+          if (const char* e = exp_env("CDR_S32BS_W")) {
             wenv[0] = 0;
             int v[4] = {0, 0, 0, 0};
             if (std::sscanf(e, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 &&
@@ -3931,7 +3938,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
           for (int q = 0; q < 4; ++q) b.wsl[q] = wenv[q];
         }
         // contiguous chunk ranges per wave (CDR_S32BS_CONTIG=1)
-        if (std::getenv("CDR_S32BS_CONTIG") && std::atoi(std::getenv("CDR_S32BS_CONTIG")))
+        if (exp_env("CDR_S32BS_CONTIG") && std::atoi(exp_env("CDR_S32BS_CONTIG")))
           b.slot_wg = -1;
       }
       // the dynamic tail (2-byte words in generation regions): CDR_S32BS_DYN
@@ -3943,7 +3950,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
         static int dyn_env = -1;
         if (dyn_env < 0) {
           dyn_env = kS32DynPct;
-          if (const char* e = std::getenv("CDR_S32BS_DYN")) dyn_env = std::atoi(e);
+          if (const char* e = exp_env("CDR_S32BS_DYN")) dyn_env = std::atoi(e);
           dyn_env = std::min(std::max(dyn_env, 0), 100);
         }
         if (dyn_env < 100 && bs_max_region(b, nwg) < (1 << 17) && b.slot_wg % 8 == 0 &&
@@ -3960,7 +3967,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
       }
 #ifdef CDR_EXPERIMENTS
       static unsigned long long* tprof_buf = nullptr;
-      const bool tprof_on = BS && std::getenv("CDR_S32BS_TPROF");
+      const bool tprof_on = BS && exp_env("CDR_S32BS_TPROF");
       if (tprof_on) {
         if (!tprof_buf) HIP_CHECK(hipMalloc(&tprof_buf, sizeof(unsigned long long) * 8 * 65536));
         b.tprof = tprof_buf;
@@ -4025,7 +4032,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
             nb += double(r[6]);
             mv += double(r[7]);
           }
-          if (const char* path = std::getenv("CDR_S32BS_TPROF_FILE")) {  // raw, appended
+          if (const char* path = exp_env("CDR_S32BS_TPROF_FILE")) {  // raw, appended
             if (FILE* fo = std::fopen(path, "ab")) {
               std::fwrite(h.data(), 8, h.size(), fo);
               std::fclose(fo);
@@ -4056,6 +4063,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     screen32p_launch(PQ, MT, PPD, grid, c.stream, p);
     }
   } else {
+#ifdef CDR_EXPERIMENTS
   if (LRn)
     snprintf(c.prof_kernel, sizeof(c.prof_kernel), "screen32h<%d,%d>lds", MT, PD);
   else if (HO)
@@ -4083,14 +4091,16 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
     CDR_S32D_LAUNCH(2)
   }
 #undef CDR_S32D_LAUNCH
+#endif
   }
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
   // list regions per fixup workgroup: CDR_FIX_FR (1..16); A/B at config 3 (100M and
   // the 12.5M shard): 8 leaves 79-82 / 34 us beside the screen, 4 91-93 / 42, 16 106 / 39
-  static const int fr_env = std::getenv("CDR_FIX_FR") ? std::atoi(std::getenv("CDR_FIX_FR")) : 8;
+  static const int fr_env = exp_env("CDR_FIX_FR") ? std::atoi(exp_env("CDR_FIX_FR")) : 8;
   f.fr = fr_env >= 1 && fr_env <= kFixMaxR ? fr_env : 8;
   const dim3 fgrid((nwaves + f.fr - 1) / f.fr);
+#ifdef CDR_EXPERIMENTS
   if (!fused && !BS) switch (d4_of(c.d) / 4) {  // (screen32bs applies its own moves)
 #define CDR_FIX(Q_)                                                                  \
   case Q_:                                                                           \
@@ -4101,6 +4111,7 @@ static void screen32d_step(Ctx& c, int QH, int MT, int k, const h8* dfrag, const
 #undef CDR_FIX
     default: CDR_FAIL(CDR_ERR_STATE, "screen32d: d > 16");
   }
+#endif
   HIP_CHECK(hipGetLastError());
   const int len = k * (c.d + 1);
   long long* hout_dev = nullptr;
@@ -4197,7 +4208,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
       reinterpret_cast<const double*>(static_cast<char*>(c.frag.p) + b_frag + b_cinit);
   const float* dthr =
       devplan ? reinterpret_cast<const float*>(static_cast<char*>(c.frag.p) + b_all) : nullptr;
-  const bool lean = delta && !dbg && !std::getenv("CDR_NO_LEAN");
+  const bool lean = delta && !dbg && !exp_env("CDR_NO_LEAN");
   if (lean) {
     screen32d_step(c, pl.QH, pl.MT, k, dfrag, dcinit, dcent, pl.thr0, pl.thr_rel, pl.Dv, dthr,
                    dout, hout, prof, gate);
@@ -4225,7 +4236,7 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   c.fb_regions = nwaves;
   c.fb_total_slot = nwaves + 1;
   // pre-centred screen copy (exact; built once per point set)
-  const bool pre = c.pre_ok && !std::getenv("CDR_NO_PRE");
+  const bool pre = c.pre_ok && !exp_env("CDR_NO_PRE");
   if (pre) ensure_precentered(c);
   S32Args a;
   a.X = pre ? c.xt32.as<float>() : c.x32.as<float>();
@@ -4260,12 +4271,21 @@ bool screen32_step(Ctx& c, const double* C, int k, long long* dout, long long* h
   if (prof) prof_mark(c, 0);
   const dim3 grid(nwg), blk(256);
   const bool fullq = Q == 2 * pl.QH;
+#ifdef CDR_EXPERIMENTS
 #define CDR_S32P(QH_, MT_, P_)                                                                  \
   if (dbg) hipLaunchKernelGGL((screen32<QH_, MT_, false, false, true, P_>), grid, blk, lds, c.stream, a); \
   else if (fullq && delta) hipLaunchKernelGGL((screen32<QH_, MT_, true, true, false, P_>), grid, blk, lds, c.stream, a); \
   else if (fullq) hipLaunchKernelGGL((screen32<QH_, MT_, true, false, false, P_>), grid, blk, lds, c.stream, a); \
   else if (delta) hipLaunchKernelGGL((screen32<QH_, MT_, false, true, false, P_>), grid, blk, lds, c.stream, a); \
   else hipLaunchKernelGGL((screen32<QH_, MT_, false, false, false, P_>), grid, blk, lds, c.stream, a);
+#else
+  // (product: DELTA steps take the lean path above, CDR_NO_LEAN is experiments-only)
+  if (delta) CDR_FAIL(CDR_ERR_STATE, "screen32: the full DELTA screen is in the experiments build");
+#define CDR_S32P(QH_, MT_, P_)                                                                  \
+  if (dbg) hipLaunchKernelGGL((screen32<QH_, MT_, false, false, true, P_>), grid, blk, lds, c.stream, a); \
+  else if (fullq) hipLaunchKernelGGL((screen32<QH_, MT_, true, false, false, P_>), grid, blk, lds, c.stream, a); \
+  else hipLaunchKernelGGL((screen32<QH_, MT_, false, false, false, P_>), grid, blk, lds, c.stream, a);
+#endif
 #define CDR_S32(QH_, MT_) \
   if (pre) { CDR_S32P(QH_, MT_, true) } else { CDR_S32P(QH_, MT_, false) }
 #ifdef CDR_EXPERIMENTS

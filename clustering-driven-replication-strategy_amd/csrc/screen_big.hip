@@ -1118,7 +1118,7 @@ static int big_dq(int d) { return (d + 15) / 16; }
 // L1 workgroup size: 3 waves per SIMD while the pipelined kernel fits 168
 // VGPRs (DQ <= 2), else 2 (CDR_BIG_SP_NT=512|768 overrides, for comparisons)
 static int big_sp_threads(int DQ) {
-  static const int env = std::getenv("CDR_BIG_SP_NT") ? std::atoi(std::getenv("CDR_BIG_SP_NT")) : 0;
+  static const int env = exp_env("CDR_BIG_SP_NT") ? std::atoi(exp_env("CDR_BIG_SP_NT")) : 0;
   if (env == 512 || env == 768) return env;
   return DQ <= 2 ? 768 : 512;
 }
@@ -1353,7 +1353,7 @@ static void launch_big_levels(Ctx& c, const BigArgs& a1, const BigArgs& a2, dim3
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);  // the L1 screen alone
 #ifdef CDR_EXPERIMENTS
-  static const int abl = std::getenv("CDR_BIG_ABL") ? std::atoi(std::getenv("CDR_BIG_ABL")) : 0;
+  static const int abl = exp_env("CDR_BIG_ABL") ? std::atoi(exp_env("CDR_BIG_ABL")) : 0;
 #else
   constexpr int abl = 0;
 #endif
@@ -1481,7 +1481,7 @@ static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* th
   // level 1: persistent, one kBigThreads workgroup per CU (LDS-bound)
   const size_t lds1 = big_l1_lds(k, d);
   const int64_t groups = (c.n + 63) / 64;
-  static const bool sp = !(std::getenv("CDR_BIG_L1") && std::atoi(std::getenv("CDR_BIG_L1")) == 0);
+  static const bool sp = !(exp_env("CDR_BIG_L1") && std::atoi(exp_env("CDR_BIG_L1")) == 0);
   const int wpb1 = (sp ? big_sp_threads(DQ) : kBigThreads) / 64;
   const int nwg1 = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (groups + wpb1 - 1) / wpb1));
   const int nw1 = nwg1 * wpb1;
@@ -1532,7 +1532,7 @@ static bool big_launch(Ctx& c, int k, float thr1, float thr_rel, const float* th
   // DELTA: the running sums follow the labels of the previous large-k step
   // of this k (pipelined L1 only); moves go to c.mv_list, the sums are
   // updated by fixup_big instead of a pass over every point
-  static const bool nodelta = std::getenv("CDR_BIG_NODELTA") != nullptr;
+  static const bool nodelta = exp_env("CDR_BIG_NODELTA") != nullptr;
   const bool delta = sp && !nodelta && c.big_valid && c.big_k == k;
   a.delta = delta ? 1 : 0;
   a.mv1 = nullptr;

@@ -1868,7 +1868,7 @@ void seed_update(Ctx& c, const double* cen) {
                                    CDR_SU(15), CDR_SU(16)};
 #undef CDR_SU
     const int64_t nfull = c.n / kSeedBlock;
-    static const bool no16 = std::getenv("CDR_SEED16") && std::atoi(std::getenv("CDR_SEED16")) == 0;
+    static const bool no16 = exp_env("CDR_SEED16") && std::atoi(exp_env("CDR_SEED16")) == 0;
     const int d = c.d;
     if (c.mode == CDR_MODE_F32X && (d == 8 || d == 16 || d == 32 || d == 64) && !no16) {
       const int tau = c.sigma + kSeed16Tau;
@@ -1894,15 +1894,15 @@ void seed_update(Ctx& c, const double* cen) {
       typedef void (*S16Fn)(const float*, const uint4*, const float*, int64_t, int64_t,
                             const double*, const float*, const float*, double, double*,
                             double*, int32_t*, const double*, int);
-      static const int u16 = std::getenv("CDR_SEED16_U") ? std::atoi(std::getenv("CDR_SEED16_U")) : 0;
-      static const bool pr16 = std::getenv("CDR_SEED16_PR") != nullptr;  // A/B: prune at d <= 16
+      static const int u16 = exp_env("CDR_SEED16_U") ? std::atoi(exp_env("CDR_SEED16_U")) : 0;
+      static const bool pr16 = exp_env("CDR_SEED16_PR") != nullptr;  // A/B: prune at d <= 16
       // the pairwise tree in registers (d = 8, 16; CDR_SEED16_LDS=1: staged in LDS)
-      const bool lds16 = std::getenv("CDR_SEED16_LDS") && std::atoi(std::getenv("CDR_SEED16_LDS"));
+      const bool lds16 = exp_env("CDR_SEED16_LDS") && std::atoi(exp_env("CDR_SEED16_LDS"));
       if ((d == 8 || d == 16) && !lds16 && !pr16 && !u16) {
         // the exact path's rows from the row-major copy (built once per point
         // set; the bounded Lloyd screen gathers from it too); CDR_SEED_XA=0:
         // from the quad planes
-        const bool xa = !std::getenv("CDR_SEED_XA") || std::atoi(std::getenv("CDR_SEED_XA"));
+        const bool xa = !exp_env("CDR_SEED_XA") || std::atoi(exp_env("CDR_SEED_XA"));
         if (xa) ensure_rowmajor(c);
         hipLaunchKernelGGL(d == 8 ? seed_update16r_kernel<8> : seed_update16r_kernel<16>,
                            dim3(nb), dim3(512), 0, c.stream, c.x32.as<float>(),
@@ -1987,7 +1987,7 @@ static void seed_scan_walk(Ctx& c, double total, double c_in, double* c_out,
   HIP_CHECK(hipGetLastError());
   c.seed_scalar.ensure(sizeof(double) * (2 * c.d + 8));
   double* dres = dres_dev ? dres_dev : c.seed_scalar.as<double>() + c.d;
-  static const bool want_stats = std::getenv("CDR_SEED_STATS") != nullptr;
+  static const bool want_stats = exp_env("CDR_SEED_STATS") != nullptr;
   long long* dstats = nullptr;
   if (want_stats) {
     static long long* ds = nullptr;
@@ -2078,7 +2078,7 @@ static bool seed_scan_finish(Ctx& c, double c_in, double* c_out,
   double h[2];
   HIP_CHECK(hipMemcpyAsync(h, res, sizeof(h), hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
-  static const bool want_stats = std::getenv("CDR_SEED_STATS") != nullptr;
+  static const bool want_stats = exp_env("CDR_SEED_STATS") != nullptr;
   if (want_stats) {
     long long m[3];
     HIP_CHECK(hipMemcpy(m, c.seg_meta.p, sizeof(m), hipMemcpyDeviceToHost));
@@ -2104,7 +2104,7 @@ void seed_scan(Ctx& c, double total, double c_in, double* c_out) {
     *c_out = c_in;
     return;
   }
-  static const bool walk_only = std::getenv("CDR_SEED_WALK") != nullptr;
+  static const bool walk_only = exp_env("CDR_SEED_WALK") != nullptr;
   bool done = false;
   if (!walk_only) {
     seed_scan_program(c, total, c_in);
@@ -2208,7 +2208,7 @@ void seed_run(Ctx& c, int64_t first, int k, const double* u, int64_t* picks) {
   c.seed_scalar.ensure(sizeof(double) * (2 * c.d + 8));
   c.cend.ensure(sizeof(double) * nb * 2);
   c.seg_meta.ensure(sizeof(long long) * 8);
-  static const bool walk_only = std::getenv("CDR_SEED_WALK") != nullptr;
+  static const bool walk_only = exp_env("CDR_SEED_WALK") != nullptr;
   const float* x32 = c.mode == CDR_MODE_F32X ? c.x32.as<float>() : nullptr;
   const double* x64 = c.mode == CDR_MODE_F64 ? c.x64.as<double>() : nullptr;
   for (int i = 1; i < k; ++i) {

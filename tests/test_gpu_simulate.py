@@ -148,6 +148,9 @@ def test_config4_one_billion_events_one_gpu(ctx):
     got, mx = ctx.features_aggregate_resident()
     info = ctx.features_groupby_info()
     print(f"\n1B-event group-by: {ne} events x {nf} files, {info}")
+    # 23 file bits: three partition passes (9 + 9 + 3) leave 4-file buckets
+    # in the one-wave LDS kernel, none over the LDS tables
+    assert info["passes"] == 3 and info["L"] == 2 and info["big_buckets"] == 0
     cnt = got[:, 0]
     assert int(cnt.sum()) == ne
     np.testing.assert_array_equal(got[:, 4], cnt)
@@ -174,3 +177,22 @@ def test_config4_one_billion_events_one_gpu(ctx):
     exp, _ = fo.counts_from_arrays(fs, ops, cls, tss, prs, m)
     np.testing.assert_array_equal(sub, exp)
     assert ne_s == fs.size
+
+
+@pytest.mark.parametrize("nf,dur", [(600_000, 60.0), (300_001, 20.0)])
+def test_three_pass_partition_matches_oracle(ctx, monkeypatch, nf, dur):
+    """The third partition pass (csrc/groupby.hip: the pass-2 regions split
+    again by B3 more file bits; on by itself above ~3M files, forced here by
+    CDR_GB_PASS3) gives the oracle's counters and the two-pass result."""
+    ne = ctx.features_simulate(nf, dur, 3, seed=17, t0_us=T0)
+    two, mx2 = ctx.features_aggregate_resident()
+    assert ctx.features_groupby_info()["passes"] == 2
+    monkeypatch.setenv("CDR_GB_PASS3", "1")
+    three, mx3 = ctx.features_aggregate_resident()
+    assert ctx.features_groupby_info()["passes"] == 3
+    f, op, cl, ts, pr = ctx.features_events_read()
+    exp, emx = fo.counts_from_arrays(f, op, cl, ts, pr, nf)
+    assert ne == f.size
+    np.testing.assert_array_equal(three, exp)
+    np.testing.assert_array_equal(two, exp)
+    assert mx3 == mx2 == emx

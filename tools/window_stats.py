@@ -9,6 +9,13 @@
         (FETCH_SIZE KiB x 1024 x 2: the gfx950 half-count of MI355X_MICROARCH.md;
         WRITE_SIZE KiB x 1024) written into profiles/pmc_traffic.json[CONFIG]
 
+    python tools/window_stats.py dram DIR KERNEL FIRST_STEP CONFIG N_LOCAL
+        the same table from one pass of the gfx950 memory-side 32-byte
+        request counters (TCC_EA0_RDREQ_DRAM_32B, TCC_EA0_WRREQ_WRITE_DRAM_32B,
+        TCC_EA0_WRREQ_WRITE_ATOMIC_32B: x 32 bytes, every request width
+        counted at its size - calibrated on known byte counts by
+        tools/micro/fetch_calib.hip, profiles/r06_dram_counter_calibration.txt)
+
 KERNEL is a substring of the kernel name; several kernels of one step can be
 given as "a+b" (their per-step values are summed, dispatches paired in order).
 """
@@ -61,6 +68,27 @@ def _counter(dirpath, name, kern):
     return [sum(per[p][i]["v"] for p in per) for i in range(n)]
 
 
+def dram(ddir, kern, first, config, n_local):
+    rd = [v * 32 for v in _counter(ddir, "TCC_EA0_RDREQ_DRAM_32B_sum", kern)]
+    wr = [v * 32 for v in _counter(ddir, "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum", kern)]
+    at = [v * 32 for v in _counter(ddir, "TCC_EA0_WRREQ_WRITE_ATOMIC_32B_sum", kern)]
+    n = min(len(rd), len(wr))
+    wa = [wr[i] + (at[i] if i < len(at) else 0.0) for i in range(n)]
+    for i in range(n):
+        print(f"step {first + i:3d}: read {rd[i] / 1e6:10.1f} MB  write {wa[i] / 1e6:8.1f} MB")
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    rec = json.load(open(path)) if os.path.exists(path) else {}
+    rec[config] = {"n_local": n_local, "kernel": kern, "first_step": first,
+                   "per_step_read": rd[:n], "per_step_write": wa[:n],
+                   "source": f"rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_32B_sum "
+                             f"TCC_EA0_WRREQ_WRITE_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_ATOMIC_32B_sum "
+                             f"({ddir}), one row per device-loop step",
+                   "note": "32-byte memory-side request counts x 32 (exact for every access "
+                           "width: profiles/r06_dram_counter_calibration.txt); bench.py averages "
+                           "the rows of the steps it times"}
+    json.dump(rec, open(path, "w"), indent=1)
+
+
 def pmc(fdir, wdir, kern, first, config, n_local):
     rd = [v * 1024 * 2 for v in _counter(fdir, "FETCH_SIZE", kern)]
     wr = [v * 1024 for v in _counter(wdir, "WRITE_SIZE", kern)]
@@ -82,5 +110,7 @@ def pmc(fdir, wdir, kern, first, config, n_local):
 if __name__ == "__main__":
     if sys.argv[1] == "trace":
         trace(sys.argv[2], sys.argv[3], int(sys.argv[4]), [int(s) for s in sys.argv[5:]])
+    elif sys.argv[1] == "dram":
+        dram(sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5], int(sys.argv[6]))
     else:
         pmc(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6], int(sys.argv[7]))
