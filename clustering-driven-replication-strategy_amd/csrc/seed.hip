@@ -1656,45 +1656,72 @@ __global__ __launch_bounds__(256) void seg_fill_kernel(const SegScan* __restrict
 
 // ---- device-resident seeding (seed_run) -----------------------------------
 
-// The left-to-right sum of v[0 .. n) in one wave (the value in every lane):
-// windows of 64 W values held one per lane per register (value 64 j + l in
-// lane l of register j), the next window's loads in flight, and the chain of
-// adds reading each value through v_readlane (an SGPR operand), so the only
-// serial latency is the adds' own.  Padding past n adds +0.0, which leaves a
-// sum of non-negative terms unchanged.
-template <typename T>
-__device__ __forceinline__ T rl_lane(T v, int l) {
-  if constexpr (sizeof(T) == 8) {
-    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
-    return __builtin_bit_cast(T, (unsigned long long)hi << 32 | lo);
-  } else {
-    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-  }
-}
+// The left-to-right sum of v[0 .. n) in one wave (the value in every lane).
+// The chain of n dependent fp64 (or fp32) adds is the whole cost, so each add
+// takes its operand from LDS (a broadcast read, in order under lgkmcnt) and
+// the values arrive in chunks: the wave loads chunk c + 1 into registers
+// (coalesced, one value per lane per load) while the chain runs over chunk c,
+// then writes it to the other LDS buffer.  (Round 5 read each value through
+// two v_readlane into SGPRs: three VALU instructions and a hazard wait per
+// add, ~2.5x slower.)  Padding past n adds +0.0, which leaves a sum of
+// non-negative terms unchanged.
 template <typename T>
 __device__ __forceinline__ T wave_seq_sum(const T* __restrict__ v, int64_t n) {
-  constexpr int W = 8;
+  constexpr int kChunk = 1024;       // values per chunk
+  constexpr int kPer = kChunk / 64;  // per lane
+  __shared__ __attribute__((aligned(16))) T buf[2][kChunk];
   const int lane = threadIdx.x & 63;
-  T cur[W], nxt[W];
-  auto load = [&](T (&r)[W], int64_t w0) __attribute__((always_inline)) {
+  T r[kPer];
+  // lane l holds values c0 + l + 64 j of the chunk at c0 (coalesced; no
+  // branches: a clamped address and a select, so the loads stay in flight)
+  auto load = [&](int64_t c0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < W; ++j) {
-      const int64_t i = w0 + 64 * j + lane;
-      r[j] = i < n ? v[i] : T(0);
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = c0 + lane + 64 * j;
+      r[j] = v[i < n ? i : n - 1];
     }
   };
-  load(cur, 0);
+  // (the select past n here, after the chain: not at the load, where it
+  // would wait for the data)
+  auto store = [&](T* dst, int64_t c0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) dst[lane + 64 * j] = c0 + lane + 64 * j < n ? r[j] : T(0);
+  };
   T s = T(0);
-  for (int64_t w0 = 0; w0 < n; w0 += 64 * W) {
-    load(nxt, w0 + 64 * W);
+  if (n <= 0) return s;
+  load(0);
+  store(buf[0], 0);
+  int cb = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += kChunk) {
+    const bool more = c0 + kChunk < n;  // (uniform)
+    if (more) load(c0 + kChunk);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const T* src = buf[cb];
+    const int m = n - c0 < kChunk ? (int)(n - c0) : kChunk;
+    if (m == kChunk) {
+      // 16-byte reads kP ahead of the chain (the LDS latency covered by the
+      // adds of the kP - 1 reads before)
+      constexpr int kVec = 16 / sizeof(T);
+      constexpr int kNV = kChunk / kVec;
+      constexpr int kP = 8;
+      typedef T tv __attribute__((ext_vector_type(kVec)));
+      const tv* q = reinterpret_cast<const tv*>(src);
+      tv pipe[kP];
 #pragma unroll
-    for (int j = 0; j < W; ++j)
+      for (int i = 0; i < kP; ++i) pipe[i] = q[i];
 #pragma unroll
-      for (int l = 0; l < 64; ++l) s = s + rl_lane(cur[j], l);
+      for (int i = 0; i < kNV; ++i) {
+        const tv cur = pipe[i % kP];
+        if (i + kP < kNV) pipe[i % kP] = q[i + kP];
 #pragma unroll
-    for (int j = 0; j < W; ++j) cur[j] = nxt[j];
+        for (int e = 0; e < kVec; ++e) s = s + cur[e];
+      }
+    } else {
+      for (int j = 0; j < m; ++j) s = s + src[j];
+    }
+    if (more) store(buf[cb ^ 1], c0 + kChunk);
+    cb ^= 1;
   }
   return s;
 }

@@ -262,12 +262,14 @@ def test_hi_only_screen_near_ties(ctx, d):
             assert ctx.fallback_count() > m // 10, ctx.fallback_count()
 
 
-@pytest.mark.parametrize("n,outlier", [(3_000_001, False), (1_200_000, True)])
+@pytest.mark.parametrize("n,outlier", [(3_000_001, False), (1_200_000, True), (9_000_001, False)])
 def test_seeding_many_blocks_vs_oracle(ctx, n, outlier):
     """Seeding over hundreds of 8192-blocks: the block-transfer walk crosses
     binades between blocks and inside them, and the 64-ary block search runs
     several rounds.  The outlier case makes one D^2 dominate (tiny
-    probabilities everywhere else, many crossings in the first blocks)."""
+    probabilities everywhere else, many crossings in the first blocks).  9M
+    rows: 1099 block sums, so the device total runs over two staged chunks
+    of 1024, the second one partial."""
     import kmeans_plusplus as kp
 
     X = synth.generate(n, 0, n, 16, 8, 77 + n)
