@@ -441,10 +441,13 @@ def f64_bench(args, world: int, rank: int, dist, device, json_fd) -> dict:
                    f"rows sharded over {world} GPUs; exact sequential sums composed from the "
                    "shards' programs after two all-gathers per step"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBPS,
+                     "traffic": pmc_traffic("f64", n_local, ctx.profile_kernel()),
                      "kernel": ctx.profile_kernel(), "alg_bytes_per_launch": alg,
                      "kernel_ms": assign_ms},
         "step_kernels_ms": kern_ms,
+        # every kernel of one step (DRAM counters, profiles/pmc_traffic.json["f64"])
+        "step_traffic": pmc_step_bytes("f64", n_local),
         "f64_blocks_walked": ctx.f64_walked(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -499,6 +502,19 @@ def pmc_traffic(config: str, n_local: int, kname: str | None = None, steps=None)
             return None
         return float(sum(vals) / len(vals))
     return float(r["hbm_bytes_per_launch"])
+
+
+def pmc_step_bytes(config: str, n_local: int):
+    """All the step's kernels' HBM bytes from a committed per-step DRAM pass
+    (tools/window_stats.py dramstep), when taken on this size."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        r = json.load(fh).get(config)
+    if not r or int(r.get("n_local", -1)) != n_local or "step_bytes" not in r:
+        return None
+    return float(r["step_bytes"])
 
 
 def kernel_bytes(kname: str, n_local: int, prof: dict, steps: int) -> int:

@@ -16,6 +16,14 @@
         counted at its size - calibrated on known byte counts by
         tools/micro/fetch_calib.hip, profiles/r06_dram_counter_calibration.txt)
 
+    python tools/window_stats.py dramstep DIR MARKER PREFIX SKIP CONFIG N_LOCAL [DOMINANT]
+        the same counters summed over every kernel whose name contains PREFIX
+        within each step (a step = the dispatches from one MARKER dispatch to
+        the next), the first SKIP steps dropped (warmup): the mean step bytes,
+        each kernel's mean bytes per dispatch, and - with DOMINANT - that
+        kernel's bytes per launch as the entry's hbm_bytes_per_launch (else the
+        whole step's), written into profiles/pmc_traffic.json[CONFIG]
+
 KERNEL is a substring of the kernel name; several kernels of one step can be
 given as "a+b" (their per-step values are summed, dispatches paired in order).
 """
@@ -89,6 +97,65 @@ def dram(ddir, kern, first, config, n_local):
     json.dump(rec, open(path, "w"), indent=1)
 
 
+def _dram_rows(dirpath):
+    """{dispatch id: [kernel name, read bytes, written bytes]} from one DRAM
+    counter pass (the counters summed over their instances)."""
+    files = glob.glob(os.path.join(dirpath, "**", "*_counter_collection.csv"), recursive=True)
+    out = {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            name = r["Counter_Name"]
+            if name not in ("TCC_EA0_RDREQ_DRAM_32B_sum", "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum",
+                            "TCC_EA0_WRREQ_WRITE_ATOMIC_32B_sum"):
+                continue
+            e = out.setdefault(int(r["Dispatch_Id"]), [r["Kernel_Name"], 0.0, 0.0])
+            e[1 if name.startswith("TCC_EA0_RDREQ") else 2] += 32.0 * float(r["Counter_Value"])
+    return out
+
+
+def dramstep(ddir, marker, prefix, skip, config, n_local, dominant=None):
+    rows = _dram_rows(ddir)
+    ids = sorted(rows)
+    marks = [i for i in ids if marker in rows[i][0]]
+    steps, per_kernel = [], {}
+    for a, b in zip(marks, marks[1:] + [ids[-1] + 1]):
+        rd = wr = 0.0
+        for i in ids:
+            if a <= i < b and prefix in rows[i][0]:
+                rd += rows[i][1]
+                wr += rows[i][2]
+                if len(steps) >= skip:
+                    per_kernel.setdefault(rows[i][0].split("(")[0], []).append(rows[i][1] + rows[i][2])
+        steps.append((rd, wr))
+    kept = steps[skip:]
+    for j, (rd, wr) in enumerate(steps):
+        print(f"step {j:3d}{' (skipped)' if j < skip else ''}: read {rd / 1e6:10.1f} MB  "
+              f"write {wr / 1e6:8.1f} MB")
+    mr = sum(r for r, _ in kept) / len(kept)
+    mw = sum(w for _, w in kept) / len(kept)
+    pk = {k: sum(v) / len(v) for k, v in per_kernel.items()}
+    for k, v in sorted(pk.items(), key=lambda kv: -kv[1]):
+        print(f"  {v / 1e6:10.1f} MB per dispatch  {k}")
+    rec_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    rec = json.load(open(rec_path)) if os.path.exists(rec_path) else {}
+    dom = None
+    if dominant:
+        dom = [v for k, v in pk.items() if dominant in k]
+        dom = dom[0] if dom else None
+    rec[config] = {"n_local": n_local,
+                   "kernel": dominant if dom is not None else f"all {prefix}* kernels of one step",
+                   "hbm_bytes_per_launch": dom if dom is not None else mr + mw,
+                   "step_bytes": mr + mw, "step_read_bytes": mr, "step_write_bytes": mw,
+                   "per_kernel_bytes_per_dispatch": pk, "steps_averaged": len(kept),
+                   "source": f"rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_32B_sum "
+                             f"TCC_EA0_WRREQ_WRITE_DRAM_32B_sum TCC_EA0_WRREQ_WRITE_ATOMIC_32B_sum "
+                             f"({ddir}); steps split at each {marker} dispatch, the first {skip} "
+                             "dropped",
+                   "note": "32-byte memory-side request counts x 32 (exact for every access "
+                           "width: profiles/r06_dram_counter_calibration.txt)"}
+    json.dump(rec, open(rec_path, "w"), indent=1)
+
+
 def pmc(fdir, wdir, kern, first, config, n_local):
     rd = [v * 1024 * 2 for v in _counter(fdir, "FETCH_SIZE", kern)]
     wr = [v * 1024 for v in _counter(wdir, "WRITE_SIZE", kern)]
@@ -110,6 +177,9 @@ def pmc(fdir, wdir, kern, first, config, n_local):
 if __name__ == "__main__":
     if sys.argv[1] == "trace":
         trace(sys.argv[2], sys.argv[3], int(sys.argv[4]), [int(s) for s in sys.argv[5:]])
+    elif sys.argv[1] == "dramstep":
+        dramstep(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6],
+                 int(sys.argv[7]), sys.argv[8] if len(sys.argv) > 8 else None)
     elif sys.argv[1] == "dram":
         dram(sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5], int(sys.argv[6]))
     else:
