@@ -798,7 +798,10 @@ __global__ __launch_bounds__(256) void xfer_kernel(const double* __restrict__ dm
   if (live && lane == 0) out[b] = Xfer{T0, T1, e, tv, 0};
 }
 
-// approx[b] = c_in + sum_{b' < b} blocksums[b'] / S   (guesses only)
+// approx[b] = c_in + sum_{b' < b} blocksums[b'] / S   (guesses only: any
+// summation order will do).  Each thread's run of block sums is loaded 8 at a
+// time (the loads in flight together), the 1024 partials are scanned by waves
+// (shfl) and then across the 16 waves.
 __global__ __launch_bounds__(1024) void approx_prefix_kernel(const double* __restrict__ bs,
                                                              int64_t nb, double S, double c_in,
                                                              double* __restrict__ approx,
@@ -806,27 +809,42 @@ __global__ __launch_bounds__(1024) void approx_prefix_kernel(const double* __res
   if (dv.gate && dv.gate[0] != 0.0) return;
   if (dv.S) S = dv.S[0];
   if (dv.c_in) c_in = dv.c_in[0];
-  __shared__ double part[1024];
-  const int t = threadIdx.x;
+  __shared__ double wsum[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t per = (nb + 1023) / 1024;
   const int64_t lo = t * per, hi = (lo + per) < nb ? (lo + per) : nb;
+  constexpr int kB = 8;
   double s = 0.0;
-  for (int64_t i = lo; i < hi; ++i) s += bs[i] / S;
-  part[t] = s;
-  __syncthreads();
-  if (t == 0) {
-    double acc = c_in;
-    for (int i = 0; i < 1024; ++i) {
-      const double v = part[i];
-      part[i] = acc;
-      acc += v;
-    }
+  for (int64_t b0 = lo; b0 < hi; b0 += kB) {
+    double v[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) v[j] = bs[b0 + j < hi ? b0 + j : lo];
+#pragma unroll
+    for (int j = 0; j < kB; ++j)
+      if (b0 + j < hi) s += v[j] / S;
   }
+  double inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wsum[w] = inc;
   __syncthreads();
-  double acc = part[t];
-  for (int64_t i = lo; i < hi; ++i) {
-    approx[i] = acc;
-    acc += bs[i] / S;
+  double acc = c_in;
+  for (int i = 0; i < w; ++i) acc += wsum[i];
+  acc += inc - s;  // the exclusive prefix of this thread's run
+  for (int64_t b0 = lo; b0 < hi; b0 += kB) {
+    double v[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) v[j] = bs[b0 + j < hi ? b0 + j : lo];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      if (b0 + j < hi) {
+        approx[b0 + j] = acc;
+        acc += v[j] / S;
+      }
+    }
   }
 }
 
@@ -1475,20 +1493,34 @@ __global__ __launch_bounds__(1024) void seg_plan_kernel(const SegTail* __restric
   const int64_t per = (nb + kPlanT - 1) / kPlanT;
   const int64_t lo = (int64_t)t * per;
   const int64_t hi = (lo + per) < nb ? (lo + per) : nb;
+  // a thread's tails are loaded kPB at a time, the loads in flight together
+  // (one at a time paid a memory latency per block: 60 us at 12 208 blocks)
+  constexpr int kPB = 4;
+  auto load_tails = [&](int64_t b0, SegTail (&T)[kPB]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kPB; ++j) T[j] = tails[b0 + j < hi ? b0 + j : lo];
+  };
   {
     Part agg = part_empty();
     int hh = 0;
     long long ni = 0, lh = -1, nf = 0;
-    for (int64_t b = lo; b < hi; ++b) {
-      const SegTail T = tails[b];
-      if (T.ncross > 0 || T.opaque) {
-        agg = T.opaque ? part_empty() : T.t;
-        hh = 1;
-        lh = b;
-        ni += T.opaque ? 3 : 2 + 2 * (long long)T.ncross;
-        nf += T.opaque;
-      } else {
-        agg = part_compose(agg, T.t);
+    for (int64_t b0 = lo; b0 < hi; b0 += kPB) {
+      SegTail TT[kPB];
+      load_tails(b0, TT);
+#pragma unroll
+      for (int j = 0; j < kPB; ++j) {
+        const int64_t b = b0 + j;
+        if (b >= hi) break;
+        const SegTail& T = TT[j];
+        if (T.ncross > 0 || T.opaque) {
+          agg = T.opaque ? part_empty() : T.t;
+          hh = 1;
+          lh = b;
+          ni += T.opaque ? 3 : 2 + 2 * (long long)T.ncross;
+          nf += T.opaque;
+        } else {
+          agg = part_compose(agg, T.t);
+        }
       }
     }
     sP[t] = agg;
@@ -1524,28 +1556,35 @@ __global__ __launch_bounds__(1024) void seg_plan_kernel(const SegTail* __restric
   long long lastH = t ? sL[t - 1] : -1;
   const long long total = sI[kPlanT - 1];
   const bool over = total + 2 > cap;
-  for (int64_t b = lo; b < hi; ++b) {
-    const SegTail T = tails[b];
-    if (T.ncross > 0 || T.opaque) {
-      if (!over) {
-        items[off++] = run_item(run);
-        if (T.opaque) {
-          items[off++] = SeedItem{b, 0, 0.0, 0, kItFine};
-        } else {
-          for (int j = 0; j < T.ncross; ++j) {
-            const SegEnt E = ents[b * kKC + j];
-            items[off++] = run_item(E.pre);
-            items[off++] = SeedItem{0, 0, E.p, 0, kItCross};
+  for (int64_t b0 = lo; b0 < hi; b0 += kPB) {
+    SegTail TT[kPB];
+    load_tails(b0, TT);
+#pragma unroll
+    for (int jb = 0; jb < kPB; ++jb) {
+      const int64_t b = b0 + jb;
+      if (b >= hi) break;
+      const SegTail& T = TT[jb];
+      if (T.ncross > 0 || T.opaque) {
+        if (!over) {
+          items[off++] = run_item(run);
+          if (T.opaque) {
+            items[off++] = SeedItem{b, 0, 0.0, 0, kItFine};
+          } else {
+            for (int j = 0; j < T.ncross; ++j) {
+              const SegEnt E = ents[b * kKC + j];
+              items[off++] = run_item(E.pre);
+              items[off++] = SeedItem{0, 0, E.p, 0, kItCross};
+            }
           }
+          items[off++] = SeedItem{b, 0, 0.0, 0, kItMark};
         }
-        items[off++] = SeedItem{b, 0, 0.0, 0, kItMark};
+        run = T.opaque ? part_empty() : T.t;
+        lastH = b;
+      } else {
+        run = part_compose(run, T.t);
       }
-      run = T.opaque ? part_empty() : T.t;
-      lastH = b;
-    } else {
-      run = part_compose(run, T.t);
+      scan[b] = SegScan{run, lastH};
     }
-    scan[b] = SegScan{run, lastH};
   }
   if (t == 0) {
     if (!over) {

@@ -125,7 +125,8 @@ def dramstep(ddir, marker, prefix, skip, config, n_local, dominant=None):
                 rd += rows[i][1]
                 wr += rows[i][2]
                 if len(steps) >= skip:
-                    per_kernel.setdefault(rows[i][0].split("(")[0], []).append(rows[i][1] + rows[i][2])
+                    key = rows[i][0].replace("(anonymous namespace)::", "").split("(")[0]
+                    per_kernel.setdefault(key, []).append(rows[i][1] + rows[i][2])
         steps.append((rd, wr))
     kept = steps[skip:]
     for j, (rd, wr) in enumerate(steps):
