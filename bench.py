@@ -330,14 +330,21 @@ F64_CFG = (10_000_000, 5, "F64 leg: 10M files x d=5 min-max-normalised features 
                           "2^-S grid: src/main.py:81 data), k={k}")
 
 
-def f64_data(n: int, d: int, k: int, seed: int):
+def f64_data(n: int, d: int, k: int, seed: int, device_index: int = 0):
     """Blob data min-max normalised per column as src/main.py:81 does (values
-    off any 2^-S grid, so the points load in F64 mode)."""
+    off any 2^-S grid, so the points load in F64 mode).  The blobs come from
+    the library's own device generator (cdr_points_generate: the
+    oracle/synth.py formula) and are read back for the host normalisation."""
     import numpy as np
 
-    from oracle import synth
+    import _cdr
 
-    X = synth.generate(n, 0, n, d, k, seed)
+    g = _cdr.Context(device_index)
+    try:
+        g.generate_points(n, 0, n, d, k, seed)
+        X = g.get_rows(np.arange(n, dtype=np.int64))
+    finally:
+        g.close()
     mn, mx = X.min(axis=0), X.max(axis=0)
     return (X - mn) / (mx - mn)
 
@@ -360,7 +367,7 @@ def f64_bench(args, world: int, rank: int, dist, device, json_fd) -> dict:
         n = args.n_total
     k = args.k or 16
     n_total = n * world if args.scaling == "weak" else n
-    X = f64_data(n_total, d, k, args.seed)
+    X = f64_data(n_total, d, k, args.seed, int(os.environ.get("LOCAL_RANK", "0")))
     ctx = _cdr.Context(int(os.environ.get("LOCAL_RANK", "0")))
     comm = None
     if dist is not None and world > 1:

@@ -77,13 +77,21 @@ constexpr int kSeedBlock = 8192;  // NumPy reduction buffer (add.reduce chunk)
 // slice b % kRunSlices: 1/16 of the atomic contention); readers sum them.
 constexpr int kRunSlices = 16;
 
-// Point layout in HBM ("quad-interleaved SoA"): features are grouped in quads;
-// quad q of point i is 4 consecutive values at ((q * n_pad) + i) * 4.  One
-// 16-byte load gives a lane four features of one point, and a wave reading
-// quad q of 64 consecutive points reads 1 KiB contiguously.  d is padded to
-// d4 = ceil(d/4)*4 with zero features.
-__host__ __device__ __forceinline__ int64_t xidx(int64_t f, int64_t i, int64_t n_pad) {
+// Point layout in HBM.  F32X points (float, x32): "quad-interleaved SoA",
+// features grouped in quads; quad q of point i is 4 consecutive values at
+// ((q * n_pad) + i) * 4.  One 16-byte load gives a lane four features of one
+// point, and a wave reading quad q of 64 consecutive points reads 1 KiB
+// contiguously.  d is padded to d4 = ceil(d/4)*4 with zero features.
+// F64 points (double, x64): planar, feature f of point i at f * n_pad + i.
+// The F64 kernels read a point's features one at a time, and in quads the
+// zero padding (d = 5 -> 8) made every pass over the points read 64 bytes per
+// point for 40.  The index follows the element type, so a kernel templated on
+// it indexes either copy.
+__host__ __device__ __forceinline__ int64_t xidx(const float*, int64_t f, int64_t i, int64_t n_pad) {
   return (((f >> 2) * n_pad) + i) * 4 + (f & 3);
+}
+__host__ __device__ __forceinline__ int64_t xidx(const double*, int64_t f, int64_t i, int64_t n_pad) {
+  return f * n_pad + i;
 }
 __host__ __device__ __forceinline__ int d4_of(int d) { return (d + 3) & ~3; }
 constexpr int kPointGroup = 64;   // points per wave iteration in the screen
@@ -116,7 +124,7 @@ struct Ctx {
   int32_t mode = 0;        // CDR_MODE_*
   int32_t scale_bits = 0;  // F32X fixed-point scale S
   DevBuf x32;              // F32X: float  [d4/4][n_pad][4]   (xidx)
-  DevBuf x64;              // F64 : double [d4/4][n_pad][4]   (xidx)
+  DevBuf x64;              // F64 : double [d4][n_pad] planar  (xidx)
   std::vector<double> fmin, fmax;  // per-feature min / max (host)
   // this shard's statistics (run_stats layout, 2d + 3 words): kept so that a
   // sharded caller can combine them over the ranks (cdr_points_restat)

@@ -1,7 +1,7 @@
 // cdr_runtime.hip — context, buffers, point loading / generation and the C ABI
 // entry points of libcdr.so (declared in include/cdr.h).
 //
-// Point layout in HBM: quad-interleaved structure of arrays (xidx() in
+// Point layout in HBM: F32X quad-interleaved structure of arrays, F64 planar (xidx() in
 // cdr_internal.h), padded to a multiple of 8192 points (the NumPy reduction
 // block, see seeding).  Rows i >= n and features f >= d are zero and never
 // produce labels, sums or probabilities.
@@ -77,7 +77,7 @@ __global__ void stats_kernel(const T* __restrict__ X, int64_t n, int64_t n_pad,
   int not32 = 0, nonfin = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    double v = (double)X[xidx(f, i, n_pad)];
+    double v = (double)X[xidx(X, f, i, n_pad)];
     if (!isfinite(v)) {
       nonfin = 1;
       continue;
@@ -113,22 +113,28 @@ __global__ void rowmajor_to_soa64(const double* __restrict__ src, int64_t rows,
        t < rows * d; t += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = t / d;
     int f = (int)(t - r * d);
-    dst[xidx(f, row0 + r, n_pad)] = src[t];
+    dst[xidx(dst, f, row0 + r, n_pad)] = src[t];
   }
 }
 
-__global__ void soa32_to_soa64(const float* __restrict__ src, int64_t count,
+// Between the two layouts (xidx): element t of the quad layout (x32) is
+// feature 4 (t / (4 n_pad)) + t % 4 of point (t / 4) % n_pad; count = d4 n_pad.
+__global__ void soa32_to_soa64(const float* __restrict__ src, int64_t count, int64_t n_pad,
                                double* __restrict__ dst) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count;
-       t += (int64_t)gridDim.x * blockDim.x)
-    dst[t] = (double)src[t];
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = t / (4 * n_pad), r = t - q * 4 * n_pad;
+    dst[xidx(dst, 4 * q + (r & 3), r >> 2, n_pad)] = (double)src[t];
+  }
 }
 
-__global__ void soa64_to_soa32(const double* __restrict__ src, int64_t count,
+__global__ void soa64_to_soa32(const double* __restrict__ src, int64_t count, int64_t n_pad,
                                float* __restrict__ dst) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count;
-       t += (int64_t)gridDim.x * blockDim.x)
-    dst[t] = (float)src[t];
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = t / (4 * n_pad), r = t - q * 4 * n_pad;
+    dst[t] = (float)src[xidx(src, 4 * q + (r & 3), r >> 2, n_pad)];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -164,7 +170,7 @@ __global__ void generate_kernel(float* __restrict__ X, int64_t row_begin,
                         (int64_t)((hn >> 32) & 0xFFFF) + (int64_t)(hn >> 48);
       int64_t u = center + 13 * (s - 131070);
       u = u < 0 ? 0 : (u > 0xFFFFFF ? 0xFFFFFF : u);
-      X[xidx(f, i, n_pad)] = (float)u * (1.0f / 16777216.0f);
+      X[xidx(X, f, i, n_pad)] = (float)u * (1.0f / 16777216.0f);
     }
   }
 }
@@ -283,7 +289,7 @@ static void decide_mode(Ctx& c, const std::vector<unsigned long long>& st,
     c.x32.ensure(sizeof(float) * (size_t)d4_of(d) * c.n_pad);
     hipLaunchKernelGGL(soa64_to_soa32, dim3(grid_for((int64_t)d4_of(d) * c.n_pad, 256)),
                        dim3(256), 0, c.stream, c.x64.as<double>(),
-                       (int64_t)d4_of(d) * c.n_pad, c.x32.as<float>());
+                       (int64_t)d4_of(d) * c.n_pad, c.n_pad, c.x32.as<float>());
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(c.stream));
     c.x64.release();
@@ -376,7 +382,7 @@ __global__ void gather_rows_kernel(const float* __restrict__ x32,
     int64_t r = t / d;
     int f = (int)(t - r * d);
     int64_t i = idx[r];
-    out[t] = x32 ? (double)x32[xidx(f, i, n_pad)] : x64[xidx(f, i, n_pad)];
+    out[t] = x32 ? (double)x32[xidx(x32, f, i, n_pad)] : x64[xidx(x64, f, i, n_pad)];
   }
 }
 
@@ -535,7 +541,7 @@ int cdr_points_restat(cdr_ctx* h, const uint64_t* st, int64_t n_sum) {
     const int64_t cnt = (int64_t)d4_of(d) * c.n_pad;
     c.x64.ensure(sizeof(double) * (size_t)cnt);
     hipLaunchKernelGGL(soa32_to_soa64, dim3(grid_for(cnt, 256)), dim3(256), 0, c.stream,
-                       c.x32.as<float>(), cnt, c.x64.as<double>());
+                       c.x32.as<float>(), cnt, c.n_pad, c.x64.as<double>());
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(c.stream));
     c.x32.release();

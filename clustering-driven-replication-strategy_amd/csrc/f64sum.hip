@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kFB) void f64_blocksum(const T* __restrict__ X, int
   if (row < n) {
     const int j = labels[row];
     atomicAdd(&c[j], 1u);
-    for (int f = 0; f < d; ++f) atomicAdd(&tab[j * d + f], (double)X[xidx(f, row, n_pad)]);
+    for (int f = 0; f < d; ++f) atomicAdd(&tab[j * d + f], (double)X[xidx(X, f, row, n_pad)]);
   }
   __syncthreads();
   // sequence-major ([cluster * d + feature][block], [cluster][block]): the
@@ -284,14 +284,14 @@ __global__ __launch_bounds__(256) void f64_transfer(const S* __restrict__ X, int
 #pragma unroll
       for (int u = 0; u < kCh; ++u) {
         jj[u] = labels[rc + u];
-        xx[u] = (double)X[xidx(f, rc + u, n_pad)];
+        xx[u] = (double)X[xidx(X, f, rc + u, n_pad)];
       }
     } else {
 #pragma unroll
       for (int u = 0; u < kCh; ++u) {
         const int64_t row = rc + u;
         jj[u] = row < r1 ? labels[row] : -1;
-        xx[u] = row < r1 ? (double)X[xidx(f, row, n_pad)] : 0.0;
+        xx[u] = row < r1 ? (double)X[xidx(X, f, row, n_pad)] : 0.0;
       }
     }
   };
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256) void f64_walk(const S* __restrict__ X, int64_t
       for (int q = 0; q < 4; ++q) {
         const int64_t row = r0 + 64 * q + lane;
         lj[q] = row < n ? labels[row] : -1;
-        lx[q] = row < n ? (double)X[xidx(f, row, n_pad)] : 0.0;
+        lx[q] = row < n ? (double)X[xidx(X, f, row, n_pad)] : 0.0;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -814,7 +814,7 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
   double xr[D];
   if (row < n) {
 #pragma unroll
-    for (int f = 0; f < D; ++f) xr[f] = X[xidx(f, row, n_pad)];
+    for (int f = 0; f < D; ++f) xr[f] = X[xidx(X, f, row, n_pad)];
   }
   // the centroids in LDS: fp64 for the exact pass, fp32 and their fp32
   // squared norms for the screen (k <= 16, every value 0 or within
@@ -928,7 +928,7 @@ __global__ __launch_bounds__(kFB) void f64_transfer_block(const S* __restrict__ 
   const int64_t row = b * kFB + t;
   const bool in = row < n;
   const int lj = in ? labels[row] : -1;
-  for (int f = 0; f < d; ++f) tsx[f * kFB + t] = in ? (double)X[xidx(f, row, n_pad)] : 0.0;
+  for (int f = 0; f < d; ++f) tsx[f * kFB + t] = in ? (double)X[xidx(X, f, row, n_pad)] : 0.0;
   wcnt[t] = 0;  // (4 x 64 = kFB)
   if (t < k) off[t + 1] = (int)cnt[(int64_t)t * nb + b];
   __syncthreads();
@@ -1013,7 +1013,7 @@ __global__ __launch_bounds__(256) void f64_transfer_sorted(const S* __restrict__
     for (int u = 0; u < 16; ++u) {
       const unsigned word = u < 4 ? oq.x : u < 8 ? oq.y : u < 12 ? oq.z : oq.w;
       const int r = (int)((word >> (8 * (u & 3))) & 255u);
-      xv[u] = c0 + u < nrow ? (double)X[xidx(f, r0 + r, n_pad)] : 0.0;
+      xv[u] = c0 + u < nrow ? (double)X[xidx(X, f, r0 + r, n_pad)] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -1413,7 +1413,7 @@ __global__ __launch_bounds__(256) void f64s_program(const double* __restrict__ X
         for (int q = 0; q < 4; ++q) {
           const int64_t row = r0 + 64 * q + lane;
           lj[q] = row < n ? labels[row] : -1;
-          lx[q] = row < n ? (double)X[xidx(f, row, n_pad)] : 0.0;
+          lx[q] = row < n ? (double)X[xidx(X, f, row, n_pad)] : 0.0;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {

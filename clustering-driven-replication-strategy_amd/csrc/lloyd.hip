@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void screen_kernel(ScreenArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int f = 16 * c + 4 * g + i;
-          xr[p][c][i] = fok[c][i] ? a.X[xidx(f, base + 16 * p + col, a.n_pad)] : 0.0f;
+          xr[p][c][i] = fok[c][i] ? a.X[xidx(a.X, f, base + 16 * p + col, a.n_pad)] : 0.0f;
         }
     if (a.ablate & 8) {
 #pragma unroll
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(256) void fallback_exact_wave(
   if (cnt > 0) {
     chunk = lst[lane < cnt ? lane : 0];
     pt = __builtin_amdgcn_readfirstlane(chunk);
-    if (lane < d) xf = X[xidx(lane, pt, n_pad)];
+    if (lane < d) xf = X[xidx(X, lane, pt, n_pad)];
   }
   for (int e = 0; e < cnt; ++e) {
     const int64_t cpt = pt;
@@ -685,7 +685,7 @@ __global__ __launch_bounds__(256) void fallback_exact_wave(
       const int e1 = e + 1;
       if ((e1 & 63) == 0) chunk = lst[e1 + lane < cnt ? e1 + lane : e1];
       pt = __builtin_amdgcn_readlane(chunk, e1 & 63);
-      if (lane < d) xf = X[xidx(lane, pt, n_pad)];
+      if (lane < d) xf = X[xidx(X, lane, pt, n_pad)];
     }
     auto xv = [&](int f) { return (double)__int_as_float(__builtin_amdgcn_readlane(cx, f)); };
     double rb = INFINITY;
@@ -726,7 +726,7 @@ __global__ void assign_exact_all(const T* __restrict__ X, int64_t n, int64_t n_p
                                  int32_t* __restrict__ labels) {
   for (int64_t pt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pt < n;
        pt += (int64_t)gridDim.x * blockDim.x) {
-    auto xv = [&](int f) { return (double)X[xidx(f, pt, n_pad)]; };
+    auto xv = [&](int f) { return (double)X[xidx(X, f, pt, n_pad)]; };
     labels[pt] = exact_argmin(xv, C, k, d);
   }
 }
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(256) void assign_exact_d(const T* __restrict__ X, i
        pt += (int64_t)gridDim.x * blockDim.x) {
     double xr[D];
 #pragma unroll
-    for (int f = 0; f < D; ++f) xr[f] = (double)X[xidx(f, pt, n_pad)];
+    for (int f = 0; f < D; ++f) xr[f] = (double)X[xidx(X, f, pt, n_pad)];
     labels[pt] = exact_argmin([&](int f) { return xr[f]; }, C, k, D);
   }
 }
@@ -782,7 +782,7 @@ __global__ __launch_bounds__(256) void update_from_labels_f32x(
     const int j = labels[pt];
     unsigned long long* row = tbl + (size_t)j * kd1;
     for (int f = 0; f < d; ++f)
-      atomicAdd(&row[f], (unsigned long long)(long long)(int)(X[xidx(f, pt, n_pad)] * fx));
+      atomicAdd(&row[f], (unsigned long long)(long long)(int)(X[xidx(X, f, pt, n_pad)] * fx));
     atomicAdd(&row[d], 1ull);
   }
   __syncthreads();
@@ -806,7 +806,7 @@ __global__ void seq_sums_f64(const double* __restrict__ X, int64_t n, int64_t n_
     counts[j] = c;
     return;
   }
-  auto col = [&](int64_t i) { return X[xidx(f, i, n_pad)]; };
+  auto col = [&](int64_t i) { return X[xidx(X, f, i, n_pad)]; };
   if (d >= 2) {
     double s = 0.0;
     for (int64_t i = 0; i < n; ++i)
@@ -1541,9 +1541,9 @@ __global__ __launch_bounds__(256) void f32r_assign_kernel(const S* __restrict__ 
     float xr[D ? D : 1];
     if constexpr (D > 0) {
 #pragma unroll
-      for (int f = 0; f < D; ++f) xr[f] = (float)X[xidx(f, pt, n_pad)];
+      for (int f = 0; f < D; ++f) xr[f] = (float)X[xidx(X, f, pt, n_pad)];
     }
-    auto xv = [&](int f) { return D ? xr[D ? f : 0] : (float)X[xidx(f, pt, n_pad)]; };
+    auto xv = [&](int f) { return D ? xr[D ? f : 0] : (float)X[xidx(X, f, pt, n_pad)]; };
     float Rb = INFINITY, rb = INFINITY;
     int jb = 0;
     for (int j = 0; j < k; ++j) {
@@ -1573,7 +1573,7 @@ __global__ void f32r_seq_sums(const S* __restrict__ X, int64_t n, int64_t n_pad,
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= k * d) return;
   const int j = t / d, f = t % d;
-  auto col = [&](int64_t i) { return (float)X[xidx(f, i, n_pad)]; };
+  auto col = [&](int64_t i) { return (float)X[xidx(X, f, i, n_pad)]; };
   if (d >= 2) {
     float s = 0.0f;
     bool any = false;

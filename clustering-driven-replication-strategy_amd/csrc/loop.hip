@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void sqdev_kernel(const float* __restrict__ X,
        i += (int64_t)gridDim.x * blockDim.x) {
     double p = 0.0;
     for (int f = 0; f < d; ++f) {
-      const double v = (double)X[xidx(f, i, n_pad)] - ref[f];
+      const double v = (double)X[xidx(X, f, i, n_pad)] - ref[f];
       p += v * v;
     }
     s += p;

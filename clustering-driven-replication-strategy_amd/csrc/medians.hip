@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void mg_scatter(const V* __restrict__ X, int64
     const int pi = p0 + sub;
     if (pi >= np) continue;
     V* dst = rows + (int64_t)pos[pi] * d;
-    for (int f = fl; f < d; f += D2) dst[f] = X[xidx(f, i0 + pi, n_pad)];
+    for (int f = fl; f < d; f += D2) dst[f] = X[xidx(X, f, i0 + pi, n_pad)];
   }
 }
 

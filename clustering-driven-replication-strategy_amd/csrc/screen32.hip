@@ -650,7 +650,7 @@ __global__ void split_copy_kernel(const float* __restrict__ x, int64_t n, int64_
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int f = 4 * (QH * h + u) + c;
-        xt[c] = (f < d && i < n) ? fmaf(x[xidx(f, i, n_pad)], sig, ms[f]) : 0.0f;
+        xt[c] = (f < d && i < n) ? fmaf(x[xidx(x, f, i, n_pad)], sig, ms[f]) : 0.0f;
       }
       split4(xt, hw[2 * u], hw[2 * u + 1], lw[2 * u], lw[2 * u + 1]);
     }

@@ -931,7 +931,7 @@ __global__ __launch_bounds__(64) void exact_big(const float* __restrict__ X, int
   for (int e = blockIdx.x; e < total; e += gridDim.x) {
     const int64_t pt = list[e];
     __syncthreads();
-    for (int f = lane; f < d; f += 64) sx[f] = (double)X[xidx(f, pt, n_pad)];
+    for (int f = lane; f < d; f += 64) sx[f] = (double)X[xidx(X, f, pt, n_pad)];
     __syncthreads();
     double rb = INFINITY;
     int jmin = 0x7fffffff;

@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
           const double old = dmin[i];
           v = old;
           if (cidx == 0 || !seed_prunable(ccd[near[i]], old)) {
-            auto xv = [&](int f) { return (double)X[xidx(f, i, n_pad)]; };
+            auto xv = [&](int f) { return (double)X[xidx(X, f, i, n_pad)]; };
             auto cv = [&](int f) { return cen[f]; };
             const double R = np_sqdist(xv, cv, d);
             const double r = sqrt(R);
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void seed16_pack_kernel(const float* __restric
       for (int j = 0; j < 8; ++j) {
         const int f = 8 * g + j;
         double v = 0.0;
-        if (f < d && i < n) v = ((double)x32[xidx(f, i, n_pad)] - (double)mu[f]) * scale;
+        if (f < d && i < n) v = ((double)x32[xidx(x32, f, i, n_pad)] - (double)mu[f]) * scale;
         const __half h = __float2half_rn((float)v);
         const double dv = v - (double)__half2float(h);
         err += dv * dv;
@@ -1797,7 +1797,7 @@ __global__ __launch_bounds__(64) void seed_gather_kernel(const float* __restrict
     }
   }
   for (int f = threadIdx.x; f < d; f += 64)
-    out[f] = x32 ? (double)x32[xidx(f, i, n_pad)] : x64[xidx(f, i, n_pad)];
+    out[f] = x32 ? (double)x32[xidx(x32, f, i, n_pad)] : x64[xidx(x64, f, i, n_pad)];
 }
 
 // ---------------------------------------------------------------------------
@@ -2455,7 +2455,7 @@ __global__ __launch_bounds__(64) void shard_red_kernel(const float* __restrict__
   int64_t i = hit[0];
   if (i == 0 && u && sc[kSsMine] / sc[kSsLast] > u[0]) i = -1;
   for (int f = threadIdx.x; f < d; f += 64)
-    red[f] = i < 0 ? 0.0 : x32 ? (double)x32[xidx(f, i, n_pad)] : x64[xidx(f, i, n_pad)];
+    red[f] = i < 0 ? 0.0 : x32 ? (double)x32[xidx(x32, f, i, n_pad)] : x64[xidx(x64, f, i, n_pad)];
   if (threadIdx.x == 0) {
     red[d] = i < 0 ? 0.0 : (double)(row_begin + i + 1);
     // own program run from the composed start must end where the composition did
@@ -2710,7 +2710,7 @@ __global__ __launch_bounds__(256) void f32r_min_kernel(const S* __restrict__ X, 
   bool inf = false;
   for (int64_t pt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pt < n;
        pt += (int64_t)gridDim.x * blockDim.x) {
-    auto xv = [&](int f) { return (float)X[xidx(f, pt, n_pad)]; };  // exact: fp32 values
+    auto xv = [&](int f) { return (float)X[xidx(X, f, pt, n_pad)]; };  // exact: fp32 values
     auto cv = [&](int f) { return cen[f]; };
     const float R = np_sqdist<decltype(xv), decltype(cv), float>(xv, cv, dd);
     const float t = (float)sqrt((double)R);  // = the correctly rounded fp32 sqrt
@@ -2846,7 +2846,7 @@ __global__ __launch_bounds__(64) void f32r_gather_kernel(const float* __restrict
   int64_t p = pick[0];
   if (p < 0 || p >= n_pad) p = 0;
   for (int f = threadIdx.x; f < d; f += 64)
-    cen[f] = x32 ? x32[xidx(f, p, n_pad)] : (float)x64[xidx(f, p, n_pad)];
+    cen[f] = x32 ? x32[xidx(x32, f, p, n_pad)] : (float)x64[xidx(x64, f, p, n_pad)];
 }
 // dist_sq.sum() in fp32: the chunk sums from 0, left to right (one lane:
 // the additions are sequential), and the step's verdict as Generator.choice
