@@ -503,46 +503,59 @@ __global__ __launch_bounds__(kGbThreads) void gb_hist2(const T* __restrict__ in,
 // Pass 3 (large file counts): the R regions of pass 2 (bases bbase[0..R])
 // become the regions pass 3 splits; tstart[r] = the 8192-event tiles before
 // region r (exclusive scan of ceil(size / tile)), tstart[R] and *tot the
-// total.  One workgroup of 1024 threads, each a contiguous run of regions.
-__global__ __launch_bounds__(1024) void gb_tilestart3(const unsigned* __restrict__ bbase, int R,
-                                                      int* __restrict__ tstart,
-                                                      long long* __restrict__ tot) {
-  __shared__ unsigned wsum[16];
+// total.  Two launches of kGbT3Per regions per workgroup, one region per
+// thread: gb_tilecount3 sums each workgroup's tile counts, gb_tilestart3 adds
+// the earlier workgroups' sums and scans its own regions.  (One workgroup
+// walking all 2^18 regions of the 1B-event log took 0.43 ms per step.)
+constexpr int kGbT3Per = 1024;
+__device__ __forceinline__ unsigned gb_tiles_of(const unsigned* __restrict__ bbase, int r, int R) {
+  return r < R ? (bbase[r + 1] - bbase[r] + kGbTile - 1) / kGbTile : 0u;
+}
+__global__ __launch_bounds__(kGbT3Per) void gb_tilecount3(const unsigned* __restrict__ bbase, int R,
+                                                          unsigned* __restrict__ wsum) {
+  __shared__ unsigned ws[kGbT3Per / 64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int per = (R + 1023) / 1024, lo = t * per, hi = min(lo + per, R);
-  unsigned s = 0;
-  for (int r0 = lo; r0 < hi; r0 += 16) {  // 17 bases in flight per batch
-    unsigned v[17];
-#pragma unroll
-    for (int j = 0; j < 17; ++j) v[j] = r0 + j <= R ? bbase[r0 + j] : 0u;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (r0 + j < hi) s += (v[j + 1] - v[j] + kGbTile - 1) / kGbTile;
+  unsigned c = gb_tiles_of(bbase, blockIdx.x * kGbT3Per + t, R);
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if (lane == 0) ws[w] = c;
+  __syncthreads();
+  if (t == 0) {
+    unsigned s = 0;
+    for (int i = 0; i < kGbT3Per / 64; ++i) s += ws[i];
+    wsum[blockIdx.x] = s;
   }
-  unsigned inc = s;
+}
+__global__ __launch_bounds__(kGbT3Per) void gb_tilestart3(const unsigned* __restrict__ bbase, int R,
+                                                          const unsigned* __restrict__ wsum,
+                                                          int* __restrict__ tstart,
+                                                          long long* __restrict__ tot) {
+  __shared__ unsigned wb[kGbT3Per / 64], wi[kGbT3Per / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // this workgroup's base: the earlier workgroups' tile sums (a share per
+  // wave, added up below)
+  unsigned bs = 0;
+  for (int i = t; i < (int)blockIdx.x; i += kGbT3Per) bs += wsum[i];
+  for (int o = 32; o > 0; o >>= 1) bs += __shfl_xor(bs, o);
+  // its regions' tile counts, scanned by waves and then across them
+  const int r = blockIdx.x * kGbT3Per + t;
+  const unsigned c = gb_tiles_of(bbase, r, R);
+  unsigned inc = c;
   for (int o = 1; o < 64; o <<= 1) {
     const unsigned u = __shfl_up(inc, o);
     if (lane >= o) inc += u;
   }
-  if (lane == 63) wsum[w] = inc;
+  if (lane == 0) wb[w] = bs;
+  if (lane == 63) wi[w] = inc;
   __syncthreads();
-  unsigned run = inc - s;
-  for (int i = 0; i < w; ++i) run += wsum[i];
-  for (int r0 = lo; r0 < hi; r0 += 16) {
-    unsigned v[17];
-#pragma unroll
-    for (int j = 0; j < 17; ++j) v[j] = r0 + j <= R ? bbase[r0 + j] : 0u;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (r0 + j < hi) {
-        tstart[r0 + j] = (int)run;
-        run += (v[j + 1] - v[j] + kGbTile - 1) / kGbTile;
-      }
-    }
+  unsigned run = inc - c;
+  for (int i = 0; i < kGbT3Per / 64; ++i) {
+    run += wb[i];             // the earlier workgroups' tiles
+    if (i < w) run += wi[i];  // the earlier waves' regions
   }
-  if (t == 1023) {
-    tstart[R] = (int)run;
-    *tot = run;
+  if (r < R) tstart[r] = (int)run;
+  if (r == R - 1) {
+    tstart[R] = (int)(run + c);
+    *tot = (long long)(run + c);
   }
 }
 
@@ -1385,10 +1398,14 @@ void gb_run(Ctx& c, int64_t ne, int64_t nf, int fbits, int L, int B1, int B2, in
     // regions take the place of pass 1's digits); output into p1's buffer
     const int R12 = R1 * R2, R3 = 1 << B3;
     const int shift3 = p.fshift + L;
-    c.gb_t3.ensure(sizeof(int) * ((size_t)R12 + 1) + 64);
+    const int g3 = (R12 + kGbT3Per - 1) / kGbT3Per;
+    c.gb_t3.ensure(sizeof(int) * ((size_t)R12 + 1 + g3) + 64);
     int* tstart3 = c.gb_t3.as<int>();
+    unsigned* wsum3 = reinterpret_cast<unsigned*>(tstart3 + R12 + 1);  // (after the starts)
     long long* tot3 = reinterpret_cast<long long*>(c.gb_res.as<long long>() + 6);
-    hipLaunchKernelGGL(gb_tilestart3, dim3(1), dim3(1024), 0, c.stream, bbase, R12, tstart3, tot3);
+    hipLaunchKernelGGL(gb_tilecount3, dim3(g3), dim3(kGbT3Per), 0, c.stream, bbase, R12, wsum3);
+    hipLaunchKernelGGL(gb_tilestart3, dim3(g3), dim3(kGbT3Per), 0, c.stream, bbase, R12, wsum3,
+                       tstart3, tot3);
     HIP_CHECK(hipGetLastError());
     long long T3 = 0;
     HIP_CHECK(hipMemcpyAsync(&T3, tot3, sizeof(T3), hipMemcpyDeviceToHost, c.stream));
