@@ -182,6 +182,7 @@ struct Ctx {
   DevBuf f64x_E2;
   DevBuf f64x_GC;  // f64_step_fused: per (cluster, group of 64 blocks) member counts
   DevBuf f64x_ord;  // f64_step_fused: each block's rows in cluster order (uint8 offsets)
+  DevBuf f64x_cs;   // f64_cent_prep: the screen's fp32 centroid rows + norms, then its ok flag
   DevBuf f64s_off;  // sharded F64 sums: earlier shards' approximate totals, end binades
   int32_t f64s_k = 0, f64s_nranks = 0, f64s_rank = 0;  // cdr_f64s_begin's step
   bool f64x_e_ok = false;

@@ -37,6 +37,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 #include "cdr_internal.h"
@@ -772,6 +773,40 @@ __device__ __forceinline__ int f64_screen_argmin(const double (&xr)[D], const do
   return jb;
 }
 
+// The screen's centroid table for one step (every f64_assign_block workgroup
+// staged it in LDS before): the fp32 rows with their fp32 squared norms, as
+// f64_screen_argmin reads them, and ok[0] = 1 when the screen applies (k <= 16,
+// every value 0 or within [2^-60, 2^60]).  The assignment reads the rows with
+// uniform addresses, i.e. scalar loads, instead of 32 LDS reads per row.
+template <int D>
+__global__ __launch_bounds__(64) void f64_cent_prep(const double* __restrict__ C, int k,
+                                                    float* __restrict__ cs32, int* __restrict__ ok) {
+  constexpr int DP = F64ScrRow<D>::P;
+  const int t = threadIdx.x;
+  bool bad = k > kF64ScrK;
+  if (t < kF64ScrK) {
+    float row[DP];
+#pragma unroll
+    for (int q = 0; q < DP; ++q) row[q] = 0.0f;
+    if (t < k) {
+#pragma unroll
+      for (int f = 0; f < D; ++f) {
+        const double v = C[t * D + f];
+        row[f] = (float)v;
+        bad |= !f64_screen_ok(v);
+      }
+      float sq = 0.0f;
+#pragma unroll
+      for (int f = 0; f < D; ++f) sq = fmaf(row[f], row[f], sq);
+      row[D] = sq;
+    }
+#pragma unroll
+    for (int q = 0; q < DP; ++q) cs32[t * DP + q] = row[q];
+  }
+  const bool any_bad = __ballot(bad) != 0ull;
+  if (t == 0) ok[0] = any_bad ? 0 : 1;
+}
+
 // F64 mode, the assignment fused with the block pass (one workgroup per
 // block of kFB rows): labels (exact_argmin, src/kmeans_plusplus.py:33-34),
 // the block's approximate sums and exact counts in f64_blocksum's layout,
@@ -790,7 +825,9 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
                                                         const int* __restrict__ Eprev,
                                                         Xfer* __restrict__ T,
                                                         unsigned char* __restrict__ ordr,
-                                                        const long long* __restrict__ gate) {
+                                                        const long long* __restrict__ gate,
+                                                        const float* __restrict__ cs32g,
+                                                        const int* __restrict__ scr_ok) {
   // (the device-resident F64 run: a stopped run keeps the labels of the
   // assignment that stopped it)
   if (gate && gate[0] == 0) return;
@@ -816,31 +853,14 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
 #pragma unroll
     for (int f = 0; f < D; ++f) xr[f] = X[xidx(X, f, row, n_pad)];
   }
-  // the centroids in LDS: fp64 for the exact pass, fp32 and their fp32
-  // squared norms for the screen (k <= 16, every value 0 or within
-  // [2^-60, 2^60]: see f64_screen_argmin)
-  constexpr int DP = F64ScrRow<D>::P;
-  __shared__ double cs64[kF64ScrK * D];
-  __shared__ __attribute__((aligned(16))) float cs32[kF64ScrK * DP];
-  bool cbad = k > kF64ScrK;
-  for (int i = threadIdx.x; i < k * D && !cbad; i += kFB) {
-    const double v = C[i];
-    cs64[i] = v;
-    cs32[(i / D) * DP + i % D] = (float)v;
-    cbad |= !f64_screen_ok(v);
-  }
-  const bool scr = !__syncthreads_or(cbad);  // (block-uniform)
-  if (scr && threadIdx.x < k) {
-    float sq = 0.0f;
-#pragma unroll
-    for (int f = 0; f < D; ++f) sq = fmaf(cs32[threadIdx.x * DP + f], cs32[threadIdx.x * DP + f], sq);
-    cs32[threadIdx.x * DP + D] = sq;
-  }
-  __syncthreads();
+  // the screen's table (f64_cent_prep: fp32 rows and their fp32 squared
+  // norms, read with uniform addresses) and the fp64 centroids for its
+  // candidates, straight from global memory
+  __syncthreads();  // (the zeroed tables)
   int j = -1;
   if (row < n) {
-    j = scr ? f64_screen_argmin<D>(xr, cs64, cs32, k)
-            : exact_argmin([&](int f) { return xr[f]; }, C, k, D);
+    j = scr_ok[0] ? f64_screen_argmin<D>(xr, C, cs32g, k)
+                  : exact_argmin([&](int f) { return xr[f]; }, C, k, D);
     labels[row] = j;
   }
   if constexpr (XF) {
@@ -1160,6 +1180,24 @@ bool f64_sums_parallel(Ctx& c, int k, double* d_sums, bool pre) {
 // predictions for this (k, n) — the transfers), the cluster counts, the new
 // predictions, the transfers otherwise, groups and walk.  false: shape not
 // covered (d > 16, d < 2, k > 64), nothing launched.
+// The step's screen table (f64_cent_prep) into c.f64x_cs; returns {rows, ok}.
+static std::pair<const float*, const int*> f64_cent_table(Ctx& c, int d, int k, const double* dC) {
+  constexpr int kRows = kF64ScrK * 20;  // (DP <= 20 floats at d <= 16)
+  c.f64x_cs.ensure(sizeof(float) * kRows + 64);
+  float* cs = c.f64x_cs.as<float>();
+  int* ok = reinterpret_cast<int*>(cs + kRows);
+  typedef void (*Pf)(const double*, int, float*, int*);
+#define CDR_FCP(D_) f64_cent_prep<D_>
+  static const Pf pfn[17] = {nullptr,     CDR_FCP(1),  CDR_FCP(2),  CDR_FCP(3),  CDR_FCP(4),
+                             CDR_FCP(5),  CDR_FCP(6),  CDR_FCP(7),  CDR_FCP(8),  CDR_FCP(9),
+                             CDR_FCP(10), CDR_FCP(11), CDR_FCP(12), CDR_FCP(13), CDR_FCP(14),
+                             CDR_FCP(15), CDR_FCP(16)};
+#undef CDR_FCP
+  hipLaunchKernelGGL(pfn[d], dim3(1), dim3(64), 0, c.stream, dC, k, cs, ok);
+  HIP_CHECK(hipGetLastError());
+  return {cs, ok};
+}
+
 bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
                     unsigned long long* d_counts, bool prof, const long long* gate) {
   const int d = c.d;
@@ -1189,7 +1227,8 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
     ordr = c.f64x_ord.as<unsigned char>();
   }
   typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
-                     unsigned*, const int*, Xfer*, unsigned char*, const long long*);
+                     unsigned*, const int*, Xfer*, unsigned char*, const long long*, const float*,
+                     const int*);
 #define CDR_FAB(D_) f64_assign_block<D_, false>, f64_assign_block<D_, true>
   static const Fn fns[17][2] = {{nullptr, nullptr}, {CDR_FAB(1)},  {CDR_FAB(2)},  {CDR_FAB(3)},
                                 {CDR_FAB(4)},       {CDR_FAB(5)},  {CDR_FAB(6)},  {CDR_FAB(7)},
@@ -1197,10 +1236,11 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
                                 {CDR_FAB(12)},      {CDR_FAB(13)}, {CDR_FAB(14)}, {CDR_FAB(15)},
                                 {CDR_FAB(16)}};
 #undef CDR_FAB
+  const auto ctab = f64_cent_table(c, d, k, dC);
   hipLaunchKernelGGL(fns[d][xf ? 1 : 0], dim3((unsigned)nb), dim3(kFB), 0, c.stream,
                      c.x64.as<double>(), n, c.n_pad, dC, k, c.labels.as<int32_t>(),
                      c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), Ecur, c.f64x_T.as<Xfer>(),
-                     ordr, gate);
+                     ordr, gate, ctab.first, ctab.second);
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
   // (the counts: written by f64_predict_b from f64_predict_a's group counts)
@@ -1512,7 +1552,8 @@ bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot) {
   c.f64x_e_ok = false;  // (the fused step's carried predictions belong to other rows)
   if (n > 0) {
     typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
-                       unsigned*, const int*, Xfer*, unsigned char*, const long long*);
+                       unsigned*, const int*, Xfer*, unsigned char*, const long long*,
+                       const float*, const int*);
     static const Fn fns[17] = {nullptr, f64_assign_block<1, false>, f64_assign_block<2, false>,
                                f64_assign_block<3, false>, f64_assign_block<4, false>,
                                f64_assign_block<5, false>, f64_assign_block<6, false>,
@@ -1521,10 +1562,11 @@ bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot) {
                                f64_assign_block<11, false>, f64_assign_block<12, false>,
                                f64_assign_block<13, false>, f64_assign_block<14, false>,
                                f64_assign_block<15, false>, f64_assign_block<16, false>};
+    const auto ctab = f64_cent_table(c, d, k, dC);
     hipLaunchKernelGGL(fns[d], dim3((unsigned)nb), dim3(kFB), 0, c.stream, c.x64.as<double>(), n,
                        c.n_pad, dC, k, c.labels.as<int32_t>(), c.f64x_A.as<double>(),
                        c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(),
-                       nullptr, nullptr);
+                       nullptr, nullptr, ctab.first, ctab.second);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(f64s_totals, dim3((unsigned)ceil_div((int64_t)kd + k, 4)), dim3(256), 0,
                        c.stream, c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), nb, (int)kd, k,
