@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void seed_update_kernel(
 // points without reading them in fp32: x16 = fp16 of xh = (x - mu) 2^tau
 // (tau = sigma + 14, |xh| < 2^14), grouped by 8 features, [G][n_pad] x 16 B,
 // with e16[i] >= ||xh_i - x16_i|| (computed exactly in fp64 when the copy is
-// built, rounded up).  With ch = (c - mu) 2^tau rounded to fp32 (Ec >=
+// built, rounded up to fp16).  With ch = (c - mu) 2^tau rounded to fp32 (Ec >=
 // ||ch32 - ch||), the fp32 a = ||x16_i - ch32|| has relative error below
 // (D + 8) 2^-23, so
 //     ||x_i - c|| >= (a (1 - (D + 8) 2^-23) - e16[i] - Ec) 2^-tau = r_lo,
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void seed16_pack_kernel(const float* __restric
                                                           const float* __restrict__ mu,
                                                           double scale,
                                                           uint4* __restrict__ x16,
-                                                          float* __restrict__ e16) {
+                                                          unsigned short* __restrict__ e16) {
   const int G = (d + 7) / 8;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -300,9 +300,17 @@ __global__ __launch_bounds__(256) void seed16_pack_kernel(const float* __restric
       w.w = hv[6] | ((unsigned)hv[7] << 16);
       x16[(int64_t)g * n_pad + i] = w;
     }
-    // non-finite (an fp16 overflow) never certifies
+    // stored as fp16 rounded up (an upper bound; 2 bytes a point, not 4);
+    // non-finite (an fp16 overflow) and anything past fp16's range is +inf,
+    // which never certifies
     const double e = sqrt(err) * (1.0 + 0x1p-20) + 0x1p-60;
-    e16[i] = isfinite(e) ? (float)e : INFINITY;
+    unsigned short eb = 0x7C00u;
+    if (isfinite(e) && e < 65504.0) {
+      const __half h = __float2half_rn((float)e);
+      eb = __half_as_ushort(h);
+      if ((double)__half2float(h) < e) ++eb;  // the next fp16 up (e > 0)
+    }
+    e16[i] = eb;
   }
 }
 
@@ -329,7 +337,7 @@ __global__ void seed_ch_kernel(const double* __restrict__ cen, const float* __re
 // dmin and the copy are loaded together in one round trip instead.
 template <int D, int UU = 0, bool PR = (D > 16)>
 __global__ __launch_bounds__(256) void seed_update16_kernel(
-    const float* __restrict__ X, const uint4* __restrict__ x16, const float* __restrict__ e16,
+    const float* __restrict__ X, const uint4* __restrict__ x16, const unsigned short* __restrict__ e16,
     int64_t n, int64_t n_pad, const double* __restrict__ cen, const float* __restrict__ ch,
     const float* __restrict__ Ecp, double rscale, double* __restrict__ dmin,
     double* __restrict__ blocksums,
@@ -375,7 +383,7 @@ __global__ __launch_bounds__(256) void seed_update16_kernel(
           if (go[u]) {
 #pragma unroll
             for (int g = 0; g < G; ++g) hv[u][g] = x16[(int64_t)g * n_pad + i];
-            ev[u] = e16[i];
+            ev[u] = __half2float(__ushort_as_half(e16[i]));
           }
         }
       } else {
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(256) void seed_update16_kernel(
             old[u] = dmin[i];
 #pragma unroll
             for (int g = 0; g < G; ++g) hv[u][g] = x16[(int64_t)g * n_pad + i];
-            ev[u] = e16[i];
+            ev[u] = __half2float(__ushort_as_half(e16[i]));
           }
         }
       }
@@ -483,7 +491,7 @@ __global__ __launch_bounds__(256) void seed_update16_kernel(
 // certificate cannot prove the minimum unchanged.
 template <int D>
 __global__ __launch_bounds__(512) void seed_update16r_kernel(
-    const float* __restrict__ X, const uint4* __restrict__ x16, const float* __restrict__ e16,
+    const float* __restrict__ X, const uint4* __restrict__ x16, const unsigned short* __restrict__ e16,
     int64_t n, int64_t n_pad, const double* __restrict__ cen, const float* __restrict__ ch,
     const float* __restrict__ Ecp, double rscale, double* __restrict__ dmin,
     double* __restrict__ blocksums, int32_t* __restrict__ near, int cidx,
@@ -523,7 +531,7 @@ __global__ __launch_bounds__(512) void seed_update16r_kernel(
       sb.old[u] = dmin[i];
 #pragma unroll
       for (int g = 0; g < G; ++g) sb.hv[u][g] = x16[(int64_t)g * n_pad + i];
-      sb.ev[u] = e16[i];
+      sb.ev[u] = __half2float(__ushort_as_half(e16[i]));
     }
   };
   SB sbuf[2];
@@ -1941,13 +1949,13 @@ void seed_update(Ctx& c, const double* cen) {
       const int G = (d + 7) / 8;
       if (!c.seed16_valid) {
         c.seed_x16.ensure(sizeof(uint4) * (size_t)G * c.n_pad);
-        c.seed_e16.ensure(sizeof(float) * c.n_pad);
+        c.seed_e16.ensure(sizeof(unsigned short) * c.n_pad);
         c.seed_mu.ensure(sizeof(float) * d);
         HIP_CHECK(hipMemcpyAsync(c.seed_mu.p, c.mu.data(), sizeof(float) * d,
                                  hipMemcpyHostToDevice, c.stream));
         hipLaunchKernelGGL(seed16_pack_kernel, dim3(4096), dim3(256), 0, c.stream,
                            c.x32.as<float>(), c.n, c.n_pad, d, c.seed_mu.as<float>(),
-                           std::ldexp(1.0, tau), c.seed_x16.as<uint4>(), c.seed_e16.as<float>());
+                           std::ldexp(1.0, tau), c.seed_x16.as<uint4>(), c.seed_e16.as<unsigned short>());
         HIP_CHECK(hipGetLastError());
         c.seed16_valid = true;
       }
@@ -1957,7 +1965,7 @@ void seed_update(Ctx& c, const double* cen) {
       hipLaunchKernelGGL(seed_ch_kernel, dim3(1), dim3(64), 0, c.stream,
                          c.seed_scalar.as<double>(), c.seed_mu.as<float>(), d,
                          std::ldexp(1.0, tau), dch, dEc);
-      typedef void (*S16Fn)(const float*, const uint4*, const float*, int64_t, int64_t,
+      typedef void (*S16Fn)(const float*, const uint4*, const unsigned short*, int64_t, int64_t,
                             const double*, const float*, const float*, double, double*,
                             double*, int32_t*, const double*, int);
       static const int u16 = exp_env("CDR_SEED16_U") ? std::atoi(exp_env("CDR_SEED16_U")) : 0;
@@ -1972,7 +1980,7 @@ void seed_update(Ctx& c, const double* cen) {
         if (xa) ensure_rowmajor(c);
         hipLaunchKernelGGL(d == 8 ? seed_update16r_kernel<8> : seed_update16r_kernel<16>,
                            dim3(nb), dim3(512), 0, c.stream, c.x32.as<float>(),
-                           c.seed_x16.as<uint4>(), c.seed_e16.as<float>(), c.n, c.n_pad,
+                           c.seed_x16.as<uint4>(), c.seed_e16.as<unsigned short>(), c.n, c.n_pad,
                            c.seed_scalar.as<double>(), dch, dEc, std::ldexp(1.0, -tau),
                            c.dmin.as<double>(), c.blocksums.as<double>(), near, cidx,
                            xa ? c.xa32.as<float>() : nullptr);
@@ -1996,7 +2004,7 @@ void seed_update(Ctx& c, const double* cen) {
                         : d == 32 ? seed_update16_kernel<32>
                                   : seed_update16_kernel<64>;
       hipLaunchKernelGGL(f16, dim3(nb), dim3(256), 0, c.stream, c.x32.as<float>(),
-                         c.seed_x16.as<uint4>(), c.seed_e16.as<float>(), c.n, c.n_pad,
+                         c.seed_x16.as<uint4>(), c.seed_e16.as<unsigned short>(), c.n, c.n_pad,
                          c.seed_scalar.as<double>(), dch, dEc, std::ldexp(1.0, -tau),
                          c.dmin.as<double>(), c.blocksums.as<double>(), near, ccd, cidx);
       HIP_CHECK(hipGetLastError());
