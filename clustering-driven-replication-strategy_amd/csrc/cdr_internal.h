@@ -183,6 +183,11 @@ struct Ctx {
   DevBuf f64x_GC;  // f64_step_fused: per (cluster, group of 64 blocks) member counts
   DevBuf f64x_ord;  // f64_step_fused: each block's rows in cluster order (uint8 offsets)
   DevBuf f64x_cs;   // f64_cent_prep: the screen's fp32 centroid rows + norms, then its ok flag
+  // f64_step_fused's transfer cache (cdr_lloyd_f64_run): per block {labels
+  // changed this step, step stamp of its last binade change}, the list of the
+  // blocks whose transfers are recomputed, and two list counters
+  DevBuf f64x_dirty;
+  int f64x_stamp = 0;
   DevBuf f64s_off;  // sharded F64 sums: earlier shards' approximate totals, end binades
   int32_t f64s_k = 0, f64s_nranks = 0, f64s_rank = 0;  // cdr_f64s_begin's step
   bool f64x_e_ok = false;
@@ -397,8 +402,12 @@ void f64s_build(Ctx& c, int k, int nranks, int rank, const double* tot_all, void
 void f64s_compose_all(Ctx& c, int k, int nranks, const double* tot_all, const void* prog_all,
                       double* d_sums, long long* d_counts, int* d_status);
 void f64s_chain_walk(Ctx& c, int k, double* chain);
+// tcache: 0 every transfer formed; 1 every transfer formed and the cache
+// started; 2 only the blocks whose labels or binade predictions changed since
+// the previous tcache step (the others keep their transfers)
 bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
-                    unsigned long long* d_counts, bool prof, const long long* gate = nullptr);
+                    unsigned long long* d_counts, bool prof, const long long* gate = nullptr,
+                    int tcache = 0);
 void features_finalize(Ctx& c, int64_t n_files, const int64_t* counts,
                        const double* creation_s, double observation_end,
                        double* out);

@@ -447,7 +447,7 @@ int cdr_destroy(cdr_ctx* h) {
                     &c.gb_tilepref, &c.gb_chunk, &c.gb_rsum, &c.gb_part, &c.gb_small, &c.gb_res, &c.gb_bbase,
                     &c.gb_p1, &c.gb_p2, &c.gb_hist2, &c.gb_list, &c.gb_slots, &c.sim_cnt, &c.sim_off,
                     &c.sim_tmp, &c.sim_ms, &c.sim_mbase, &c.x_small, &c.x_buf, &c.x_prim, &c.f64x_A, &c.f64x_cnt, &c.f64x_E,
-                    &c.f64x_T, &c.f64x_walk, &c.f64x_G, &c.f64x_GS, &c.f64x_GC, &c.f64x_prof, &c.f64x_E2, &c.f64x_ord, &c.med_hist,
+                    &c.f64x_T, &c.f64x_walk, &c.f64x_G, &c.f64x_GS, &c.f64x_GC, &c.f64x_prof, &c.f64x_E2, &c.f64x_ord, &c.f64x_dirty, &c.med_hist,
                     &c.fb_accum, &c.q_acc, &c.xs16, &c.xa32, &c.xb16, &c.big_sums, &c.big_chunks, &c.seed_near, &c.seed_cents, &c.seed_ccd, &c.seg_tails, &c.seg_ents, &c.seg_scan, &c.seg_items, &c.seg_meta, &c.seed_tail_plan, &c.seed_x16, &c.seed_e16, &c.seed_mu, &c.seed_run_buf, &c.mv_list, &c.lab8, &c.zb, &c.xh16, &c.bnd, &c.t_acc, &c.dmin32, &c.bs32, &c.cent32r, &c.mv_count, &c.ll_C, &c.ll_new, &c.ll_sums, &c.ll_ref,
                     &c.ll_state};
   for (DevBuf* b : bufs) b->release();

@@ -224,7 +224,8 @@ __global__ __launch_bounds__(256) void f64_predict_c(const double* __restrict__ 
                                                      const unsigned* __restrict__ cnt,
                                                      int64_t nb, int d, int k, int64_t ng,
                                                      const double* __restrict__ GS,
-                                                     int* __restrict__ E) {
+                                                     int* __restrict__ E,
+                                                     int* __restrict__ dE, int stamp) {
   const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (w >= (int64_t)k * d * ng) return;
@@ -238,18 +239,64 @@ __global__ __launch_bounds__(256) void f64_predict_c(const double* __restrict__ 
     const double u = __shfl_up(inc, o);
     if (lane >= o) inc += u;
   }
-  if (b < nb) E[(int64_t)t * nb + b] = binade_e(GS[w] + (inc - v));
+  if (b < nb) {
+    const int e = binade_e(GS[w] + (inc - v));
+    // (the transfer cache: a block whose prediction moved for any sequence
+    // gets this step's stamp, so its transfers are formed again; every
+    // writer of one block writes the same value)
+    if (dE && E[(int64_t)t * nb + b] != e) dE[b] = stamp;
+    E[(int64_t)t * nb + b] = e;
+  }
 }
 
-// One thread per (block, feature); the per-cluster transfer states live in
-// LDS, cluster-major ([cluster][thread]): a lane's state for cluster j sits
-// at j * nt + lane, so the lanes of a wave hit distinct banks whatever
-// clusters their rows belong to (thread-major rows k * 8 bytes apart put
-// every other lane on the same bank).
+// The transfer cache's work list: the blocks whose transfers are formed this
+// step (all, or those whose labels changed in the assignment or whose binade
+// predictions moved), compacted in any order by one atomic per wave into
+// list; counters[par] is this step's count, and the other counter is zeroed
+// for the next step (the one that read it last has finished: stream order).
+__global__ __launch_bounds__(256) void f64_dirty_list(const int* __restrict__ dlab,
+                                                      const int* __restrict__ dE, int stamp,
+                                                      int all, int64_t nb, int* __restrict__ list,
+                                                      int* __restrict__ counters, int par) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool need = b < nb && (all || dlab[b] != 0 || dE[b] == stamp);
+  const unsigned long long m = __ballot(need);
+  int base = 0;
+  if (lane == 0 && m) base = atomicAdd(&counters[par], __popcll(m));
+  base = __shfl(base, 0);
+  if (need) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int)b;
+  if (b == 0) counters[par ^ 1] = 0;
+}
+
+// One block's transfers for every cluster, split over kTQ threads per (block,
+// feature): thread q walks the rows [q R, (q + 1) R), R = kFB / kTQ, with its
+// per-cluster states in LDS, cluster-major ([cluster][thread]): a lane's
+// state for cluster j sits at j * nt + lane, so the lanes of a wave hit
+// distinct banks whatever clusters their rows belong to.  The kTQ parts are
+// then composed in row order with shuffles (xfer_join).  Each row's update
+// is a serial LDS read-modify-write, so a wave's time is its rows' chain:
+// with the whole block in one thread (256 rows) a launch could not go below
+// one ~80 us chain however few blocks the transfer cache leaves.  Measured
+// over the bench's F64 window (10M x 5, k = 16, steps 3-22, with the cache):
+// 1, 2 and 4 parts 0.413-0.417 / 0.404-0.405 / 0.414-0.415 ms per step (more
+// parts shorten the chains but add the per-thread setup and joins).
+constexpr int kTQ = 2;
+// a then b, both Xfer (d0: steps for an even entry, dd: odd - even, flags:
+// bit0 P0, bit1 P1, bit2 invalid, bit3 members)
+__device__ __forceinline__ void xfer_join(long long& d0, int& dd, int& fl, long long bd0, int bdd,
+                                          int bfl) {
+  const int p0 = fl & 1, p1 = (fl >> 1) & 1;
+  const int q0 = bfl & 1, q1 = (bfl >> 1) & 1;
+  d0 += bd0 + (p0 ? bdd : 0);
+  dd += (p1 ? bdd : 0) - (p0 ? bdd : 0);
+  fl = (p0 ? q1 : q0) | ((p1 ? q1 : q0) << 1) | ((fl | bfl) & 12);
+}
 template <typename TA, typename S>
 __global__ __launch_bounds__(256) void f64_transfer(const S* __restrict__ X, int64_t n, int64_t n_pad, int d,
                              int k, int64_t nb, const int32_t* __restrict__ labels,
-                             const int* __restrict__ E, Xfer* __restrict__ T) {
+                             const int* __restrict__ E, Xfer* __restrict__ T,
+                             const int* __restrict__ list, const int* __restrict__ lcount) {
   extern __shared__ unsigned char smem[];
   const int nt = blockDim.x;
   long long* s0 = reinterpret_cast<long long*>(smem);   // [k][nt]
@@ -257,27 +304,34 @@ __global__ __launch_bounds__(256) void f64_transfer(const S* __restrict__ X, int
   int* sfl = sdd + (size_t)nt * k;                        // [k][nt]
   int* se = sfl + (size_t)nt * k;                         // [k][nt]
   const int64_t t = (int64_t)blockIdx.x * nt + threadIdx.x;
-  const bool live = t < nb * d;
-  // the d threads of one block are neighbours: they share its label stream
-  const int64_t b = live ? t / d : 0;
-  const int f = live ? (int)(t % d) : 0;
+  // the d * kTQ threads of one block are neighbours (they share its label
+  // stream), the kTQ parts of one (block, feature) in consecutive lanes.
+  // (list: the transfer cache's blocks, lcount[0] of them; the others keep
+  // the transfers they have)
+  const int64_t item = t / (d * kTQ);
+  const bool live = list ? item < (int64_t)lcount[0] : item < nb;
+  const int64_t b = live ? (list ? (int64_t)list[item] : item) : 0;
+  const int f = live ? (int)(t / kTQ % d) : 0;
+  const int q = (int)(t % kTQ);
   long long* m0 = s0 + threadIdx.x;  // [j * nt]
   int* mdd = sdd + threadIdx.x;
   int* mfl = sfl + threadIdx.x;
   int* me = se + threadIdx.x;
-  if (!live) return;
+  if (!live) return;  // (whole groups of kTQ lanes)
   for (int j = 0; j < k; ++j) {
     m0[j * nt] = 0;
     mdd[j * nt] = 0;
     mfl[j * nt] = 2;  // P0 = 0, P1 = 1
     me[j * nt] = E[((int64_t)j * d + f) * nb + b];
   }
-  const int64_t r0 = b * kFB, r1 = min(n, r0 + kFB);
+  constexpr int kR = kFB / kTQ;
+  const int64_t r0 = b * kFB + q * kR, r1 = min(n, r0 + kR);
   // rows in chunks of 16, the next chunk's labels and values loaded while
   // the current one goes through the (serial, LDS-dependent) updates: at two
   // waves per SIMD (LDS-bound) the memory latency is not hidden otherwise
   // (0.27 ms at 10M x 5, k = 16 with the loads of a chunk issued only at its start)
   constexpr int kCh = 16;
+  static_assert(kR % kCh == 0, "whole chunks per part");
   int lj[kCh], nj[kCh];
   double lx[kCh], nx[kCh];
   auto load = [&](int64_t rc, int* jj, double* xx) {
@@ -296,7 +350,7 @@ __global__ __launch_bounds__(256) void f64_transfer(const S* __restrict__ X, int
       }
     }
   };
-  load(r0, lj, lx);
+  if (r0 < r1) load(r0, lj, lx);
   for (int64_t rc = r0; rc < r1; rc += kCh) {
     if (rc + kCh < r1) load(rc + kCh, nj, nx);
     // the chunk's binades (read-only), then its state-free parts, then the
@@ -317,12 +371,12 @@ __global__ __launch_bounds__(256) void f64_transfer(const S* __restrict__ X, int
       const bool live_row = lj[u] >= 0;
       const int o = (live_row ? lj[u] : 0) * nt;
       long long a = m0[o];
-      int b = mdd[o], c = mfl[o];
+      int bq = mdd[o], c = mfl[o];
       const long long a0 = a;
-      const int b0 = b, c0 = c;
-      xfer_apply(pr[u], a, b, c);
+      const int b0 = bq, c0 = c;
+      xfer_apply(pr[u], a, bq, c);
       m0[o] = live_row ? a : a0;
-      mdd[o] = live_row ? b : b0;
+      mdd[o] = live_row ? bq : b0;
       mfl[o] = live_row ? c : c0;
     }
 #pragma unroll
@@ -331,12 +385,19 @@ __global__ __launch_bounds__(256) void f64_transfer(const S* __restrict__ X, int
       lx[u] = nx[u];
     }
   }
+  // the parts in row order: lane q takes q + o's composition when q is a
+  // multiple of 2o (a tree over the kTQ consecutive lanes), lane 0 writes
   for (int j = 0; j < k; ++j) {
-    Xfer x;
-    x.d0 = m0[j * nt];
-    x.dd = mdd[j * nt];
-    x.flags = mfl[j * nt];
-    T[((int64_t)j * d + f) * nb + b] = x;
+    long long x0 = m0[j * nt];
+    int xdd = mdd[j * nt], xfl = mfl[j * nt];
+#pragma unroll
+    for (int o = 1; o < kTQ; o <<= 1) {
+      const long long y0 = __shfl_down(x0, o, kTQ);
+      const int ydd = __shfl_down(xdd, o, kTQ);
+      const int yfl = __shfl_down(xfl, o, kTQ);
+      if ((q & (2 * o - 1)) == 0) xfer_join(x0, xdd, xfl, y0, ydd, yfl);
+    }
+    if (q == 0) T[((int64_t)j * d + f) * nb + b] = Xfer{x0, xdd, xfl};
   }
 }
 
@@ -827,7 +888,8 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
                                                         unsigned char* __restrict__ ordr,
                                                         const long long* __restrict__ gate,
                                                         const float* __restrict__ cs32g,
-                                                        const int* __restrict__ scr_ok) {
+                                                        const int* __restrict__ scr_ok,
+                                                        int* __restrict__ dlab) {
   // (the device-resident F64 run: a stopped run keeps the labels of the
   // assignment that stopped it)
   if (gate && gate[0] == 0) return;
@@ -849,9 +911,11 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
   if (threadIdx.x < kFMaxK) cc[threadIdx.x] = 0u;
   const int64_t row = b * kFB + threadIdx.x;
   double xr[D];
+  int jold = -1;  // (dlab: the previous label, for the transfer cache)
   if (row < n) {
 #pragma unroll
     for (int f = 0; f < D; ++f) xr[f] = X[xidx(X, f, row, n_pad)];
+    if (dlab) jold = labels[row];
   }
   // the screen's table (f64_cent_prep: fp32 rows and their fp32 squared
   // norms, read with uniform addresses) and the fp64 centroids for its
@@ -868,7 +932,9 @@ __global__ __launch_bounds__(kFB) void f64_assign_block(const double* __restrict
 #pragma unroll
     for (int f = 0; f < D; ++f) sx[f * kFB + threadIdx.x] = j >= 0 ? xr[f] : 0.0;
   }
-  __syncthreads();
+  // (the barrier; with dlab also whether any row of the block changed label)
+  const int moved = __syncthreads_or(j != jold && dlab != nullptr);
+  if (dlab && threadIdx.x == 0) dlab[b] = moved;
   if (j >= 0) {
     atomicAdd(&cc[j], 1u);
 #pragma unroll
@@ -1066,11 +1132,25 @@ struct F64Shard {
   const double* entry = nullptr;
   bool walk = true;
 };
+// The transfer cache of a device F64 run (f64_step_fused, tcache != 0): the
+// assignment's per-block label-change flags, the per-block stamps of moved
+// predictions, this step's stamp, whether every block is formed, the list and
+// its counter pair.
+struct F64TCache {
+  const int* dlab = nullptr;
+  int* dE = nullptr;
+  int stamp = 0;
+  int all = 1;
+  int* list = nullptr;
+  int* counters = nullptr;
+  int par = 0;
+};
 template <typename TA, typename S>
 static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
                              const int* Ewalk, bool have_T, const unsigned char* ordr = nullptr,
                              const F64Shard& sh = F64Shard(),
-                             unsigned long long* d_counts = nullptr);
+                             unsigned long long* d_counts = nullptr,
+                             const F64TCache* tc = nullptr);
 
 // TA: the summed (arithmetic) type; S: the storage type of X.  pre: the
 // block sums and counts (f64x_A, f64x_cnt) were already written by the
@@ -1101,7 +1181,8 @@ static bool sums_parallel(Ctx& c, const S* X, int k, double* d_sums, bool pre = 
 template <typename TA, typename S>
 static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Enew,
                              const int* Ewalk, bool have_T, const unsigned char* ordr,
-                             const F64Shard& sh, unsigned long long* d_counts) {
+                             const F64Shard& sh, unsigned long long* d_counts,
+                             const F64TCache* tc) {
   const int d = c.d;
   const int64_t n = c.n, nb = ceil_div(n, kFB);
   const size_t kd = (size_t)k * d;
@@ -1118,8 +1199,19 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
   hipLaunchKernelGGL(f64_predict_b, dim3(ceil_div((int64_t)kd, 4)), dim3(256), 0, c.stream,
                      c.f64x_GS.as<double>(), (int)kd, ng, sh.off, GC, d, d_counts);
   hipLaunchKernelGGL(f64_predict_c, gwaves, dim3(256), 0, c.stream, c.f64x_A.as<double>(),
-                     c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>(), Enew);
+                     c.f64x_cnt.as<unsigned>(), nb, d, k, ng, c.f64x_GS.as<double>(), Enew,
+                     tc ? tc->dE : nullptr, tc ? tc->stamp : 0);
   HIP_CHECK(hipGetLastError());
+  const int* tlist = nullptr;
+  const int* tcount = nullptr;
+  if (tc && !have_T && !ordr) {
+    hipLaunchKernelGGL(f64_dirty_list, dim3((unsigned)ceil_div(nb, (int64_t)256)), dim3(256), 0,
+                       c.stream, tc->dlab, tc->dE, tc->stamp, tc->all, nb, tc->list,
+                       tc->counters, tc->par);
+    HIP_CHECK(hipGetLastError());
+    tlist = tc->list;
+    tcount = tc->counters + tc->par;
+  }
   const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
   const size_t lds = (size_t)nt * k * (8 + 4 + 4 + 4);
   // (CDR_F64_TBLOCK=1: the one-workgroup-per-block transfer; measured slower
@@ -1138,9 +1230,10 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
                        c.f64x_T.as<Xfer>());
     HIP_CHECK(hipGetLastError());
   } else if (!have_T) {
-    hipLaunchKernelGGL((f64_transfer<TA, S>), dim3(ceil_div(nb * d, nt)), dim3(nt), lds, c.stream,
+    hipLaunchKernelGGL((f64_transfer<TA, S>), dim3(ceil_div(nb * d * kTQ, (int64_t)nt)), dim3(nt),
+                       lds, c.stream,
                        X, n, c.n_pad, d, k, nb, c.labels.as<int32_t>(), Ewalk,
-                       c.f64x_T.as<Xfer>());
+                       c.f64x_T.as<Xfer>(), tlist, tcount);
     HIP_CHECK(hipGetLastError());
   }
   c.f64x_G.ensure(sizeof(GXfer) * ng * kd);
@@ -1199,7 +1292,8 @@ static std::pair<const float*, const int*> f64_cent_table(Ctx& c, int d, int k, 
 }
 
 bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
-                    unsigned long long* d_counts, bool prof, const long long* gate) {
+                    unsigned long long* d_counts, bool prof, const long long* gate,
+                    int tcache) {
   const int d = c.d;
   if (d < 2 || d > 16 || k < 1 || k > kFMaxK || c.n < 1) return false;
   const int64_t n = c.n, nb = ceil_div(n, kFB);
@@ -1226,9 +1320,30 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
     c.f64x_ord.ensure((size_t)nb * kFB);
     ordr = c.f64x_ord.as<unsigned char>();
   }
+  // The transfer cache (tcache != 0, the device run's steps): a block keeps
+  // its transfers when none of its labels changed in this assignment and none
+  // of its binade predictions moved since they were formed — its (cluster,
+  // feature) sequences then hold the same values under the same binades, so
+  // the transfers are the same integers.  Near convergence few blocks change.
+  F64TCache tc;
+  const bool use_tc = tcache != 0 && !xf && !ordr;
+  if (use_tc) {
+    const size_t need = sizeof(int) * (3 * (size_t)nb + 2);
+    const bool fresh = c.f64x_dirty.bytes < need;
+    c.f64x_dirty.ensure(need);
+    int* base = c.f64x_dirty.as<int>();
+    tc.dlab = base;
+    tc.dE = base + nb;
+    tc.list = base + 2 * nb;
+    tc.counters = base + 3 * nb;
+    tc.stamp = ++c.f64x_stamp;
+    tc.par = tc.stamp & 1;
+    tc.all = tcache == 1 || fresh;
+    if (tc.all) HIP_CHECK(hipMemsetAsync(tc.counters, 0, 2 * sizeof(int), c.stream));
+  }
   typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
                      unsigned*, const int*, Xfer*, unsigned char*, const long long*, const float*,
-                     const int*);
+                     const int*, int*);
 #define CDR_FAB(D_) f64_assign_block<D_, false>, f64_assign_block<D_, true>
   static const Fn fns[17][2] = {{nullptr, nullptr}, {CDR_FAB(1)},  {CDR_FAB(2)},  {CDR_FAB(3)},
                                 {CDR_FAB(4)},       {CDR_FAB(5)},  {CDR_FAB(6)},  {CDR_FAB(7)},
@@ -1240,7 +1355,8 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   hipLaunchKernelGGL(fns[d][xf ? 1 : 0], dim3((unsigned)nb), dim3(kFB), 0, c.stream,
                      c.x64.as<double>(), n, c.n_pad, dC, k, c.labels.as<int32_t>(),
                      c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), Ecur, c.f64x_T.as<Xfer>(),
-                     ordr, gate, ctab.first, ctab.second);
+                     ordr, gate, ctab.first, ctab.second,
+                     use_tc ? const_cast<int*>(tc.dlab) : nullptr);
   HIP_CHECK(hipGetLastError());
   if (prof) prof_mark(c, 1);
   // (the counts: written by f64_predict_b from f64_predict_a's group counts)
@@ -1248,15 +1364,16 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   // under Ecur; else predict into Ecur and form the transfers under it
   int* Enew = xf ? Eoth : Ecur;
   sums_after_block<double, double>(c, c.x64.as<double>(), k, d_sums, Enew, xf ? Ecur : Enew, xf,
-                                   ordr, F64Shard(), d_counts);
+                                   ordr, F64Shard(), d_counts, use_tc ? &tc : nullptr);
   static const bool xcheck = exp_env("CDR_F64_XCHECK") != nullptr;
   if (xcheck && xf) {  // (diagnostics) the fused transfers vs f64_transfer under the same E
     DevBuf t2;
     t2.ensure(sizeof(Xfer) * nb * kd);
     const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
-    hipLaunchKernelGGL((f64_transfer<double, double>), dim3(ceil_div(nb * d, nt)), dim3(nt),
+    hipLaunchKernelGGL((f64_transfer<double, double>), dim3(ceil_div(nb * d * kTQ, (int64_t)nt)), dim3(nt),
                        (size_t)nt * k * 20, c.stream, c.x64.as<double>(), n, c.n_pad, d, k, nb,
-                       c.labels.as<int32_t>(), Ecur, t2.as<Xfer>());
+                       c.labels.as<int32_t>(), Ecur, t2.as<Xfer>(), (const int*)nullptr,
+                       (const int*)nullptr);
     std::vector<Xfer> a(nb * kd), b(nb * kd);
     std::vector<int> e0(nb * kd), e1(nb * kd);
     HIP_CHECK(hipMemcpyAsync(a.data(), c.f64x_T.p, sizeof(Xfer) * a.size(), hipMemcpyDeviceToHost, c.stream));
@@ -1553,7 +1670,7 @@ bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot) {
   if (n > 0) {
     typedef void (*Fn)(const double*, int64_t, int64_t, const double*, int, int32_t*, double*,
                        unsigned*, const int*, Xfer*, unsigned char*, const long long*,
-                       const float*, const int*);
+                       const float*, const int*, int*);
     static const Fn fns[17] = {nullptr, f64_assign_block<1, false>, f64_assign_block<2, false>,
                                f64_assign_block<3, false>, f64_assign_block<4, false>,
                                f64_assign_block<5, false>, f64_assign_block<6, false>,
@@ -1566,7 +1683,7 @@ bool f64s_assign_totals(Ctx& c, int k, const double* dC, double* tot_slot) {
     hipLaunchKernelGGL(fns[d], dim3((unsigned)nb), dim3(kFB), 0, c.stream, c.x64.as<double>(), n,
                        c.n_pad, dC, k, c.labels.as<int32_t>(), c.f64x_A.as<double>(),
                        c.f64x_cnt.as<unsigned>(), c.f64x_E.as<int>(), c.f64x_T.as<Xfer>(),
-                       nullptr, nullptr, ctab.first, ctab.second);
+                       nullptr, nullptr, ctab.first, ctab.second, nullptr);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(f64s_totals, dim3((unsigned)ceil_div((int64_t)kd + k, 4)), dim3(256), 0,
                        c.stream, c.f64x_A.as<double>(), c.f64x_cnt.as<unsigned>(), nb, (int)kd, k,

@@ -1400,6 +1400,11 @@ void lloyd_run_f64(Ctx& c, const double* C, int32_t k, int32_t max_steps, double
   // run the rest of every queued step's kernels.  One host sync
   // per chunk costs ~20 us against ~0.5 ms per step.
   int chunk = 4, queued = 0;
+  // the transfer cache across the run's steps (f64_step_fused; the first step
+  // forms every transfer).  CDR_F64_TCACHE=0 forms every transfer every step
+  // (tests/test_gpu_f64_update.py compares the two).
+  const char* tce = getenv("CDR_F64_TCACHE");
+  const bool tc_on = !tce || std::atoi(tce) != 0;
   for (int s = 0; s < max_steps; ++s) {
     if (queued == chunk) {
       HIP_CHECK(hipMemcpyAsync(hst, st, sizeof(long long), hipMemcpyDeviceToHost, c.stream));
@@ -1413,7 +1418,7 @@ void lloyd_run_f64(Ctx& c, const double* C, int32_t k, int32_t max_steps, double
     if (prof) prof_mark(c, 0);
     if (!f64_step_fused(c, k, c.cent64.as<double>(), c.f64_sums.as<double>(),
                         reinterpret_cast<unsigned long long*>(c.f64_counts.as<long long>()), prof,
-                        st))
+                        st, tc_on ? (s == 0 ? 1 : 2) : 0))
       CDR_FAIL(CDR_ERR_UNSUPPORTED, "device F64 run: shape not covered");
     hipLaunchKernelGGL(f64_run_update, dim3(1), dim3(kF64RunThreads), 0, c.stream,
                        c.f64_sums.as<double>(),

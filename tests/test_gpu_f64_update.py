@@ -245,6 +245,39 @@ def test_device_run_matches_host_steps(ctx):
     np.testing.assert_array_equal(C_b, C_host)
 
 
+def test_device_run_transfer_cache(ctx, monkeypatch):
+    """The device run's transfer cache (f64_step_fused, tcache): a block
+    keeps its transfers while its labels and binade predictions stay, so
+    converging blob data recomputes few blocks per step.  25 steps in one call,
+    in two calls (3 + 22: the second starts the cache again) and with the
+    cache off (CDR_F64_TCACHE=0) give the same centroids and labels bit for
+    bit, and so does the host loop of single steps (no cache)."""
+    gen = type(ctx)(0)
+    try:
+        gen.generate_points(1_000_003, 0, 1_000_003, 5, 16, 0x5EED)
+        X = gen.get_rows(np.arange(1_000_003, dtype=np.int64))
+    finally:
+        gen.close()
+    X = (X - X.min(axis=0)) / (X.max(axis=0) - X.min(axis=0))
+    ctx.load_points(X)
+    assert ctx.info()["mode"] == 2
+    C0 = X[np.sort(np.random.default_rng(42).choice(X.shape[0], 16, replace=False))].copy()
+    C_one, n_one, _, _, _ = ctx.lloyd_f64_run(C0, 25, -1.0)
+    lab_one = ctx.labels()
+    C_a, n_a, _, _, _ = ctx.lloyd_f64_run(C0, 3, -1.0)
+    C_two, n_b, _, _, _ = ctx.lloyd_f64_run(C_a, 22, -1.0)
+    assert (n_one, n_a, n_b) == (25, 3, 22)
+    np.testing.assert_array_equal(C_two, C_one)
+    np.testing.assert_array_equal(ctx.labels(), lab_one)
+    monkeypatch.setenv("CDR_F64_TCACHE", "0")
+    C_off, _, _, _, _ = ctx.lloyd_f64_run(C0, 25, -1.0)
+    monkeypatch.delenv("CDR_F64_TCACHE")
+    np.testing.assert_array_equal(C_off, C_one)
+    np.testing.assert_array_equal(ctx.labels(), lab_one)
+    np.testing.assert_array_equal(_host_steps(ctx, C0, 25), C_one)
+    np.testing.assert_array_equal(ctx.labels(), lab_one)
+
+
 def test_device_run_hands_back_empty_cluster(ctx):
     """A cluster without members stops the run before that step is applied:
     C_out = the centroids the step started from, means / counts = the step's
