@@ -254,17 +254,26 @@ __global__ __launch_bounds__(256) void f64_predict_c(const double* __restrict__ 
 // predictions moved), compacted in any order by one atomic per wave into
 // list; counters[par] is this step's count, and the other counter is zeroed
 // for the next step (the one that read it last has finished: stream order).
+// One atomic per workgroup (one per wave on a single address serialised to
+// ~9 us per launch).
 __global__ __launch_bounds__(256) void f64_dirty_list(const int* __restrict__ dlab,
                                                       const int* __restrict__ dE, int stamp,
                                                       int all, int64_t nb, int* __restrict__ list,
                                                       int* __restrict__ counters, int par) {
+  __shared__ int wsum[4], wbase;
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool need = b < nb && (all || dlab[b] != 0 || dE[b] == stamp);
   const unsigned long long m = __ballot(need);
-  int base = 0;
-  if (lane == 0 && m) base = atomicAdd(&counters[par], __popcll(m));
-  base = __shfl(base, 0);
+  if (lane == 0) wsum[w] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    wbase = tot ? atomicAdd(&counters[par], tot) : 0;
+  }
+  __syncthreads();
+  int base = wbase;
+  for (int q = 0; q < w; ++q) base += wsum[q];
   if (need) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int)b;
   if (b == 0) counters[par ^ 1] = 0;
 }
