@@ -305,13 +305,15 @@ __device__ __forceinline__ void xfer_join(long long& d0, int& dd, int& fl, long 
   dd += (p1 ? bdd : 0) - (p0 ? bdd : 0);
   fl = (p0 ? q1 : q0) | ((p1 ? q1 : q0) << 1) | ((fl | bfl) & 12);
 }
-template <typename TA, typename S>
+// NTS: log2 of the workgroup size (the state rows' stride: shifts, not
+// quarter-rate multiplies, in the per-row LDS addresses)
+template <typename TA, typename S, int NTS>
 __global__ __launch_bounds__(256) void f64_transfer(const S* __restrict__ X, int64_t n, int64_t n_pad, int d,
                              int k, int64_t nb, const int32_t* __restrict__ labels,
                              const int* __restrict__ E, Xfer* __restrict__ T,
                              const int* __restrict__ list, const int* __restrict__ lcount) {
   extern __shared__ unsigned char smem[];
-  const int nt = blockDim.x;
+  constexpr int nt = 1 << NTS;
   long long* s0 = reinterpret_cast<long long*>(smem);   // [k][nt]
   int* sdd = reinterpret_cast<int*>(s0 + (size_t)nt * k);  // [k][nt]
   int* sfl = sdd + (size_t)nt * k;                        // [k][nt]
@@ -1225,7 +1227,9 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
     tlist = tc->list;
     tcount = tc->counters + tc->par;
   }
-  const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
+  // 80 KB of per-thread states per workgroup (k <= 64): two workgroups per CU
+  const int nts = k <= 16 ? 8 : (k <= 32 ? 7 : 6);
+  const int nt = 1 << nts;
   const size_t lds = (size_t)nt * k * (8 + 4 + 4 + 4);
   // (CDR_F64_TBLOCK=1: the one-workgroup-per-block transfer; measured slower
   // at 10M x 5, k = 16: 0.25-0.30 ms against f64_transfer's 0.24 ms)
@@ -1243,8 +1247,9 @@ static bool sums_after_block(Ctx& c, const S* X, int k, double* d_sums, int* Ene
                        c.f64x_T.as<Xfer>());
     HIP_CHECK(hipGetLastError());
   } else if (!have_T) {
-    hipLaunchKernelGGL((f64_transfer<TA, S>), dim3(ceil_div(nb * d * kTQ, (int64_t)nt)), dim3(nt),
-                       lds, c.stream,
+    auto fn = nts == 8 ? f64_transfer<TA, S, 8> : (nts == 7 ? f64_transfer<TA, S, 7>
+                                                              : f64_transfer<TA, S, 6>);
+    hipLaunchKernelGGL(fn, dim3(ceil_div(nb * d * kTQ, (int64_t)nt)), dim3(nt), lds, c.stream,
                        X, n, c.n_pad, d, k, nb, c.labels.as<int32_t>(), Ewalk,
                        c.f64x_T.as<Xfer>(), tlist, tcount);
     HIP_CHECK(hipGetLastError());
@@ -1382,8 +1387,8 @@ bool f64_step_fused(Ctx& c, int k, const double* dC, double* d_sums,
   if (xcheck && xf) {  // (diagnostics) the fused transfers vs f64_transfer under the same E
     DevBuf t2;
     t2.ensure(sizeof(Xfer) * nb * kd);
-    const int nt = std::max(32, std::min(256, 4096 / k)) & ~31;
-    hipLaunchKernelGGL((f64_transfer<double, double>), dim3(ceil_div(nb * d * kTQ, (int64_t)nt)), dim3(nt),
+    const int nt = 64;  // (k <= 64)
+    hipLaunchKernelGGL((f64_transfer<double, double, 6>), dim3(ceil_div(nb * d * kTQ, (int64_t)nt)), dim3(nt),
                        (size_t)nt * k * 20, c.stream, c.x64.as<double>(), n, c.n_pad, d, k, nb,
                        c.labels.as<int32_t>(), Ecur, t2.as<Xfer>(), (const int*)nullptr,
                        (const int*)nullptr);
