@@ -413,11 +413,20 @@ def f64_bench(args, world: int, rank: int, dist, device, json_fd) -> dict:
             C = step(C)
         return C
 
+    if resident:
+        # the whole warmup + timed trajectory once, untimed, from the same
+        # start: the host-side data preparation leaves the GPU idle for
+        # seconds, and the first milliseconds after it run below full clock
+        # (tools/f64_time.py: the first of three identical runs is ~5 % slower)
+        run(C, args.warmup + args.steps)
+        ctx.synchronize()
     C = run(C, args.warmup)
     ctx.synchronize()
     if dist is not None:
         dist.barrier()
-    ctx.profile_reset(True)
+    # HIP events around every 4th step's kernels, as in the Lloyd leg (three
+    # events a step cost the GPU a few microseconds each)
+    ctx.profile_reset(True, every=4)
     t0 = time.perf_counter()
     C = run(C, args.steps)
     ctx.synchronize()
