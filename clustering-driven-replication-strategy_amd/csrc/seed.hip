@@ -475,12 +475,12 @@ __global__ __launch_bounds__(256) void seed_update16_kernel(
   if (!TAIL && threadIdx.x == 0) blocksums[b] = halves[0] + halves[1];
 }
 
-// The same update with the block's pairwise tree kept in registers (the
-// default for d = 8 and 16; CDR_SEED16_LDS=1: seed_update16_kernel).  One
+// The update with the block's pairwise tree kept in registers (the default
+// for d = 8 and 16; CDR_SEED16_LDS=1: seed_update16_kernel).  One
 // 512-thread workgroup per 8192-row block; thread (half h, leaf L, j) owns
 // NumPy's accumulator j of the 128-element leaf L of half h, i.e. the rows
 // 128 L + j + 8 i (i = 0 .. 15), and adds its 16 updated minima in NumPy's
-// order (r = v_0, then r += v_i) as it produces them: no LDS staging of the
+// order (r = v_0, then r += v_i) from registers: no LDS staging of the
 // half's 4096 values (34 KB per workgroup capped seed_update16_kernel at 4
 // workgroups per CU) and no transposed re-read.  Accumulators combine by
 // shuffles ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) and the leaves
@@ -489,8 +489,20 @@ __global__ __launch_bounds__(256) void seed_update16_kernel(
 // dmin, 128 B of each copy group).  Rows are taken 4 per batch, the batch's
 // loads issued together; the fp32 row is read only where the fp16
 // certificate cannot prove the minimum unchanged.
+// The exact path is compacted per wave (round 6).  PMC put the previous form
+// (each batch gathering its uncertified rows in place) at TD 97 % / TA 81 %
+// busy with 44K vector-memory instructions per CU and launch, ~19K of them
+// the exact path's row gathers: a batch ran them whenever any lane of the
+// wave could not certify a row, with one or two lanes active.  Here phase 1 streams every row of the thread (certificate
+// only) and keeps its 16 current minima in registers with a 16-bit mask of
+// the rows left; phase 2 lists the wave's (lane, row) pairs in LDS and
+// evaluates them 64 at a time, one per lane (a full-width gather); phase 3
+// adds the thread's 16 values in NumPy's order as before.  Same values, same
+// order: dmin, near and the block sums are bit-identical.  1.15 -> 1.08 ms per
+// launch on average at config 3 (the converged steps stay ~0.91 ms: the
+// streamed 42 B per row at ~4.8 TB/s), seeding 0.1075 -> 0.1055 s.
 template <int D>
-__global__ __launch_bounds__(512) void seed_update16r_kernel(
+__global__ __launch_bounds__(512) void seed_update16c_kernel(
     const float* __restrict__ X, const uint4* __restrict__ x16, const unsigned short* __restrict__ e16,
     int64_t n, int64_t n_pad, const double* __restrict__ cen, const float* __restrict__ ch,
     const float* __restrict__ Ecp, double rscale, double* __restrict__ dmin,
@@ -498,26 +510,26 @@ __global__ __launch_bounds__(512) void seed_update16r_kernel(
     const float* __restrict__ XA) {
   constexpr int G = (D + 7) / 8;
   constexpr int Q = (D + 3) / 4;
-  constexpr int kB = D <= 8 ? 4 : 2;  // rows per batch (registers: 4 at d = 16 left 3 waves / SIMD)
+  constexpr int kB = D <= 8 ? 4 : 2;
   constexpr float kRel = 1.0f - (float)(D + 8) * 0x1p-23f;
+  constexpr int kCap = 256;  // exact rows per wave and round
   __shared__ double swave[8];
+  __shared__ unsigned short slist[8][kCap];
+  __shared__ double supd[8][kCap];
   const float Ec = Ecp[0];
   const int64_t b = blockIdx.x;
   const int64_t base = b * kSeedBlock;
   const int m = (n - base) < kSeedBlock ? (int)(n - base) : kSeedBlock;
   const int t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6;
   const int h = t >> 8, L = (t >> 3) & 31, j = t & 7;
   const int r0 = h * 4096 + 128 * L + j;  // row of i = 0 (row of i: r0 + 8 i)
   typedef float f4v __attribute__((ext_vector_type(4)));
   const f4v* X4 = reinterpret_cast<const f4v*>(X);
+  const f4v* XA4 = reinterpret_cast<const f4v*>(XA);
   float chv[D];
 #pragma unroll
   for (int f = 0; f < D; ++f) chv[f] = ch[f];
-  double acc = 0.0;
-  // batch bi's streamed words (dmin, the fp16 copy, its error), two batches
-  // in flight: the next batch's loads are issued before this batch's
-  // certificate and exact-path gather, so the dependent gather's latency
-  // overlaps them
   struct SB {
     double old[kB];
     uint4 hv[kB][G];
@@ -534,6 +546,9 @@ __global__ __launch_bounds__(512) void seed_update16r_kernel(
       sb.ev[u] = __half2float(__ushort_as_half(e16[i]));
     }
   };
+  // phase 1: the certificate over the thread's 16 rows
+  double ov[16];
+  unsigned nm = 0;
   SB sbuf[2];
   sload(sbuf[0], 0);
 #pragma unroll
@@ -541,12 +556,11 @@ __global__ __launch_bounds__(512) void seed_update16r_kernel(
     const int i0 = bi * kB;
     if (bi + 1 < 16 / kB) sload(sbuf[(bi + 1) & 1], i0 + kB);
     const SB& sb = sbuf[bi & 1];
-    bool in[kB], need[kB];
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
-      in[u] = r0 + 8 * (i0 + u) < m;
-      need[u] = in[u];
-      if (in[u] && cidx > 0) {
+      const bool in = r0 + 8 * (i0 + u) < m;
+      bool need = in;
+      if (in && cidx > 0) {
         float sacc = 0.0f;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -564,43 +578,82 @@ __global__ __launch_bounds__(512) void seed_update16r_kernel(
         const float lo = sqrtf(sacc) * kRel - sb.ev[u] - Ec;
         if (lo > 0.0f) {
           const double rr = (double)lo * rscale;
-          need[u] = !(rr * rr >= sb.old[u] * (1.0 + 0x1p-30));
+          need = !(rr * rr >= sb.old[u] * (1.0 + 0x1p-30));
         }
       }
+      ov[i0 + u] = in ? sb.old[u] : 0.0;
+      if (need) nm |= 1u << (i0 + u);
     }
-    // the exact path for the rows left: the fp32 row from the row-major copy
-    // (one 64-byte line at d = 16; XA null: the quad planes, Q lines)
-    f4v xv[kB][Q];
-    const f4v* XA4 = reinterpret_cast<const f4v*>(XA);
+  }
+  // phase 2: the wave's uncertified rows, one per lane
+  const int cnt = __popc(nm);
+  int incl = cnt;
 #pragma unroll
-    for (int u = 0; u < kB; ++u) {
-      const int64_t i = base + r0 + 8 * (i0 + u);
-      if (need[u]) {
-#pragma unroll
-        for (int qq = 0; qq < Q; ++qq)
-          xv[u][qq] = XA4 ? XA4[i * Q + qq] : X4[(int64_t)qq * n_pad + i];
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const int total = __shfl(incl, 63);
+  const int myoff = incl - cnt;
+  for (int e0 = 0; e0 < total; e0 += kCap) {  // (wave-uniform)
+    {
+      unsigned mm = nm;
+      int e = myoff;
+      while (mm) {
+        const int i = __builtin_ctz(mm);
+        mm &= mm - 1u;
+        if (e >= e0 && e < e0 + kCap) slist[wv][e - e0] = (unsigned short)((lane << 4) | i);
+        ++e;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int nr = total - e0 < kCap ? total - e0 : kCap;
+    for (int k0 = 0; k0 < nr; k0 += 64) {
+      const int k = k0 + lane;
+      if (k < nr) {
+        const int ent = slist[wv][k];
+        const int ts = wv * 64 + (ent >> 4), i = ent & 15;
+        const int64_t row =
+            base + (ts >> 8) * 4096 + 128 * ((ts >> 3) & 31) + (ts & 7) + 8 * i;
+        f4v xv[Q];
 #pragma unroll
-    for (int u = 0; u < kB; ++u) {
-      double v = in[u] ? sb.old[u] : 0.0;
-      if (need[u]) {
-        auto xf = [&](int f) { return (double)xv[u][f >> 2][f & 3]; };
+        for (int qq = 0; qq < Q; ++qq)
+          xv[qq] = XA4 ? XA4[row * Q + qq] : X4[(int64_t)qq * n_pad + row];
+        const double old = dmin[row];
+        auto xf = [&](int f) { return (double)xv[f >> 2][f & 3]; };
         auto cf = [&](int f) { return cen[f]; };
         const double R = np_sqdist(xf, cf, D);
         const double rt = sqrt(R);
         const double tt = rt * rt;
-        if (tt < sb.old[u]) {
+        double v = old;
+        if (tt < old) {
           v = tt;
-          const int64_t i = base + r0 + 8 * (i0 + u);
-          dmin[i] = tt;
-          near[i] = cidx;
+          dmin[row] = tt;
+          near[row] = cidx;
         }
+        supd[wv][k] = v;
       }
-      acc = (i0 + u == 0) ? v : acc + v;  // NumPy: r[j] = a[j], then r[j] += a[j + 8 i]
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if ((nm >> i) & 1u) {
+        const int e = myoff + __popc(nm & ((1u << i) - 1u));
+        if (e >= e0 && e < e0 + kCap) ov[i] = supd[wv][e - e0];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
   if (m < kSeedBlock) return;  // the partial last block: seed_tail_sum_kernel sums it
+  // phase 3: NumPy's accumulator j of its leaf: r = v_0, then r += v_i
+  double acc = ov[0];
+#pragma unroll
+  for (int i = 1; i < 16; ++i) acc = acc + ov[i];
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) acc = acc + __shfl_xor(acc, o);
   if ((t & 63) == 0) swave[t >> 6] = acc;
@@ -1978,7 +2031,7 @@ void seed_update(Ctx& c, const double* cen) {
         // from the quad planes
         const bool xa = !exp_env("CDR_SEED_XA") || std::atoi(exp_env("CDR_SEED_XA"));
         if (xa) ensure_rowmajor(c);
-        hipLaunchKernelGGL(d == 8 ? seed_update16r_kernel<8> : seed_update16r_kernel<16>,
+        hipLaunchKernelGGL(d == 8 ? seed_update16c_kernel<8> : seed_update16c_kernel<16>,
                            dim3(nb), dim3(512), 0, c.stream, c.x32.as<float>(),
                            c.seed_x16.as<uint4>(), c.seed_e16.as<unsigned short>(), c.n, c.n_pad,
                            c.seed_scalar.as<double>(), dch, dEc, std::ldexp(1.0, -tau),
