@@ -1330,6 +1330,46 @@ __device__ __forceinline__ void part_add(Part& P, double p, int e) {
   if (P.d0 >= kD52 || P.d1 >= kD52) P.st = 2;
 }
 
+// part_add with the run's counts kept as fp64 integers (exact below 2^53; a
+// run stops at 2^52) and their parities as bits: no fp64 -> int64 conversion
+// per element (seg_block's loop is VALU-bound); to_part gives the Part that
+// part_add would have built from the same elements.
+struct PartD {
+  double d0, d1;
+  int p0, p1;  // parities of d0, d1
+  int e, st;
+};
+__device__ __forceinline__ PartD partd_empty() { return PartD{0.0, 0.0, 0, 0, kNoE, 0}; }
+__device__ __forceinline__ void partd_add(PartD& P, double p, int e) {
+  if (P.st == 0) P = PartD{0.0, 0.0, 0, 0, e, 1};
+  if (P.st != 1) return;
+  if (P.e != e) {
+    P.st = 2;
+    return;
+  }
+  const double f = ldexp(p, 52 - e);
+  if (!(f < 4503599627370496.0)) {
+    P.st = 2;
+    return;
+  }
+  const double fl = floor(f);
+  const double frac = f - fl;
+  // fl < 2^52: in fl + 2^52 the last significand bit is fl's parity
+  const int kp = (int)(__double_as_longlong(fl + 4503599627370496.0) & 1);
+  const int up = frac > 0.5 ? 1 : 0;
+  const int tie = frac == 0.5 ? 1 : 0;
+  const int i0 = up | (tie & (P.p0 ^ kp));
+  const int i1 = up | (tie & (1 ^ P.p1 ^ kp));
+  P.d0 = (P.d0 + fl) + (double)i0;
+  P.d1 = (P.d1 + fl) + (double)i1;
+  P.p0 ^= kp ^ i0;
+  P.p1 ^= kp ^ i1;
+  if (P.d0 >= 4503599627370496.0 || P.d1 >= 4503599627370496.0) P.st = 2;
+}
+__device__ __forceinline__ Part to_part(const PartD& P) {
+  return Part{(long long)P.d0, (long long)P.d1, P.e, P.st};
+}
+
 __device__ __forceinline__ Part shfl_up_part(const Part& P, int o) {
   return Part{__shfl_up(P.d0, o), __shfl_up(P.d1, o), __shfl_up(P.e, o), __shfl_up(P.st, o)};
 }
@@ -1398,10 +1438,23 @@ __global__ __launch_bounds__(512) void seg_block_kernel(const double* __restrict
     double2 v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = src[j];
+    // p = fl(dmin / S) by Markstein's correction from y = fl(1 / S): q0 =
+    // fl(a y), r = a - S q0 (exact in one fma), fl(q0 + r y) is the correctly
+    // rounded quotient (no underflow: a >= 2^-960, S < 2^1000; others divide).
+    // 3 fp64 instructions per element instead of the ~11 of a division
+    // (tools/markstein_div_fuzz.cpp: 3.2e8 quotients, none differs).
+    const double y = 1.0 / S;
+    const bool fastS = S < 0x1p1000;
+    auto quo = [&](double a) {
+      const double q0 = a * y;
+      double q = fma(fma(-q0, S, a), y, q0);
+      if (!(fastS && a >= 0x1p-960)) q = a / S;
+      return q;
+    };
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      p[2 * j] = 2 * j < cnt ? v[j].x / S : 0.0;
-      p[2 * j + 1] = 2 * j + 1 < cnt ? v[j].y / S : 0.0;
+      p[2 * j] = 2 * j < cnt ? quo(v[j].x) : 0.0;
+      p[2 * j + 1] = 2 * j + 1 < cnt ? quo(v[j].y) : 0.0;
     }
   }
   double s = 0.0;
@@ -1464,7 +1517,7 @@ __global__ __launch_bounds__(512) void seg_block_kernel(const double* __restrict
   bool bad = false;
   const int bl = basew + mi - m;  // this lane's first entry
   if (!over) {
-    Part cur = part_empty();
+    PartD cur = partd_empty();
     int jj = 0;
     double cb = a0;
     int gb = gbin(cb);
@@ -1474,23 +1527,23 @@ __global__ __launch_bounds__(512) void seg_block_kernel(const double* __restrict
         const double ca = (j == cnt - 1) ? a1 : cb + p[j];
         if ((xm >> j) & 1) {
           if (jj == 0) {
-            F = cur;
+            F = to_part(cur);
             p0 = p[j];
           } else {
-            eb[bl + jj] = SegEnt{cur, p[j]};
+            eb[bl + jj] = SegEnt{to_part(cur), p[j]};
             bad |= cur.st == 2;
           }
           ++jj;
-          cur = part_empty();
+          cur = partd_empty();
         } else {
-          part_add(cur, p[j], gb);
+          partd_add(cur, p[j], gb);
         }
         cb = ca;
         gb = gbin(ca);
       }
     }
     // segmented inclusive scan of the lane tails (heads: lanes with a crossing)
-    Sx = cur;
+    Sx = to_part(cur);
     int hs = m > 0;
     for (int o = 1; o < 64; o <<= 1) {
       const Part L = shfl_up_part(Sx, o);
