@@ -549,40 +549,79 @@ __global__ __launch_bounds__(512) void seed_update16c_kernel(
   // phase 1: the certificate over the thread's 16 rows
   double ov[16];
   unsigned nm = 0;
-  SB sbuf[2];
-  sload(sbuf[0], 0);
+  if (cidx == 0) {
+    // the first centre: every minimum is +inf, nothing to certify - the
+    // exact distances straight from the rows, 4 rows' loads in flight (not
+    // the stream of copies and bounds plus a list of every row)
 #pragma unroll
-  for (int bi = 0; bi < 16 / kB; ++bi) {
-    const int i0 = bi * kB;
-    if (bi + 1 < 16 / kB) sload(sbuf[(bi + 1) & 1], i0 + kB);
-    const SB& sb = sbuf[bi & 1];
+    for (int i0 = 0; i0 < 16; i0 += 4) {
+      f4v xv[4][Q];
+      double old[4];
 #pragma unroll
-    for (int u = 0; u < kB; ++u) {
-      const bool in = r0 + 8 * (i0 + u) < m;
-      bool need = in;
-      if (in && cidx > 0) {
-        float sacc = 0.0f;
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + 8 * (i0 + u);
+        const int64_t row = base + (r < m ? r : 0);
+        old[u] = dmin[row];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const unsigned w[4] = {sb.hv[u][g].x, sb.hv[u][g].y, sb.hv[u][g].z, sb.hv[u][g].w};
+        for (int qq = 0; qq < Q; ++qq)
+          xv[u][qq] = XA4 ? XA4[row * Q + qq] : X4[(int64_t)qq * n_pad + row];
+      }
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            if (8 * g + q < D) {
-              const float xv = __half2float(
-                  __ushort_as_half((unsigned short)(w[q >> 1] >> (16 * (q & 1)))));
-              const float dd = xv - chv[8 * g + q];
-              sacc = fmaf(dd, dd, sacc);
-            }
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + 8 * (i0 + u);
+        double v = 0.0;
+        if (r < m) {
+          auto xf = [&](int f) { return (double)xv[u][f >> 2][f & 3]; };
+          auto cf = [&](int f) { return cen[f]; };
+          const double R = np_sqdist(xf, cf, D);
+          const double rt = sqrt(R);
+          const double tt = rt * rt;
+          v = old[u];
+          if (tt < old[u]) {
+            v = tt;
+            dmin[base + r] = tt;
+            near[base + r] = cidx;
           }
         }
-        const float lo = sqrtf(sacc) * kRel - sb.ev[u] - Ec;
-        if (lo > 0.0f) {
-          const double rr = (double)lo * rscale;
-          need = !(rr * rr >= sb.old[u] * (1.0 + 0x1p-30));
-        }
+        ov[i0 + u] = v;
       }
-      ov[i0 + u] = in ? sb.old[u] : 0.0;
-      if (need) nm |= 1u << (i0 + u);
+    }
+  } else {
+    SB sbuf[2];
+    sload(sbuf[0], 0);
+#pragma unroll
+    for (int bi = 0; bi < 16 / kB; ++bi) {
+      const int i0 = bi * kB;
+      if (bi + 1 < 16 / kB) sload(sbuf[(bi + 1) & 1], i0 + kB);
+      const SB& sb = sbuf[bi & 1];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const bool in = r0 + 8 * (i0 + u) < m;
+        bool need = in;
+        if (in && cidx > 0) {
+          float sacc = 0.0f;
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const unsigned w[4] = {sb.hv[u][g].x, sb.hv[u][g].y, sb.hv[u][g].z, sb.hv[u][g].w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              if (8 * g + q < D) {
+                const float xv = __half2float(
+                    __ushort_as_half((unsigned short)(w[q >> 1] >> (16 * (q & 1)))));
+                const float dd = xv - chv[8 * g + q];
+                sacc = fmaf(dd, dd, sacc);
+              }
+            }
+          }
+          const float lo = sqrtf(sacc) * kRel - sb.ev[u] - Ec;
+          if (lo > 0.0f) {
+            const double rr = (double)lo * rscale;
+            need = !(rr * rr >= sb.old[u] * (1.0 + 0x1p-30));
+          }
+        }
+        ov[i0 + u] = in ? sb.old[u] : 0.0;
+        if (need) nm |= 1u << (i0 + u);
+      }
     }
   }
   // phase 2: the wave's uncertified rows, one per lane
